@@ -1,0 +1,105 @@
+/*
+ * gossip_oracle.h -- CPU restatement of aiocluster's hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This is the *checker* for the HIP simulator
+ * (aiocluster_amd/csrc), never the product: only tests/, __graft_entry__.smoke()
+ * and bench.py's cpu_baseline leg may load it.  It restates, object by object,
+ * the reference's Python semantics:
+ *
+ *   NodeState / ClusterState  -- aiocluster/state.py:106-415
+ *   SamplingWindow / FailureDetector / BoundedArrayStats
+ *                             -- aiocluster/failure_detector.py:12-162
+ *   exchange + round driver   -- aiocluster/server.py:327-376, 441-495, 523-568, 599-620
+ *
+ * Time is in microseconds (the reference's datetime resolution).  Values are
+ * interned by the host: value_id identifies the string, value_len is its UTF-8
+ * byte length (all the hot path needs for protobuf sizes).
+ *
+ * Pinned against the real reference by tests/golden/scen_*.json.gz (generated
+ * by oracle/gen_golden.py) and by ports of the reference's own unit tests.
+ */
+#ifndef GOSSIP_ORACLE_H
+#define GOSSIP_ORACLE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct orc_config {
+    int32_t n_nodes;
+    int32_t n_keys;
+    int32_t mtu;                    /* Config.max_payload_size (entities.py:105) */
+    int64_t tombstone_grace_us;     /* Config.marked_for_deletion_grace_period (entities.py:101) */
+    double  phi_threshold;          /* FailureDetectorConfig.phi_threshhold (entities.py:87) */
+    int32_t window;                 /* sampling_window_size (entities.py:88) */
+    int64_t max_interval_us;        /* entities.py:89 */
+    int64_t initial_interval_us;    /* entities.py:90 (the prior mean) */
+    int64_t dead_grace_us;          /* dead_node_grace_period (entities.py:91) */
+} orc_config;
+
+typedef struct orc orc;
+
+typedef struct orc_stats {
+    uint64_t exchanges;
+    uint64_t node_deltas;
+    uint64_t kvs_sent;
+    uint64_t delta_bytes;      /* sum of DeltaPb sizes sent */
+    uint64_t hb_reports;       /* FailureDetector.report_heartbeat calls */
+    uint64_t truncated;        /* NodeDeltas cut by the MTU */
+} orc_stats;
+
+orc *orc_create(const orc_config *cfg, const int32_t *nid_size, const int32_t *key_len);
+void orc_destroy(orc *o);
+
+/* Cluster.__init__ (server.py:90-100): self view with heartbeat 1. */
+void orc_boot(orc *o, int32_t node);
+/* Every observer learns every owner in index order (warm start injection). */
+void orc_init_warm(orc *o);
+
+/* NodeState.set / delete / set_with_ttl / delete_after_ttl (state.py:137-180). op: 0..3 */
+void orc_write(orc *o, int32_t owner, int32_t key, int32_t op, uint32_t value_id, int32_t value_len, int64_t now_us);
+
+/* server.py:471-474: inc_heartbeat + gc_marked_for_deletion. */
+void orc_begin_round(orc *o, int32_t node, int64_t now_us);
+
+/* One Syn/SynAck/Ack exchange initiated by a towards b (server.py:327-376, 524). */
+void orc_exchange(orc *o, int32_t a, int32_t b, int64_t now_us);
+
+/* _update_node_liveness (server.py:606-620).  Returns -1, or the node index whose
+ * missing sampling window raised KeyError in FailureDetector.garbage_collect (Q9). */
+int32_t orc_liveness(orc *o, int32_t node, int64_t now_us);
+
+/* ------------------------------------------------------------- readback */
+int32_t orc_node_count(const orc *o, int32_t obs);
+void    orc_node_order(const orc *o, int32_t obs, int32_t *out);
+/* out: heartbeat, max_version, last_gc_version */
+void    orc_view(const orc *o, int32_t obs, int32_t owner, uint32_t out[3]);
+/* per key: present, version, status, value_id, ts_us */
+void    orc_view_kvs(const orc *o, int32_t obs, int32_t owner, int32_t *present, uint32_t *version,
+                     int32_t *status, uint32_t *value_id, int64_t *ts_us);
+/* failure detector: window (has, last_us, len, sum); live flag; dead tod (or -1) */
+int32_t orc_fd_window(const orc *o, int32_t obs, int32_t target, int64_t *last_us, int32_t *len, double *sum);
+int32_t orc_fd_phi(const orc *o, int32_t obs, int32_t target, int64_t now_us, double *phi);
+int32_t orc_fd_live(const orc *o, int32_t obs, int32_t target);
+int64_t orc_fd_dead_since(const orc *o, int32_t obs, int32_t target);
+void    orc_get_stats(const orc *o, orc_stats *out);
+
+/* -------------------------------------------------- state injection (baseline) */
+/* Replace observer obs's whole row: order[cnt], heartbeat/max/gc[n], kv ordinals are
+ * resolved through the owner write history the caller passes (version, status,
+ * value_id, value_len per (owner, key, w)). Used to time the oracle on rows taken
+ * from a device snapshot. */
+void orc_load_row(orc *o, int32_t obs, int32_t cnt, const int32_t *order,
+                  const uint32_t *hb, const uint32_t *mv, const uint32_t *gc,
+                  const uint8_t *held_w, int32_t hist_cap,
+                  const uint32_t *hist_version, const uint32_t *hist_value_id,
+                  const int32_t *hist_value_len, const uint8_t *hist_status,
+                  const uint32_t *fd_last_tick, const uint32_t *fd_sum_tick, const uint32_t *fd_len,
+                  const uint32_t *fd_state, int64_t tick_us);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

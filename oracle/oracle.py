@@ -1,0 +1,223 @@
+"""ctypes wrapper of the C oracle (``oracle/gossip_oracle.c``).
+
+TEST INFRASTRUCTURE: the checker for the HIP path.  Only ``tests/``,
+``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg import it.
+
+``OracleSim`` implements the scenario backend protocol of
+``aiocluster_amd.scenario.replay`` and dumps the same canonical state as
+``oracle/refharness.py`` so the two compare byte for byte.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_build", "libgossip_oracle.so")
+TICK_US = 15_625
+
+
+def build(force: bool = False) -> str:
+    src = os.path.join(HERE, "gossip_oracle.c")
+    if force or not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < os.path.getmtime(src):
+        subprocess.run(["make", "-s", "-C", HERE], check=True)
+    return LIB_PATH
+
+
+class _Cfg(C.Structure):
+    _fields_ = [
+        ("n_nodes", C.c_int32),
+        ("n_keys", C.c_int32),
+        ("mtu", C.c_int32),
+        ("tombstone_grace_us", C.c_int64),
+        ("phi_threshold", C.c_double),
+        ("window", C.c_int32),
+        ("max_interval_us", C.c_int64),
+        ("initial_interval_us", C.c_int64),
+        ("dead_grace_us", C.c_int64),
+    ]
+
+
+class _Stats(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in
+                ("exchanges", "node_deltas", "kvs_sent", "delta_bytes", "hb_reports", "truncated")]
+
+
+_LIB = None
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        L = C.CDLL(build())
+        P = C.c_void_p
+        i32, i64, u32 = C.c_int32, C.c_int64, C.c_uint32
+        pi32, pu32, pi64, pdbl = C.POINTER(i32), C.POINTER(u32), C.POINTER(i64), C.POINTER(C.c_double)
+        sig = {
+            "orc_create": (P, [C.POINTER(_Cfg), pi32, pi32]),
+            "orc_destroy": (None, [P]),
+            "orc_boot": (None, [P, i32]),
+            "orc_init_warm": (None, [P]),
+            "orc_write": (None, [P, i32, i32, i32, u32, i32, i64]),
+            "orc_begin_round": (None, [P, i32, i64]),
+            "orc_exchange": (None, [P, i32, i32, i64]),
+            "orc_liveness": (i32, [P, i32, i64]),
+            "orc_node_count": (i32, [P, i32]),
+            "orc_node_order": (None, [P, i32, pi32]),
+            "orc_view": (None, [P, i32, i32, pu32]),
+            "orc_view_kvs": (None, [P, i32, i32, pi32, pu32, pi32, pu32, pi64]),
+            "orc_fd_window": (i32, [P, i32, i32, pi64, pi32, pdbl]),
+            "orc_fd_phi": (i32, [P, i32, i32, i64, pdbl]),
+            "orc_fd_live": (i32, [P, i32, i32]),
+            "orc_fd_dead_since": (i64, [P, i32, i32]),
+            "orc_get_stats": (None, [P, C.POINTER(_Stats)]),
+            "orc_load_row": (None, [P, i32, i32, P, P, P, P, P, i32, P, P, P, P, P, P, P, P, i64]),
+        }
+        for name, (res, args) in sig.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _LIB = L
+    return _LIB
+
+
+def us(seconds: float) -> int:
+    """``timedelta(seconds=...)`` in whole microseconds (round-half-even, as datetime does)."""
+    from datetime import timedelta
+
+    return timedelta(seconds=seconds) // timedelta(microseconds=1)
+
+
+class OracleSim:
+    """The C oracle as a scenario backend (``aiocluster_amd.scenario.replay``)."""
+
+    def __init__(self, node_ids, keys, cfg: dict, init: str, initial_values, nid_sizes=None):
+        from aiocluster_amd.pbsize import nodeid_size
+
+        self.L = lib()
+        self.n = len(node_ids)
+        self.keys = list(keys)
+        self.k = len(keys)
+        self.cfg = cfg
+        c = _Cfg(
+            self.n, self.k, int(cfg["mtu"]), us(cfg["tombstone_grace_s"]), float(cfg["phi_threshold"]),
+            int(cfg["window"]), us(cfg["max_interval_s"]), us(cfg["initial_interval_s"]), us(cfg["dead_grace_s"]),
+        )
+        if nid_sizes is None:
+            nid_sizes = [nodeid_size(n.name, n.generation_id, n.gossip_advertise_addr[0],
+                                     n.gossip_advertise_addr[1], n.tls_name) for n in node_ids]
+        ns = (C.c_int32 * self.n)(*nid_sizes)
+        kl = (C.c_int32 * self.k)(*[len(k.encode()) for k in keys])
+        self.h = self.L.orc_create(C.byref(c), ns, kl)
+        self.values = [""]
+        self.value_ids = {"": 0}
+        self.last_tick = 0
+        self.q9_events = []
+        for j in range(self.n):
+            self.L.orc_boot(self.h, j)
+        if initial_values:
+            for j in range(self.n):
+                for k, v in initial_values.get(j, []):
+                    self.write(0, j, k, 0, v)
+        if init == "warm":
+            self.L.orc_init_warm(self.h)
+
+    def close(self):
+        if self.h:
+            self.L.orc_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def intern(self, value: str) -> int:
+        vid = self.value_ids.get(value)
+        if vid is None:
+            vid = len(self.values)
+            self.values.append(value)
+            self.value_ids[value] = vid
+        return vid
+
+    # -------------------------------------------------------- backend protocol
+    def write(self, t: int, j: int, k: int, op: int, value: str):
+        self.L.orc_write(self.h, j, k, op, self.intern(value), len(value.encode()), t * TICK_US)
+
+    def begin_round(self, t: int, up):
+        for o in range(self.n):
+            if up[o]:
+                self.L.orc_begin_round(self.h, o, t * TICK_US)
+
+    def run_phase(self, t: int, pairs):
+        for a, b in pairs:
+            self.L.orc_exchange(self.h, int(a), int(b), t * TICK_US)
+
+    def exchange(self, a: int, b: int, t: int):
+        self.L.orc_exchange(self.h, int(a), int(b), t * TICK_US)
+
+    def liveness(self, t: int, up, r: int = -1):
+        self.last_tick = t
+        for o in range(self.n):
+            if up[o]:
+                q = self.L.orc_liveness(self.h, o, t * TICK_US)
+                if q >= 0:
+                    self.q9_events.append([r, o, q])
+
+    def stats(self) -> dict:
+        s = _Stats()
+        self.L.orc_get_stats(self.h, C.byref(s))
+        return {n: getattr(s, n) for n, _ in _Stats._fields_}
+
+    # ------------------------------------------------------------------ dump
+    def order(self, o: int) -> list[int]:
+        cnt = self.L.orc_node_count(self.h, o)
+        buf = (C.c_int32 * max(cnt, 1))()
+        self.L.orc_node_order(self.h, o, buf)
+        return list(buf[:cnt])
+
+    def view(self, o: int, j: int) -> tuple[int, int, int]:
+        out = (C.c_uint32 * 3)()
+        self.L.orc_view(self.h, o, j, out)
+        return out[0], out[1], out[2]
+
+    def view_kvs(self, o: int, j: int) -> list:
+        K = self.k
+        pres, ver, st = (C.c_int32 * K)(), (C.c_uint32 * K)(), (C.c_int32 * K)()
+        vid, ts = (C.c_uint32 * K)(), (C.c_int64 * K)()
+        self.L.orc_view_kvs(self.h, o, j, pres, ver, st, vid, ts)
+        out = []
+        for k in range(K):
+            if pres[k]:
+                out.append([self.keys[k], self.values[vid[k]], ver[k], st[k],
+                            None if st[k] == 0 else ts[k] // TICK_US])
+        out.sort()
+        return out
+
+    def observer_state(self, o: int) -> dict:
+        now = self.last_tick * TICK_US
+        nodes = []
+        for j in self.order(o):
+            hb, mv, gc = self.view(o, j)
+            nodes.append([j, hb, mv, gc, self.view_kvs(o, j)])
+        live, dead, wins = [], [], []
+        last, ln, sm, phi = C.c_int64(), C.c_int32(), C.c_double(), C.c_double()
+        for j in range(self.n):
+            if self.L.orc_fd_live(self.h, o, j):
+                live.append(j)
+            tod = self.L.orc_fd_dead_since(self.h, o, j)
+            if tod >= 0:
+                dead.append([j, tod // TICK_US])
+            if self.L.orc_fd_window(self.h, o, j, C.byref(last), C.byref(ln), C.byref(sm)):
+                has = self.L.orc_fd_phi(self.h, o, j, now, C.byref(phi))
+                wins.append([j, None if last.value < 0 else last.value // TICK_US, ln.value, sm.value,
+                             phi.value if has else None])
+        return {"nodes": nodes, "live": live, "dead": dead, "windows": wins}
+
+    def state(self) -> list[dict]:
+        return [self.observer_state(o) for o in range(self.n)]
