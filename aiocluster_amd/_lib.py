@@ -1,0 +1,125 @@
+"""ctypes binding of ``libgossip_sim.so`` (C ABI: ``include/gossip_sim.h``).
+
+The shared library is built in-tree by ``__graft_entry__.build()`` (hipcc,
+``--offload-arch=gfx950``).  There is no fallback: if the library is missing
+or fails to load, every entry point of the package raises.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(PKG)
+LIB_DIR = os.path.join(PKG, "lib")
+LIB_PATH = os.path.join(LIB_DIR, "libgossip_sim.so")
+SRC = os.path.join(PKG, "csrc", "gossip_sim.hip")
+HEADER = os.path.join(REPO, "include", "gossip_sim.h")
+
+HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-ffp-contract=off", "-std=c++17", "-fPIC", "-shared"]
+
+GS_CANONICAL = 1
+GS_TOMBSTONES = 2
+GS_FD_RING = 4
+GS_NONE = 0xFFFFFFFF
+TICK_US = 15_625
+
+REGIONS = [
+    "HB", "MV", "GC", "HELD", "FD_LAST", "FD_SUM", "FD_CNT", "FD_STATE", "TS", "RING", "POS", "ORD", "ROW",
+    "LAST_W", "HIST_VER", "HIST_META", "HIST_VID", "NID_SIZE", "KEY_LEN", "STAMP", "COUNTERS",
+]
+REGION = {n: i for i, n in enumerate(REGIONS)}
+
+ERRORS = {-1: "GS_E_INVALID", -2: "GS_E_UNBOUND", -3: "GS_E_HIP", -4: "GS_E_DEVICE", -5: "GS_E_UNSUPPORTED"}
+
+COUNTER_FIELDS = [
+    "exchanges", "hb_reports", "node_deltas", "kvs_sent", "truncated", "delta_bytes", "alg_bytes", "hb_writes",
+    "candidates", "live_pairs", "tomb_gc", "err_fd_overflow", "err_hist_full", "err_bad_index", "err_conflict",
+    "err_fd_gc", "err_insert",
+]
+
+# Every symbol include/gossip_sim.h declares (checked by tests/test_abi.py).
+EXPORTS = [
+    "gs_create", "gs_destroy", "gs_last_error", "gs_api_version", "gs_region_bytes", "gs_bind", "gs_set_stream",
+    "gs_boot", "gs_warm", "gs_owner_writes", "gs_begin_round", "gs_run_phase", "gs_liveness", "gs_phi_row",
+    "gs_read_counters", "gs_reset_counters", "gs_sync",
+]
+
+
+class GsConfig(C.Structure):
+    _fields_ = [
+        ("n_nodes", C.c_uint32),
+        ("n_keys", C.c_uint32),
+        ("hist_cap", C.c_uint32),
+        ("mtu", C.c_uint32),
+        ("flags", C.c_uint32),
+        ("window", C.c_uint32),
+        ("max_interval_ticks", C.c_uint32),
+        ("tombstone_grace_ticks", C.c_uint32),
+        ("dead_grace_ticks", C.c_uint32),
+        ("sched_delay_ticks", C.c_uint32),
+        ("phi_threshold", C.c_double),
+        ("prior_weighted", C.c_double),
+    ]
+
+
+class GsCounters(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in COUNTER_FIELDS] + [("reserved", C.c_uint64 * 15)]
+
+
+class GsError(RuntimeError):
+    pass
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    """Compile the HIP library for gfx950 in-tree (cross-compiles without a GPU)."""
+    os.makedirs(LIB_DIR, exist_ok=True)
+    newest = max(os.path.getmtime(SRC), os.path.getmtime(HEADER))
+    if force or not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < newest:
+        cmd = ["hipcc", *HIPCC_FLAGS, "-o", LIB_PATH, SRC]
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.run(cmd, check=True)
+    return LIB_PATH
+
+
+_LIB = None
+
+
+def load():
+    """Load (never silently replace) the HIP library."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise GsError(f"{LIB_PATH} missing: run __graft_entry__.build() (hipcc, gfx950)")
+    L = C.CDLL(LIB_PATH)
+    P, u32, i32, u64 = C.c_void_p, C.c_uint32, C.c_int32, C.c_uint64
+    sig = {
+        "gs_api_version": (C.c_int, []),
+        "gs_create": (C.c_int, [C.POINTER(GsConfig), C.POINTER(P)]),
+        "gs_destroy": (None, [P]),
+        "gs_last_error": (C.c_char_p, [P]),
+        "gs_region_bytes": (C.c_int, [P, C.c_int, C.POINTER(u64)]),
+        "gs_bind": (C.c_int, [P, C.c_int, P]),
+        "gs_set_stream": (C.c_int, [P, P]),
+        "gs_boot": (C.c_int, [P, P, P]),
+        "gs_warm": (C.c_int, [P]),
+        "gs_owner_writes": (C.c_int, [P, P, u32, u32]),
+        "gs_begin_round": (C.c_int, [P, P, u32]),
+        "gs_run_phase": (C.c_int, [P, P, P, u32, u32]),
+        "gs_liveness": (C.c_int, [P, P, u32]),
+        "gs_phi_row": (C.c_int, [P, u32, u32, P]),
+        "gs_read_counters": (C.c_int, [P, C.POINTER(GsCounters)]),
+        "gs_reset_counters": (C.c_int, [P]),
+        "gs_sync": (C.c_int, [P]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    del i32
+    _LIB = L
+    return L

@@ -1,0 +1,1032 @@
+// gossip_sim.hip -- MI355X (gfx950) batched scuttlebutt + phi-accrual simulator.
+//
+// Hand-written HIP for CDNA4 (wave64).  The whole simulated cluster lives in HBM
+// as dense observer x owner matrices (layout: include/gossip_sim.h).
+// One launch of k_exchange runs one conflict-free phase, one 128-thread
+// workgroup (2 waves) per exchange (a = initiator, b = responder):
+//
+//   pass 1 (both waves, both rows streamed with 16-byte loads): responder
+//          heartbeat, both heartbeat merges + failure-detector reports,
+//          digest membership, stale-owner bitmaps of both directions (LDS);
+//   pass 2 (wave 0, general mode only): dict insertions in digest order;
+//   pass 3 (wave 0: b -> a, wave 1: a -> b, concurrently): exact
+//          protobuf-size MTU packing in the sender's dict order with a
+//          wave prefix sum for the part that fits and a ballot-driven
+//          first-fit scan once the budget is nearly spent, then apply_delta
+//          at the receiver, one lane per NodeDelta.
+//
+// The two directions touch disjoint owner columns ("why the two
+// deltas commute"), so pass 3 needs no synchronisation between the waves.
+//
+// Reference semantics restated here (aiocluster @ /root/reference):
+//   digest            state.py:244-251, 324-331
+//   heartbeat merge   server.py:336-337, 356-357, 599-604; state.py:280-287
+//   delta             state.py:340-415 (+ staleness_score 425-433)
+//   apply             state.py:190-233, 310-322
+//   tombstone GC      state.py:253-274, 333-338
+//   owner writes      state.py:124-180
+//   failure detector  failure_detector.py:12-128
+
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/gossip_sim.h"
+
+namespace {
+
+constexpr uint32_t NONE = GS_NONE;
+constexpr int WAVE = 64;
+constexpr int XB = 128;  // exchange workgroup: 2 waves
+constexpr int LB = 256;  // liveness / elementwise workgroups
+constexpr int NSHARD = 64;
+constexpr double TICK_S = 1.0 / 64.0;
+
+enum Ctr {
+    C_EXCH = 0, C_REPORTS, C_ND, C_KVS, C_TRUNC, C_DBYTES, C_ALG, C_HBW, C_CAND, C_LIVE, C_TOMBGC,
+    C_E_FDOVF, C_E_HIST, C_E_IDX, C_E_CONFLICT, C_E_FDGC, C_E_INSERT, C_NUM
+};
+static_assert(C_NUM <= 32, "counter region");
+static_assert(sizeof(gs_counters) == 32 * 8, "gs_counters layout");
+
+struct Dev {
+    uint32_t N, NP, K, KP, C, mtu, flags, W;
+    uint32_t max_iv, tomb_grace, dead_grace, sched_delay, lb_min;
+    double phi_thr, prior5;
+    uint32_t *hb, *mv, *gc;
+    uint8_t *held;
+    uint32_t *fd_last, *fd_sum, *fd_cnt, *fd_state, *ts;
+    uint16_t *ring;
+    uint32_t *pos, *ord, *row;
+    uint8_t *last_w;
+    uint32_t *hist_ver, *hist_meta, *hist_vid;
+    uint16_t *nid_size;
+    uint8_t *key_len;
+    uint32_t *stamp;
+    unsigned long long *ctr;
+};
+
+// ------------------------------------------------------------------ protobuf sizes
+// proto3 wire sizes for messages.proto:39-74 (all field numbers < 16: one-byte tags).
+__host__ __device__ inline uint32_t vlen(uint32_t x) {
+    return x < (1u << 7) ? 1u : x < (1u << 14) ? 2u : x < (1u << 21) ? 3u : x < (1u << 28) ? 4u : 5u;
+}
+__host__ __device__ inline uint32_t ufield(uint32_t x) { return x ? 1u + vlen(x) : 0u; }
+__host__ __device__ inline uint32_t sfield(uint32_t n) { return n ? 1u + vlen(n) + n : 0u; }
+__host__ __device__ inline uint32_t msgf(uint32_t n) { return 1u + vlen(n) + n; }
+
+__device__ inline size_t pix(const Dev &d, uint32_t o, uint32_t j) { return (size_t)o * d.NP + j; }
+__device__ inline size_t hix(const Dev &d, uint32_t j, uint32_t w, uint32_t k) {
+    return ((size_t)j * d.C + w) * d.K + k;
+}
+__device__ inline uint32_t meta_kvlen(uint32_t m) { return m & 0xFFFFu; }
+__device__ inline uint32_t meta_status(uint32_t m) { return (m >> 16) & 3u; }
+__device__ inline uint32_t meta_vlen(uint32_t m) { return m >> 18; }
+__device__ inline uint32_t make_meta(uint32_t kvlen, uint32_t status, uint32_t value_len) {
+    return kvlen | (status << 16) | (value_len << 18);
+}
+
+// FailureDetector.scheduled_for_deletion_nodes (failure_detector.py:121-128): now >= tod + grace/2.
+__device__ inline bool is_sched(uint32_t st, uint32_t t, uint32_t delay) {
+    return st >= 2u && (t - (st - 2u)) >= delay;
+}
+
+__device__ inline int lane_id() { return (int)__lane_id(); }
+__device__ inline bool bit(const uint32_t *bm, uint32_t j) { return (bm[j >> 5] >> (j & 31u)) & 1u; }
+
+__device__ inline uint32_t wave_incl_scan(uint32_t x) {
+    const int l = lane_id();
+#pragma unroll
+    for (int dd = 1; dd < WAVE; dd <<= 1) {
+        const uint32_t y = __shfl_up(x, dd, WAVE);
+        if (l >= dd) x += y;
+    }
+    return x;
+}
+
+__device__ inline unsigned long long wave_sum(unsigned long long x) {
+#pragma unroll
+    for (int dd = 32; dd >= 1; dd >>= 1) x += __shfl_xor(x, dd, WAVE);
+    return x;
+}
+
+__device__ inline void shard_add(const Dev &d, int c, unsigned long long v) {
+    if (v) atomicAdd(&d.ctr[(blockIdx.x % NSHARD) * 32 + c], v);
+}
+
+// ------------------------------------------------------------------ failure detector
+// FailureDetector.report_heartbeat -> SamplingWindow.report_heartbeat
+// (failure_detector.py:79-81, 32-38): the first report creates the window and only
+// records the time; later intervals <= max_interval go to BoundedArrayStats (139-150).
+__device__ inline void fd_report(const Dev &d, size_t p, uint32_t t, uint32_t &alg, uint32_t &ovf) {
+    const uint32_t last = d.fd_last[p];
+    alg += 8;
+    if (last != NONE) {
+        const uint32_t iv = t - last;
+        if (iv <= d.max_iv) {
+            uint32_t cnt = d.fd_cnt[p], sum = d.fd_sum[p];
+            if (d.flags & GS_FD_RING) {
+                uint16_t *rg = d.ring + p * d.W;
+                const uint32_t slot = cnt % d.W;
+                if (cnt >= d.W) sum -= rg[slot];  // subtract-then-add (failure_detector.py:140-143)
+                rg[slot] = (uint16_t)iv;
+                sum += iv;
+                cnt += 1;
+                if (cnt >= 2u * d.W) cnt -= d.W;
+                alg += 4;
+            } else if (cnt >= d.W) {
+                ovf += 1;  // eviction needs the ring: flagged, the run is reported inexact
+            } else {
+                sum += iv;
+                cnt += 1;
+            }
+            d.fd_cnt[p] = cnt;
+            d.fd_sum[p] = sum;
+            alg += 16;
+        }
+    }
+    d.fd_last[p] = t;
+}
+
+// ------------------------------------------------------------------ packing / apply
+struct DigestSide {
+    uint32_t o;      // whose digest the sender compares against
+    uint32_t limit;  // general mode: owners with dict position < limit were in that digest
+    bool sched;      // some target of o may be scheduled for deletion at t
+};
+
+struct Cand {
+    uint32_t j, from, gs, ms, base, emsg, min1, nkv;
+};
+
+struct WStats {
+    uint32_t nd, kvs, trunc, cand, alg;
+};
+
+// NodeDelta candidate (state.py:347-390): from_version_excluded, the NodeDeltaPb body
+// size without kvs, the DeltaPb bytes of the whole NodeDelta (all kvs with version > from)
+// and of its smallest-version kv alone.
+__device__ inline void eval_cand(const Dev &d, uint32_t s, const DigestSide &ds, bool genm, uint32_t j,
+                                 uint32_t t, Cand &c, uint32_t &alg) {
+    const size_t ps = pix(d, s, j), pd = pix(d, ds.o, j);
+    const uint32_t ms = d.mv[ps], gs = d.gc[ps];
+    bool in_d = true;
+    if (genm) { in_d = d.pos[pd] < ds.limit; alg += 4; }
+    if (in_d && ds.sched) { in_d = !is_sched(d.fd_state[pd], t, d.sched_delay); alg += 4; }
+    const uint32_t dm = in_d ? d.mv[pd] : 0u;
+    const uint32_t dg = in_d ? d.gc[pd] : 0u;
+    const uint32_t from = (dg < gs && dm < gs) ? 0u : dm;  // should_reset (state.py:359-362)
+    const uint32_t base = msgf(d.nid_size[j]) + ufield(from) + ufield(gs) + 1u + vlen(ms);
+    const uint8_t *hs = d.held + ps * d.KP;
+    uint32_t sum = 0, nk = 0, minv = NONE, minkv = 0;
+    for (uint32_t k4 = 0; k4 < d.KP; k4 += 4) {
+        const uint32_t ww = *reinterpret_cast<const uint32_t *>(hs + k4);
+        if (!ww) continue;
+#pragma unroll
+        for (uint32_t q = 0; q < 4; q++) {
+            const uint32_t w = (ww >> (8 * q)) & 0xFFu;
+            const uint32_t k = k4 + q;
+            if (!w || k >= d.K) continue;
+            const size_t h = hix(d, j, w, k);
+            const uint32_t v = d.hist_ver[h];
+            alg += 4;
+            if (v <= from) continue;
+            const uint32_t kvm = msgf(meta_kvlen(d.hist_meta[h]));
+            alg += 4;
+            sum += kvm;
+            nk += 1;
+            if (v < minv) { minv = v; minkv = kvm; }
+        }
+    }
+    alg += 16 + d.KP;
+    c.j = j;
+    c.from = from;
+    c.gs = gs;
+    c.ms = ms;
+    c.base = base;
+    c.nkv = nk;
+    c.emsg = nk ? msgf(base + sum) : 0u;
+    c.min1 = nk ? msgf(base + minkv) : 0u;
+}
+
+// NodeState.apply_delta (state.py:190-233) of the NodeDelta {owner j, kvs of the sender's
+// view with from < version <= vmax, last_gc gs, max_version ms} at receiver r.
+__device__ inline void apply_nd(const Dev &d, uint32_t s, uint32_t r, uint32_t j, uint32_t from, uint32_t vmax,
+                                uint32_t gs, uint32_t ms, uint32_t t, bool &tomb, uint32_t &alg) {
+    const size_t ps = pix(d, s, j), pr = pix(d, r, j);
+    uint32_t g = d.gc[pr];
+    const uint32_t m0 = d.mv[pr];
+    const bool jump = gs > g;  // last_gc_version raised: drop entries <= it (200-207)
+    if (jump) g = gs;
+    uint32_t maxv = m0;
+    uint8_t *hr = d.held + pr * d.KP;
+    const uint8_t *hs = d.held + ps * d.KP;
+    const bool tt = (d.flags & GS_TOMBSTONES) != 0;
+    uint32_t *tsr = tt ? d.ts + pr * d.KP : nullptr;
+    for (uint32_t k4 = 0; k4 < d.KP; k4 += 4) {
+        const uint32_t wsw = *reinterpret_cast<const uint32_t *>(hs + k4);
+        uint32_t wrw = *reinterpret_cast<const uint32_t *>(hr + k4);
+        const uint32_t wr0 = wrw;
+        if (!wsw && !(jump && wrw)) continue;
+        for (uint32_t q = 0; q < 4; q++) {
+            const uint32_t k = k4 + q;
+            if (k >= d.K) break;
+            uint32_t wr = (wrw >> (8 * q)) & 0xFFu;
+            const uint32_t ws = (wsw >> (8 * q)) & 0xFFu;
+            if (jump && wr && d.hist_ver[hix(d, j, wr, k)] <= g) {
+                wr = 0;
+                if (tt) tsr[k] = NONE;
+                alg += 4;
+            }
+            if (ws) {
+                const size_t h = hix(d, j, ws, k);
+                const uint32_t v = d.hist_ver[h];
+                alg += 4;
+                // skip: not in the delta / version <= max_version / existing >= / GC'd tombstone
+                if (v > from && v <= vmax && v > m0 && wr < ws) {
+                    const uint32_t st = meta_status(d.hist_meta[h]);
+                    alg += 4;
+                    if (!(st != 0u && v <= g)) {
+                        wr = ws;
+                        if (tt) { tsr[k] = st ? t : NONE; alg += 4; }
+                        if (st) tomb = true;
+                        if (v > maxv) maxv = v;
+                    }
+                }
+            }
+            wrw = (wrw & ~(0xFFu << (8 * q))) | (wr << (8 * q));
+        }
+        if (wrw != wr0) { *reinterpret_cast<uint32_t *>(hr + k4) = wrw; alg += 4; }
+    }
+    if (ms > maxv) maxv = ms;  // max_version (232-233)
+    d.mv[pr] = maxv;
+    d.gc[pr] = g;
+    alg += 16 + 2 * d.KP + 8;
+}
+
+// compute_partial_delta_respecting_mtu (state.py:340-415) from sender s's view for receiver r,
+// fused with r's apply_delta.  One wave; lanes walk the sender's dict order 64 positions at a
+// time.  Exactness argument (same decisions as the sequential loop): DESIGN.md.
+__device__ void pack_dir(const Dev &d, uint32_t s, uint32_t r, const DigestSide ds, const uint32_t *order,
+                         uint32_t cnt, const uint32_t *bits, uint32_t t, bool genm, WStats &st, bool &tomb) {
+    const int lane = lane_id();
+    const uint32_t mtu = d.mtu;
+    uint32_t S = 0;  // DeltaPb bytes committed (wave-uniform)
+    bool tail = false;
+    for (uint32_t p0 = 0; p0 < cnt; p0 += WAVE) {
+        const uint32_t p = p0 + lane;
+        uint32_t j = NONE;
+        if (p < cnt) j = order ? order[p] : p;
+        const bool cand = (j != NONE) && bit(bits, j);
+        if (__ballot(cand) == 0ull) continue;
+        Cand c{};
+        if (cand) { eval_cand(d, s, ds, genm, j, t, c, st.alg); st.cand++; }
+        const uint32_t em = cand ? c.emsg : 0u;
+        int start = 0;
+        if (!tail) {
+            const uint32_t incl = wave_incl_scan(em);
+            const uint32_t total = __shfl(incl, WAVE - 1, WAVE);
+            if (S + total <= mtu) {  // every candidate of this group fits whole
+                if (em) {
+                    apply_nd(d, s, r, c.j, c.from, NONE, c.gs, c.ms, t, tomb, st.alg);
+                    st.nd++;
+                    st.kvs += c.nkv;
+                }
+                S += total;
+                if (S >= mtu || mtu - S < d.lb_min) break;
+                continue;
+            }
+            const bool fail = em && (S + incl > mtu);
+            const unsigned long long fm = __ballot(fail);
+            const int f = __builtin_ctzll(fm);
+            if (lane < f && em) {
+                apply_nd(d, s, r, c.j, c.from, NONE, c.gs, c.ms, t, tomb, st.alg);
+                st.nd++;
+                st.kvs += c.nkv;
+            }
+            S += __shfl(incl - em, f, WAVE);
+            tail = true;
+            start = f;
+        }
+        // First-fit continuation (state.py:392-413): each later candidate sends the longest
+        // prefix of its version-sorted kvs that still fits; stop once the delta is >= mtu.
+        int cur = start;
+        bool stop = false;
+        while (true) {
+            const uint32_t R = mtu - S;
+            const bool elig = em && lane >= cur && c.min1 <= R;
+            const unsigned long long m = __ballot(elig);
+            if (!m) break;
+            const int x = __builtin_ctzll(m);
+            const uint32_t emx = __shfl(em, x, WAVE);
+            if (emx <= R) {
+                if (lane == x) {
+                    apply_nd(d, s, r, c.j, c.from, NONE, c.gs, c.ms, t, tomb, st.alg);
+                    st.nd++;
+                    st.kvs += c.nkv;
+                }
+                S += emx;
+            } else {
+                // truncated NodeDelta: lanes = keys, rank kvs by version, longest fitting prefix
+                const uint32_t jx = __shfl(c.j, x, WAVE), fx = __shfl(c.from, x, WAVE);
+                const uint32_t bx = __shfl(c.base, x, WAVE);
+                bool inc = false;
+                uint32_t v = 0, kvm = 0;
+                if (lane < (int)d.K) {
+                    const uint32_t w = d.held[pix(d, s, jx) * d.KP + lane];
+                    if (w) {
+                        const size_t h = hix(d, jx, w, lane);
+                        v = d.hist_ver[h];
+                        if (v > fx) { inc = true; kvm = msgf(meta_kvlen(d.hist_meta[h])); }
+                    }
+                }
+                const unsigned long long im = __ballot(inc);
+                uint32_t rank = 0, P = 0;
+                for (int l = 0; l < (int)d.K; l++) {
+                    const uint32_t vl = __shfl(v, l, WAVE);
+                    if (((im >> l) & 1ull) && vl < v) rank++;
+                }
+                for (int l = 0; l < (int)d.K; l++) {
+                    const uint32_t rl = __shfl(rank, l, WAVE);
+                    const uint32_t kl = __shfl(kvm, l, WAVE);
+                    if (((im >> l) & 1ull) && (int)rl < lane) P += kl;
+                }
+                const uint32_t nkv = (uint32_t)__popcll(im);
+                const bool fit = lane >= 1 && (uint32_t)lane <= nkv && S + msgf(bx + P) <= mtu;
+                const uint32_t n = (uint32_t)__popcll(__ballot(fit));
+                if (n >= 1) {
+                    const unsigned long long ym = __ballot(inc && rank == n - 1);
+                    const uint32_t vmax = __shfl(v, __builtin_ctzll(ym), WAVE);
+                    const uint32_t used = msgf(bx + __shfl(P, (int)n, WAVE));
+                    if (lane == x) {
+                        apply_nd(d, s, r, c.j, c.from, vmax, c.gs, c.ms, t, tomb, st.alg);
+                        st.nd++;
+                        st.kvs += n;
+                        st.trunc++;
+                    }
+                    S += used;
+                }
+            }
+            if (S >= mtu) { stop = true; break; }
+            cur = x + 1;
+        }
+        if (stop || mtu - S < d.lb_min) break;
+    }
+    // DeltaPb bytes of this direction, counted once per wave
+    if (lane == 0) shard_add(d, C_DBYTES, S);
+}
+
+// ------------------------------------------------------------------ exchange kernel
+__global__ __launch_bounds__(XB) void k_exchange(Dev d, const int32_t *ini, const int32_t *res, uint32_t n,
+                                                 uint32_t t, uint32_t seq) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    __shared__ uint32_t s_flag[4];
+    const uint32_t e = blockIdx.x;
+    if (e >= n) return;
+    const int tid = threadIdx.x, lane = tid & (WAVE - 1), wid = tid >> 6;
+    const int32_t ai = ini[e], bi = res[e];
+    if (ai < 0 || bi < 0 || (uint32_t)ai >= d.N || (uint32_t)bi >= d.N || ai == bi) {
+        if (tid == 0) shard_add(d, C_E_IDX, 1);
+        return;
+    }
+    const uint32_t a = (uint32_t)ai, b = (uint32_t)bi;
+    const bool genm = !(d.flags & GS_CANONICAL);
+    const uint32_t words = d.NP / 32;
+    uint32_t *bBA = lds, *bAB = lds + words, *bNB = lds + 2 * words, *bNA = lds + 3 * words;
+    for (uint32_t i = tid; i < words * (genm ? 4u : 2u); i += XB) lds[i] = 0u;
+    if (tid == 0) {
+        s_flag[0] = 0;
+        const uint32_t oa = atomicMax(&d.stamp[a], seq), ob = atomicMax(&d.stamp[b], seq);
+        if (oa == seq || ob == seq) shard_add(d, C_E_CONFLICT, 1);
+    }
+    const uint32_t cntA0 = genm ? d.row[a * 4 + 0] : d.N;
+    const uint32_t cntB0 = genm ? d.row[b * 4 + 0] : d.N;
+    const bool schA = t >= d.row[a * 4 + 2];
+    const bool schB = t >= d.row[b * 4 + 2];
+    __syncthreads();
+
+    // ---- pass 1: Syn at a, heartbeat merge at b, SynAck digest, heartbeat merge at a
+    const size_t ra = (size_t)a * d.NP, rb = (size_t)b * d.NP;
+    uint32_t alg = 0, reports = 0, hbw = 0, ovf = 0;
+    bool anynew = false;
+    for (uint32_t c0 = (uint32_t)tid * 4u; c0 < d.N; c0 += XB * 4u) {
+        uint4 hA4 = *reinterpret_cast<const uint4 *>(d.hb + ra + c0);
+        uint4 hB4 = *reinterpret_cast<const uint4 *>(d.hb + rb + c0);
+        const uint4 mA4 = *reinterpret_cast<const uint4 *>(d.mv + ra + c0);
+        const uint4 mB4 = *reinterpret_cast<const uint4 *>(d.mv + rb + c0);
+        uint4 pA4 = make_uint4(0, 0, 0, 0), pB4 = make_uint4(0, 0, 0, 0);
+        uint4 fA4 = make_uint4(0, 0, 0, 0), fB4 = make_uint4(0, 0, 0, 0);
+        alg += 64;
+        if (genm) {
+            pA4 = *reinterpret_cast<const uint4 *>(d.pos + ra + c0);
+            pB4 = *reinterpret_cast<const uint4 *>(d.pos + rb + c0);
+            alg += 32;
+        }
+        if (schA) { fA4 = *reinterpret_cast<const uint4 *>(d.fd_state + ra + c0); alg += 16; }
+        if (schB) { fB4 = *reinterpret_cast<const uint4 *>(d.fd_state + rb + c0); alg += 16; }
+        uint32_t *hA = reinterpret_cast<uint32_t *>(&hA4), *hB = reinterpret_cast<uint32_t *>(&hB4);
+        const uint32_t *mA = reinterpret_cast<const uint32_t *>(&mA4), *mB = reinterpret_cast<const uint32_t *>(&mB4);
+        const uint32_t *pA = reinterpret_cast<const uint32_t *>(&pA4), *pB = reinterpret_cast<const uint32_t *>(&pB4);
+        const uint32_t *fA = reinterpret_cast<const uint32_t *>(&fA4), *fB = reinterpret_cast<const uint32_t *>(&fB4);
+        bool dA = false, dB = false;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const uint32_t j = c0 + i;
+            if (j >= d.N) break;
+            const bool pa = genm ? pA[i] != NONE : true;
+            const bool pb = genm ? pB[i] != NONE : true;
+            const bool sa = schA && pa && is_sched(fA[i], t, d.sched_delay);
+            const bool sb = schB && pb && is_sched(fB[i], t, d.sched_delay);
+            const bool inA = pa && !sa;  // j is in a's digest (compute_digest, state.py:324-331)
+            if (j == b) { hB[i] += 1u; dB = true; hbw++; }  // responder inc_heartbeat (server.py:524)
+            bool newB = false;
+            if (inA && j != b) {  // b: _report_heartbeat over a's digest (server.py:336-337, 599-604)
+                if (!pb) { newB = true; hB[i] = hA[i]; dB = true; hbw++; }
+                else if (hB[i] == 0u) { if (hA[i]) { hB[i] = hA[i]; dB = true; hbw++; } }
+                else if (hA[i] > hB[i]) {
+                    hB[i] = hA[i]; dB = true; hbw++; reports++;
+                    fd_report(d, rb + j, t, alg, ovf);
+                }
+            }
+            const bool pb2 = pb || newB;
+            const bool inB = pb2 && !sb;  // j is in b's digest, computed after the merge (server.py:340)
+            bool newA = false;
+            if (inB && j != a) {  // a: _report_heartbeat over b's digest (server.py:356-357)
+                if (!pa) { newA = true; hA[i] = hB[i]; dA = true; hbw++; }
+                else if (hA[i] == 0u) { if (hB[i]) { hA[i] = hB[i]; dA = true; hbw++; } }
+                else if (hB[i] > hA[i]) {
+                    hA[i] = hB[i]; dA = true; hbw++; reports++;
+                    fd_report(d, ra + j, t, alg, ovf);
+                }
+            }
+            // stale owners (state.py:347-357): sender's max_version above the digest's
+            const uint32_t dmA = inA ? mA[i] : 0u;
+            if (pb2 && !sb && mB[i] > dmA) atomicOr(&bBA[j >> 5], 1u << (j & 31u));
+            const uint32_t dmB = inB ? mB[i] : 0u;
+            if (pa && !sa && mA[i] > dmB) atomicOr(&bAB[j >> 5], 1u << (j & 31u));
+            if (newB) { atomicOr(&bNB[j >> 5], 1u << (j & 31u)); anynew = true; }
+            if (newA) { atomicOr(&bNA[j >> 5], 1u << (j & 31u)); anynew = true; }
+        }
+        if (dA) { *reinterpret_cast<uint4 *>(d.hb + ra + c0) = hA4; alg += 16; }
+        if (dB) { *reinterpret_cast<uint4 *>(d.hb + rb + c0) = hB4; alg += 16; }
+    }
+    if (anynew) s_flag[0] = 1u;
+    __syncthreads();
+
+    // ---- pass 2: dict insertions (node_state_or_default appends in digest order)
+    uint32_t cntA = cntA0, cntB = cntB0;
+    if (s_flag[0]) {
+        if (!genm) {
+            if (tid == 0) shard_add(d, C_E_INSERT, 1);
+        } else if (wid == 0) {
+            uint32_t baseB = cntB0;  // b inserts in a's digest order (a's dict order at Syn time)
+            for (uint32_t p0 = 0; p0 < cntA0; p0 += WAVE) {
+                const uint32_t p = p0 + lane;
+                const uint32_t j = p < cntA0 ? d.ord[ra + p] : NONE;
+                const bool f = j != NONE && bit(bNB, j);
+                const unsigned long long m = __ballot(f);
+                const uint32_t rk = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+                if (f) { d.pos[rb + j] = baseB + rk; d.ord[rb + baseB + rk] = j; }
+                baseB += (uint32_t)__popcll(m);
+            }
+            __threadfence_block();
+            uint32_t baseA = cntA0;  // a inserts in b's digest order (b's dict after its insertions)
+            for (uint32_t p0 = 0; p0 < baseB; p0 += WAVE) {
+                const uint32_t p = p0 + lane;
+                const uint32_t j = p < baseB ? d.ord[rb + p] : NONE;
+                const bool f = j != NONE && bit(bNA, j);
+                const unsigned long long m = __ballot(f);
+                const uint32_t rk = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+                if (f) { d.pos[ra + j] = baseA + rk; d.ord[ra + baseA + rk] = j; }
+                baseA += (uint32_t)__popcll(m);
+            }
+            if (lane == 0) {
+                d.row[b * 4 + 0] = baseB;
+                d.row[a * 4 + 0] = baseA;
+                s_flag[1] = baseB;
+                s_flag[2] = baseA;
+            }
+            __threadfence_block();
+        }
+        __syncthreads();
+        if (genm) { cntB = s_flag[1]; cntA = s_flag[2]; }
+    }
+
+    // ---- pass 3: SynAck delta b -> a (wave 0) and Ack delta a -> b (wave 1), each applied
+    WStats st{0, 0, 0, 0, 0};
+    bool tomb = false;
+    if (wid == 0) {
+        const DigestSide ds{a, cntA0, schA};
+        pack_dir(d, b, a, ds, genm ? d.ord + rb : nullptr, cntB, bBA, t, genm, st, tomb);
+    } else {
+        const DigestSide ds{b, cntB, schB};
+        pack_dir(d, a, b, ds, genm ? d.ord + ra : nullptr, cntA, bAB, t, genm, st, tomb);
+    }
+    if (tomb) d.row[(wid == 0 ? a : b) * 4 + 1] = 1u;
+
+    // ---- counters: wave-reduced, sharded atomics
+    const unsigned long long s_alg = wave_sum((unsigned long long)alg + st.alg);
+    const unsigned long long s_rep = wave_sum(reports), s_hbw = wave_sum(hbw), s_ovf = wave_sum(ovf);
+    const unsigned long long s_nd = wave_sum(st.nd), s_kv = wave_sum(st.kvs), s_tr = wave_sum(st.trunc);
+    const unsigned long long s_cd = wave_sum(st.cand);
+    if (lane == 0) {
+        shard_add(d, C_ALG, s_alg);
+        shard_add(d, C_REPORTS, s_rep);
+        shard_add(d, C_HBW, s_hbw);
+        shard_add(d, C_E_FDOVF, s_ovf);
+        shard_add(d, C_ND, s_nd);
+        shard_add(d, C_KVS, s_kv);
+        shard_add(d, C_TRUNC, s_tr);
+        shard_add(d, C_CAND, s_cd);
+        if (wid == 0) shard_add(d, C_EXCH, 1);
+    }
+}
+
+// ------------------------------------------------------------------ round start
+// inc_heartbeat + ClusterState.gc_marked_for_deletion (server.py:471-474; state.py:253-274, 333-338)
+__global__ __launch_bounds__(LB) void k_begin_round(Dev d, const uint8_t *up, uint32_t t) {
+    const uint32_t o = blockIdx.x;
+    if (o >= d.N || !up[o]) return;
+    if (threadIdx.x == 0) d.hb[pix(d, o, o)] += 1u;
+    if (!(d.flags & GS_TOMBSTONES) || !d.row[o * 4 + 1]) return;
+    const bool genm = !(d.flags & GS_CANONICAL);
+    bool remaining = false;
+    uint32_t gcn = 0;
+    for (uint32_t j = threadIdx.x; j < d.N; j += LB) {
+        const size_t p = pix(d, o, j);
+        if (genm && d.pos[p] == NONE) continue;
+        uint32_t maxdel = d.gc[p];
+        bool changed = false;
+        for (uint32_t k = 0; k < d.K; k++) {
+            const uint32_t tv = d.ts[p * d.KP + k];
+            if (tv == NONE) continue;
+            if ((uint64_t)t >= (uint64_t)tv + d.tomb_grace) {
+                const uint32_t w = d.held[p * d.KP + k];
+                const uint32_t v = d.hist_ver[hix(d, j, w, k)];
+                d.held[p * d.KP + k] = 0;
+                d.ts[p * d.KP + k] = NONE;
+                if (v > maxdel) maxdel = v;
+                changed = true;
+                gcn++;
+            } else {
+                remaining = true;
+            }
+        }
+        if (changed) d.gc[p] = maxdel;
+    }
+    remaining = __syncthreads_or(remaining);
+    if (threadIdx.x == 0) d.row[o * 4 + 1] = remaining ? 1u : 0u;
+    const unsigned long long s = wave_sum(gcn);
+    if ((threadIdx.x & 63) == 0) shard_add(d, C_TOMBGC, s);
+}
+
+// ------------------------------------------------------------------ liveness
+__global__ __launch_bounds__(LB) void k_reset_sched(Dev d, const uint8_t *up) {
+    const uint32_t o = blockIdx.x * LB + threadIdx.x;
+    if (o < d.N && up[o]) d.row[o * 4 + 2] = NONE;
+}
+
+// Cluster._update_node_liveness -> FailureDetector.update_node_liveness for every known node but
+// self (server.py:606-610; failure_detector.py:89-106), phi in binary64 exactly as
+// SamplingWindow.phi (43-53).  Also folds the earliest "scheduled for deletion" tick per row.
+__global__ __launch_bounds__(LB) void k_liveness(Dev d, const uint8_t *up, uint32_t t, uint32_t chunks) {
+    const uint32_t o = blockIdx.x / chunks, cb = blockIdx.x % chunks;
+    if (!up[o]) return;
+    const bool genm = !(d.flags & GS_CANONICAL);
+    const bool ring = (d.flags & GS_FD_RING) != 0;
+    uint32_t minS = NONE, live = 0, gcdue = 0;
+    const uint32_t c0 = (cb * LB + threadIdx.x) * 4u;
+    if (c0 < d.N) {
+        const size_t p = pix(d, o, c0);
+        const uint4 L4 = *reinterpret_cast<const uint4 *>(d.fd_last + p);
+        uint4 S4 = *reinterpret_cast<const uint4 *>(d.fd_sum + p);
+        uint4 C4 = *reinterpret_cast<const uint4 *>(d.fd_cnt + p);
+        uint4 T4 = *reinterpret_cast<const uint4 *>(d.fd_state + p);
+        uint4 P4 = make_uint4(0, 0, 0, 0);
+        if (genm) P4 = *reinterpret_cast<const uint4 *>(d.pos + p);
+        const uint32_t *L = reinterpret_cast<const uint32_t *>(&L4);
+        uint32_t *Sm = reinterpret_cast<uint32_t *>(&S4), *Cn = reinterpret_cast<uint32_t *>(&C4);
+        uint32_t *St = reinterpret_cast<uint32_t *>(&T4);
+        const uint32_t *Ps = reinterpret_cast<const uint32_t *>(&P4);
+        bool dirty = false;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const uint32_t j = c0 + i;
+            if (j >= d.N) break;
+            if (j == o || (genm && Ps[i] == NONE)) continue;
+            live++;
+            const bool has = L[i] != NONE;
+            const uint32_t len = ring ? (Cn[i] < d.W ? Cn[i] : d.W) : Cn[i];
+            bool alive = false;
+            if (has && len) {
+                const double mean = ((double)Sm[i] * TICK_S + d.prior5) / ((double)len + 5.0);
+                const double phi = ((double)(t - L[i]) * TICK_S) / mean;
+                alive = phi <= d.phi_thr;
+            }
+            if (alive) {
+                if (St[i] != 1u) { St[i] = 1u; dirty = true; }
+            } else {
+                if (St[i] < 2u) { St[i] = 2u + t; dirty = true; }  // time_of_death recorded once
+                if (has && (Sm[i] | Cn[i])) { Sm[i] = 0; Cn[i] = 0; dirty = true; }  // window reset
+                const uint32_t tod = St[i] - 2u;
+                const uint32_t sat = tod + d.sched_delay;
+                if (sat < minS) minS = sat;
+                if ((uint64_t)t >= (uint64_t)tod + d.dead_grace) gcdue++;
+            }
+        }
+        if (dirty) {
+            *reinterpret_cast<uint4 *>(d.fd_sum + p) = S4;
+            *reinterpret_cast<uint4 *>(d.fd_cnt + p) = C4;
+            *reinterpret_cast<uint4 *>(d.fd_state + p) = T4;
+        }
+    }
+    // earliest scheduled-for-deletion tick of this row
+    for (int dd = 32; dd >= 1; dd >>= 1) {
+        const uint32_t y = __shfl_xor(minS, dd, WAVE);
+        if (y < minS) minS = y;
+    }
+    const unsigned long long sl = wave_sum(live), sg = wave_sum(gcdue);
+    if ((threadIdx.x & 63) == 0) {
+        if (minS != NONE) atomicMin(&d.row[o * 4 + 2], minS);
+        shard_add(d, C_LIVE, sl);
+        shard_add(d, C_E_FDGC, sg);
+    }
+}
+
+// SamplingWindow.phi (failure_detector.py:43-53) of every target of observer o; NaN for None.
+__global__ __launch_bounds__(LB) void k_phi_row(Dev d, uint32_t o, uint32_t t, double *out) {
+    const uint32_t j = blockIdx.x * LB + threadIdx.x;
+    if (j >= d.N) return;
+    const size_t p = pix(d, o, j);
+    const uint32_t last = d.fd_last[p], cnt = d.fd_cnt[p];
+    const uint32_t len = (d.flags & GS_FD_RING) ? (cnt < d.W ? cnt : d.W) : cnt;
+    double phi = __builtin_nan("");
+    if (last != NONE && len) {
+        const double mean = ((double)d.fd_sum[p] * TICK_S + d.prior5) / ((double)len + 5.0);
+        phi = ((double)(t - last) * TICK_S) / mean;
+    }
+    out[j] = phi;
+}
+
+// ------------------------------------------------------------------ owner writes
+// NodeState.set / delete / set_with_ttl / delete_after_ttl on the owner's own view (state.py:124-180).
+__global__ __launch_bounds__(LB) void k_owner_writes(Dev d, const gs_write *ops, uint32_t n, uint32_t t) {
+    const uint32_t i = blockIdx.x * LB + threadIdx.x;
+    if (i >= n) return;
+    const gs_write op = ops[i];
+    if (op.owner >= d.N || op.key >= d.K || op.op > 3u) { shard_add(d, C_E_IDX, 1); return; }
+    const uint32_t j = op.owner, k = op.key;
+    const size_t pj = pix(d, j, j);
+    uint8_t *held = d.held + pj * d.KP + k;
+    const uint32_t w = *held;
+    const uint32_t M = d.mv[pj];
+    uint32_t st, vid, vl;
+    if (op.op == GS_OP_SET || op.op == GS_OP_SET_WITH_TTL) {
+        st = op.op == GS_OP_SET ? 0u : 2u;
+        if (w) {  // same value with the same status: no-op (state.py:140-141, 146-151)
+            const size_t h = hix(d, j, w, k);
+            if (d.hist_vid[h] == op.value_id && meta_status(d.hist_meta[h]) == st) return;
+        }
+        vid = op.value_id;
+        vl = op.value_len;
+    } else {
+        if (!w) return;  // delete of an absent key is a no-op (state.py:163-164, 175-176)
+        const size_t h = hix(d, j, w, k);
+        st = op.op == GS_OP_DELETE ? 1u : 2u;
+        vid = op.op == GS_OP_DELETE ? 0u : d.hist_vid[h];        // delete clears the value (171)
+        vl = op.op == GS_OP_DELETE ? 0u : meta_vlen(d.hist_meta[h]);
+    }
+    const uint32_t nw = (uint32_t)d.last_w[(size_t)j * d.KP + k] + 1u;
+    if (nw >= d.C || vl >= (1u << 14)) { shard_add(d, C_E_HIST, 1); return; }
+    const uint32_t ver = M + 1u;
+    const size_t h = hix(d, j, nw, k);
+    d.hist_ver[h] = ver;
+    d.hist_meta[h] = make_meta(sfield(d.key_len[k]) + sfield(vl) + ufield(ver) + ufield(st), st, vl);
+    d.hist_vid[h] = vid;
+    d.last_w[(size_t)j * d.KP + k] = (uint8_t)nw;
+    *held = (uint8_t)nw;
+    d.mv[pj] = ver;
+    if (d.flags & GS_TOMBSTONES) {
+        d.ts[pj * d.KP + k] = st ? t : NONE;
+        if (st) d.row[j * 4 + 1] = 1u;
+    }
+}
+
+// ------------------------------------------------------------------ boot / warm
+__global__ __launch_bounds__(LB) void k_boot_self(Dev d) {
+    const uint32_t o = blockIdx.x * LB + threadIdx.x;
+    if (o >= d.N) return;
+    const size_t p = pix(d, o, o);
+    d.hb[p] = 1u;  // Cluster.__init__: inc_heartbeat (server.py:95-96)
+    d.row[o * 4 + 0] = 1u;
+    d.row[o * 4 + 1] = 0u;
+    d.row[o * 4 + 2] = NONE;
+    d.row[o * 4 + 3] = 0u;
+    if (!(d.flags & GS_CANONICAL)) {
+        d.pos[p] = 0u;
+        d.ord[(size_t)o * d.NP] = o;
+    }
+}
+
+__global__ __launch_bounds__(LB) void k_warm(Dev d, uint32_t chunks) {
+    const uint32_t o = blockIdx.x / chunks;
+    const uint32_t j = (blockIdx.x % chunks) * LB + threadIdx.x;
+    if (j >= d.N) return;
+    const size_t p = pix(d, o, j);
+    if (!(d.flags & GS_CANONICAL)) {
+        d.pos[p] = j;
+        d.ord[p] = j;
+        if (j == 0) d.row[o * 4 + 0] = d.N;
+    }
+    if (j == o) return;
+    const size_t q = pix(d, j, j);
+    d.hb[p] = d.hb[q];
+    d.mv[p] = d.mv[q];
+    d.gc[p] = d.gc[q];
+    for (uint32_t k = 0; k < d.KP; k++) d.held[p * d.KP + k] = d.held[q * d.KP + k];
+    if (d.flags & GS_TOMBSTONES) {
+        bool tb = false;
+        for (uint32_t k = 0; k < d.KP; k++) {
+            const uint32_t v = d.ts[q * d.KP + k];
+            d.ts[p * d.KP + k] = v;
+            tb |= v != NONE;
+        }
+        if (tb) d.row[o * 4 + 1] = 1u;
+    }
+}
+
+}  // namespace
+
+// ====================================================================== C ABI
+struct gs_handle {
+    gs_config cfg;
+    Dev d;
+    uint32_t N, NP, K, KP, C, W;
+    void *reg[GS_NUM_REGIONS];
+    uint64_t bytes[GS_NUM_REGIONS];
+    hipStream_t stream;
+    uint32_t seq;
+    bool booted;
+    std::string err;
+};
+
+namespace {
+
+int fail(gs_handle *h, int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    if (h) h->err = buf;
+    return code;
+}
+
+#define HIPCHK(h, x)                                                                         \
+    do {                                                                                     \
+        hipError_t _e = (x);                                                                 \
+        if (_e != hipSuccess) return fail((h), GS_E_HIP, "%s: %s", #x, hipGetErrorString(_e)); \
+    } while (0)
+
+uint32_t round_up(uint32_t x, uint32_t m) { return (x + m - 1) / m * m; }
+
+int check_bound(gs_handle *h) {
+    for (int r = 0; r < GS_NUM_REGIONS; r++)
+        if (h->bytes[r] && !h->reg[r]) return fail(h, GS_E_UNBOUND, "region %d not bound", r);
+    Dev &d = h->d;
+    d.hb = (uint32_t *)h->reg[GS_R_HB];
+    d.mv = (uint32_t *)h->reg[GS_R_MV];
+    d.gc = (uint32_t *)h->reg[GS_R_GC];
+    d.held = (uint8_t *)h->reg[GS_R_HELD];
+    d.fd_last = (uint32_t *)h->reg[GS_R_FD_LAST];
+    d.fd_sum = (uint32_t *)h->reg[GS_R_FD_SUM];
+    d.fd_cnt = (uint32_t *)h->reg[GS_R_FD_CNT];
+    d.fd_state = (uint32_t *)h->reg[GS_R_FD_STATE];
+    d.ts = (uint32_t *)h->reg[GS_R_TS];
+    d.ring = (uint16_t *)h->reg[GS_R_RING];
+    d.pos = (uint32_t *)h->reg[GS_R_POS];
+    d.ord = (uint32_t *)h->reg[GS_R_ORD];
+    d.row = (uint32_t *)h->reg[GS_R_ROW];
+    d.last_w = (uint8_t *)h->reg[GS_R_LAST_W];
+    d.hist_ver = (uint32_t *)h->reg[GS_R_HIST_VER];
+    d.hist_meta = (uint32_t *)h->reg[GS_R_HIST_META];
+    d.hist_vid = (uint32_t *)h->reg[GS_R_HIST_VID];
+    d.nid_size = (uint16_t *)h->reg[GS_R_NID_SIZE];
+    d.key_len = (uint8_t *)h->reg[GS_R_KEY_LEN];
+    d.stamp = (uint32_t *)h->reg[GS_R_STAMP];
+    d.ctr = (unsigned long long *)h->reg[GS_R_COUNTERS];
+    return GS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gs_api_version(void) { return GS_API_VERSION; }
+
+const char *gs_last_error(const gs_handle *h) { return h ? h->err.c_str() : "null handle"; }
+
+int gs_create(const gs_config *cfg, gs_handle **out) {
+    if (!cfg || !out) return GS_E_INVALID;
+    *out = nullptr;
+    const gs_config &c = *cfg;
+    if (c.n_nodes < 2 || c.n_nodes > (1u << 20)) return GS_E_INVALID;
+    if (c.n_keys < 1 || c.n_keys > 64) return GS_E_INVALID;
+    if (c.hist_cap < 2 || c.hist_cap > 255) return GS_E_INVALID;
+    if (c.mtu < 1 || c.window < 1) return GS_E_INVALID;
+    if ((c.flags & GS_FD_RING) && (c.window > (1u << 20) || c.max_interval_ticks > 0xFFFFu)) return GS_E_INVALID;
+    if ((uint64_t)c.window * c.max_interval_ticks >= (1ull << 32)) return GS_E_INVALID;
+    gs_handle *h = new gs_handle();
+    h->cfg = c;
+    h->N = c.n_nodes;
+    h->NP = round_up(c.n_nodes, 64);
+    h->K = c.n_keys;
+    h->KP = round_up(c.n_keys, 4);
+    h->C = c.hist_cap;
+    h->W = c.window;
+    h->stream = nullptr;
+    h->seq = 0;
+    h->booted = false;
+    const uint64_t N = h->N, NP = h->NP, KP = h->KP, K = h->K, C = h->C, W = h->W;
+    const uint64_t pairs = N * NP;
+    const bool genm = !(c.flags & GS_CANONICAL);
+    uint64_t *b = h->bytes;
+    b[GS_R_HB] = b[GS_R_MV] = b[GS_R_GC] = pairs * 4;
+    b[GS_R_HELD] = pairs * KP;
+    b[GS_R_FD_LAST] = b[GS_R_FD_SUM] = b[GS_R_FD_CNT] = b[GS_R_FD_STATE] = pairs * 4;
+    b[GS_R_TS] = (c.flags & GS_TOMBSTONES) ? pairs * KP * 4 : 0;
+    b[GS_R_RING] = (c.flags & GS_FD_RING) ? pairs * W * 2 : 0;
+    b[GS_R_POS] = b[GS_R_ORD] = genm ? pairs * 4 : 0;
+    b[GS_R_ROW] = N * 16;
+    b[GS_R_LAST_W] = N * KP;
+    b[GS_R_HIST_VER] = b[GS_R_HIST_META] = b[GS_R_HIST_VID] = N * C * K * 4;
+    b[GS_R_NID_SIZE] = NP * 2;
+    b[GS_R_KEY_LEN] = KP;
+    b[GS_R_STAMP] = NP * 4;
+    b[GS_R_COUNTERS] = (uint64_t)NSHARD * 32 * 8;
+    Dev &d = h->d;
+    memset(&d, 0, sizeof d);
+    d.N = h->N;
+    d.NP = h->NP;
+    d.K = h->K;
+    d.KP = h->KP;
+    d.C = h->C;
+    d.mtu = c.mtu;
+    d.flags = c.flags;
+    d.W = c.window;
+    d.max_iv = c.max_interval_ticks;
+    d.tomb_grace = c.tombstone_grace_ticks;
+    d.dead_grace = c.dead_grace_ticks;
+    d.sched_delay = c.sched_delay_ticks;
+    d.phi_thr = c.phi_threshold;
+    d.prior5 = c.prior_weighted;
+    *out = h;
+    return GS_OK;
+}
+
+void gs_destroy(gs_handle *h) { delete h; }
+
+int gs_region_bytes(const gs_handle *h, int region, uint64_t *bytes) {
+    if (!h || !bytes || region < 0 || region >= GS_NUM_REGIONS) return GS_E_INVALID;
+    *bytes = h->bytes[region];
+    return GS_OK;
+}
+
+int gs_bind(gs_handle *h, int region, void *ptr) {
+    if (!h || region < 0 || region >= GS_NUM_REGIONS) return GS_E_INVALID;
+    if (ptr && (reinterpret_cast<uintptr_t>(ptr) & 15u))
+        return fail(h, GS_E_INVALID, "region %d: device pointer must be 16-byte aligned", region);
+    h->reg[region] = ptr;
+    return GS_OK;
+}
+
+int gs_set_stream(gs_handle *h, void *stream) {
+    if (!h) return GS_E_INVALID;
+    h->stream = (hipStream_t)stream;
+    return GS_OK;
+}
+
+int gs_boot(gs_handle *h, const uint16_t *nid_size, const uint8_t *key_len) {
+    if (!h || !nid_size || !key_len) return GS_E_INVALID;
+    int rc = check_bound(h);
+    if (rc) return rc;
+    hipStream_t s = h->stream;
+    const uint64_t pairs = (uint64_t)h->N * h->NP;
+    // regions that start at zero
+    const int zero[] = {GS_R_HB, GS_R_MV, GS_R_GC, GS_R_HELD, GS_R_FD_SUM, GS_R_FD_CNT, GS_R_FD_STATE,
+                        GS_R_RING, GS_R_ROW, GS_R_LAST_W, GS_R_HIST_VER, GS_R_HIST_META, GS_R_HIST_VID,
+                        GS_R_STAMP, GS_R_COUNTERS};
+    for (int r : zero)
+        if (h->bytes[r]) HIPCHK(h, hipMemsetAsync(h->reg[r], 0, h->bytes[r], s));
+    HIPCHK(h, hipMemsetAsync(h->reg[GS_R_FD_LAST], 0xFF, pairs * 4, s));
+    if (h->bytes[GS_R_TS]) HIPCHK(h, hipMemsetAsync(h->reg[GS_R_TS], 0xFF, h->bytes[GS_R_TS], s));
+    if (h->bytes[GS_R_POS]) HIPCHK(h, hipMemsetAsync(h->reg[GS_R_POS], 0xFF, h->bytes[GS_R_POS], s));
+    if (h->bytes[GS_R_ORD]) HIPCHK(h, hipMemsetAsync(h->reg[GS_R_ORD], 0xFF, h->bytes[GS_R_ORD], s));
+    // tables
+    std::vector<uint16_t> ns(h->NP, 0);
+    uint32_t min_nid = 0xFFFFFFFFu, min_key = 0xFFFFFFFFu;
+    for (uint32_t j = 0; j < h->N; j++) {
+        ns[j] = nid_size[j];
+        if (nid_size[j] < min_nid) min_nid = nid_size[j];
+    }
+    std::vector<uint8_t> kl(h->KP, 0);
+    for (uint32_t k = 0; k < h->K; k++) {
+        kl[k] = key_len[k];
+        if (key_len[k] < min_key) min_key = key_len[k];
+    }
+    HIPCHK(h, hipMemcpyAsync(h->reg[GS_R_NID_SIZE], ns.data(), h->NP * 2, hipMemcpyHostToDevice, s));
+    HIPCHK(h, hipMemcpyAsync(h->reg[GS_R_KEY_LEN], kl.data(), h->KP, hipMemcpyHostToDevice, s));
+    // smallest possible single-kv NodeDelta: no NodeDelta can fit once fewer bytes remain
+    const uint32_t kv_min = msgf(sfield(min_key) + 2u);
+    h->d.lb_min = msgf(msgf(min_nid) + 2u + kv_min);
+    k_boot_self<<<(h->N + LB - 1) / LB, LB, 0, s>>>(h->d);
+    HIPCHK(h, hipGetLastError());
+    HIPCHK(h, hipStreamSynchronize(s));
+    h->booted = true;
+    return GS_OK;
+}
+
+int gs_warm(gs_handle *h) {
+    if (!h || !h->booted) return GS_E_INVALID;
+    const uint32_t chunks = (h->N + LB - 1) / LB;
+    k_warm<<<chunks * h->N, LB, 0, h->stream>>>(h->d, chunks);
+    HIPCHK(h, hipGetLastError());
+    return GS_OK;
+}
+
+int gs_owner_writes(gs_handle *h, const gs_write *ops, uint32_t n, uint32_t tick) {
+    if (!h || !h->booted) return GS_E_INVALID;
+    if (!n) return GS_OK;
+    k_owner_writes<<<(n + LB - 1) / LB, LB, 0, h->stream>>>(h->d, ops, n, tick);
+    HIPCHK(h, hipGetLastError());
+    return GS_OK;
+}
+
+int gs_begin_round(gs_handle *h, const uint8_t *up, uint32_t tick) {
+    if (!h || !h->booted || !up) return GS_E_INVALID;
+    k_begin_round<<<h->N, LB, 0, h->stream>>>(h->d, up, tick);
+    HIPCHK(h, hipGetLastError());
+    return GS_OK;
+}
+
+int gs_run_phase(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t n, uint32_t tick) {
+    if (!h || !h->booted) return GS_E_INVALID;
+    if (!n) return GS_OK;
+    if (!ini || !res) return GS_E_INVALID;
+    const bool genm = !(h->cfg.flags & GS_CANONICAL);
+    const size_t lds = (size_t)(h->NP / 32) * (genm ? 4 : 2) * 4;
+    if (lds > 160 * 1024) return fail(h, GS_E_UNSUPPORTED, "n_nodes too large for the LDS bitmaps (%zu B)", lds);
+    if (lds > 64 * 1024)
+        HIPCHK(h, hipFuncSetAttribute((const void *)k_exchange, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    h->seq += 1;
+    k_exchange<<<n, XB, lds, h->stream>>>(h->d, ini, res, n, tick, h->seq);
+    HIPCHK(h, hipGetLastError());
+    return GS_OK;
+}
+
+int gs_liveness(gs_handle *h, const uint8_t *up, uint32_t tick) {
+    if (!h || !h->booted || !up) return GS_E_INVALID;
+    k_reset_sched<<<(h->N + LB - 1) / LB, LB, 0, h->stream>>>(h->d, up);
+    HIPCHK(h, hipGetLastError());
+    const uint32_t chunks = (h->N + 4 * LB - 1) / (4 * LB);
+    k_liveness<<<chunks * h->N, LB, 0, h->stream>>>(h->d, up, tick, chunks);
+    HIPCHK(h, hipGetLastError());
+    return GS_OK;
+}
+
+int gs_phi_row(gs_handle *h, uint32_t observer, uint32_t tick, double *out) {
+    if (!h || !h->booted || !out || observer >= h->N) return GS_E_INVALID;
+    k_phi_row<<<(h->N + LB - 1) / LB, LB, 0, h->stream>>>(h->d, observer, tick, out);
+    HIPCHK(h, hipGetLastError());
+    return GS_OK;
+}
+
+int gs_read_counters(gs_handle *h, gs_counters *out) {
+    if (!h || !out || !h->reg[GS_R_COUNTERS]) return GS_E_INVALID;
+    std::vector<unsigned long long> buf((size_t)NSHARD * 32);
+    HIPCHK(h, hipMemcpyAsync(buf.data(), h->reg[GS_R_COUNTERS], buf.size() * 8, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    uint64_t acc[32] = {0};
+    for (int s = 0; s < NSHARD; s++)
+        for (int c = 0; c < 32; c++) acc[c] += buf[(size_t)s * 32 + c];
+    memcpy(out, acc, sizeof acc);
+    return GS_OK;
+}
+
+int gs_reset_counters(gs_handle *h) {
+    if (!h || !h->reg[GS_R_COUNTERS]) return GS_E_INVALID;
+    HIPCHK(h, hipMemsetAsync(h->reg[GS_R_COUNTERS], 0, h->bytes[GS_R_COUNTERS], h->stream));
+    return GS_OK;
+}
+
+int gs_sync(gs_handle *h) {
+    if (!h) return GS_E_INVALID;
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return GS_OK;
+}
+
+}  // extern "C"

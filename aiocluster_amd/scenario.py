@@ -83,14 +83,20 @@ def replay(backend, scen: dict, on_round=None, rounds: int | None = None):
     ``run_phase(t, pairs)``, ``liveness(t, up, r)``.
     """
     rs = scen["rounds"] if rounds is None else scen["rounds"][:rounds]
-    for r, rd in enumerate(rs):
-        t = round_tick(r)
-        up = rd["up"]
-        for j, k, op, v in rd["writes"]:
-            backend.write(t, j, k, op, v)
-        backend.begin_round(t, up)
-        for p, ph in enumerate(rd["phases"]):
-            backend.run_phase(phase_tick(r, p), ph)
-        backend.liveness(liveness_tick(r, len(rd["phases"])), up, r)
+    for r in range(len(rs)):
+        replay_round(backend, scen, r)
         if on_round is not None:
             on_round(r)
+
+
+def replay_round(backend, scen: dict, r: int):
+    """Round ``r`` of ``scen`` on ``backend`` (writes, round start, phases, liveness)."""
+    rd = scen["rounds"][r]
+    t = round_tick(r)
+    up = rd["up"]
+    for j, k, op, v in rd["writes"]:
+        backend.write(t, j, k, op, v)
+    backend.begin_round(t, up)
+    for p, ph in enumerate(rd["phases"]):
+        backend.run_phase(phase_tick(r, p), ph)
+    backend.liveness(liveness_tick(r, len(rd["phases"])), up, r)

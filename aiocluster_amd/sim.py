@@ -1,0 +1,420 @@
+"""Host side of the MI355X batched gossip backend.
+
+``GossipSim`` holds a whole simulated aiocluster cluster in HBM and drives the
+hand-written gfx950 kernels of ``csrc/gossip_sim.hip`` through the C ABI of
+``include/gossip_sim.h``.  PyTorch is used only to allocate the device regions
+and to provide the HIP stream.  There is no CPU fallback: without the HIP
+library (or without a GPU) construction raises.
+
+The public methods mirror the reference call sites the backend replaces
+(``aiocluster/server.py`` and ``aiocluster/state.py``):
+
+==============================  ==========================================================
+``GossipSim``                   reference
+==============================  ==========================================================
+``set/delete/set_with_ttl/      ``Cluster.set/...`` -> ``NodeState.set/...``
+delete_after_ttl``              (server.py:193-215, state.py:137-180)
+``begin_round``                 ``_gossip_multiple``: inc_heartbeat + gc_marked_for_deletion
+                                (server.py:471-474)
+``run_phase``                   ``_gossip`` / ``_handle_message`` for a set of disjoint pairs
+                                (server.py:327-376, 523-568)
+``update_node_liveness``        ``_update_node_liveness`` (server.py:606-620)
+``node_state``, ``snapshot``,   ``ClusterState.node_state``, ``Cluster.snapshot``,
+``live_nodes``, ``dead_nodes``, ``FailureDetector.live_nodes/dead_nodes/phi``
+``phi``
+==============================  ==========================================================
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import math
+from datetime import timedelta
+
+import numpy as np
+
+from . import _lib
+from ._lib import GS_CANONICAL, GS_FD_RING, GS_NONE, GS_TOMBSTONES, REGION, TICK_US, GsError
+from .entities import NodeId, NodeState, VersionedValue, VersionStatusEnum
+from .pbsize import nodeid_size
+
+OPS = {"set": 0, "delete": 1, "set_with_ttl": 2, "delete_after_ttl": 3}
+
+
+def _us(seconds: float) -> int:
+    return timedelta(seconds=seconds) // timedelta(microseconds=1)
+
+
+def _ticks(seconds: float, what: str) -> int:
+    us = _us(seconds)
+    if us % TICK_US:
+        raise ValueError(f"{what}={seconds}s is not a whole number of 1/64 s ticks")
+    return us // TICK_US
+
+
+def sched_delay_ticks(dead_grace_s: float) -> int:
+    """Smallest tick count d with d*TICK_US >= dead_grace/2.0 as timedelta rounds it (half to even)."""
+    g = _us(dead_grace_s)
+    half = g // 2
+    if (g & 1) and (half & 1):
+        half += 1
+    return -(-half // TICK_US)
+
+
+def make_config(n: int, k: int, cfg: dict, flags: int, hist_cap: int) -> _lib.GsConfig:
+    c = _lib.GsConfig()
+    c.n_nodes = n
+    c.n_keys = k
+    c.hist_cap = hist_cap
+    c.mtu = int(cfg["mtu"])
+    c.flags = flags
+    c.window = int(cfg["window"])
+    c.max_interval_ticks = _ticks(cfg["max_interval_s"], "max_interval")
+    c.tombstone_grace_ticks = _ticks(cfg["tombstone_grace_s"], "marked_for_deletion_grace_period")
+    c.dead_grace_ticks = _ticks(cfg["dead_grace_s"], "dead_node_grace_period")
+    c.sched_delay_ticks = sched_delay_ticks(cfg["dead_grace_s"])
+    c.phi_threshold = float(cfg["phi_threshold"])
+    # SamplingWindow: _prev_weight * _prev_mean (failure_detector.py:22-23, 51)
+    c.prior_weighted = 5.0 * timedelta(seconds=cfg["initial_interval_s"]).total_seconds()
+    return c
+
+
+class GossipSim:
+    """A simulated cluster of ``len(node_ids)`` aiocluster nodes resident on one MI355X."""
+
+    def __init__(self, node_ids: list[NodeId], keys: list[str], cfg: dict, init: str = "cold",
+                 initial_values: dict[int, list[tuple[int, str]]] | None = None, *, device: str = "cuda:0",
+                 tombstones: bool = True, fd_ring: bool | None = None, hist_cap: int = 64,
+                 nid_sizes: list[int] | None = None):
+        import torch
+
+        if not torch.cuda.is_available():
+            raise GsError("GossipSim needs a ROCm GPU (no CPU fallback)")
+        self.torch = torch
+        self.L = _lib.load()
+        self.device = torch.device(device)
+        self.n = n = len(node_ids) if node_ids is not None else len(nid_sizes)
+        self.node_ids = node_ids
+        self.keys = list(keys)
+        self.k = k = len(keys)
+        self.cfg = dict(cfg)
+        self.np_ = (n + 63) // 64 * 64
+        self.kp = (k + 3) // 4 * 4
+        self.hist_cap = hist_cap
+        self.init = init
+        flags = 0
+        if init == "warm":
+            flags |= GS_CANONICAL
+        if tombstones:
+            flags |= GS_TOMBSTONES
+        W = int(cfg["window"])
+        if fd_ring is None:
+            fd_ring = n * self.np_ * W * 2 <= (1 << 30)
+        if fd_ring:
+            flags |= GS_FD_RING
+        self.flags = flags
+        self.canonical = bool(flags & GS_CANONICAL)
+        c = make_config(n, k, cfg, flags, hist_cap)
+        h = C.c_void_p()
+        rc = self.L.gs_create(C.byref(c), C.byref(h))
+        if rc:
+            raise GsError(f"gs_create failed ({_lib.ERRORS.get(rc, rc)}): invalid config {cfg}")
+        self.h = h
+        self.regions = {}
+        try:
+            for name, idx in REGION.items():
+                nb = C.c_uint64()
+                self._chk(self.L.gs_region_bytes(h, idx, C.byref(nb)), "gs_region_bytes")
+                if nb.value:
+                    t = torch.empty(int(nb.value), dtype=torch.uint8, device=self.device)
+                    self.regions[name] = t
+                    self._chk(self.L.gs_bind(h, idx, C.c_void_p(t.data_ptr())), "gs_bind")
+            self.stream = torch.cuda.current_stream(self.device)
+            self._chk(self.L.gs_set_stream(h, C.c_void_p(self.stream.cuda_stream)), "gs_set_stream")
+            if nid_sizes is None:
+                nid_sizes = [nodeid_size(x.name, x.generation_id, x.gossip_advertise_addr[0],
+                                         x.gossip_advertise_addr[1], x.tls_name) for x in node_ids]
+            ns = np.asarray(nid_sizes, dtype=np.uint16)
+            kl = np.asarray([len(s.encode()) for s in self.keys], dtype=np.uint8)
+            self._chk(self.L.gs_boot(h, ns.ctypes.data_as(C.c_void_p), kl.ctypes.data_as(C.c_void_p)), "gs_boot")
+        except Exception:
+            self.close()
+            raise
+        self.values = [""]
+        self.value_ids = {"": 0}
+        self._pending: list[tuple[int, int, int, int, str]] = []
+        self.last_tick = 0
+        self.q9_events: list = []
+        if initial_values:
+            for j in range(n):
+                for kk, v in initial_values.get(j, []):
+                    self.write(0, j, kk, 0, v)
+            self._flush()
+        if init == "warm":
+            self._chk(self.L.gs_warm(h), "gs_warm")
+
+    # ------------------------------------------------------------------ plumbing
+    def _chk(self, rc: int, what: str):
+        if rc:
+            msg = self.L.gs_last_error(self.h).decode() if getattr(self, "h", None) else ""
+            raise GsError(f"{what}: {_lib.ERRORS.get(rc, rc)} {msg}")
+
+    def close(self):
+        h = getattr(self, "h", None)
+        if h:
+            self.L.gs_destroy(h)
+            self.h = None
+        self.regions = {}
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def region(self, name: str, dtype, shape):
+        return self.regions[name].view(dtype).view(*shape)
+
+    def intern(self, value: str) -> int:
+        vid = self.value_ids.get(value)
+        if vid is None:
+            vid = len(self.values)
+            self.values.append(value)
+            self.value_ids[value] = vid
+        return vid
+
+    def _dev(self, arr: np.ndarray, dtype):
+        return self.torch.from_numpy(np.ascontiguousarray(arr)).to(self.device, non_blocking=False).view(dtype)
+
+    # --------------------------------------------------------------- owner writes
+    def write(self, t: int, j: int, k: int, op: int, value: str):
+        if op in (1, 2, 3) and not self.flags & GS_TOMBSTONES:
+            raise GsError("deletes / TTL writes need tombstones=True (GS_TOMBSTONES)")
+        # interned at call time, so ids follow the caller's write order (as the oracle's do)
+        self._pending.append((t, j, k, op, self.intern(value), len(value.encode())))
+
+    def set(self, t: int, owner: int, key: str, value: str):
+        self.write(t, owner, self.keys.index(key), 0, value)
+
+    def delete(self, t: int, owner: int, key: str):
+        self.write(t, owner, self.keys.index(key), 1, "")
+
+    def set_with_ttl(self, t: int, owner: int, key: str, value: str):
+        self.write(t, owner, self.keys.index(key), 2, value)
+
+    def delete_after_ttl(self, t: int, owner: int, key: str):
+        self.write(t, owner, self.keys.index(key), 3, "")
+
+    def _flush(self):
+        if not self._pending:
+            return
+        # split into batches of distinct owners, keeping each owner's order
+        batches: list[list] = []
+        seen: dict[int, int] = {}
+        for t, j, k, op, vid, vl in self._pending:
+            b = seen.get(j, 0)
+            seen[j] = b + 1
+            while len(batches) <= b:
+                batches.append([])
+            batches[b].append((t, j, k, op, vid, vl))
+        self._pending = []
+        for batch in batches:
+            ticks = {x[0] for x in batch}
+            for tick in sorted(ticks):
+                rows = [[j, k, op, vid, vl] for t, j, k, op, vid, vl in batch if t == tick]
+                self.owner_writes(np.asarray(rows, dtype=np.uint32), tick)
+
+    def owner_writes(self, ops: np.ndarray, tick: int):
+        """Device batch of owner writes; ``ops`` is uint32 [m, 5] (owner, key, op, value_id, value_len)."""
+        if len(ops) == 0:
+            return
+        ops = np.ascontiguousarray(ops, dtype=np.uint32)
+        if len(np.unique(ops[:, 0])) != len(ops):
+            raise GsError("owner_writes: owners must be distinct within one batch")
+        d = self._dev(ops.view(np.int32), self.torch.int32)
+        self._chk(self.L.gs_owner_writes(self.h, C.c_void_p(d.data_ptr()), len(ops), tick), "gs_owner_writes")
+
+    # --------------------------------------------------------------- round driver
+    def begin_round(self, t: int, up):
+        self._flush()
+        u = self._dev(np.asarray(up, dtype=np.uint8), self.torch.uint8)
+        self._chk(self.L.gs_begin_round(self.h, C.c_void_p(u.data_ptr()), t), "gs_begin_round")
+
+    def run_phase(self, t: int, pairs):
+        self._flush()
+        if len(pairs) == 0:
+            return
+        arr = np.asarray(pairs, dtype=np.int32).reshape(-1, 2)
+        self.run_phase_arrays(t, arr[:, 0], arr[:, 1])
+
+    def run_phase_arrays(self, t: int, initiators, responders):
+        ini = initiators if hasattr(initiators, "data_ptr") else self._dev(np.asarray(initiators, np.int32),
+                                                                           self.torch.int32)
+        res = responders if hasattr(responders, "data_ptr") else self._dev(np.asarray(responders, np.int32),
+                                                                           self.torch.int32)
+        n = int(ini.numel())
+        if n == 0:
+            return
+        self._chk(self.L.gs_run_phase(self.h, C.c_void_p(ini.data_ptr()), C.c_void_p(res.data_ptr()), n, t),
+                  "gs_run_phase")
+
+    def update_node_liveness(self, t: int, up):
+        self._flush()
+        u = up if hasattr(up, "data_ptr") else self._dev(np.asarray(up, dtype=np.uint8), self.torch.uint8)
+        self._chk(self.L.gs_liveness(self.h, C.c_void_p(u.data_ptr()), t), "gs_liveness")
+        self.last_tick = t
+
+    def liveness(self, t: int, up, r: int = -1):
+        self.update_node_liveness(t, up)
+
+    # --------------------------------------------------------------- counters
+    def counters(self) -> dict:
+        c = _lib.GsCounters()
+        self._chk(self.L.gs_read_counters(self.h, C.byref(c)), "gs_read_counters")
+        return {n: int(getattr(c, n)) for n in _lib.COUNTER_FIELDS}
+
+    def reset_counters(self):
+        self._chk(self.L.gs_reset_counters(self.h), "gs_reset_counters")
+
+    def check(self) -> dict:
+        """Raise if any device-side check failed; return the counters."""
+        c = self.counters()
+        errs = {k: v for k, v in c.items() if k.startswith("err_") and v}
+        if errs.get("err_fd_gc"):
+            raise GsError(f"FailureDetector.garbage_collect is due but not implemented on the device: {errs}")
+        if errs:
+            raise GsError(f"device checks failed: {errs}")
+        return c
+
+    def sync(self):
+        self._chk(self.L.gs_sync(self.h), "gs_sync")
+
+    # --------------------------------------------------------------- readback
+    def _host(self):
+        n, NP, KP, K, Cc = self.n, self.np_, self.kp, self.k, self.hist_cap
+        torch = self.torch
+        self.sync()
+        g = {}
+        for name in ("HB", "MV", "GC", "FD_LAST", "FD_SUM", "FD_CNT", "FD_STATE"):
+            g[name] = self.region(name, torch.int32, (n, NP)).cpu().numpy().view(np.uint32)
+        g["HELD"] = self.region("HELD", torch.uint8, (n, NP, KP)).cpu().numpy()
+        for name in ("HIST_VER", "HIST_META", "HIST_VID"):
+            g[name] = self.region(name, torch.int32, (n, Cc, K)).cpu().numpy().view(np.uint32)
+        g["ROW"] = self.region("ROW", torch.int32, (n, 4)).cpu().numpy().view(np.uint32)
+        if "TS" in self.regions:
+            g["TS"] = self.region("TS", torch.int32, (n, NP, KP)).cpu().numpy().view(np.uint32)
+        if "ORD" in self.regions:
+            g["ORD"] = self.region("ORD", torch.int32, (n, NP)).cpu().numpy().view(np.uint32)
+        return g
+
+    def export(self, g=None) -> dict:
+        """All observers as numpy arrays in the oracle's ``export_row`` format (times in ticks)."""
+        g = self._host() if g is None else g
+        n, K = self.n, self.k
+        held = g["HELD"][:, :n, :K].astype(np.int64)
+        jj = np.arange(n)[None, :, None]
+        kk = np.arange(K)[None, None, :]
+        ver = g["HIST_VER"][jj, held, kk]
+        meta = g["HIST_META"][jj, held, kk]
+        vid = g["HIST_VID"][jj, held, kk]
+        present = held > 0
+        out = {
+            "hb": g["HB"][:, :n], "mv": g["MV"][:, :n], "gc": g["GC"][:, :n],
+            "kv_version": np.where(present, ver, 0).astype(np.uint32),
+            "kv_status": np.where(present, (meta >> 16) & 3, 0).astype(np.int32),
+            "kv_value_id": np.where(present, vid, 0).astype(np.uint32),
+        }
+        if self.canonical:
+            out["pos"] = np.broadcast_to(np.arange(n, dtype=np.int32), (n, n)).copy()
+        else:
+            pos = self.region("POS", self.torch.int32, (n, self.np_)).cpu().numpy()[:, :n]
+            out["pos"] = np.where(pos == -1, -1, pos).astype(np.int32)
+        ts = g["TS"][:, :n, :K].astype(np.int64) if "TS" in g else np.zeros((n, n, K), np.int64)
+        out["kv_ts"] = np.where(out["kv_status"] != 0, ts, 0)
+        last = g["FD_LAST"][:, :n]
+        out["fd_last"] = np.where(last == GS_NONE, -1, last.astype(np.int64))
+        cnt = g["FD_CNT"][:, :n].astype(np.int32)
+        W = int(self.cfg["window"])
+        out["fd_len"] = np.where(last == GS_NONE, 0, np.minimum(cnt, W) if self.flags & GS_FD_RING else cnt)
+        out["fd_sum"] = np.where(last == GS_NONE, 0.0, g["FD_SUM"][:, :n] / 64.0)
+        st = g["FD_STATE"][:, :n]
+        out["live"] = (st == 1).astype(np.int32)
+        out["tod"] = np.where(st >= 2, st.astype(np.int64) - 2, -1)
+        return out
+
+    def phi_row(self, observer: int, tick: int | None = None) -> np.ndarray:
+        """Device-computed phi (binary64) of every target of ``observer``; NaN = None."""
+        t = self.last_tick if tick is None else tick
+        out = self.torch.empty(self.n, dtype=self.torch.float64, device=self.device)
+        self._chk(self.L.gs_phi_row(self.h, observer, t, C.c_void_p(out.data_ptr())), "gs_phi_row")
+        return out.cpu().numpy()
+
+    def _order(self, g, o: int) -> list[int]:
+        if self.canonical:
+            return list(range(self.n))
+        return [int(x) for x in g["ORD"][o, : g["ROW"][o, 0]]]
+
+    def _kvs(self, g, o: int, j: int) -> list:
+        out = []
+        for k in range(self.k):
+            w = int(g["HELD"][o, j, k])
+            if not w:
+                continue
+            ver = int(g["HIST_VER"][j, w, k])
+            meta = int(g["HIST_META"][j, w, k])
+            st = (meta >> 16) & 3
+            ts = int(g["TS"][o, j, k]) if (st and "TS" in g) else None
+            out.append([self.keys[k], self.values[int(g["HIST_VID"][j, w, k])], ver, st, ts])
+        out.sort()
+        return out
+
+    def _window_len(self, cnt: int) -> int:
+        W = int(self.cfg["window"])
+        return min(cnt, W) if self.flags & GS_FD_RING else cnt
+
+    def observer_state(self, o: int, g=None) -> dict:
+        """Canonical dump, identical in format to ``oracle/refharness.py`` (golden fixtures)."""
+        g = self._host() if g is None else g
+        nodes = []
+        for j in self._order(g, o):
+            nodes.append([j, int(g["HB"][o, j]), int(g["MV"][o, j]), int(g["GC"][o, j]), self._kvs(g, o, j)])
+        st = g["FD_STATE"][o, : self.n]
+        live = [int(j) for j in np.flatnonzero(st == 1)]
+        dead = [[int(j), int(st[j]) - 2] for j in np.flatnonzero(st >= 2)]
+        phis = self.phi_row(o)
+        wins = []
+        for j in np.flatnonzero(g["FD_LAST"][o, : self.n] != GS_NONE):
+            j = int(j)
+            phi = float(phis[j])
+            wins.append([j, int(g["FD_LAST"][o, j]), self._window_len(int(g["FD_CNT"][o, j])),
+                         int(g["FD_SUM"][o, j]) / 64.0, None if math.isnan(phi) else phi])
+        return {"nodes": nodes, "live": live, "dead": dead, "windows": wins}
+
+    def state(self) -> list[dict]:
+        g = self._host()
+        return [self.observer_state(o, g) for o in range(self.n)]
+
+    # --------------------------------------------------------------- reference-shaped views
+    def node_state(self, observer: int, owner: int) -> NodeState | None:
+        """``ClusterState.node_state`` of ``observer`` for ``owner`` (state.py:295-296)."""
+        g = self._host()
+        if owner not in self._order(g, observer):
+            return None
+        kvs = {
+            key: VersionedValue(val, ver, VersionStatusEnum(st), ts)
+            for key, val, ver, st, ts in self._kvs(g, observer, owner)
+        }
+        return NodeState(self.node_ids[owner], int(g["HB"][observer, owner]), kvs, int(g["MV"][observer, owner]),
+                         int(g["GC"][observer, owner]))
+
+    def live_nodes(self, observer: int) -> list[NodeId]:
+        st = self.region("FD_STATE", self.torch.int32, (self.n, self.np_))[observer, : self.n].cpu().numpy()
+        return [self.node_ids[j] for j in np.flatnonzero(st == 1)]
+
+    def dead_nodes(self, observer: int) -> list[NodeId]:
+        st = self.region("FD_STATE", self.torch.int32, (self.n, self.np_))[observer, : self.n].cpu().numpy()
+        return [self.node_ids[j] for j in np.flatnonzero(st >= 2)]
+
+    def phi(self, observer: int, target: int, tick: int | None = None) -> float | None:
+        v = float(self.phi_row(observer, tick)[target])
+        return None if math.isnan(v) else v

@@ -1,0 +1,163 @@
+/*
+ * gossip_sim.h -- C ABI of the MI355X batched gossip simulator.
+ *
+ * A drop-in batched backend for aiocluster's scuttlebutt anti-entropy
+ * (aiocluster/state.py) and phi failure detector (aiocluster/failure_detector.py).
+ * The reference has no FFI for this path: its hot path is plain Python called
+ * in-process by aiocluster/server.py.  Each entry point below replaces, for a
+ * whole simulated cluster at once, the reference calls named next to it; the
+ * ctypes binding a maintainer would add to the reference is in INTEGRATION.md.
+ *
+ * Ownership: every device buffer is allocated by the caller (PyTorch in this
+ * repo) and bound with gs_bind(); the library never allocates or frees device
+ * memory.  Threading: one host thread per handle; all kernels run on the
+ * stream given to gs_set_stream() (default: the null stream); only
+ * gs_read_counters()/gs_sync() block.  Errors: every function returns 0 on
+ * success or a negative GS_E_* code; gs_last_error() describes the last one.
+ *
+ * Time is simulated in ticks of 1/64 s (15 625 us): whole microseconds, like
+ * the reference's datetimes, and dyadic, so the failure detector's
+ * interval sums are exact in binary64.
+ */
+#ifndef GOSSIP_SIM_H
+#define GOSSIP_SIM_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GS_API_VERSION 1
+#define GS_TICK_US 15625u
+#define GS_NONE 0xFFFFFFFFu
+
+/* error codes */
+#define GS_OK 0
+#define GS_E_INVALID (-1)     /* bad argument / config */
+#define GS_E_UNBOUND (-2)     /* a required region is not bound */
+#define GS_E_HIP (-3)         /* HIP runtime error */
+#define GS_E_DEVICE (-4)      /* a device-side check failed (see gs_counters error fields) */
+#define GS_E_UNSUPPORTED (-5) /* semantics not implemented by this build (e.g. FD garbage collection) */
+
+/* config flags */
+#define GS_CANONICAL 1u   /* every observer knows every node in index order (warm start, no removals) */
+#define GS_TOMBSTONES 2u  /* track tombstone receive ticks (needed when deletes/TTL writes occur) */
+#define GS_FD_RING 4u     /* keep each sampling window's ring (exact eviction once a window is full) */
+
+/* owner write ops (NodeState.set/delete/set_with_ttl/delete_after_ttl, state.py:137-180) */
+#define GS_OP_SET 0u
+#define GS_OP_DELETE 1u
+#define GS_OP_SET_WITH_TTL 2u
+#define GS_OP_DELETE_AFTER_TTL 3u
+
+typedef struct gs_config {
+    uint32_t n_nodes;               /* N: simulated cluster size */
+    uint32_t n_keys;                /* K <= 64 keys per node */
+    uint32_t hist_cap;              /* C <= 255: writes kept per (owner, key), ordinal 0 = absent */
+    uint32_t mtu;                   /* Config.max_payload_size (entities.py:105) */
+    uint32_t flags;                 /* GS_CANONICAL | GS_TOMBSTONES | GS_FD_RING */
+    uint32_t window;                /* FailureDetectorConfig.sampling_window_size (entities.py:88) */
+    uint32_t max_interval_ticks;    /* FailureDetectorConfig.max_interval (entities.py:89) */
+    uint32_t tombstone_grace_ticks; /* Config.marked_for_deletion_grace_period (entities.py:101) */
+    uint32_t dead_grace_ticks;      /* FailureDetectorConfig.dead_node_grace_period (entities.py:91) */
+    uint32_t sched_delay_ticks;     /* smallest d with d*TICK_US >= round_half_even(dead_grace_us/2)
+                                       (failure_detector.py:124-126) */
+    double phi_threshold;           /* FailureDetectorConfig.phi_threshhold (entities.py:87) */
+    double prior_weighted;          /* 5.0 * initial_interval.total_seconds() (failure_detector.py:22-23,51) */
+} gs_config;
+
+/* device regions (all caller-allocated; row stride NP = n_nodes rounded up to 64) */
+enum gs_region {
+    GS_R_HB = 0,      /* u32 [N][NP]   NodeState.heartbeat of owner j as seen by observer o */
+    GS_R_MV,          /* u32 [N][NP]   NodeState.max_version */
+    GS_R_GC,          /* u32 [N][NP]   NodeState.last_gc_version */
+    GS_R_HELD,        /* u8  [N][NP][KP] write ordinal of each key held (0 = absent), KP = K rounded to 4 */
+    GS_R_FD_LAST,     /* u32 [N][NP]   SamplingWindow._last_heartbeat tick, GS_NONE = no window */
+    GS_R_FD_SUM,      /* u32 [N][NP]   BoundedArrayStats._sum in ticks */
+    GS_R_FD_CNT,      /* u32 [N][NP]   intervals appended since the last reset (len = min(cnt, W)) */
+    GS_R_FD_STATE,    /* u32 [N][NP]   0 = unknown, 1 = live, >= 2: dead since tick (v - 2) */
+    GS_R_TS,          /* u32 [N][NP][KP] tombstone receive tick, GS_NONE for SET entries (GS_TOMBSTONES) */
+    GS_R_RING,        /* u16 [N][NP][W] interval ring in ticks (GS_FD_RING) */
+    GS_R_POS,         /* u32 [N][NP]   insertion index of owner j in observer o's dict, GS_NONE = absent (general) */
+    GS_R_ORD,         /* u32 [N][NP]   owner at insertion index q (general) */
+    GS_R_ROW,         /* u32 [N][4]    {dict size, tombstone-present flag, first tick a dead target is
+                                        scheduled for deletion, reserved} */
+    GS_R_LAST_W,      /* u8  [N][KP]   owner's latest write ordinal per key */
+    GS_R_HIST_VER,    /* u32 [N][C][K] version of write w of (owner, key) */
+    GS_R_HIST_META,   /* u32 [N][C][K] KeyValueUpdatePb size | status << 16 | value bytes << 18 */
+    GS_R_HIST_VID,    /* u32 [N][C][K] interned value id (host string table) */
+    GS_R_NID_SIZE,    /* u16 [NP]      NodeIdPb size per node (entities.py:62-72) */
+    GS_R_KEY_LEN,     /* u8  [KP]      UTF-8 key length per key index */
+    GS_R_STAMP,       /* u32 [NP]      per-node phase stamp (conflict check) */
+    GS_R_COUNTERS,    /* u64 [64][32]  sharded gs_counters (summed by gs_read_counters) */
+    GS_NUM_REGIONS
+};
+
+typedef struct gs_counters {
+    uint64_t exchanges;     /* exchanges executed */
+    uint64_t hb_reports;    /* FailureDetector.report_heartbeat calls */
+    uint64_t node_deltas;   /* NodeDeltas sent */
+    uint64_t kvs_sent;      /* KeyValueUpdates sent */
+    uint64_t truncated;     /* NodeDeltas cut by the MTU (sent with a prefix of their kvs) */
+    uint64_t delta_bytes;   /* sum of DeltaPb sizes */
+    uint64_t alg_bytes;     /* element-granular bytes loaded + stored by the exchange kernel */
+    uint64_t hb_writes;     /* heartbeat entries changed */
+    uint64_t candidates;    /* stale owners evaluated by the packers */
+    uint64_t live_pairs;    /* (observer, target) pairs swept by the liveness kernel */
+    uint64_t tomb_gc;       /* tombstones removed by gc_marked_for_deletion */
+    uint64_t err_fd_overflow;  /* compact window full without GS_FD_RING (result inexact) */
+    uint64_t err_hist_full;    /* a (owner, key) wrote more than hist_cap - 1 times */
+    uint64_t err_bad_index;    /* exchange endpoint out of range or a == b */
+    uint64_t err_conflict;     /* a node appeared twice in one phase */
+    uint64_t err_fd_gc;        /* a dead target reached dead_node_grace_period (FD GC not implemented) */
+    uint64_t err_insert;       /* insertion into a GS_CANONICAL state */
+    uint64_t reserved[15];
+} gs_counters;
+
+typedef struct gs_write {   /* one owner write */
+    uint32_t owner, key, op, value_id, value_len;
+} gs_write;
+
+typedef struct gs_handle gs_handle;
+
+int gs_create(const gs_config *cfg, gs_handle **out);
+void gs_destroy(gs_handle *h);
+const char *gs_last_error(const gs_handle *h);
+int gs_api_version(void);
+
+/* bytes the caller must allocate for a region (0 = unused under this config) */
+int gs_region_bytes(const gs_handle *h, int region, uint64_t *bytes);
+int gs_bind(gs_handle *h, int region, void *device_ptr);
+int gs_set_stream(gs_handle *h, void *hip_stream);
+
+/* Fill every bound region with the boot state: each node knows only itself with
+ * heartbeat 1 (Cluster.__init__, server.py:90-96).  nid_size/key_len are host arrays. */
+int gs_boot(gs_handle *h, const uint16_t *nid_size, const uint8_t *key_len);
+/* Warm start: every observer learns every owner's current state, in index order. */
+int gs_warm(gs_handle *h);
+
+/* Owner writes at `tick` (state.py:137-180).  `ops` is a DEVICE array; owners must be distinct. */
+int gs_owner_writes(gs_handle *h, const gs_write *ops, uint32_t n, uint32_t tick);
+/* Round start for every node with up[o] != 0 (DEVICE u8 array): inc_heartbeat +
+ * gc_marked_for_deletion (server.py:471-474, state.py:253-274, 333-338). */
+int gs_begin_round(gs_handle *h, const uint8_t *up, uint32_t tick);
+/* One conflict-free phase of exchanges initiators[e] -> responders[e] (DEVICE int32 arrays):
+ * Syn/SynAck/Ack = server.py:327-376 + 524, i.e. compute_digest, _report_heartbeat,
+ * compute_partial_delta_respecting_mtu and apply_delta on both sides. */
+int gs_run_phase(gs_handle *h, const int32_t *initiators, const int32_t *responders, uint32_t n, uint32_t tick);
+/* _update_node_liveness for every up node (server.py:606-620; failure_detector.py:89-128). */
+int gs_liveness(gs_handle *h, const uint8_t *up, uint32_t tick);
+
+/* SamplingWindow.phi (failure_detector.py:43-53) of every target of `observer` at `tick`
+ * into the DEVICE array out[n_nodes] (binary64; NaN where the reference returns None). */
+int gs_phi_row(gs_handle *h, uint32_t observer, uint32_t tick, double *out);
+
+int gs_read_counters(gs_handle *h, gs_counters *out);
+int gs_reset_counters(gs_handle *h);
+int gs_sync(gs_handle *h);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -626,6 +626,32 @@ int64_t orc_fd_dead_since(const orc *o, int32_t i, int32_t j) {
 
 void orc_get_stats(const orc *o, orc_stats *out) { *out = o->st; }
 
+void orc_export_row(const orc *o, int32_t i, int32_t *pos, uint32_t *hb, uint32_t *mv, uint32_t *gc,
+                    uint32_t *kv_version, int32_t *kv_status, uint32_t *kv_value_id, int64_t *kv_ts,
+                    int64_t *fd_last, int32_t *fd_len, double *fd_sum, int32_t *live, int64_t *tod) {
+    const oobs *b = &o->obs[i];
+    const int32_t N = o->N, K = o->K;
+    for (int32_t j = 0; j < N; j++) {
+        pos[j] = b->alloc ? b->pos[j] : -1;
+        const oview *v = b->alloc ? &b->v[j] : NULL;
+        hb[j] = v ? v->hb : 0; mv[j] = v ? v->mv : 0; gc[j] = v ? v->gc : 0;
+        for (int32_t k = 0; k < K; k++) {
+            const okv *e = b->alloc ? &b->kv[(size_t)j * K + k] : NULL;
+            const int pr = e && e->present;
+            kv_version[(size_t)j * K + k] = pr ? e->version : 0;
+            kv_status[(size_t)j * K + k] = pr ? e->status : 0;
+            kv_value_id[(size_t)j * K + k] = pr ? e->value_id : 0;
+            kv_ts[(size_t)j * K + k] = pr ? e->ts : 0;
+        }
+        const owin *w = b->alloc ? &b->w[j] : NULL;
+        fd_last[j] = (w && w->has && w->has_last) ? w->last : -1;
+        fd_len[j] = (w && w->has) ? win_len(w, o->c.window) : 0;
+        fd_sum[j] = (w && w->has) ? w->sum : 0.0;
+        live[j] = b->alloc ? b->live[j] : 0;
+        tod[j] = (b->alloc && b->dead_pos[j] >= 0) ? b->tod[j] : -1;
+    }
+}
+
 /* --------------------------------------------------- state injection */
 void orc_load_row(orc *o, int32_t obs, int32_t cnt, const int32_t *order,
                   const uint32_t *hb, const uint32_t *mv, const uint32_t *gc,

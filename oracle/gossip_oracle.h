@@ -85,6 +85,12 @@ int32_t orc_fd_phi(const orc *o, int32_t obs, int32_t target, int64_t now_us, do
 int32_t orc_fd_live(const orc *o, int32_t obs, int32_t target);
 int64_t orc_fd_dead_since(const orc *o, int32_t obs, int32_t target);
 void    orc_get_stats(const orc *o, orc_stats *out);
+/* Bulk export of one observer row (arrays sized N, or N*K for per-key fields):
+ * present[j] = dict position or -1; per-key version/status/value_id/ts (version 0 = absent);
+ * FD: window last (-1 = no window), len, sum; live flag; time of death (-1 = not dead). */
+void    orc_export_row(const orc *o, int32_t obs, int32_t *pos, uint32_t *hb, uint32_t *mv, uint32_t *gc,
+                       uint32_t *kv_version, int32_t *kv_status, uint32_t *kv_value_id, int64_t *kv_ts,
+                       int64_t *fd_last, int32_t *fd_len, double *fd_sum, int32_t *live, int64_t *tod);
 
 /* -------------------------------------------------- state injection (baseline) */
 /* Replace observer obs's whole row: order[cnt], heartbeat/max/gc[n], kv ordinals are

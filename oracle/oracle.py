@@ -75,6 +75,7 @@ def lib():
             "orc_fd_live": (i32, [P, i32, i32]),
             "orc_fd_dead_since": (i64, [P, i32, i32]),
             "orc_get_stats": (None, [P, C.POINTER(_Stats)]),
+            "orc_export_row": (None, [P, i32] + [P] * 13),
             "orc_load_row": (None, [P, i32, i32, P, P, P, P, P, i32, P, P, P, P, P, P, P, P, i64]),
         }
         for name, (res, args) in sig.items():
@@ -221,3 +222,25 @@ class OracleSim:
 
     def state(self) -> list[dict]:
         return [self.observer_state(o) for o in range(self.n)]
+
+    def export(self) -> dict:
+        rows = [self.export_row(o) for o in range(self.n)]
+        return {k: np.stack([r[k] for r in rows]) for k in rows[0]}
+
+    def export_row(self, o: int) -> dict:
+        """Numpy view of observer ``o`` (see ``orc_export_row``); times in ticks."""
+        N, K = self.n, self.k
+        a = {
+            "pos": np.empty(N, np.int32), "hb": np.empty(N, np.uint32), "mv": np.empty(N, np.uint32),
+            "gc": np.empty(N, np.uint32), "kv_version": np.empty((N, K), np.uint32),
+            "kv_status": np.empty((N, K), np.int32), "kv_value_id": np.empty((N, K), np.uint32),
+            "kv_ts": np.empty((N, K), np.int64), "fd_last": np.empty(N, np.int64), "fd_len": np.empty(N, np.int32),
+            "fd_sum": np.empty(N, np.float64), "live": np.empty(N, np.int32), "tod": np.empty(N, np.int64),
+        }
+        order = ["pos", "hb", "mv", "gc", "kv_version", "kv_status", "kv_value_id", "kv_ts", "fd_last", "fd_len",
+                 "fd_sum", "live", "tod"]
+        self.L.orc_export_row(self.h, o, *[a[n].ctypes.data_as(C.c_void_p) for n in order])
+        for n in ("kv_ts", "fd_last", "tod"):
+            m = a[n] >= 0
+            a[n][m] //= TICK_US
+        return a

@@ -1,0 +1,58 @@
+"""The C-ABI library builds for gfx950, loads, and exports every symbol the header declares (CPU).
+
+No compute call is made here: the container has no GPU.
+"""
+
+import ctypes
+import os
+import re
+
+import pytest
+
+from aiocluster_amd import _lib
+
+
+def header_functions():
+    src = open(_lib.HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|void|const char \*)\s*(gs_\w+)\s*\(", src, re.M)))
+
+
+def test_header_declares_what_the_binding_binds():
+    assert header_functions() == sorted(_lib.EXPORTS)
+
+
+def test_library_loads_and_exports_every_symbol():
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("library not built (run __graft_entry__.build())")
+    L = ctypes.CDLL(_lib.LIB_PATH)
+    for name in header_functions():
+        assert hasattr(L, name), name
+    lib = _lib.load()
+    assert lib.gs_api_version() == 1
+
+
+def test_create_validates_config_without_gpu():
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("library not built")
+    from aiocluster_amd.scenario import DEFAULT_CFG
+    from aiocluster_amd.sim import make_config
+
+    lib = _lib.load()
+    h = ctypes.c_void_p()
+    good = make_config(1000, 16, DEFAULT_CFG, 0, 32)
+    assert lib.gs_create(ctypes.byref(good), ctypes.byref(h)) == 0
+    nb = ctypes.c_uint64()
+    assert lib.gs_region_bytes(h, _lib.REGION["HB"], ctypes.byref(nb)) == 0
+    assert nb.value == 1000 * 1024 * 4
+    assert lib.gs_region_bytes(h, _lib.REGION["POS"], ctypes.byref(nb)) == 0 and nb.value == 1000 * 1024 * 4
+    lib.gs_destroy(h)
+    bad = make_config(1000, 65, DEFAULT_CFG, 0, 32)  # K > 64
+    assert lib.gs_create(ctypes.byref(bad), ctypes.byref(h)) == -1
+
+
+def test_sched_delay_rounding():
+    from aiocluster_amd.sim import sched_delay_ticks
+
+    assert sched_delay_ticks(86400.0) == 43200 * 64
+    assert sched_delay_ticks(1 / 64) == 1  # 7812.5 us rounds half-even to 7812 -> 1 tick
+    assert sched_delay_ticks(30.0) == 15 * 64

@@ -1,0 +1,112 @@
+"""Parity of the HIP path (through the C ABI) with the reference and the C oracle.  GPU only.
+
+* golden: the device reproduces the REAL reference's canonical state after every
+  round of every golden fixture (byte-identical JSON, phi computed on the device);
+* oracle: larger seeded scenarios (cold/general and warm/canonical layouts, MTU
+  truncation, deletes + TTL + tombstone GC, churn, ring and compact windows) are
+  compared array by array with the C oracle after every round.
+Integer state must be bit-exact; phi is binary64 and is compared exactly too
+(the north-star tolerance is 1e-9 relative; the tick model makes it exact).
+"""
+
+import numpy as np
+import pytest
+from helpers import SCENARIOS, compare_exports, load_scenario, make_backend, replay_and_compare
+from oracle import OracleSim
+
+from aiocluster_amd._lib import GsError
+from aiocluster_amd.scenario import make_scenario, replay, replay_round
+from aiocluster_amd.sim import GossipSim
+from aiocluster_amd.workload import WorkloadSpec
+
+pytestmark = pytest.mark.gpu
+
+PHI_RTOL = 1e-9  # north_star tolerance for phi
+
+
+@pytest.mark.parametrize("name", [s for s in SCENARIOS if s != "fdgc12"])
+def test_gpu_matches_reference_golden(name):
+    scen = load_scenario(name)
+    exp = scen["expect"]
+    sim = make_backend(GossipSim, scen)
+    res = replay_and_compare(sim, scen, exp["states"], exp["hashes"])
+    assert res is None, f"{name}: first mismatch at round {res[0]}: {res[1]}"
+    sim.check()
+
+
+def test_fd_garbage_collection_fails_loudly():
+    """FailureDetector.garbage_collect + remove_node are not on the device yet: must raise, never diverge silently."""
+    scen = load_scenario("fdgc12")
+    sim = make_backend(GossipSim, scen)
+    with pytest.raises(GsError, match="garbage_collect"):
+        replay(sim, scen, on_round=lambda r: sim.check())
+
+
+def lockstep_vs_oracle(scen, every=1, **kw):
+    gpu = make_backend(GossipSim, scen, **kw)
+    orc = make_backend(OracleSim, scen)
+    for r in range(len(scen["rounds"])):
+        replay_round(gpu, scen, r)
+        replay_round(orc, scen, r)
+        if r % every == 0 or r == len(scen["rounds"]) - 1:
+            diff = compare_exports(gpu.export(), orc.export())
+            assert diff is None, f"round {r}: {diff}"
+            c = gpu.check()
+    return gpu, orc, c
+
+
+def test_cold_general_layout_vs_oracle():
+    spec = WorkloadSpec(n=200, k=8, fanout=3, seed=11, init="cold", write_frac=0.2, delete_frac=0.15,
+                        ttl_frac=0.1, down_frac=0.1, down_rounds=3)
+    cfg = {"mtu": 700, "tombstone_grace_s": 2, "window": 6, "max_interval_s": 2.0, "initial_interval_s": 1.0,
+           "phi_threshold": 3.0}
+    scen = make_scenario("cold200", spec, 14, cfg)
+    gpu, orc, c = lockstep_vs_oracle(scen)
+    s = orc.stats()
+    assert c["exchanges"] == s["exchanges"] and c["node_deltas"] == s["node_deltas"]
+    assert c["kvs_sent"] == s["kvs_sent"] and c["truncated"] == s["truncated"] > 0
+    assert c["delta_bytes"] == s["delta_bytes"] and c["hb_reports"] == s["hb_reports"]
+
+
+def test_warm_canonical_compact_fd_vs_oracle():
+    spec = WorkloadSpec(n=512, k=16, fanout=3, seed=12, init="warm", write_frac=0.05, down_frac=0.05,
+                        down_rounds=3)
+    scen = make_scenario("warm512", spec, 10, {"mtu": 2500})
+    gpu, orc, c = lockstep_vs_oracle(scen, tombstones=False, fd_ring=False)
+    s = orc.stats()
+    assert c["node_deltas"] == s["node_deltas"] and c["truncated"] == s["truncated"]
+    assert c["delta_bytes"] == s["delta_bytes"]
+
+
+def test_phi_matches_oracle_within_tolerance():
+    spec = WorkloadSpec(n=64, k=4, fanout=2, seed=13, init="warm", write_frac=0.1, down_frac=0.2, down_rounds=4)
+    scen = make_scenario("phi64", spec, 12, {"initial_interval_s": 1.0, "phi_threshold": 3.0})
+    gpu = make_backend(GossipSim, scen)
+    orc = make_backend(OracleSim, scen)
+    replay(gpu, scen)
+    replay(orc, scen)
+    t = gpu.last_tick
+    import ctypes
+
+    got = np.stack([gpu.phi_row(o, t) for o in range(64)])
+    want = np.full((64, 64), np.nan)
+    phi = ctypes.c_double()
+    for o in range(64):
+        for j in range(64):
+            if orc.L.orc_fd_phi(orc.h, o, j, t * 15625, ctypes.byref(phi)):
+                want[o, j] = phi.value
+    assert np.array_equal(np.isnan(got), np.isnan(want))
+    m = ~np.isnan(want)
+    assert m.sum() > 0
+    np.testing.assert_allclose(got[m], want[m], rtol=PHI_RTOL, atol=0)
+
+
+def test_config2_cold_1024x64_converges_bit_exact():
+    """BASELINE config 2: 1,024 nodes x 64 keys, fanout 3, cold start, run to version convergence."""
+    spec = WorkloadSpec(n=1024, k=64, fanout=3, seed=2, init="cold", write_frac=0.0)
+    scen = make_scenario("config2", spec, 24, {})
+    gpu, orc, c = lockstep_vs_oracle(scen, every=6, tombstones=False, fd_ring=False)
+    ex = gpu.export()
+    owner_mv = np.diag(ex["mv"])
+    assert np.all(ex["mv"] <= owner_mv[None, :])
+    assert np.all(ex["mv"] == owner_mv[None, :]), "version matrix did not converge"
