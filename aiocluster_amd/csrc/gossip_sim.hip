@@ -747,7 +747,8 @@ __global__ __launch_bounds__(LB) void k_warm(Dev d, uint32_t chunks) {
     d.hb[p] = d.hb[q];
     d.mv[p] = d.mv[q];
     d.gc[p] = d.gc[q];
-    for (uint32_t k = 0; k < d.KP; k++) d.held[p * d.KP + k] = d.held[q * d.KP + k];
+    for (uint32_t k = 0; k < d.KP; k += 4)
+        *reinterpret_cast<uint32_t *>(d.held + p * d.KP + k) = *reinterpret_cast<const uint32_t *>(d.held + q * d.KP + k);
     if (d.flags & GS_TOMBSTONES) {
         bool tb = false;
         for (uint32_t k = 0; k < d.KP; k++) {

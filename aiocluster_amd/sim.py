@@ -85,7 +85,7 @@ class GossipSim:
     def __init__(self, node_ids: list[NodeId], keys: list[str], cfg: dict, init: str = "cold",
                  initial_values: dict[int, list[tuple[int, str]]] | None = None, *, device: str = "cuda:0",
                  tombstones: bool = True, fd_ring: bool | None = None, hist_cap: int = 64,
-                 nid_sizes: list[int] | None = None):
+                 nid_sizes: list[int] | None = None, initial_ops: list[np.ndarray] | None = None):
         import torch
 
         if not torch.cuda.is_available():
@@ -150,6 +150,8 @@ class GossipSim:
                 for kk, v in initial_values.get(j, []):
                     self.write(0, j, kk, 0, v)
             self._flush()
+        for batch in initial_ops or []:  # pre-interned boot writes (owner, key, op, value_id, value_len)
+            self.owner_writes(batch, 0)
         if init == "warm":
             self._chk(self.L.gs_warm(h), "gs_warm")
 

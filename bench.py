@@ -1,0 +1,306 @@
+"""Headline benchmark: simulated gossip exchanges/s at 65,536 nodes (BASELINE.json configs[2]).
+
+Workload (synthetic, seeded; see aiocluster_amd/workload.py): 65,536 nodes x 16 keys,
+fanout 3, warm start (every node knows every node, index order), every round 5% of
+the nodes write one key and 5% churn up/down (down nodes neither initiate nor
+answer), phi window 1000, mtu 65,507.  One step = one gossip round: owner writes,
+heartbeat + tombstone GC, 9 conflict-free exchange phases, liveness sweep.  All
+inputs (schedules, write batches, up masks) are uploaded to HBM before timing.
+
+Multi-GPU: ``--gpus N`` under torch.distributed runs one 65,536-node simulation per
+GPU (independent replicas, seed + rank; observer-row sharding across GPUs is not
+built yet -- DESIGN.md).  ``value`` is the exchanges of all ranks / max rank time.
+
+Prints ONE JSON line (rank 0) with the roofline of the dominant kernel (k_exchange,
+HIP-event timed on the library's stream) and the CPU baseline (the C oracle on one
+host core, timed on a bounded sample of exchanges whose rows are copied from the
+device state).
+"""
+
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def log(*a):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def digits(x: np.ndarray) -> np.ndarray:
+    return np.floor(np.log10(np.maximum(x, 1))).astype(np.int64) + 1
+
+
+def prepare(sim, spec, rounds, torch, dev):
+    """Precompute every round's device inputs (host schedule generation is not timed)."""
+    from aiocluster_amd.workload import Workload, liveness_tick, phase_tick, round_tick
+
+    wl = Workload(spec)
+    out = []
+    vid = 1 << 24
+    for _ in range(rounds):
+        p = wl.next_round(materialize_values=False)
+        w = p.writes
+        ops = np.zeros((len(w), 5), dtype=np.int64)
+        if len(w):
+            # value "v{j}.{k}.{r}" (workload.write_value): byte length without materialising strings
+            ops[:, 0], ops[:, 1], ops[:, 2] = w[:, 0], w[:, 1], w[:, 2]
+            ops[:, 3] = vid + np.arange(len(w))
+            vid += len(w)
+            ops[:, 4] = 3 + digits(w[:, 0]) + digits(w[:, 1]) + digits(np.full(len(w), p.r))
+        r = p.r
+        out.append({
+            "r": r,
+            "t": round_tick(r),
+            "ops": torch.from_numpy(ops.astype(np.int32)).to(dev),
+            "nops": len(w),
+            "up": torch.from_numpy(p.up.astype(np.uint8)).to(dev),
+            "phases": [(torch.from_numpy(a).to(dev), torch.from_numpy(b).to(dev), len(a), phase_tick(r, i))
+                       for i, (a, b) in enumerate(p.phases)],
+            "t_live": liveness_tick(r, len(p.phases)),
+            "exchanges": p.n_exchanges,
+        })
+    return out
+
+
+def run_round(sim, rd, events=None):
+    L, h = sim.L, sim.h
+    if rd["nops"]:
+        sim._chk(L.gs_owner_writes(h, C.c_void_p(rd["ops"].data_ptr()), rd["nops"], rd["t"]), "gs_owner_writes")
+    sim._chk(L.gs_begin_round(h, C.c_void_p(rd["up"].data_ptr()), rd["t"]), "gs_begin_round")
+    for a, b, n, t in rd["phases"]:
+        if not n:
+            continue
+        if events is not None:
+            e0 = sim.torch.cuda.Event(enable_timing=True)
+            e1 = sim.torch.cuda.Event(enable_timing=True)
+            e0.record(sim.stream)
+        sim._chk(L.gs_run_phase(h, C.c_void_p(a.data_ptr()), C.c_void_p(b.data_ptr()), n, t), "gs_run_phase")
+        if events is not None:
+            e1.record(sim.stream)
+            events.append((e0, e1))
+    sim._chk(L.gs_liveness(h, C.c_void_p(rd["up"].data_ptr()), rd["t_live"]), "gs_liveness")
+
+
+def cpu_baseline(sim, spec, cfg, next_plan, sample: int):
+    """The C oracle (one host core) on `sample` exchanges whose two rows are copied from the device."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle as orc_mod  # test infrastructure: the checker, timed here as the CPU baseline
+
+    torch = sim.torch
+    n, K, NP, KP, Cc = sim.n, sim.k, sim.np_, sim.kp, sim.hist_cap
+    L = orc_mod.lib()
+    from aiocluster_amd.workload import synthetic_node_ids
+    from aiocluster_amd.pbsize import nodeid_size
+
+    ids = synthetic_node_ids(n)
+    ns = (C.c_int32 * n)(*[nodeid_size(x.name, x.generation_id, x.gossip_advertise_addr[0],
+                                       x.gossip_advertise_addr[1], x.tls_name) for x in ids])
+    kl = (C.c_int32 * K)(*[6] * K)
+    oc = orc_mod._Cfg(n, K, int(cfg["mtu"]), orc_mod.us(cfg["tombstone_grace_s"]), float(cfg["phi_threshold"]),
+                      int(cfg["window"]), orc_mod.us(cfg["max_interval_s"]), orc_mod.us(cfg["initial_interval_s"]),
+                      orc_mod.us(cfg["dead_grace_s"]))
+    h = L.orc_create(C.byref(oc), ns, kl)
+    hist_ver = sim.region("HIST_VER", torch.int32, (n, Cc, K)).cpu().numpy().view(np.uint32).copy()
+    hist_vid = sim.region("HIST_VID", torch.int32, (n, Cc, K)).cpu().numpy().view(np.uint32).copy()
+    meta = sim.region("HIST_META", torch.int32, (n, Cc, K)).cpu().numpy().view(np.uint32)
+    hist_vlen = (meta >> 18).astype(np.int32)
+    hist_st = ((meta >> 16) & 3).astype(np.uint8)
+    # disjoint pairs from the first phase of the next round
+    a_all, b_all, _, t = next_plan["phases"][0]
+    a_all, b_all = a_all.cpu().numpy(), b_all.cpu().numpy()
+    pairs = list(zip(a_all[:sample].tolist(), b_all[:sample].tolist()))
+    order = np.arange(n, dtype=np.int32)
+
+    def rows(name, dt, shape):
+        return sim.region(name, dt, shape)
+
+    hb, mv, gc = (rows(x, torch.int32, (n, NP)) for x in ("HB", "MV", "GC"))
+    fl, fs, fc, fst = (rows(x, torch.int32, (n, NP)) for x in ("FD_LAST", "FD_SUM", "FD_CNT", "FD_STATE"))
+    held = rows("HELD", torch.uint8, (n, NP, KP))
+    P = C.c_void_p
+    for a, b in pairs:
+        for o in (a, b):
+            def g(x):
+                return np.ascontiguousarray(x[o, :n].cpu().numpy().view(np.uint32))
+            hw = np.ascontiguousarray(held[o, :n, :K].cpu().numpy())
+            L.orc_load_row(h, o, n, order.ctypes.data_as(P), g(hb).ctypes.data_as(P), g(mv).ctypes.data_as(P),
+                           g(gc).ctypes.data_as(P), hw.ctypes.data_as(P), Cc, hist_ver.ctypes.data_as(P),
+                           hist_vid.ctypes.data_as(P), hist_vlen.ctypes.data_as(P), hist_st.ctypes.data_as(P),
+                           g(fl).ctypes.data_as(P), g(fs).ctypes.data_as(P), g(fc).ctypes.data_as(P),
+                           g(fst).ctypes.data_as(P), 15625)
+    t0 = time.perf_counter()
+    for a, b in pairs:
+        L.orc_exchange(h, a, b, t * 15625)
+    dt = time.perf_counter() - t0
+    st = orc_mod._Stats()
+    L.orc_get_stats(h, C.byref(st))
+    L.orc_destroy(h)
+    return {
+        "value": len(pairs) / dt,
+        "unit": "exchanges/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"{len(pairs)} exchanges (disjoint pairs of the next round's first phase) at N={n}, K={K}, "
+                  f"oracle rows copied from the device state after the timed rounds; {dt:.2f} s of CPU work; "
+                  f"{st.node_deltas} NodeDeltas",
+    }
+
+
+def load_traffic(workload: str):
+    """Per-launch HBM bytes of k_exchange from a committed rocprofv3 PMC summary, if present."""
+    path = os.path.join(REPO, "profiles", "pmc_summary.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        d = json.load(open(path))
+        e = d.get(workload)
+        return None if e is None else e.get("k_exchange_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--nodes", type=int, default=65536)
+    ap.add_argument("--keys", type=int, default=16)
+    ap.add_argument("--fanout", type=int, default=3)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--cpu-sample", type=int, default=64)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from aiocluster_amd.scenario import DEFAULT_CFG
+    from aiocluster_amd.sim import GossipSim
+    from aiocluster_amd.workload import WorkloadSpec, key_names, synthetic_node_ids
+
+    n, K = args.nodes, args.keys
+    cfg = dict(DEFAULT_CFG)  # mtu 65507, window 1000, phi 8, max_interval 10 s, prior 5 s
+    spec = WorkloadSpec(n=n, k=K, fanout=args.fanout, seed=args.seed + rank, init="warm", write_frac=0.05,
+                        down_frac=0.05, down_rounds=3)
+    workload = f"N={n} K={K} F={args.fanout} warm, 5% writes + 5% down churn/round, window 1000, mtu 65507"
+    t_setup = time.perf_counter()
+    ids = synthetic_node_ids(n)
+    boot = []  # Cluster(initial_key_values): key k of owner j = "v{j}.{k}.i", as K batches of distinct owners
+    for k in range(K):
+        ops = np.zeros((n, 5), dtype=np.uint32)
+        ops[:, 0] = np.arange(n)
+        ops[:, 1] = k
+        ops[:, 3] = 1 + k * n + np.arange(n)
+        ops[:, 4] = 3 + digits(np.arange(n)) + digits(np.full(n, k)) + 1
+        boot.append(ops)
+    sim = GossipSim(ids, key_names(K), cfg, init="warm", device=str(dev), tombstones=False, fd_ring=False,
+                    hist_cap=16, initial_ops=boot)
+    plans = prepare(sim, spec, args.warmup + args.steps + 1, torch, dev)
+    torch.cuda.synchronize(dev)
+    log(f"setup {time.perf_counter() - t_setup:.1f}s")
+
+    for r in range(args.warmup):
+        run_round(sim, plans[r])
+    torch.cuda.synchronize(dev)
+    sim.check()
+    sim.reset_counters()
+    events = []
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for r in range(args.warmup, args.warmup + args.steps):
+        run_round(sim, plans[r], events)
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    c = sim.check()
+    exch = sum(plans[r]["exchanges"] for r in range(args.warmup, args.warmup + args.steps))
+    assert c["exchanges"] == exch, (c["exchanges"], exch)
+    kern_ms = sum(e0.elapsed_time(e1) for e0, e1 in events)
+    launches = len(events)
+    tot = torch.tensor([exch, elapsed], dtype=torch.float64, device=dev)
+    if dist is not None:
+        ex_all = tot[:1].clone()
+        dist.all_reduce(ex_all, op=dist.ReduceOp.SUM)
+        t_max = tot[1:].clone()
+        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+        exch_total, elapsed_max = float(ex_all.item()), float(t_max.item())
+    else:
+        exch_total, elapsed_max = float(exch), elapsed
+    achieved = c["alg_bytes"] / (kern_ms / 1e3) / 1e9 if kern_ms > 0 else 0.0
+    traffic = load_traffic(workload)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(sim, spec, cfg, plans[args.warmup + args.steps], args.cpu_sample)
+    if rank == 0:
+        line = {
+            "metric": "simulated gossip exchanges/sec at 65,536 nodes, 1-8 GPUs; % HBM peak",
+            "value": exch_total / elapsed_max,
+            "unit": "exchanges/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed_max / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic (seeded workload generator; no dataset)",
+            "config": {
+                "workload": workload,
+                "nodes": n,
+                "keys": K,
+                "fanout": args.fanout,
+                "exchanges_per_step": exch / args.steps,
+                "parallelism": f"replicas x{world}" if world > 1 else "1 GPU",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "k_exchange",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBPS,
+                "traffic": traffic,
+                "alg_bytes_per_launch": c["alg_bytes"] / max(1, launches),
+                "avg_launch_ms": kern_ms / max(1, launches),
+                "launches": launches,
+                "kernel_share_of_step": kern_ms / 1e3 / elapsed,
+            },
+            "cpu_baseline": cpu,
+            "counters": {k: v for k, v in c.items() if not k.startswith("err_")},
+        }
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -285,6 +285,7 @@ void orc_write(orc *o, int32_t owner, int32_t key, int32_t op, uint32_t value_id
 static void win_append(owin *w, int32_t cap, double x) { /* BoundedArrayStats.append (139-150) */
     if (w->idx >= w->cap_alloc) {
         int32_t nc = w->cap_alloc ? w->cap_alloc * 2 : 8;
+        while (nc <= w->idx) nc *= 2;
         if (nc > cap) nc = cap;
         w->vals = realloc(w->vals, sizeof(double) * nc);
         if (!w->vals) abort();
@@ -663,7 +664,6 @@ void orc_load_row(orc *o, int32_t obs, int32_t cnt, const int32_t *order,
     oobs *b = row(o, obs);
     const int32_t N = o->N, K = o->K;
     for (int32_t j = 0; j < N; j++) { b->pos[j] = -1; b->dead_pos[j] = -1; b->live[j] = 0; }
-    b->cnt = 0;
     b->ndead = 0;
     for (int32_t q = 0; q < cnt; q++) {
         int32_t j = order[q];
@@ -687,7 +687,7 @@ void orc_load_row(orc *o, int32_t obs, int32_t cnt, const int32_t *order,
         win->has_last = win->has;
         win->last = (int64_t)fd_last_tick[j] * tick_us;
         win->sum = (double)fd_sum_tick[j] * ((double)tick_us / 1e6);
-        win->idx = (int32_t)fd_len[j];
+        win->idx = win->has ? (int32_t)fd_len[j] : 0;
         win->filled = 0;
         uint32_t s = fd_state[j];
         if (s == 1) b->live[j] = 1;
