@@ -31,6 +31,7 @@
 
 #include <cstdarg>
 #include <cstdio>
+#include <algorithm>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -732,31 +733,34 @@ __global__ __launch_bounds__(LB) void k_boot_self(Dev d) {
     }
 }
 
-__global__ __launch_bounds__(LB) void k_warm(Dev d, uint32_t chunks) {
-    const uint32_t o = blockIdx.x / chunks;
-    const uint32_t j = (blockIdx.x % chunks) * LB + threadIdx.x;
-    if (j >= d.N) return;
-    const size_t p = pix(d, o, j);
-    if (!(d.flags & GS_CANONICAL)) {
-        d.pos[p] = j;
-        d.ord[p] = j;
-        if (j == 0) d.row[o * 4 + 0] = d.N;
-    }
-    if (j == o) return;
-    const size_t q = pix(d, j, j);
-    d.hb[p] = d.hb[q];
-    d.mv[p] = d.mv[q];
-    d.gc[p] = d.gc[q];
-    for (uint32_t k = 0; k < d.KP; k += 4)
-        *reinterpret_cast<uint32_t *>(d.held + p * d.KP + k) = *reinterpret_cast<const uint32_t *>(d.held + q * d.KP + k);
-    if (d.flags & GS_TOMBSTONES) {
-        bool tb = false;
-        for (uint32_t k = 0; k < d.KP; k++) {
-            const uint32_t v = d.ts[q * d.KP + k];
-            d.ts[p * d.KP + k] = v;
-            tb |= v != NONE;
+__global__ __launch_bounds__(LB) void k_warm(Dev d) {
+    // grid-stride over (observer, owner) pairs: N^2 exceeds one launch's 2^32 work-items at N = 65,536
+    const uint64_t total = (uint64_t)d.N * d.N;
+    for (uint64_t x = (uint64_t)blockIdx.x * LB + threadIdx.x; x < total; x += (uint64_t)gridDim.x * LB) {
+        const uint32_t o = (uint32_t)(x / d.N), j = (uint32_t)(x % d.N);
+        const size_t p = pix(d, o, j);
+        if (!(d.flags & GS_CANONICAL)) {
+            d.pos[p] = j;
+            d.ord[p] = j;
+            if (j == 0) d.row[o * 4 + 0] = d.N;
         }
-        if (tb) d.row[o * 4 + 1] = 1u;
+        if (j == o) continue;
+        const size_t q = pix(d, j, j);
+        d.hb[p] = d.hb[q];
+        d.mv[p] = d.mv[q];
+        d.gc[p] = d.gc[q];
+        for (uint32_t k = 0; k < d.KP; k += 4)
+            *reinterpret_cast<uint32_t *>(d.held + p * d.KP + k) =
+                *reinterpret_cast<const uint32_t *>(d.held + q * d.KP + k);
+        if (d.flags & GS_TOMBSTONES) {
+            bool tb = false;
+            for (uint32_t k = 0; k < d.KP; k++) {
+                const uint32_t v = d.ts[q * d.KP + k];
+                d.ts[p * d.KP + k] = v;
+                tb |= v != NONE;
+            }
+            if (tb) d.row[o * 4 + 1] = 1u;
+        }
     }
 }
 
@@ -953,8 +957,9 @@ int gs_boot(gs_handle *h, const uint16_t *nid_size, const uint8_t *key_len) {
 
 int gs_warm(gs_handle *h) {
     if (!h || !h->booted) return GS_E_INVALID;
-    const uint32_t chunks = (h->N + LB - 1) / LB;
-    k_warm<<<chunks * h->N, LB, 0, h->stream>>>(h->d, chunks);
+    const uint64_t pairs = (uint64_t)h->N * h->N;
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>((pairs + LB - 1) / LB, 1u << 20);
+    k_warm<<<blocks, LB, 0, h->stream>>>(h->d);
     HIPCHK(h, hipGetLastError());
     return GS_OK;
 }

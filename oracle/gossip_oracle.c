@@ -593,12 +593,14 @@ void orc_node_order(const orc *o, int32_t i, int32_t *out) {
 }
 
 void orc_view(const orc *o, int32_t i, int32_t j, uint32_t out[3]) {
+    if (!o->obs[i].alloc) { out[0] = out[1] = out[2] = 0; return; }
     const oview *v = &o->obs[i].v[j];
     out[0] = v->hb; out[1] = v->mv; out[2] = v->gc;
 }
 
 void orc_view_kvs(const orc *o, int32_t i, int32_t j, int32_t *present, uint32_t *version, int32_t *status,
                   uint32_t *value_id, int64_t *ts) {
+    if (!o->obs[i].alloc) { memset(present, 0, sizeof(int32_t) * o->K); return; }
     const okv *kv = &o->obs[i].kv[(size_t)j * o->K];
     for (int32_t k = 0; k < o->K; k++) {
         present[k] = kv[k].present; version[k] = kv[k].version; status[k] = kv[k].status;
@@ -607,6 +609,7 @@ void orc_view_kvs(const orc *o, int32_t i, int32_t j, int32_t *present, uint32_t
 }
 
 int32_t orc_fd_window(const orc *o, int32_t i, int32_t j, int64_t *last, int32_t *len, double *sum) {
+    if (!o->obs[i].alloc) return 0;
     const owin *w = &o->obs[i].w[j];
     if (!w->has) return 0;
     *last = w->has_last ? w->last : -1;
@@ -616,12 +619,14 @@ int32_t orc_fd_window(const orc *o, int32_t i, int32_t j, int64_t *last, int32_t
 }
 
 int32_t orc_fd_phi(const orc *o, int32_t i, int32_t j, int64_t now, double *phi) {
+    if (!o->obs[i].alloc) return 0;
     return win_phi(o, &o->obs[i].w[j], now, phi);
 }
 
-int32_t orc_fd_live(const orc *o, int32_t i, int32_t j) { return o->obs[i].live[j]; }
+int32_t orc_fd_live(const orc *o, int32_t i, int32_t j) { return o->obs[i].alloc ? o->obs[i].live[j] : 0; }
 
 int64_t orc_fd_dead_since(const orc *o, int32_t i, int32_t j) {
+    if (!o->obs[i].alloc) return -1;
     return o->obs[i].dead_pos[j] >= 0 ? o->obs[i].tod[j] : -1;
 }
 
@@ -699,3 +704,120 @@ void orc_load_row(orc *o, int32_t obs, int32_t cnt, const int32_t *order,
     }
     b->cnt = cnt;
 }
+
+/* ------------------------------------------- method-level hooks (KAT ports) */
+void orc_kat_set_view(orc *o, int32_t obs, int32_t owner, uint32_t hb, uint32_t mv, uint32_t gc) {
+    oobs *b = row(o, obs);
+    insert_node(o, b, owner);
+    b->v[owner].hb = hb; b->v[owner].mv = mv; b->v[owner].gc = gc;
+}
+
+void orc_kat_set_kv(orc *o, int32_t obs, int32_t owner, int32_t key, uint32_t value_id, int32_t value_len,
+                    uint32_t version, int32_t status, int64_t ts) {
+    oobs *b = row(o, obs);
+    insert_node(o, b, owner);
+    okv *e = &kvp(o, b, owner)[key];
+    e->present = 1; e->value_id = value_id; e->value_len = value_len; e->version = version;
+    e->status = (uint8_t)status; e->ts = ts;
+}
+
+int32_t orc_kat_apply_heartbeat(orc *o, int32_t obs, int32_t owner, uint32_t h) {
+    oobs *b = row(o, obs);
+    insert_node(o, b, owner);
+    oview *v = &b->v[owner];
+    if (v->hb == 0) { v->hb = h; return 0; }
+    if (h > v->hb) { v->hb = h; return 1; }
+    return 0;
+}
+
+void orc_kat_apply_nodedelta(orc *o, int32_t obs, int32_t owner, uint32_t from, uint32_t gc, uint32_t mv,
+                             int32_t nkv, const int32_t *keys, const uint32_t *vids, const int32_t *vlens,
+                             const uint32_t *versions, const int32_t *statuses, int64_t now) {
+    odelta dl;
+    memset(&dl, 0, sizeof dl);
+    ond nd = {owner, from, gc, mv, 0, nkv};
+    okvu *kv = xcalloc(nkv ? nkv : 1, sizeof(okvu));
+    for (int32_t x = 0; x < nkv; x++) {
+        kv[x].key = keys[x]; kv[x].value_id = vids[x]; kv[x].value_len = vlens[x];
+        kv[x].version = versions[x]; kv[x].status = statuses[x];
+    }
+    dl.nd = &nd; dl.nnd = 1; dl.kv = kv; dl.nkv = nkv;
+    apply_delta(o, obs, &dl, now);
+    free(kv);
+}
+
+void orc_kat_gc(orc *o, int32_t obs, int32_t owner, int64_t grace_us, int64_t now) {
+    int64_t saved = o->c.tombstone_grace_us;
+    o->c.tombstone_grace_us = grace_us;
+    gc_view(o, row(o, obs), owner, now);
+    o->c.tombstone_grace_us = saved;
+}
+
+int32_t orc_kat_compute_delta(orc *o, int32_t sender, int32_t n_digest, const int32_t *dg_node,
+                              const uint32_t *dg_gc, const uint32_t *dg_mv, int32_t mtu,
+                              int32_t *nd_node, uint32_t *nd_from, int32_t *nd_nkv, uint32_t *kv_versions,
+                              int32_t max_out) {
+    odigest *d = &o->dg[0];
+    memset(d->has, 0, o->N);
+    d->n = 0;
+    for (int32_t q = 0; q < n_digest; q++) {
+        int32_t j = dg_node[q];
+        d->has[j] = 1; d->gc[j] = dg_gc[q]; d->mv[j] = dg_mv[q]; d->hb[j] = 0;
+        d->list[d->n++] = j;
+    }
+    memset(o->sched[1], 0, o->N);
+    int32_t saved = o->c.mtu;
+    o->c.mtu = mtu;
+    compute_delta(o, sender, d, o->sched[1], &o->dl[0]);
+    o->c.mtu = saved;
+    const odelta *dl = &o->dl[0];
+    int32_t nk = 0;
+    for (int32_t q = 0; q < dl->nnd && q < max_out; q++) {
+        nd_node[q] = dl->nd[q].node; nd_from[q] = dl->nd[q].from; nd_nkv[q] = dl->nd[q].nkv;
+        for (int32_t x = 0; x < dl->nd[q].nkv && nk < max_out; x++) kv_versions[nk++] = dl->kv[dl->nd[q].kv0 + x].version;
+    }
+    return dl->nnd;
+}
+
+void orc_kat_fd_report(orc *o, int32_t obs, int32_t target, int64_t now) { fd_report(o, row(o, obs), target, now); }
+
+void orc_kat_fd_update(orc *o, int32_t obs, int32_t target, int64_t now) { fd_update(o, row(o, obs), target, now); }
+
+void orc_kat_fd_reset(orc *o, int32_t obs, int32_t target) {
+    owin *w = &row(o, obs)->w[target];
+    w->sum = 0.0; w->idx = 0; w->filled = 0;
+}
+
+int32_t orc_kat_fd_gc(orc *o, int32_t obs, int64_t now, int32_t *out) {
+    oobs *b = row(o, obs);
+    int32_t nres = 0;
+    for (int32_t q = 0; q < b->ndead; q++) {
+        int32_t j = b->dead_order[q];
+        if (now >= b->tod[j] + o->c.dead_grace_us) out[nres++] = j;
+    }
+    for (int32_t r = 0; r < nres; r++) {
+        int32_t j = out[r];
+        dead_pop(b, j);
+        if (!b->w[j].has) return -1 - r;                              /* KeyError (Q9) */
+        b->w[j].has = 0; b->w[j].has_last = 0; b->w[j].sum = 0.0; b->w[j].idx = 0; b->w[j].filled = 0;
+    }
+    return nres;
+}
+
+int32_t orc_kat_fd_scheduled(orc *o, int32_t obs, int64_t now, int32_t *out) {
+    oobs *b = row(o, obs);
+    fd_scheduled(o, b, now, o->sched[0]);
+    int32_t n = 0;
+    for (int32_t q = 0; q < b->ndead; q++)
+        if (o->sched[0][b->dead_order[q]]) out[n++] = b->dead_order[q];
+    return n;
+}
+
+void orc_kat_win_append(orc *o, int32_t obs, int32_t target, double x) {
+    owin *w = &row(o, obs)->w[target];
+    w->has = 1;
+    win_append(w, o->c.window, x);
+}
+double orc_kat_win_sum(orc *o, int32_t obs, int32_t target) { return row(o, obs)->w[target].sum; }
+int32_t orc_kat_win_len(orc *o, int32_t obs, int32_t target) { return win_len(&row(o, obs)->w[target], o->c.window); }
+int32_t orc_kat_win_filled(orc *o, int32_t obs, int32_t target) { return row(o, obs)->w[target].filled; }

@@ -105,6 +105,43 @@ void orc_load_row(orc *o, int32_t obs, int32_t cnt, const int32_t *order,
                   const uint32_t *fd_last_tick, const uint32_t *fd_sum_tick, const uint32_t *fd_len,
                   const uint32_t *fd_state, int64_t tick_us);
 
+/* ------------------------------------------- method-level hooks (KAT ports)
+ * Direct access to single NodeState / ClusterState / FailureDetector methods so the
+ * reference's own unit tests (tests/test_state.py, test_node_state.py,
+ * test_failure_detector.py) can be replayed against the oracle. */
+void    orc_kat_set_view(orc *o, int32_t obs, int32_t owner, uint32_t hb, uint32_t mv, uint32_t gc);
+void    orc_kat_set_kv(orc *o, int32_t obs, int32_t owner, int32_t key, uint32_t value_id, int32_t value_len,
+                       uint32_t version, int32_t status, int64_t ts_us);
+/* NodeState.apply_heartbeat (state.py:280-287) */
+int32_t orc_kat_apply_heartbeat(orc *o, int32_t obs, int32_t owner, uint32_t value);
+/* NodeState.apply_delta (state.py:190-233) of one NodeDelta (kvs in the given order) */
+void    orc_kat_apply_nodedelta(orc *o, int32_t obs, int32_t owner, uint32_t from, uint32_t gc, uint32_t mv,
+                                int32_t nkv, const int32_t *keys, const uint32_t *value_ids,
+                                const int32_t *value_lens, const uint32_t *versions, const int32_t *statuses,
+                                int64_t now_us);
+/* NodeState.gc_marked_for_deletion (state.py:253-274) with an explicit grace */
+void    orc_kat_gc(orc *o, int32_t obs, int32_t owner, int64_t grace_us, int64_t now_us);
+/* compute_partial_delta_respecting_mtu (state.py:340-415) of `sender` for a digest given as
+ * (node, last_gc, max_version) triples; returns the NodeDelta count, fills per NodeDelta
+ * (node, from, kv count) and the kv versions in order. */
+int32_t orc_kat_compute_delta(orc *o, int32_t sender, int32_t n_digest, const int32_t *dg_node,
+                              const uint32_t *dg_gc, const uint32_t *dg_mv, int32_t mtu,
+                              int32_t *nd_node, uint32_t *nd_from, int32_t *nd_nkv, uint32_t *kv_versions,
+                              int32_t max_out);
+/* FailureDetector.report_heartbeat / update_node_liveness / garbage_collect /
+ * scheduled_for_deletion_nodes (failure_detector.py:79-128) */
+void    orc_kat_fd_report(orc *o, int32_t obs, int32_t target, int64_t now_us);
+void    orc_kat_fd_update(orc *o, int32_t obs, int32_t target, int64_t now_us);
+int32_t orc_kat_fd_gc(orc *o, int32_t obs, int64_t now_us, int32_t *out);
+int32_t orc_kat_fd_scheduled(orc *o, int32_t obs, int64_t now_us, int32_t *out);
+/* SamplingWindow.reset (failure_detector.py:40-41) */
+void    orc_kat_fd_reset(orc *o, int32_t obs, int32_t target);
+/* BoundedArrayStats.append / sum / __len__ / clear (failure_detector.py:139-162) on a window */
+void    orc_kat_win_append(orc *o, int32_t obs, int32_t target, double x);
+double  orc_kat_win_sum(orc *o, int32_t obs, int32_t target);
+int32_t orc_kat_win_len(orc *o, int32_t obs, int32_t target);
+int32_t orc_kat_win_filled(orc *o, int32_t obs, int32_t target);
+
 #ifdef __cplusplus
 }
 #endif

@@ -77,6 +77,21 @@ def lib():
             "orc_get_stats": (None, [P, C.POINTER(_Stats)]),
             "orc_export_row": (None, [P, i32] + [P] * 13),
             "orc_load_row": (None, [P, i32, i32, P, P, P, P, P, i32, P, P, P, P, P, P, P, P, i64]),
+            "orc_kat_set_view": (None, [P, i32, i32, u32, u32, u32]),
+            "orc_kat_set_kv": (None, [P, i32, i32, i32, u32, i32, u32, i32, i64]),
+            "orc_kat_apply_heartbeat": (i32, [P, i32, i32, u32]),
+            "orc_kat_apply_nodedelta": (None, [P, i32, i32, u32, u32, u32, i32, P, P, P, P, P, i64]),
+            "orc_kat_gc": (None, [P, i32, i32, i64, i64]),
+            "orc_kat_compute_delta": (i32, [P, i32, i32, P, P, P, i32, P, P, P, P, i32]),
+            "orc_kat_fd_report": (None, [P, i32, i32, i64]),
+            "orc_kat_fd_update": (None, [P, i32, i32, i64]),
+            "orc_kat_fd_gc": (i32, [P, i32, i64, P]),
+            "orc_kat_fd_scheduled": (i32, [P, i32, i64, P]),
+            "orc_kat_fd_reset": (None, [P, i32, i32]),
+            "orc_kat_win_append": (None, [P, i32, i32, C.c_double]),
+            "orc_kat_win_sum": (C.c_double, [P, i32, i32]),
+            "orc_kat_win_len": (i32, [P, i32, i32]),
+            "orc_kat_win_filled": (i32, [P, i32, i32]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
