@@ -28,7 +28,7 @@ TICK_US = 15_625
 
 REGIONS = [
     "HB", "MV", "GC", "HELD", "FD_LAST", "FD_SUM", "FD_CNT", "FD_STATE", "TS", "RING", "POS", "ORD", "ROW",
-    "LAST_W", "HIST_VER", "HIST_META", "HIST_VID", "NID_SIZE", "KEY_LEN", "STAMP", "COUNTERS",
+    "LAST_W", "HIST", "HIST_VID", "NID_SIZE", "KEY_LEN", "STAMP", "COUNTERS",
 ]
 REGION = {n: i for i, n in enumerate(REGIONS)}
 

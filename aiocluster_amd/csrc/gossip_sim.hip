@@ -64,7 +64,8 @@ struct Dev {
     uint16_t *ring;
     uint32_t *pos, *ord, *row;
     uint8_t *last_w;
-    uint32_t *hist_ver, *hist_meta, *hist_vid;
+    uint64_t *hist;  // version | meta << 32
+    uint32_t *hist_vid;
     uint16_t *nid_size;
     uint8_t *key_len;
     uint32_t *stamp;
@@ -119,269 +120,413 @@ __device__ inline void shard_add(const Dev &d, int c, unsigned long long v) {
     if (v) atomicAdd(&d.ctr[(blockIdx.x % NSHARD) * 32 + c], v);
 }
 
-// ------------------------------------------------------------------ failure detector
-// FailureDetector.report_heartbeat -> SamplingWindow.report_heartbeat
-// (failure_detector.py:79-81, 32-38): the first report creates the window and only
-// records the time; later intervals <= max_interval go to BoundedArrayStats (139-150).
-__device__ inline void fd_report(const Dev &d, size_t p, uint32_t t, uint32_t &alg, uint32_t &ovf) {
-    const uint32_t last = d.fd_last[p];
-    alg += 8;
-    if (last != NONE) {
-        const uint32_t iv = t - last;
-        if (iv <= d.max_iv) {
-            uint32_t cnt = d.fd_cnt[p], sum = d.fd_sum[p];
-            if (d.flags & GS_FD_RING) {
-                uint16_t *rg = d.ring + p * d.W;
-                const uint32_t slot = cnt % d.W;
-                if (cnt >= d.W) sum -= rg[slot];  // subtract-then-add (failure_detector.py:140-143)
-                rg[slot] = (uint16_t)iv;
-                sum += iv;
-                cnt += 1;
-                if (cnt >= 2u * d.W) cnt -= d.W;
-                alg += 4;
-            } else if (cnt >= d.W) {
-                ovf += 1;  // eviction needs the ring: flagged, the run is reported inexact
-            } else {
-                sum += iv;
-                cnt += 1;
-            }
-            d.fd_cnt[p] = cnt;
-            d.fd_sum[p] = sum;
-            alg += 16;
-        }
-    }
-    d.fd_last[p] = t;
-}
-
 // ------------------------------------------------------------------ packing / apply
 struct DigestSide {
-    uint32_t o;      // whose digest the sender compares against
+    uint32_t o;      // whose digest the sender compares against (always the receiver)
     uint32_t limit;  // general mode: owners with dict position < limit were in that digest
     bool sched;      // some target of o may be scheduled for deletion at t
-};
-
-struct Cand {
-    uint32_t j, from, gs, ms, base, emsg, min1, nkv;
 };
 
 struct WStats {
     uint32_t nd, kvs, trunc, cand, alg;
 };
 
-// NodeDelta candidate (state.py:347-390): from_version_excluded, the NodeDeltaPb body
-// size without kvs, the DeltaPb bytes of the whole NodeDelta (all kvs with version > from)
-// and of its smallest-version kv alone.
-__device__ inline void eval_cand(const Dev &d, uint32_t s, const DigestSide &ds, bool genm, uint32_t j,
-                                 uint32_t t, Cand &c, uint32_t &alg) {
-    const size_t ps = pix(d, s, j), pd = pix(d, ds.o, j);
-    const uint32_t ms = d.mv[ps], gs = d.gc[ps];
-    bool in_d = true;
-    if (genm) { in_d = d.pos[pd] < ds.limit; alg += 4; }
-    if (in_d && ds.sched) { in_d = !is_sched(d.fd_state[pd], t, d.sched_delay); alg += 4; }
-    const uint32_t dm = in_d ? d.mv[pd] : 0u;
-    const uint32_t dg = in_d ? d.gc[pd] : 0u;
-    const uint32_t from = (dg < gs && dm < gs) ? 0u : dm;  // should_reset (state.py:359-362)
-    const uint32_t base = msgf(d.nid_size[j]) + ufield(from) + ufield(gs) + 1u + vlen(ms);
-    const uint8_t *hs = d.held + ps * d.KP;
-    uint32_t sum = 0, nk = 0, minv = NONE, minkv = 0;
-    for (uint32_t k4 = 0; k4 < d.KP; k4 += 4) {
-        const uint32_t ww = *reinterpret_cast<const uint32_t *>(hs + k4);
-        if (!ww) continue;
+__device__ inline uint32_t byte_of(const uint32_t *w, int q) { return (w[q >> 2] >> (8 * (q & 3))) & 0xFFu; }
+
+// One stale owner j of the sender's dict: everything its NodeDelta and its apply need, loaded
+// in two dependent round trips (both rows' scalars + held words, then the sender's kv history).
+template <int KW>
+struct Cand {
+    uint32_t j, from, gs, ms, gr, mr, base, emsg, min1, nkv;
+    uint32_t hs[KW], hr[KW];  // held write ordinals, 4 keys per word (sender / receiver)
+    uint32_t ver[4 * KW];     // version of each key the sender holds (0 = absent)
+    uint32_t km[4 * KW];      // DeltaPb bytes of that kv | status << 16
+};
+
+// NodeDelta candidate (state.py:347-390): from_version_excluded, the NodeDeltaPb body without
+// kvs, the DeltaPb bytes of the whole NodeDelta (all kvs with version > from, 392-398) and of
+// its smallest-version kv alone.
+template <int KW>
+__device__ __forceinline__ void eval_cand(const Dev &d, uint32_t s, uint32_t r, const DigestSide &ds, bool genm, uint32_t j,
+                                 uint32_t t, Cand<KW> &c, uint32_t &alg) {
+    const size_t ps = pix(d, s, j), pr = pix(d, r, j);
+    const uint32_t kw = d.KP >> 2;
+    // round trip 1
+    const uint32_t ms = d.mv[ps], gs = d.gc[ps], mr = d.mv[pr], gr = d.gc[pr];
+    const uint32_t pos_r = genm ? d.pos[pr] : 0u;
+    const uint32_t fst = ds.sched ? d.fd_state[pr] : 0u;
+    const uint32_t *hsp = reinterpret_cast<const uint32_t *>(d.held + ps * d.KP);
+    const uint32_t *hrp = reinterpret_cast<const uint32_t *>(d.held + pr * d.KP);
 #pragma unroll
-        for (uint32_t q = 0; q < 4; q++) {
-            const uint32_t w = (ww >> (8 * q)) & 0xFFu;
-            const uint32_t k = k4 + q;
-            if (!w || k >= d.K) continue;
-            const size_t h = hix(d, j, w, k);
-            const uint32_t v = d.hist_ver[h];
-            alg += 4;
-            if (v <= from) continue;
-            const uint32_t kvm = msgf(meta_kvlen(d.hist_meta[h]));
-            alg += 4;
-            sum += kvm;
-            nk += 1;
-            if (v < minv) { minv = v; minkv = kvm; }
+    for (int q = 0; q < KW; q++) {
+        c.hs[q] = (uint32_t)q < kw ? hsp[q] : 0u;
+        c.hr[q] = (uint32_t)q < kw ? hrp[q] : 0u;
+    }
+    alg += 16 + 2 * d.KP + (genm ? 4 : 0) + (ds.sched ? 4 : 0);
+    bool in_d = genm ? pos_r < ds.limit : true;
+    if (in_d && ds.sched) in_d = !is_sched(fst, t, d.sched_delay);
+    const uint32_t dm = in_d ? mr : 0u;
+    const uint32_t dg = in_d ? gr : 0u;
+    const uint32_t from = (dg < gs && dm < gs) ? 0u : dm;  // should_reset (state.py:359-362)
+    // round trip 2: the sender's kv history entries
+#pragma unroll
+    for (int q = 0; q < 4 * KW; q++) {
+        const uint32_t w = byte_of(c.hs, q);
+        c.ver[q] = 0u;
+        c.km[q] = 0u;
+        if (w && (uint32_t)q < d.K) {
+            const uint64_t e = d.hist[hix(d, j, w, q)];
+            const uint32_t meta = (uint32_t)(e >> 32);
+            c.ver[q] = (uint32_t)e;
+            c.km[q] = msgf(meta_kvlen(meta)) | (meta_status(meta) << 16);
+            alg += 8;
         }
     }
-    alg += 16 + d.KP;
+    uint32_t sum = 0, nk = 0, minv = NONE, minkv = 0;
+#pragma unroll
+    for (int q = 0; q < 4 * KW; q++) {
+        if (c.ver[q] > from) {
+            const uint32_t kvm = c.km[q] & 0xFFFFu;
+            sum += kvm;
+            nk += 1;
+            if (c.ver[q] < minv) { minv = c.ver[q]; minkv = kvm; }
+        }
+    }
     c.j = j;
     c.from = from;
     c.gs = gs;
     c.ms = ms;
-    c.base = base;
+    c.gr = gr;
+    c.mr = mr;
+    c.base = msgf(d.nid_size[j]) + ufield(from) + ufield(gs) + 1u + vlen(ms);
     c.nkv = nk;
-    c.emsg = nk ? msgf(base + sum) : 0u;
-    c.min1 = nk ? msgf(base + minkv) : 0u;
+    c.emsg = nk ? msgf(c.base + sum) : 0u;
+    c.min1 = nk ? msgf(c.base + minkv) : 0u;
 }
 
-// NodeState.apply_delta (state.py:190-233) of the NodeDelta {owner j, kvs of the sender's
-// view with from < version <= vmax, last_gc gs, max_version ms} at receiver r.
-__device__ inline void apply_nd(const Dev &d, uint32_t s, uint32_t r, uint32_t j, uint32_t from, uint32_t vmax,
-                                uint32_t gs, uint32_t ms, uint32_t t, bool &tomb, uint32_t &alg) {
-    const size_t ps = pix(d, s, j), pr = pix(d, r, j);
-    uint32_t g = d.gc[pr];
-    const uint32_t m0 = d.mv[pr];
-    const bool jump = gs > g;  // last_gc_version raised: drop entries <= it (200-207)
-    if (jump) g = gs;
+// NodeState.apply_delta (state.py:190-233) at receiver r of the NodeDelta {owner c.j, the
+// sender's kvs with from < version <= vmax, last_gc c.gs, max_version c.ms}.  Keys are
+// independent (kvs arrive in version order, so "version <= max_version" only ever compares
+// against the view's max_version before the delta, 209-210).
+template <int KW>
+__device__ __forceinline__ void apply_cand(const Dev &d, uint32_t r, const Cand<KW> &c, uint32_t vmax, uint32_t t, bool &tomb,
+                                  uint32_t &alg) {
+    const size_t pr = pix(d, r, c.j);
+    uint32_t g = c.gr;
+    const uint32_t m0 = c.mr;
+    const bool jump = c.gs > g;  // last_gc_version raised: drop entries <= it (200-207)
+    if (jump) g = c.gs;
     uint32_t maxv = m0;
-    uint8_t *hr = d.held + pr * d.KP;
-    const uint8_t *hs = d.held + ps * d.KP;
     const bool tt = (d.flags & GS_TOMBSTONES) != 0;
     uint32_t *tsr = tt ? d.ts + pr * d.KP : nullptr;
-    for (uint32_t k4 = 0; k4 < d.KP; k4 += 4) {
-        const uint32_t wsw = *reinterpret_cast<const uint32_t *>(hs + k4);
-        uint32_t wrw = *reinterpret_cast<const uint32_t *>(hr + k4);
-        const uint32_t wr0 = wrw;
-        if (!wsw && !(jump && wrw)) continue;
-        for (uint32_t q = 0; q < 4; q++) {
-            const uint32_t k = k4 + q;
-            if (k >= d.K) break;
-            uint32_t wr = (wrw >> (8 * q)) & 0xFFu;
-            const uint32_t ws = (wsw >> (8 * q)) & 0xFFu;
-            if (jump && wr && d.hist_ver[hix(d, j, wr, k)] <= g) {
-                wr = 0;
-                if (tt) tsr[k] = NONE;
-                alg += 4;
-            }
-            if (ws) {
-                const size_t h = hix(d, j, ws, k);
-                const uint32_t v = d.hist_ver[h];
-                alg += 4;
-                // skip: not in the delta / version <= max_version / existing >= / GC'd tombstone
-                if (v > from && v <= vmax && v > m0 && wr < ws) {
-                    const uint32_t st = meta_status(d.hist_meta[h]);
-                    alg += 4;
-                    if (!(st != 0u && v <= g)) {
-                        wr = ws;
-                        if (tt) { tsr[k] = st ? t : NONE; alg += 4; }
-                        if (st) tomb = true;
-                        if (v > maxv) maxv = v;
-                    }
-                }
-            }
-            wrw = (wrw & ~(0xFFu << (8 * q))) | (wr << (8 * q));
+    uint32_t hr[KW];
+#pragma unroll
+    for (int q = 0; q < KW; q++) hr[q] = c.hr[q];
+#pragma unroll
+    for (int q = 0; q < 4 * KW; q++) {
+        if ((uint32_t)q >= d.K) continue;
+        uint32_t wr = byte_of(hr, q);
+        const uint32_t ws = byte_of(c.hs, q);
+        if (jump && wr && (uint32_t)d.hist[hix(d, c.j, wr, q)] <= g) {
+            wr = 0;
+            if (tt) tsr[q] = NONE;
+            alg += 8;
         }
-        if (wrw != wr0) { *reinterpret_cast<uint32_t *>(hr + k4) = wrw; alg += 4; }
+        const uint32_t v = c.ver[q];
+        // skip: not in the delta / version <= max_version / existing >= / GC'd tombstone (209-220)
+        if (ws && v > c.from && v <= vmax && v > m0 && wr < ws) {
+            const uint32_t st = c.km[q] >> 16;
+            if (!(st != 0u && v <= g)) {
+                wr = ws;
+                if (tt) { tsr[q] = st ? t : NONE; alg += 4; }
+                if (st) tomb = true;
+                if (v > maxv) maxv = v;
+            }
+        }
+        const int sh = 8 * (q & 3);
+        hr[q >> 2] = (hr[q >> 2] & ~(0xFFu << sh)) | (wr << sh);
     }
-    if (ms > maxv) maxv = ms;  // max_version (232-233)
+    uint32_t *hrp = reinterpret_cast<uint32_t *>(d.held + pr * d.KP);
+#pragma unroll
+    for (int q = 0; q < KW; q++)
+        if (hr[q] != c.hr[q]) { hrp[q] = hr[q]; alg += 4; }
+    if (c.ms > maxv) maxv = c.ms;  // max_version (232-233)
     d.mv[pr] = maxv;
-    d.gc[pr] = g;
-    alg += 16 + 2 * d.KP + 8;
+    if (g != c.gr) d.gc[pr] = g;
+    alg += 8;
 }
 
-// compute_partial_delta_respecting_mtu (state.py:340-415) from sender s's view for receiver r,
-// fused with r's apply_delta.  One wave; lanes walk the sender's dict order 64 positions at a
-// time.  Exactness argument (same decisions as the sequential loop): DESIGN.md.
-__device__ void pack_dir(const Dev &d, uint32_t s, uint32_t r, const DigestSide ds, const uint32_t *order,
-                         uint32_t cnt, const uint32_t *bits, uint32_t t, bool genm, WStats &st, bool &tomb) {
+// compute_partial_delta_respecting_mtu (state.py:340-415) of sender s for receiver r, fused with
+// r's apply_delta, by one wave.  The sender's dict order is walked in windows of 2048 positions;
+// each window's stale owners are compacted (ballot + popcount scan) into a wave-private LDS list
+// and evaluated 64 at a time, one per lane.  Exactness vs the sequential loop: DESIGN.md.
+template <int KW>
+__device__ __forceinline__ void pack_dir(const Dev &d, uint32_t s, uint32_t r, const DigestSide ds, const uint32_t *order,
+                         uint32_t cnt, const uint32_t *bits, uint16_t *wbuf, uint32_t t, bool genm, WStats &st,
+                         bool &tomb) {
     const int lane = lane_id();
     const uint32_t mtu = d.mtu;
     uint32_t S = 0;  // DeltaPb bytes committed (wave-uniform)
-    bool tail = false;
-    for (uint32_t p0 = 0; p0 < cnt; p0 += WAVE) {
-        const uint32_t p = p0 + lane;
-        uint32_t j = NONE;
-        if (p < cnt) j = order ? order[p] : p;
-        const bool cand = (j != NONE) && bit(bits, j);
-        if (__ballot(cand) == 0ull) continue;
-        Cand c{};
-        if (cand) { eval_cand(d, s, ds, genm, j, t, c, st.alg); st.cand++; }
-        const uint32_t em = cand ? c.emsg : 0u;
-        int start = 0;
-        if (!tail) {
-            const uint32_t incl = wave_incl_scan(em);
-            const uint32_t total = __shfl(incl, WAVE - 1, WAVE);
-            if (S + total <= mtu) {  // every candidate of this group fits whole
-                if (em) {
-                    apply_nd(d, s, r, c.j, c.from, NONE, c.gs, c.ms, t, tomb, st.alg);
-                    st.nd++;
-                    st.kvs += c.nkv;
-                }
-                S += total;
-                if (S >= mtu || mtu - S < d.lb_min) break;
-                continue;
-            }
-            const bool fail = em && (S + incl > mtu);
-            const unsigned long long fm = __ballot(fail);
-            const int f = __builtin_ctzll(fm);
-            if (lane < f && em) {
-                apply_nd(d, s, r, c.j, c.from, NONE, c.gs, c.ms, t, tomb, st.alg);
-                st.nd++;
-                st.kvs += c.nkv;
-            }
-            S += __shfl(incl - em, f, WAVE);
-            tail = true;
-            start = f;
-        }
-        // First-fit continuation (state.py:392-413): each later candidate sends the longest
-        // prefix of its version-sorted kvs that still fits; stop once the delta is >= mtu.
-        int cur = start;
-        bool stop = false;
-        while (true) {
-            const uint32_t R = mtu - S;
-            const bool elig = em && lane >= cur && c.min1 <= R;
-            const unsigned long long m = __ballot(elig);
-            if (!m) break;
-            const int x = __builtin_ctzll(m);
-            const uint32_t emx = __shfl(em, x, WAVE);
-            if (emx <= R) {
-                if (lane == x) {
-                    apply_nd(d, s, r, c.j, c.from, NONE, c.gs, c.ms, t, tomb, st.alg);
-                    st.nd++;
-                    st.kvs += c.nkv;
-                }
-                S += emx;
+    bool tail = false, stop = false;
+    for (uint32_t win = 0; win < cnt && !stop; win += 32 * WAVE) {
+        // -- compact this window's stale owners (sender order) into wbuf
+        uint32_t m = 0;
+        const uint32_t pb = win + 32u * lane;
+        if (pb < cnt) {
+            if (!order) {
+                m = bits[pb >> 5];
             } else {
-                // truncated NodeDelta: lanes = keys, rank kvs by version, longest fitting prefix
-                const uint32_t jx = __shfl(c.j, x, WAVE), fx = __shfl(c.from, x, WAVE);
-                const uint32_t bx = __shfl(c.base, x, WAVE);
-                bool inc = false;
-                uint32_t v = 0, kvm = 0;
-                if (lane < (int)d.K) {
-                    const uint32_t w = d.held[pix(d, s, jx) * d.KP + lane];
-                    if (w) {
-                        const size_t h = hix(d, jx, w, lane);
-                        v = d.hist_ver[h];
-                        if (v > fx) { inc = true; kvm = msgf(meta_kvlen(d.hist_meta[h])); }
-                    }
-                }
-                const unsigned long long im = __ballot(inc);
-                uint32_t rank = 0, P = 0;
-                for (int l = 0; l < (int)d.K; l++) {
-                    const uint32_t vl = __shfl(v, l, WAVE);
-                    if (((im >> l) & 1ull) && vl < v) rank++;
-                }
-                for (int l = 0; l < (int)d.K; l++) {
-                    const uint32_t rl = __shfl(rank, l, WAVE);
-                    const uint32_t kl = __shfl(kvm, l, WAVE);
-                    if (((im >> l) & 1ull) && (int)rl < lane) P += kl;
-                }
-                const uint32_t nkv = (uint32_t)__popcll(im);
-                const bool fit = lane >= 1 && (uint32_t)lane <= nkv && S + msgf(bx + P) <= mtu;
-                const uint32_t n = (uint32_t)__popcll(__ballot(fit));
-                if (n >= 1) {
-                    const unsigned long long ym = __ballot(inc && rank == n - 1);
-                    const uint32_t vmax = __shfl(v, __builtin_ctzll(ym), WAVE);
-                    const uint32_t used = msgf(bx + __shfl(P, (int)n, WAVE));
-                    if (lane == x) {
-                        apply_nd(d, s, r, c.j, c.from, vmax, c.gs, c.ms, t, tomb, st.alg);
-                        st.nd++;
-                        st.kvs += n;
-                        st.trunc++;
-                    }
-                    S += used;
+                for (uint32_t q = 0; q < 32; q++) {
+                    const uint32_t p = pb + q;
+                    if (p < cnt && bit(bits, order[p])) m |= 1u << q;
                 }
             }
-            if (S >= mtu) { stop = true; break; }
-            cur = x + 1;
+            const uint32_t lim = cnt - pb;
+            if (lim < 32) m &= (1u << lim) - 1u;
         }
-        if (stop || mtu - S < d.lb_min) break;
+        const uint32_t cl = (uint32_t)__popc(m);
+        const uint32_t incl = wave_incl_scan(cl);
+        const uint32_t tot = __shfl(incl, WAVE - 1, WAVE);
+        if (tot == 0) continue;
+        __builtin_amdgcn_wave_barrier();
+        uint32_t wp = incl - cl;
+        while (m) {
+            const uint32_t b = (uint32_t)__builtin_ctz(m);
+            m &= m - 1u;
+            wbuf[wp++] = (uint16_t)(32u * lane + b);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        for (uint32_t c0 = 0; c0 < tot && !stop; c0 += WAVE) {
+            const uint32_t ci = c0 + lane;
+            const bool cand = ci < tot;
+            Cand<KW> c;
+            c.emsg = 0;
+            c.min1 = 0;
+            if (cand) {
+                const uint32_t p = win + wbuf[ci];
+                const uint32_t j = order ? order[p] : p;
+                eval_cand<KW>(d, s, r, ds, genm, j, t, c, st.alg);
+                st.cand++;
+            }
+            const uint32_t em = cand ? c.emsg : 0u;
+            // this lane's NodeDelta: 0 = not sent, NONE = all its kvs, else kvs up to that version
+            uint32_t vsel = 0, nsel = 0;
+            int cur = 0;
+            bool seq = tail;
+            if (!tail) {
+                const uint32_t inc = wave_incl_scan(em);
+                const uint32_t total = __shfl(inc, WAVE - 1, WAVE);
+                if (S + total <= mtu) {  // every candidate of this group fits whole
+                    if (em) vsel = NONE;
+                    S += total;
+                    if (S >= mtu || mtu - S < d.lb_min) stop = true;
+                } else {
+                    const bool fail = em && (S + inc > mtu);
+                    const int f = __builtin_ctzll(__ballot(fail));
+                    if (lane < f && em) vsel = NONE;
+                    S += __shfl(inc - em, f, WAVE);
+                    tail = true;
+                    seq = true;
+                    cur = f;
+                }
+            }
+            // First-fit continuation (state.py:392-413): each later candidate sends the longest
+            // prefix of its version-sorted kvs that still fits; stop once the delta is >= mtu.
+            while (seq) {
+                const uint32_t R = mtu - S;
+                const bool elig = em && lane >= cur && c.min1 <= R;
+                const unsigned long long mm = __ballot(elig);
+                if (!mm) break;
+                const int x = __builtin_ctzll(mm);
+                const uint32_t emx = __shfl(em, x, WAVE);
+                if (emx <= R) {
+                    if (lane == x) vsel = NONE;
+                    S += emx;
+                } else {
+                    // truncated NodeDelta: lanes = keys, rank kvs by version, longest fitting prefix
+                    const uint32_t fx = __shfl(c.from, x, WAVE);
+                    const uint32_t bx = __shfl(c.base, x, WAVE);
+                    uint32_t v = 0, kvm = 0;
+#pragma unroll
+                    for (int q = 0; q < 4 * KW; q++) {
+                        const uint32_t vq = __shfl(c.ver[q], x, WAVE);
+                        const uint32_t kq = __shfl(c.km[q], x, WAVE);
+                        if (lane == q) { v = vq; kvm = kq & 0xFFFFu; }
+                    }
+                    const bool inc = lane < (int)d.K && v > fx;
+                    const unsigned long long im = __ballot(inc);
+                    uint32_t rank = 0, P = 0;
+                    for (int l = 0; l < (int)d.K; l++) {
+                        const uint32_t vl = __shfl(v, l, WAVE);
+                        if (((im >> l) & 1ull) && vl < v) rank++;
+                    }
+                    for (int l = 0; l < (int)d.K; l++) {
+                        const uint32_t rl = __shfl(rank, l, WAVE);
+                        const uint32_t kl = __shfl(kvm, l, WAVE);
+                        if (((im >> l) & 1ull) && (int)rl < lane) P += kl;
+                    }
+                    const uint32_t nkv = (uint32_t)__popcll(im);
+                    const bool fit = lane >= 1 && (uint32_t)lane <= nkv && S + msgf(bx + P) <= mtu;
+                    const uint32_t n = (uint32_t)__popcll(__ballot(fit));
+                    if (n >= 1) {
+                        const unsigned long long ym = __ballot(inc && rank == n - 1);
+                        const uint32_t vmax = __shfl(v, __builtin_ctzll(ym), WAVE);
+                        if (lane == x) { vsel = vmax; nsel = n; }
+                        S += msgf(bx + __shfl(P, (int)n, WAVE));
+                    }
+                }
+                if (S >= mtu) { stop = true; break; }
+                cur = x + 1;
+            }
+            if (tail && mtu - S < d.lb_min) stop = true;
+            // apply_delta at the receiver: one lane per NodeDelta, distinct owners, any order
+            if (vsel) {
+                apply_cand<KW>(d, r, c, vsel, t, tomb, st.alg);
+                st.nd++;
+                if (vsel == NONE) {
+                    st.kvs += c.nkv;
+                } else {
+                    st.kvs += nsel;
+                    st.trunc++;
+                }
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
     }
-    // DeltaPb bytes of this direction, counted once per wave
-    if (lane == 0) shard_add(d, C_DBYTES, S);
+    if (lane == 0) shard_add(d, C_DBYTES, S);  // DeltaPb bytes of this direction
 }
 
 // ------------------------------------------------------------------ exchange kernel
+// Pass-1 work of one group of 4 consecutive owners (one 16-byte load per array and row), held
+// as scalar arrays so every element stays in a register after unrolling.
+struct Grp {
+    uint32_t hA[4], hB[4], mA[4], mB[4], lA[4], lB[4], sA[4], sB[4], cA[4], cB[4], pA[4], pB[4], fA[4], fB[4];
+};
+
+__device__ __forceinline__ void ld4(const uint32_t *p, uint32_t (&v)[4]) {
+    const uint4 x = *reinterpret_cast<const uint4 *>(p);
+    v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+}
+__device__ __forceinline__ void st4(uint32_t *p, const uint32_t (&v)[4]) {
+    *reinterpret_cast<uint4 *>(p) = make_uint4(v[0], v[1], v[2], v[3]);
+}
+
+__device__ __forceinline__ void load_grp(const Dev &d, size_t ra, size_t rb, uint32_t c0, bool genm, bool schA,
+                                         bool schB, Grp &g) {
+    ld4(d.hb + ra + c0, g.hA);
+    ld4(d.hb + rb + c0, g.hB);
+    ld4(d.mv + ra + c0, g.mA);
+    ld4(d.mv + rb + c0, g.mB);
+    // failure-detector fields are prefetched unconditionally: about half the owners report per
+    // exchange, so every 64-byte line of both rows is touched anyway
+    ld4(d.fd_last + ra + c0, g.lA);
+    ld4(d.fd_last + rb + c0, g.lB);
+    ld4(d.fd_sum + ra + c0, g.sA);
+    ld4(d.fd_sum + rb + c0, g.sB);
+    ld4(d.fd_cnt + ra + c0, g.cA);
+    ld4(d.fd_cnt + rb + c0, g.cB);
+#pragma unroll
+    for (int i = 0; i < 4; i++) { g.pA[i] = g.pB[i] = g.fA[i] = g.fB[i] = 0u; }
+    if (genm) { ld4(d.pos + ra + c0, g.pA); ld4(d.pos + rb + c0, g.pB); }
+    if (schA) ld4(d.fd_state + ra + c0, g.fA);
+    if (schB) ld4(d.fd_state + rb + c0, g.fB);
+}
+
+struct Fd {
+    uint32_t last, sum, cnt;
+};
+
+// FailureDetector.report_heartbeat -> SamplingWindow.report_heartbeat on prefetched fields
+// (failure_detector.py:79-81, 32-38): the first report only records the time; later intervals
+// <= max_interval go to BoundedArrayStats (139-150).
+__device__ __forceinline__ Fd fd_report_val(const Dev &d, size_t p, uint32_t t, Fd f, uint32_t &alg, uint32_t &ovf) {
+    if (f.last != NONE) {
+        const uint32_t iv = t - f.last;
+        if (iv <= d.max_iv) {
+            if (d.flags & GS_FD_RING) {
+                uint16_t *rg = d.ring + p * d.W;
+                const uint32_t slot = f.cnt % d.W;
+                if (f.cnt >= d.W) f.sum -= rg[slot];  // subtract-then-add (failure_detector.py:140-143)
+                rg[slot] = (uint16_t)iv;
+                f.sum += iv;
+                f.cnt += 1;
+                if (f.cnt >= 2u * d.W) f.cnt -= d.W;
+                alg += 4;
+            } else if (f.cnt >= d.W) {
+                ovf += 1;  // eviction needs the ring: flagged, the run is reported inexact
+            } else {
+                f.sum += iv;
+                f.cnt += 1;
+            }
+        }
+    }
+    f.last = t;
+    alg += 24;
+    return f;
+}
+
+__device__ __forceinline__ void pass1_grp(const Dev &d, size_t ra, size_t rb, uint32_t c0, uint32_t a, uint32_t b,
+                                          uint32_t t, bool genm, bool schA, bool schB, Grp &g, uint32_t *bBA,
+                                          uint32_t *bAB, uint32_t *bNB, uint32_t *bNA, uint32_t &alg,
+                                          uint32_t &reports, uint32_t &hbw, uint32_t &ovf, bool &anynew) {
+    bool dA = false, dB = false, fdA = false, fdB = false;
+    alg += 64 + (genm ? 32 : 0) + (schA ? 16 : 0) + (schB ? 16 : 0);
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const uint32_t j = c0 + i;
+        if (j < d.N) {
+            const bool pa = genm ? g.pA[i] != NONE : true;
+            const bool pb = genm ? g.pB[i] != NONE : true;
+            const bool sa = schA && pa && is_sched(g.fA[i], t, d.sched_delay);
+            const bool sb = schB && pb && is_sched(g.fB[i], t, d.sched_delay);
+            const bool inA = pa && !sa;  // j is in a's digest (compute_digest, state.py:324-331)
+            uint32_t hA = g.hA[i], hB = g.hB[i];
+            if (j == b) { hB += 1u; dB = true; hbw++; }  // responder inc_heartbeat (server.py:524)
+            bool newB = false, repB = false;
+            if (inA && j != b) {  // b: _report_heartbeat over a's digest (server.py:336-337, 599-604)
+                if (!pb) { newB = true; hB = hA; dB = true; hbw++; }
+                else if (hB == 0u) { if (hA) { hB = hA; dB = true; hbw++; } }
+                else if (hA > hB) { hB = hA; dB = true; hbw++; repB = true; }
+            }
+            const bool pb2 = pb || newB;
+            const bool inB = pb2 && !sb;  // j is in b's digest, computed after the merge (server.py:340)
+            bool newA = false, repA = false;
+            if (inB && j != a) {  // a: _report_heartbeat over b's digest (server.py:356-357)
+                if (!pa) { newA = true; hA = hB; dA = true; hbw++; }
+                else if (hA == 0u) { if (hB) { hA = hB; dA = true; hbw++; } }
+                else if (hB > hA) { hA = hB; dA = true; hbw++; repA = true; }
+            }
+            g.hA[i] = hA;
+            g.hB[i] = hB;
+            if (repB) {
+                const Fd f = fd_report_val(d, rb + j, t, Fd{g.lB[i], g.sB[i], g.cB[i]}, alg, ovf);
+                g.lB[i] = f.last; g.sB[i] = f.sum; g.cB[i] = f.cnt;
+                fdB = true;
+                reports++;
+            }
+            if (repA) {
+                const Fd f = fd_report_val(d, ra + j, t, Fd{g.lA[i], g.sA[i], g.cA[i]}, alg, ovf);
+                g.lA[i] = f.last; g.sA[i] = f.sum; g.cA[i] = f.cnt;
+                fdA = true;
+                reports++;
+            }
+            // stale owners (state.py:347-357): sender's max_version above the digest's
+            const uint32_t dmA = inA ? g.mA[i] : 0u;
+            if (pb2 && !sb && g.mB[i] > dmA) atomicOr(&bBA[j >> 5], 1u << (j & 31u));
+            const uint32_t dmB = inB ? g.mB[i] : 0u;
+            if (pa && !sa && g.mA[i] > dmB) atomicOr(&bAB[j >> 5], 1u << (j & 31u));
+            if (newB) { atomicOr(&bNB[j >> 5], 1u << (j & 31u)); anynew = true; }
+            if (newA) { atomicOr(&bNA[j >> 5], 1u << (j & 31u)); anynew = true; }
+        }
+    }
+    if (dA) { st4(d.hb + ra + c0, g.hA); alg += 16; }
+    if (dB) { st4(d.hb + rb + c0, g.hB); alg += 16; }
+    if (fdA) { st4(d.fd_last + ra + c0, g.lA); st4(d.fd_sum + ra + c0, g.sA); st4(d.fd_cnt + ra + c0, g.cA); }
+    if (fdB) { st4(d.fd_last + rb + c0, g.lB); st4(d.fd_sum + rb + c0, g.sB); st4(d.fd_cnt + rb + c0, g.cB); }
+}
+
+template <int KW>
 __global__ __launch_bounds__(XB) void k_exchange(Dev d, const int32_t *ini, const int32_t *res, uint32_t n,
                                                  uint32_t t, uint32_t seq) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -397,8 +542,11 @@ __global__ __launch_bounds__(XB) void k_exchange(Dev d, const int32_t *ini, cons
     const uint32_t a = (uint32_t)ai, b = (uint32_t)bi;
     const bool genm = !(d.flags & GS_CANONICAL);
     const uint32_t words = d.NP / 32;
-    uint32_t *bBA = lds, *bAB = lds + words, *bNB = lds + 2 * words, *bNA = lds + 3 * words;
-    for (uint32_t i = tid; i < words * (genm ? 4u : 2u); i += XB) lds[i] = 0u;
+    // LDS: 2048-entry compaction list per wave, then the stale-owner bitmaps (+ insertion bitmaps)
+    uint16_t *wbuf = reinterpret_cast<uint16_t *>(lds) + wid * (32 * WAVE);
+    uint32_t *bm = lds + 32 * WAVE;  // 2 waves x 2048 x u16 = 8 KB
+    uint32_t *bBA = bm, *bAB = bm + words, *bNB = bm + 2 * words, *bNA = bm + 3 * words;
+    for (uint32_t i = tid; i < words * (genm ? 4u : 2u); i += XB) bm[i] = 0u;
     if (tid == 0) {
         s_flag[0] = 0;
         const uint32_t oa = atomicMax(&d.stamp[a], seq), ob = atomicMax(&d.stamp[b], seq);
@@ -415,65 +563,9 @@ __global__ __launch_bounds__(XB) void k_exchange(Dev d, const int32_t *ini, cons
     uint32_t alg = 0, reports = 0, hbw = 0, ovf = 0;
     bool anynew = false;
     for (uint32_t c0 = (uint32_t)tid * 4u; c0 < d.N; c0 += XB * 4u) {
-        uint4 hA4 = *reinterpret_cast<const uint4 *>(d.hb + ra + c0);
-        uint4 hB4 = *reinterpret_cast<const uint4 *>(d.hb + rb + c0);
-        const uint4 mA4 = *reinterpret_cast<const uint4 *>(d.mv + ra + c0);
-        const uint4 mB4 = *reinterpret_cast<const uint4 *>(d.mv + rb + c0);
-        uint4 pA4 = make_uint4(0, 0, 0, 0), pB4 = make_uint4(0, 0, 0, 0);
-        uint4 fA4 = make_uint4(0, 0, 0, 0), fB4 = make_uint4(0, 0, 0, 0);
-        alg += 64;
-        if (genm) {
-            pA4 = *reinterpret_cast<const uint4 *>(d.pos + ra + c0);
-            pB4 = *reinterpret_cast<const uint4 *>(d.pos + rb + c0);
-            alg += 32;
-        }
-        if (schA) { fA4 = *reinterpret_cast<const uint4 *>(d.fd_state + ra + c0); alg += 16; }
-        if (schB) { fB4 = *reinterpret_cast<const uint4 *>(d.fd_state + rb + c0); alg += 16; }
-        uint32_t *hA = reinterpret_cast<uint32_t *>(&hA4), *hB = reinterpret_cast<uint32_t *>(&hB4);
-        const uint32_t *mA = reinterpret_cast<const uint32_t *>(&mA4), *mB = reinterpret_cast<const uint32_t *>(&mB4);
-        const uint32_t *pA = reinterpret_cast<const uint32_t *>(&pA4), *pB = reinterpret_cast<const uint32_t *>(&pB4);
-        const uint32_t *fA = reinterpret_cast<const uint32_t *>(&fA4), *fB = reinterpret_cast<const uint32_t *>(&fB4);
-        bool dA = false, dB = false;
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            const uint32_t j = c0 + i;
-            if (j >= d.N) break;
-            const bool pa = genm ? pA[i] != NONE : true;
-            const bool pb = genm ? pB[i] != NONE : true;
-            const bool sa = schA && pa && is_sched(fA[i], t, d.sched_delay);
-            const bool sb = schB && pb && is_sched(fB[i], t, d.sched_delay);
-            const bool inA = pa && !sa;  // j is in a's digest (compute_digest, state.py:324-331)
-            if (j == b) { hB[i] += 1u; dB = true; hbw++; }  // responder inc_heartbeat (server.py:524)
-            bool newB = false;
-            if (inA && j != b) {  // b: _report_heartbeat over a's digest (server.py:336-337, 599-604)
-                if (!pb) { newB = true; hB[i] = hA[i]; dB = true; hbw++; }
-                else if (hB[i] == 0u) { if (hA[i]) { hB[i] = hA[i]; dB = true; hbw++; } }
-                else if (hA[i] > hB[i]) {
-                    hB[i] = hA[i]; dB = true; hbw++; reports++;
-                    fd_report(d, rb + j, t, alg, ovf);
-                }
-            }
-            const bool pb2 = pb || newB;
-            const bool inB = pb2 && !sb;  // j is in b's digest, computed after the merge (server.py:340)
-            bool newA = false;
-            if (inB && j != a) {  // a: _report_heartbeat over b's digest (server.py:356-357)
-                if (!pa) { newA = true; hA[i] = hB[i]; dA = true; hbw++; }
-                else if (hA[i] == 0u) { if (hB[i]) { hA[i] = hB[i]; dA = true; hbw++; } }
-                else if (hB[i] > hA[i]) {
-                    hA[i] = hB[i]; dA = true; hbw++; reports++;
-                    fd_report(d, ra + j, t, alg, ovf);
-                }
-            }
-            // stale owners (state.py:347-357): sender's max_version above the digest's
-            const uint32_t dmA = inA ? mA[i] : 0u;
-            if (pb2 && !sb && mB[i] > dmA) atomicOr(&bBA[j >> 5], 1u << (j & 31u));
-            const uint32_t dmB = inB ? mB[i] : 0u;
-            if (pa && !sa && mA[i] > dmB) atomicOr(&bAB[j >> 5], 1u << (j & 31u));
-            if (newB) { atomicOr(&bNB[j >> 5], 1u << (j & 31u)); anynew = true; }
-            if (newA) { atomicOr(&bNA[j >> 5], 1u << (j & 31u)); anynew = true; }
-        }
-        if (dA) { *reinterpret_cast<uint4 *>(d.hb + ra + c0) = hA4; alg += 16; }
-        if (dB) { *reinterpret_cast<uint4 *>(d.hb + rb + c0) = hB4; alg += 16; }
+        Grp g0;
+        load_grp(d, ra, rb, c0, genm, schA, schB, g0);
+        pass1_grp(d, ra, rb, c0, a, b, t, genm, schA, schB, g0, bBA, bAB, bNB, bNA, alg, reports, hbw, ovf, anynew);
     }
     if (anynew) s_flag[0] = 1u;
     __syncthreads();
@@ -520,14 +612,14 @@ __global__ __launch_bounds__(XB) void k_exchange(Dev d, const int32_t *ini, cons
     // ---- pass 3: SynAck delta b -> a (wave 0) and Ack delta a -> b (wave 1), each applied
     WStats st{0, 0, 0, 0, 0};
     bool tomb = false;
-    if (wid == 0) {
-        const DigestSide ds{a, cntA0, schA};
-        pack_dir(d, b, a, ds, genm ? d.ord + rb : nullptr, cntB, bBA, t, genm, st, tomb);
-    } else {
-        const DigestSide ds{b, cntB, schB};
-        pack_dir(d, a, b, ds, genm ? d.ord + ra : nullptr, cntA, bAB, t, genm, st, tomb);
+    {
+        const bool w0 = wid == 0;  // wave-uniform: one call site, so pack_dir inlines
+        const uint32_t snd = w0 ? b : a, rcv = w0 ? a : b;
+        const DigestSide ds{rcv, w0 ? cntA0 : cntB, w0 ? schA : schB};
+        const uint32_t *ord = genm ? d.ord + (w0 ? rb : ra) : nullptr;
+        pack_dir<KW>(d, snd, rcv, ds, ord, w0 ? cntB : cntA, w0 ? bBA : bAB, wbuf, t, genm, st, tomb);
+        if (tomb) d.row[rcv * 4 + 1] = 1u;
     }
-    if (tomb) d.row[(wid == 0 ? a : b) * 4 + 1] = 1u;
 
     // ---- counters: wave-reduced, sharded atomics
     const unsigned long long s_alg = wave_sum((unsigned long long)alg + st.alg);
@@ -567,7 +659,7 @@ __global__ __launch_bounds__(LB) void k_begin_round(Dev d, const uint8_t *up, ui
             if (tv == NONE) continue;
             if ((uint64_t)t >= (uint64_t)tv + d.tomb_grace) {
                 const uint32_t w = d.held[p * d.KP + k];
-                const uint32_t v = d.hist_ver[hix(d, j, w, k)];
+                const uint32_t v = (uint32_t)d.hist[hix(d, j, w, k)];
                 d.held[p * d.KP + k] = 0;
                 d.ts[p * d.KP + k] = NONE;
                 if (v > maxdel) maxdel = v;
@@ -690,7 +782,7 @@ __global__ __launch_bounds__(LB) void k_owner_writes(Dev d, const gs_write *ops,
         st = op.op == GS_OP_SET ? 0u : 2u;
         if (w) {  // same value with the same status: no-op (state.py:140-141, 146-151)
             const size_t h = hix(d, j, w, k);
-            if (d.hist_vid[h] == op.value_id && meta_status(d.hist_meta[h]) == st) return;
+            if (d.hist_vid[h] == op.value_id && meta_status((uint32_t)(d.hist[h] >> 32)) == st) return;
         }
         vid = op.value_id;
         vl = op.value_len;
@@ -699,14 +791,14 @@ __global__ __launch_bounds__(LB) void k_owner_writes(Dev d, const gs_write *ops,
         const size_t h = hix(d, j, w, k);
         st = op.op == GS_OP_DELETE ? 1u : 2u;
         vid = op.op == GS_OP_DELETE ? 0u : d.hist_vid[h];        // delete clears the value (171)
-        vl = op.op == GS_OP_DELETE ? 0u : meta_vlen(d.hist_meta[h]);
+        vl = op.op == GS_OP_DELETE ? 0u : meta_vlen((uint32_t)(d.hist[h] >> 32));
     }
     const uint32_t nw = (uint32_t)d.last_w[(size_t)j * d.KP + k] + 1u;
     if (nw >= d.C || vl >= (1u << 14)) { shard_add(d, C_E_HIST, 1); return; }
     const uint32_t ver = M + 1u;
     const size_t h = hix(d, j, nw, k);
-    d.hist_ver[h] = ver;
-    d.hist_meta[h] = make_meta(sfield(d.key_len[k]) + sfield(vl) + ufield(ver) + ufield(st), st, vl);
+    d.hist[h] = (uint64_t)ver |
+                ((uint64_t)make_meta(sfield(d.key_len[k]) + sfield(vl) + ufield(ver) + ufield(st), st, vl) << 32);
     d.hist_vid[h] = vid;
     d.last_w[(size_t)j * d.KP + k] = (uint8_t)nw;
     *held = (uint8_t)nw;
@@ -817,8 +909,7 @@ int check_bound(gs_handle *h) {
     d.ord = (uint32_t *)h->reg[GS_R_ORD];
     d.row = (uint32_t *)h->reg[GS_R_ROW];
     d.last_w = (uint8_t *)h->reg[GS_R_LAST_W];
-    d.hist_ver = (uint32_t *)h->reg[GS_R_HIST_VER];
-    d.hist_meta = (uint32_t *)h->reg[GS_R_HIST_META];
+    d.hist = (uint64_t *)h->reg[GS_R_HIST];
     d.hist_vid = (uint32_t *)h->reg[GS_R_HIST_VID];
     d.nid_size = (uint16_t *)h->reg[GS_R_NID_SIZE];
     d.key_len = (uint8_t *)h->reg[GS_R_KEY_LEN];
@@ -868,7 +959,8 @@ int gs_create(const gs_config *cfg, gs_handle **out) {
     b[GS_R_POS] = b[GS_R_ORD] = genm ? pairs * 4 : 0;
     b[GS_R_ROW] = N * 16;
     b[GS_R_LAST_W] = N * KP;
-    b[GS_R_HIST_VER] = b[GS_R_HIST_META] = b[GS_R_HIST_VID] = N * C * K * 4;
+    b[GS_R_HIST] = N * C * K * 8;
+    b[GS_R_HIST_VID] = N * C * K * 4;
     b[GS_R_NID_SIZE] = NP * 2;
     b[GS_R_KEY_LEN] = KP;
     b[GS_R_STAMP] = NP * 4;
@@ -923,7 +1015,7 @@ int gs_boot(gs_handle *h, const uint16_t *nid_size, const uint8_t *key_len) {
     const uint64_t pairs = (uint64_t)h->N * h->NP;
     // regions that start at zero
     const int zero[] = {GS_R_HB, GS_R_MV, GS_R_GC, GS_R_HELD, GS_R_FD_SUM, GS_R_FD_CNT, GS_R_FD_STATE,
-                        GS_R_RING, GS_R_ROW, GS_R_LAST_W, GS_R_HIST_VER, GS_R_HIST_META, GS_R_HIST_VID,
+                        GS_R_RING, GS_R_ROW, GS_R_LAST_W, GS_R_HIST, GS_R_HIST_VID,
                         GS_R_STAMP, GS_R_COUNTERS};
     for (int r : zero)
         if (h->bytes[r]) HIPCHK(h, hipMemsetAsync(h->reg[r], 0, h->bytes[r], s));
@@ -984,12 +1076,20 @@ int gs_run_phase(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t 
     if (!n) return GS_OK;
     if (!ini || !res) return GS_E_INVALID;
     const bool genm = !(h->cfg.flags & GS_CANONICAL);
-    const size_t lds = (size_t)(h->NP / 32) * (genm ? 4 : 2) * 4;
+    const size_t lds = 32 * WAVE * 4 + (size_t)(h->NP / 32) * (genm ? 4 : 2) * 4;
     if (lds > 160 * 1024) return fail(h, GS_E_UNSUPPORTED, "n_nodes too large for the LDS bitmaps (%zu B)", lds);
-    if (lds > 64 * 1024)
-        HIPCHK(h, hipFuncSetAttribute((const void *)k_exchange, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     h->seq += 1;
-    k_exchange<<<n, XB, lds, h->stream>>>(h->d, ini, res, n, tick, h->seq);
+    if (h->KP <= 16) {
+        if (lds > 64 * 1024)
+            HIPCHK(h, hipFuncSetAttribute((const void *)k_exchange<4>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                          (int)lds));
+        k_exchange<4><<<n, XB, lds, h->stream>>>(h->d, ini, res, n, tick, h->seq);
+    } else {
+        if (lds > 64 * 1024)
+            HIPCHK(h, hipFuncSetAttribute((const void *)k_exchange<16>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                          (int)lds));
+        k_exchange<16><<<n, XB, lds, h->stream>>>(h->d, ini, res, n, tick, h->seq);
+    }
     HIPCHK(h, hipGetLastError());
     return GS_OK;
 }

@@ -300,8 +300,10 @@ class GossipSim:
         for name in ("HB", "MV", "GC", "FD_LAST", "FD_SUM", "FD_CNT", "FD_STATE"):
             g[name] = self.region(name, torch.int32, (n, NP)).cpu().numpy().view(np.uint32)
         g["HELD"] = self.region("HELD", torch.uint8, (n, NP, KP)).cpu().numpy()
-        for name in ("HIST_VER", "HIST_META", "HIST_VID"):
-            g[name] = self.region(name, torch.int32, (n, Cc, K)).cpu().numpy().view(np.uint32)
+        hist = self.region("HIST", torch.int64, (n, Cc, K)).cpu().numpy().view(np.uint64)
+        g["HIST_VER"] = (hist & 0xFFFFFFFF).astype(np.uint32)
+        g["HIST_META"] = (hist >> 32).astype(np.uint32)
+        g["HIST_VID"] = self.region("HIST_VID", torch.int32, (n, Cc, K)).cpu().numpy().view(np.uint32)
         g["ROW"] = self.region("ROW", torch.int32, (n, 4)).cpu().numpy().view(np.uint32)
         if "TS" in self.regions:
             g["TS"] = self.region("TS", torch.int32, (n, NP, KP)).cpu().numpy().view(np.uint32)

@@ -113,9 +113,10 @@ def cpu_baseline(sim, spec, cfg, next_plan, sample: int):
                       int(cfg["window"]), orc_mod.us(cfg["max_interval_s"]), orc_mod.us(cfg["initial_interval_s"]),
                       orc_mod.us(cfg["dead_grace_s"]))
     h = L.orc_create(C.byref(oc), ns, kl)
-    hist_ver = sim.region("HIST_VER", torch.int32, (n, Cc, K)).cpu().numpy().view(np.uint32).copy()
+    hist = sim.region("HIST", torch.int64, (n, Cc, K)).cpu().numpy().view(np.uint64)
+    hist_ver = np.ascontiguousarray((hist & 0xFFFFFFFF).astype(np.uint32))
     hist_vid = sim.region("HIST_VID", torch.int32, (n, Cc, K)).cpu().numpy().view(np.uint32).copy()
-    meta = sim.region("HIST_META", torch.int32, (n, Cc, K)).cpu().numpy().view(np.uint32)
+    meta = (hist >> 32).astype(np.uint32)
     hist_vlen = (meta >> 18).astype(np.int32)
     hist_st = ((meta >> 16) & 3).astype(np.uint8)
     # disjoint pairs from the first phase of the next round

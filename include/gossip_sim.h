@@ -84,8 +84,8 @@ enum gs_region {
     GS_R_ROW,         /* u32 [N][4]    {dict size, tombstone-present flag, first tick a dead target is
                                         scheduled for deletion, reserved} */
     GS_R_LAST_W,      /* u8  [N][KP]   owner's latest write ordinal per key */
-    GS_R_HIST_VER,    /* u32 [N][C][K] version of write w of (owner, key) */
-    GS_R_HIST_META,   /* u32 [N][C][K] KeyValueUpdatePb size | status << 16 | value bytes << 18 */
+    GS_R_HIST,        /* u64 [N][C][K] write w of (owner, key): version | meta << 32, where
+                                        meta = KeyValueUpdatePb size | status << 16 | value bytes << 18 */
     GS_R_HIST_VID,    /* u32 [N][C][K] interned value id (host string table) */
     GS_R_NID_SIZE,    /* u16 [NP]      NodeIdPb size per node (entities.py:62-72) */
     GS_R_KEY_LEN,     /* u8  [KP]      UTF-8 key length per key index */
