@@ -58,6 +58,7 @@ typedef struct oobs {
     int32_t ndead;
     int64_t *tod;             /* time of death, valid when dead_pos >= 0 */
     int32_t *dead_pos;
+    struct oobs *snap;        /* orc_snapshot_row copy */
 } oobs;
 
 typedef struct ond {          /* NodeDelta (state.py:66-72) */
@@ -203,6 +204,11 @@ void orc_destroy(orc *o) {
         for (int32_t j = 0; j < o->N; j++) free(b->w[j].vals);
         free(b->order); free(b->pos); free(b->v); free(b->kv); free(b->w); free(b->live);
         free(b->dead_order); free(b->tod); free(b->dead_pos);
+        if (b->snap) {
+            oobs *c = b->snap;
+            free(c->order); free(c->pos); free(c->v); free(c->kv); free(c->w); free(c->live);
+            free(c->dead_order); free(c->tod); free(c->dead_pos); free(c);
+        }
     }
     for (int d = 0; d < 2; d++) {
         free(o->dg[d].has); free(o->dg[d].hb); free(o->dg[d].gc); free(o->dg[d].mv); free(o->dg[d].list);
@@ -821,3 +827,41 @@ void orc_kat_win_append(orc *o, int32_t obs, int32_t target, double x) {
 double orc_kat_win_sum(orc *o, int32_t obs, int32_t target) { return row(o, obs)->w[target].sum; }
 int32_t orc_kat_win_len(orc *o, int32_t obs, int32_t target) { return win_len(&row(o, obs)->w[target], o->c.window); }
 int32_t orc_kat_win_filled(orc *o, int32_t obs, int32_t target) { return row(o, obs)->w[target].filled; }
+
+/* ------------------------------------------------------------- snapshots */
+void orc_snapshot_row(orc *o, int32_t obs) {
+    oobs *b = row(o, obs);
+    const int32_t N = o->N;
+    if (!b->snap) {
+        b->snap = xcalloc(1, sizeof(oobs));
+        oobs *c = b->snap;
+        c->order = xcalloc(N, sizeof(int32_t)); c->pos = xcalloc(N, sizeof(int32_t));
+        c->v = xcalloc(N, sizeof(oview)); c->kv = xcalloc((size_t)N * o->K, sizeof(okv));
+        c->w = xcalloc(N, sizeof(owin)); c->live = xcalloc(N, 1);
+        c->dead_order = xcalloc(N, sizeof(int32_t)); c->tod = xcalloc(N, sizeof(int64_t));
+        c->dead_pos = xcalloc(N, sizeof(int32_t));
+    }
+    oobs *c = b->snap;
+    c->cnt = b->cnt; c->ndead = b->ndead;
+    memcpy(c->order, b->order, sizeof(int32_t) * N); memcpy(c->pos, b->pos, sizeof(int32_t) * N);
+    memcpy(c->v, b->v, sizeof(oview) * N); memcpy(c->kv, b->kv, sizeof(okv) * (size_t)N * o->K);
+    memcpy(c->w, b->w, sizeof(owin) * N); memcpy(c->live, b->live, N);
+    memcpy(c->dead_order, b->dead_order, sizeof(int32_t) * N); memcpy(c->tod, b->tod, sizeof(int64_t) * N);
+    memcpy(c->dead_pos, b->dead_pos, sizeof(int32_t) * N);
+    /* ring storage is not copied: snapshots are taken of rows whose windows hold no ring yet */
+    for (int32_t j = 0; j < N; j++) { c->w[j].vals = NULL; c->w[j].cap_alloc = 0; }
+}
+
+void orc_restore_row(orc *o, int32_t obs) {
+    oobs *b = row(o, obs);
+    oobs *c = b->snap;
+    if (!c) return;
+    const int32_t N = o->N;
+    for (int32_t j = 0; j < N; j++) free(b->w[j].vals);
+    b->cnt = c->cnt; b->ndead = c->ndead;
+    memcpy(b->order, c->order, sizeof(int32_t) * N); memcpy(b->pos, c->pos, sizeof(int32_t) * N);
+    memcpy(b->v, c->v, sizeof(oview) * N); memcpy(b->kv, c->kv, sizeof(okv) * (size_t)N * o->K);
+    memcpy(b->w, c->w, sizeof(owin) * N); memcpy(b->live, c->live, N);
+    memcpy(b->dead_order, c->dead_order, sizeof(int32_t) * N); memcpy(b->tod, c->tod, sizeof(int64_t) * N);
+    memcpy(b->dead_pos, c->dead_pos, sizeof(int32_t) * N);
+}

@@ -105,6 +105,11 @@ void orc_load_row(orc *o, int32_t obs, int32_t cnt, const int32_t *order,
                   const uint32_t *fd_last_tick, const uint32_t *fd_sum_tick, const uint32_t *fd_len,
                   const uint32_t *fd_state, int64_t tick_us);
 
+/* Keep a copy of observer obs's row / put it back (the CPU baseline re-runs the same
+ * exchanges on restored rows to accumulate a bounded, repeatable sample). */
+void orc_snapshot_row(orc *o, int32_t obs);
+void orc_restore_row(orc *o, int32_t obs);
+
 /* ------------------------------------------- method-level hooks (KAT ports)
  * Direct access to single NodeState / ClusterState / FailureDetector methods so the
  * reference's own unit tests (tests/test_state.py, test_node_state.py,

@@ -77,6 +77,8 @@ def lib():
             "orc_get_stats": (None, [P, C.POINTER(_Stats)]),
             "orc_export_row": (None, [P, i32] + [P] * 13),
             "orc_load_row": (None, [P, i32, i32, P, P, P, P, P, i32, P, P, P, P, P, P, P, P, i64]),
+            "orc_snapshot_row": (None, [P, i32]),
+            "orc_restore_row": (None, [P, i32]),
             "orc_kat_set_view": (None, [P, i32, i32, u32, u32, u32]),
             "orc_kat_set_kv": (None, [P, i32, i32, i32, u32, i32, u32, i32, i64]),
             "orc_kat_apply_heartbeat": (i32, [P, i32, i32, u32]),

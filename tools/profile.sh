@@ -1,0 +1,16 @@
+#!/bin/bash
+# rocprofv3 evidence for bench.py (run on the GPU box via gpurun).
+#   1. kernel trace + stats (per-kernel average duration)
+#   2. PMC FETCH_SIZE and WRITE_SIZE in separate passes (MI355X_MICROARCH.md, HBM section)
+# Usage: tools/profile.sh <tag> [bench args...]
+set -eo pipefail
+R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+TAG=$1; shift
+ARGS=${@:---steps 3 --warmup 1 --no-cpu-baseline}
+OUT=$R/gpurun_out/prof_$TAG
+mkdir -p $OUT
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/kt -o kt --output-format csv -- python3 $R/bench.py $ARGS > $OUT/bench_kt.log 2>&1
+timeout -k 10 900 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $OUT/fetch -o fetch --output-format csv -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline > $OUT/bench_fetch.log 2>&1
+timeout -k 10 900 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $OUT/write -o write --output-format csv -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline > $OUT/bench_write.log 2>&1
+find $OUT -name "*.csv" | xargs ls -la
