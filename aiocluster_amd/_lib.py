@@ -26,8 +26,16 @@ GS_FD_RING = 4
 GS_NONE = 0xFFFFFFFF
 TICK_US = 15_625
 
+
+def fd_sum_bits(window: int) -> int:
+    """Bits of the packed window's interval sum (include/gossip_sim.h, GS_R_FD)."""
+    cnt_bits = 1
+    while (1 << cnt_bits) <= 2 * window:
+        cnt_bits += 1
+    return 32 - cnt_bits
+
 REGIONS = [
-    "HB", "MV", "GC", "HELD", "FD_LAST", "FD_SUM", "FD_CNT", "FD_STATE", "TS", "RING", "POS", "ORD", "ROW",
+    "HB", "MV", "GC", "HELD", "FD", "FD_STATE", "TS", "RING", "POS", "ORD", "ROW",
     "LAST_W", "HIST", "HIST_VID", "NID_SIZE", "KEY_LEN", "STAMP", "COUNTERS",
 ]
 REGION = {n: i for i, n in enumerate(REGIONS)}

@@ -56,11 +56,12 @@ static_assert(sizeof(gs_counters) == 32 * 8, "gs_counters layout");
 
 struct Dev {
     uint32_t N, NP, K, KP, C, mtu, flags, W;
-    uint32_t max_iv, tomb_grace, dead_grace, sched_delay, lb_min;
+    uint32_t max_iv, tomb_grace, dead_grace, sched_delay, lb_min, sum_bits;
     double phi_thr, prior5;
     uint32_t *hb, *mv, *gc;
     uint8_t *held;
-    uint32_t *fd_last, *fd_sum, *fd_cnt, *fd_state, *ts;
+    uint64_t *fd;  // sampling window: (last tick + 1) | (sum | cnt << sum_bits) << 32; 0 = no window
+    uint32_t *fd_state, *ts;
     uint16_t *ring;
     uint32_t *pos, *ord, *row;
     uint8_t *last_w;
@@ -95,6 +96,21 @@ __device__ inline uint32_t make_meta(uint32_t kvlen, uint32_t status, uint32_t v
 // FailureDetector.scheduled_for_deletion_nodes (failure_detector.py:121-128): now >= tod + grace/2.
 __device__ inline bool is_sched(uint32_t st, uint32_t t, uint32_t delay) {
     return st >= 2u && (t - (st - 2u)) >= delay;
+}
+
+// One sampling window (SamplingWindow + BoundedArrayStats, failure_detector.py:12-53, 131-162) per
+// pair in 8 bytes: low word = _last_heartbeat tick + 1 (0 = no window), high word = _sum in ticks
+// (sum_bits wide, exact: every interval is a whole number of 1/64 s) | intervals appended since the
+// last reset << sum_bits.
+struct Fd {
+    uint32_t last, sum, cnt;  // last = NONE when there is no window
+};
+__device__ inline Fd fd_unpack(const Dev &d, uint64_t v) {
+    const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+    return Fd{lo - 1u, hi & ((1u << d.sum_bits) - 1u), hi >> d.sum_bits};
+}
+__device__ inline uint64_t fd_pack(const Dev &d, Fd f) {
+    return (uint64_t)(f.last + 1u) | ((uint64_t)(f.sum | (f.cnt << d.sum_bits)) << 32);
 }
 
 __device__ inline int lane_id() { return (int)__lane_id(); }
@@ -401,7 +417,8 @@ __device__ __forceinline__ void pack_dir(const Dev &d, uint32_t s, uint32_t r, c
 // Pass-1 work of one group of 4 consecutive owners (one 16-byte load per array and row), held
 // as scalar arrays so every element stays in a register after unrolling.
 struct Grp {
-    uint32_t hA[4], hB[4], mA[4], mB[4], lA[4], lB[4], sA[4], sB[4], cA[4], cB[4], pA[4], pB[4], fA[4], fB[4];
+    uint32_t hA[4], hB[4], mA[4], mB[4], pA[4], pB[4], fA[4], fB[4];
+    uint64_t wA[4], wB[4];  // packed sampling windows
 };
 
 __device__ __forceinline__ void ld4(const uint32_t *p, uint32_t (&v)[4]) {
@@ -410,6 +427,14 @@ __device__ __forceinline__ void ld4(const uint32_t *p, uint32_t (&v)[4]) {
 }
 __device__ __forceinline__ void st4(uint32_t *p, const uint32_t (&v)[4]) {
     *reinterpret_cast<uint4 *>(p) = make_uint4(v[0], v[1], v[2], v[3]);
+}
+__device__ __forceinline__ void ld4w(const uint64_t *p, uint64_t (&v)[4]) {
+    const ulonglong2 x = reinterpret_cast<const ulonglong2 *>(p)[0], y = reinterpret_cast<const ulonglong2 *>(p)[1];
+    v[0] = x.x; v[1] = x.y; v[2] = y.x; v[3] = y.y;
+}
+__device__ __forceinline__ void st4w(uint64_t *p, const uint64_t (&v)[4]) {
+    reinterpret_cast<ulonglong2 *>(p)[0] = make_ulonglong2(v[0], v[1]);
+    reinterpret_cast<ulonglong2 *>(p)[1] = make_ulonglong2(v[2], v[3]);
 }
 
 __device__ __forceinline__ void load_grp(const Dev &d, size_t ra, size_t rb, uint32_t c0, bool genm, bool schA,
@@ -420,22 +445,14 @@ __device__ __forceinline__ void load_grp(const Dev &d, size_t ra, size_t rb, uin
     ld4(d.mv + rb + c0, g.mB);
     // failure-detector fields are prefetched unconditionally: about half the owners report per
     // exchange, so every 64-byte line of both rows is touched anyway
-    ld4(d.fd_last + ra + c0, g.lA);
-    ld4(d.fd_last + rb + c0, g.lB);
-    ld4(d.fd_sum + ra + c0, g.sA);
-    ld4(d.fd_sum + rb + c0, g.sB);
-    ld4(d.fd_cnt + ra + c0, g.cA);
-    ld4(d.fd_cnt + rb + c0, g.cB);
+    ld4w(d.fd + ra + c0, g.wA);
+    ld4w(d.fd + rb + c0, g.wB);
 #pragma unroll
     for (int i = 0; i < 4; i++) { g.pA[i] = g.pB[i] = g.fA[i] = g.fB[i] = 0u; }
     if (genm) { ld4(d.pos + ra + c0, g.pA); ld4(d.pos + rb + c0, g.pB); }
     if (schA) ld4(d.fd_state + ra + c0, g.fA);
     if (schB) ld4(d.fd_state + rb + c0, g.fB);
 }
-
-struct Fd {
-    uint32_t last, sum, cnt;
-};
 
 // FailureDetector.report_heartbeat -> SamplingWindow.report_heartbeat on prefetched fields
 // (failure_detector.py:79-81, 32-38): the first report only records the time; later intervals
@@ -462,7 +479,7 @@ __device__ __forceinline__ Fd fd_report_val(const Dev &d, size_t p, uint32_t t, 
         }
     }
     f.last = t;
-    alg += 24;
+    alg += 16;
     return f;
 }
 
@@ -500,14 +517,12 @@ __device__ __forceinline__ void pass1_grp(const Dev &d, size_t ra, size_t rb, ui
             g.hA[i] = hA;
             g.hB[i] = hB;
             if (repB) {
-                const Fd f = fd_report_val(d, rb + j, t, Fd{g.lB[i], g.sB[i], g.cB[i]}, alg, ovf);
-                g.lB[i] = f.last; g.sB[i] = f.sum; g.cB[i] = f.cnt;
+                g.wB[i] = fd_pack(d, fd_report_val(d, rb + j, t, fd_unpack(d, g.wB[i]), alg, ovf));
                 fdB = true;
                 reports++;
             }
             if (repA) {
-                const Fd f = fd_report_val(d, ra + j, t, Fd{g.lA[i], g.sA[i], g.cA[i]}, alg, ovf);
-                g.lA[i] = f.last; g.sA[i] = f.sum; g.cA[i] = f.cnt;
+                g.wA[i] = fd_pack(d, fd_report_val(d, ra + j, t, fd_unpack(d, g.wA[i]), alg, ovf));
                 fdA = true;
                 reports++;
             }
@@ -522,8 +537,8 @@ __device__ __forceinline__ void pass1_grp(const Dev &d, size_t ra, size_t rb, ui
     }
     if (dA) { st4(d.hb + ra + c0, g.hA); alg += 16; }
     if (dB) { st4(d.hb + rb + c0, g.hB); alg += 16; }
-    if (fdA) { st4(d.fd_last + ra + c0, g.lA); st4(d.fd_sum + ra + c0, g.sA); st4(d.fd_cnt + ra + c0, g.cA); }
-    if (fdB) { st4(d.fd_last + rb + c0, g.lB); st4(d.fd_sum + rb + c0, g.sB); st4(d.fd_cnt + rb + c0, g.cB); }
+    if (fdA) st4w(d.fd + ra + c0, g.wA);
+    if (fdB) st4w(d.fd + rb + c0, g.wB);
 }
 
 template <int KW>
@@ -695,47 +710,40 @@ __global__ __launch_bounds__(LB) void k_liveness(Dev d, const uint8_t *up, uint3
     const uint32_t c0 = (cb * LB + threadIdx.x) * 4u;
     if (c0 < d.N) {
         const size_t p = pix(d, o, c0);
-        const uint4 L4 = *reinterpret_cast<const uint4 *>(d.fd_last + p);
-        uint4 S4 = *reinterpret_cast<const uint4 *>(d.fd_sum + p);
-        uint4 C4 = *reinterpret_cast<const uint4 *>(d.fd_cnt + p);
-        uint4 T4 = *reinterpret_cast<const uint4 *>(d.fd_state + p);
-        uint4 P4 = make_uint4(0, 0, 0, 0);
-        if (genm) P4 = *reinterpret_cast<const uint4 *>(d.pos + p);
-        const uint32_t *L = reinterpret_cast<const uint32_t *>(&L4);
-        uint32_t *Sm = reinterpret_cast<uint32_t *>(&S4), *Cn = reinterpret_cast<uint32_t *>(&C4);
-        uint32_t *St = reinterpret_cast<uint32_t *>(&T4);
-        const uint32_t *Ps = reinterpret_cast<const uint32_t *>(&P4);
-        bool dirty = false;
+        uint64_t w[4];
+        uint32_t st[4], ps[4] = {0u, 0u, 0u, 0u};
+        ld4w(d.fd + p, w);
+        ld4(d.fd_state + p, st);
+        if (genm) ld4(d.pos + p, ps);
+        bool dw = false, ds = false;
 #pragma unroll
         for (int i = 0; i < 4; i++) {
             const uint32_t j = c0 + i;
-            if (j >= d.N) break;
-            if (j == o || (genm && Ps[i] == NONE)) continue;
-            live++;
-            const bool has = L[i] != NONE;
-            const uint32_t len = ring ? (Cn[i] < d.W ? Cn[i] : d.W) : Cn[i];
-            bool alive = false;
-            if (has && len) {
-                const double mean = ((double)Sm[i] * TICK_S + d.prior5) / ((double)len + 5.0);
-                const double phi = ((double)(t - L[i]) * TICK_S) / mean;
-                alive = phi <= d.phi_thr;
-            }
-            if (alive) {
-                if (St[i] != 1u) { St[i] = 1u; dirty = true; }
-            } else {
-                if (St[i] < 2u) { St[i] = 2u + t; dirty = true; }  // time_of_death recorded once
-                if (has && (Sm[i] | Cn[i])) { Sm[i] = 0; Cn[i] = 0; dirty = true; }  // window reset
-                const uint32_t tod = St[i] - 2u;
-                const uint32_t sat = tod + d.sched_delay;
-                if (sat < minS) minS = sat;
-                if ((uint64_t)t >= (uint64_t)tod + d.dead_grace) gcdue++;
+            if (j < d.N && j != o && !(genm && ps[i] == NONE)) {
+                live++;
+                const Fd f = fd_unpack(d, w[i]);
+                const bool has = f.last != NONE;
+                const uint32_t len = ring ? (f.cnt < d.W ? f.cnt : d.W) : f.cnt;
+                bool alive = false;
+                if (has && len) {
+                    const double mean = ((double)f.sum * TICK_S + d.prior5) / ((double)len + 5.0);
+                    const double phi = ((double)(t - f.last) * TICK_S) / mean;
+                    alive = phi <= d.phi_thr;
+                }
+                if (alive) {
+                    if (st[i] != 1u) { st[i] = 1u; ds = true; }
+                } else {
+                    if (st[i] < 2u) { st[i] = 2u + t; ds = true; }  // time_of_death recorded once
+                    if (has && (f.sum | f.cnt)) { w[i] = fd_pack(d, Fd{f.last, 0u, 0u}); dw = true; }  // reset
+                    const uint32_t tod = st[i] - 2u;
+                    const uint32_t sat = tod + d.sched_delay;
+                    if (sat < minS) minS = sat;
+                    if ((uint64_t)t >= (uint64_t)tod + d.dead_grace) gcdue++;
+                }
             }
         }
-        if (dirty) {
-            *reinterpret_cast<uint4 *>(d.fd_sum + p) = S4;
-            *reinterpret_cast<uint4 *>(d.fd_cnt + p) = C4;
-            *reinterpret_cast<uint4 *>(d.fd_state + p) = T4;
-        }
+        if (dw) st4w(d.fd + p, w);
+        if (ds) st4(d.fd_state + p, st);
     }
     // earliest scheduled-for-deletion tick of this row
     for (int dd = 32; dd >= 1; dd >>= 1) {
@@ -754,13 +762,12 @@ __global__ __launch_bounds__(LB) void k_liveness(Dev d, const uint8_t *up, uint3
 __global__ __launch_bounds__(LB) void k_phi_row(Dev d, uint32_t o, uint32_t t, double *out) {
     const uint32_t j = blockIdx.x * LB + threadIdx.x;
     if (j >= d.N) return;
-    const size_t p = pix(d, o, j);
-    const uint32_t last = d.fd_last[p], cnt = d.fd_cnt[p];
-    const uint32_t len = (d.flags & GS_FD_RING) ? (cnt < d.W ? cnt : d.W) : cnt;
+    const Fd f = fd_unpack(d, d.fd[pix(d, o, j)]);
+    const uint32_t len = (d.flags & GS_FD_RING) ? (f.cnt < d.W ? f.cnt : d.W) : f.cnt;
     double phi = __builtin_nan("");
-    if (last != NONE && len) {
-        const double mean = ((double)d.fd_sum[p] * TICK_S + d.prior5) / ((double)len + 5.0);
-        phi = ((double)(t - last) * TICK_S) / mean;
+    if (f.last != NONE && len) {
+        const double mean = ((double)f.sum * TICK_S + d.prior5) / ((double)len + 5.0);
+        phi = ((double)(t - f.last) * TICK_S) / mean;
     }
     out[j] = phi;
 }
@@ -899,9 +906,7 @@ int check_bound(gs_handle *h) {
     d.mv = (uint32_t *)h->reg[GS_R_MV];
     d.gc = (uint32_t *)h->reg[GS_R_GC];
     d.held = (uint8_t *)h->reg[GS_R_HELD];
-    d.fd_last = (uint32_t *)h->reg[GS_R_FD_LAST];
-    d.fd_sum = (uint32_t *)h->reg[GS_R_FD_SUM];
-    d.fd_cnt = (uint32_t *)h->reg[GS_R_FD_CNT];
+    d.fd = (uint64_t *)h->reg[GS_R_FD];
     d.fd_state = (uint32_t *)h->reg[GS_R_FD_STATE];
     d.ts = (uint32_t *)h->reg[GS_R_TS];
     d.ring = (uint16_t *)h->reg[GS_R_RING];
@@ -935,7 +940,11 @@ int gs_create(const gs_config *cfg, gs_handle **out) {
     if (c.hist_cap < 2 || c.hist_cap > 255) return GS_E_INVALID;
     if (c.mtu < 1 || c.window < 1) return GS_E_INVALID;
     if ((c.flags & GS_FD_RING) && (c.window > (1u << 20) || c.max_interval_ticks > 0xFFFFu)) return GS_E_INVALID;
-    if ((uint64_t)c.window * c.max_interval_ticks >= (1ull << 32)) return GS_E_INVALID;
+    // packed window: cnt < 2W needs cnt_bits, the sum of <= W intervals <= max_interval the rest of 32
+    uint32_t cnt_bits = 1;
+    while ((1ull << cnt_bits) <= 2ull * c.window) cnt_bits++;
+    const uint32_t sum_bits = 32 - cnt_bits;
+    if (cnt_bits > 31 || (uint64_t)c.window * c.max_interval_ticks >= (1ull << sum_bits)) return GS_E_INVALID;
     gs_handle *h = new gs_handle();
     h->cfg = c;
     h->N = c.n_nodes;
@@ -953,7 +962,8 @@ int gs_create(const gs_config *cfg, gs_handle **out) {
     uint64_t *b = h->bytes;
     b[GS_R_HB] = b[GS_R_MV] = b[GS_R_GC] = pairs * 4;
     b[GS_R_HELD] = pairs * KP;
-    b[GS_R_FD_LAST] = b[GS_R_FD_SUM] = b[GS_R_FD_CNT] = b[GS_R_FD_STATE] = pairs * 4;
+    b[GS_R_FD] = pairs * 8;
+    b[GS_R_FD_STATE] = pairs * 4;
     b[GS_R_TS] = (c.flags & GS_TOMBSTONES) ? pairs * KP * 4 : 0;
     b[GS_R_RING] = (c.flags & GS_FD_RING) ? pairs * W * 2 : 0;
     b[GS_R_POS] = b[GS_R_ORD] = genm ? pairs * 4 : 0;
@@ -979,6 +989,7 @@ int gs_create(const gs_config *cfg, gs_handle **out) {
     d.tomb_grace = c.tombstone_grace_ticks;
     d.dead_grace = c.dead_grace_ticks;
     d.sched_delay = c.sched_delay_ticks;
+    d.sum_bits = sum_bits;
     d.phi_thr = c.phi_threshold;
     d.prior5 = c.prior_weighted;
     *out = h;
@@ -1014,12 +1025,11 @@ int gs_boot(gs_handle *h, const uint16_t *nid_size, const uint8_t *key_len) {
     hipStream_t s = h->stream;
     const uint64_t pairs = (uint64_t)h->N * h->NP;
     // regions that start at zero
-    const int zero[] = {GS_R_HB, GS_R_MV, GS_R_GC, GS_R_HELD, GS_R_FD_SUM, GS_R_FD_CNT, GS_R_FD_STATE,
+    const int zero[] = {GS_R_HB, GS_R_MV, GS_R_GC, GS_R_HELD, GS_R_FD, GS_R_FD_STATE,
                         GS_R_RING, GS_R_ROW, GS_R_LAST_W, GS_R_HIST, GS_R_HIST_VID,
                         GS_R_STAMP, GS_R_COUNTERS};
     for (int r : zero)
         if (h->bytes[r]) HIPCHK(h, hipMemsetAsync(h->reg[r], 0, h->bytes[r], s));
-    HIPCHK(h, hipMemsetAsync(h->reg[GS_R_FD_LAST], 0xFF, pairs * 4, s));
     if (h->bytes[GS_R_TS]) HIPCHK(h, hipMemsetAsync(h->reg[GS_R_TS], 0xFF, h->bytes[GS_R_TS], s));
     if (h->bytes[GS_R_POS]) HIPCHK(h, hipMemsetAsync(h->reg[GS_R_POS], 0xFF, h->bytes[GS_R_POS], s));
     if (h->bytes[GS_R_ORD]) HIPCHK(h, hipMemsetAsync(h->reg[GS_R_ORD], 0xFF, h->bytes[GS_R_ORD], s));

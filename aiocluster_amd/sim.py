@@ -79,6 +79,25 @@ def make_config(n: int, k: int, cfg: dict, flags: int, hist_cap: int) -> _lib.Gs
     return c
 
 
+def split_owner_batches(ops: list[tuple]) -> list[list[tuple]]:
+    """Split owner writes ``(tick, owner, ...)`` into device batches of distinct owners.
+
+    ``k_owner_writes`` runs one thread per write, so two writes of one owner must
+    not share a batch; the i-th write of an owner goes to batch i, which keeps
+    every owner's writes in call order (what NodeState.set/... sequences need).
+    """
+    batches: list[list[tuple]] = []
+    seen: dict[int, int] = {}
+    for op in ops:
+        j = op[1]
+        b = seen.get(j, 0)
+        seen[j] = b + 1
+        while len(batches) <= b:
+            batches.append([])
+        batches[b].append(op)
+    return batches
+
+
 class GossipSim:
     """A simulated cluster of ``len(node_ids)`` aiocluster nodes resident on one MI355X."""
 
@@ -210,15 +229,7 @@ class GossipSim:
     def _flush(self):
         if not self._pending:
             return
-        # split into batches of distinct owners, keeping each owner's order
-        batches: list[list] = []
-        seen: dict[int, int] = {}
-        for t, j, k, op, vid, vl in self._pending:
-            b = seen.get(j, 0)
-            seen[j] = b + 1
-            while len(batches) <= b:
-                batches.append([])
-            batches[b].append((t, j, k, op, vid, vl))
+        batches = split_owner_batches(self._pending)
         self._pending = []
         for batch in batches:
             ticks = {x[0] for x in batch}
@@ -297,8 +308,9 @@ class GossipSim:
         torch = self.torch
         self.sync()
         g = {}
-        for name in ("HB", "MV", "GC", "FD_LAST", "FD_SUM", "FD_CNT", "FD_STATE"):
+        for name in ("HB", "MV", "GC", "FD_STATE"):
             g[name] = self.region(name, torch.int32, (n, NP)).cpu().numpy().view(np.uint32)
+        g["FD_LAST"], g["FD_SUM"], g["FD_CNT"] = self.unpack_fd(self.region("FD", torch.int64, (n, NP)).cpu().numpy())
         g["HELD"] = self.region("HELD", torch.uint8, (n, NP, KP)).cpu().numpy()
         hist = self.region("HIST", torch.int64, (n, Cc, K)).cpu().numpy().view(np.uint64)
         g["HIST_VER"] = (hist & 0xFFFFFFFF).astype(np.uint32)
@@ -345,6 +357,15 @@ class GossipSim:
         out["live"] = (st == 1).astype(np.int32)
         out["tod"] = np.where(st >= 2, st.astype(np.int64) - 2, -1)
         return out
+
+    def unpack_fd(self, packed: np.ndarray):
+        """Split packed windows (GS_R_FD) into (last tick or GS_NONE, sum in ticks, appended count)."""
+        v = packed.view(np.uint64)
+        lo = (v & 0xFFFFFFFF).astype(np.uint32)
+        hi = (v >> 32).astype(np.uint32)
+        sb = _lib.fd_sum_bits(int(self.cfg["window"]))
+        last = (lo - np.uint32(1)).astype(np.uint32)  # 0 - 1 wraps to GS_NONE
+        return last, hi & np.uint32((1 << sb) - 1), hi >> np.uint32(sb)
 
     def phi_row(self, observer: int, tick: int | None = None) -> np.ndarray:
         """Device-computed phi (binary64) of every target of ``observer``; NaN = None."""

@@ -128,19 +128,20 @@ def cpu_baseline(sim, spec, cfg, next_plan, sample: int, min_seconds: float = 10
     def rows(name, dt, shape):
         return sim.region(name, dt, shape)
 
-    hb, mv, gc = (rows(x, torch.int32, (n, NP)) for x in ("HB", "MV", "GC"))
-    fl, fs, fc, fst = (rows(x, torch.int32, (n, NP)) for x in ("FD_LAST", "FD_SUM", "FD_CNT", "FD_STATE"))
+    hb, mv, gc, fst = (rows(x, torch.int32, (n, NP)) for x in ("HB", "MV", "GC", "FD_STATE"))
+    fdw = rows("FD", torch.int64, (n, NP))
     held = rows("HELD", torch.uint8, (n, NP, KP))
     P = C.c_void_p
     for a, b in pairs:
         for o in (a, b):
             def g(x):
                 return np.ascontiguousarray(x[o, :n].cpu().numpy().view(np.uint32))
+            fl, fs, fc = (np.ascontiguousarray(x) for x in sim.unpack_fd(fdw[o, :n].cpu().numpy()))
             hw = np.ascontiguousarray(held[o, :n, :K].cpu().numpy())
             L.orc_load_row(h, o, n, order.ctypes.data_as(P), g(hb).ctypes.data_as(P), g(mv).ctypes.data_as(P),
                            g(gc).ctypes.data_as(P), hw.ctypes.data_as(P), Cc, hist_ver.ctypes.data_as(P),
                            hist_vid.ctypes.data_as(P), hist_vlen.ctypes.data_as(P), hist_st.ctypes.data_as(P),
-                           g(fl).ctypes.data_as(P), g(fs).ctypes.data_as(P), g(fc).ctypes.data_as(P),
+                           fl.ctypes.data_as(P), fs.ctypes.data_as(P), fc.ctypes.data_as(P),
                            g(fst).ctypes.data_as(P), 15625)
     for a, b in pairs:
         L.orc_snapshot_row(h, a)
@@ -169,6 +170,19 @@ def cpu_baseline(sim, spec, cfg, next_plan, sample: int, min_seconds: float = 10
                   f"oracle rows copied from the device state after the timed rounds, run {reps}x on restored rows: "
                   f"{dt:.1f} s of single-core CPU work, {st.node_deltas // reps} NodeDeltas per pass",
     }
+
+
+def aggregate(exchanges: float, elapsed: float, dist=None, dev=None) -> tuple[float, float]:
+    """Whole-job totals: exchanges summed over ranks, time = the slowest rank's."""
+    if dist is None:
+        return float(exchanges), float(elapsed)
+    import torch
+
+    ex = torch.tensor([float(exchanges)], dtype=torch.float64, device=dev)
+    tm = torch.tensor([float(elapsed)], dtype=torch.float64, device=dev)
+    dist.all_reduce(ex, op=dist.ReduceOp.SUM)
+    dist.all_reduce(tm, op=dist.ReduceOp.MAX)
+    return float(ex.item()), float(tm.item())
 
 
 def load_traffic(workload: str):
@@ -258,15 +272,7 @@ def main():
     assert c["exchanges"] == exch, (c["exchanges"], exch)
     kern_ms = sum(e0.elapsed_time(e1) for e0, e1 in events)
     launches = len(events)
-    tot = torch.tensor([exch, elapsed], dtype=torch.float64, device=dev)
-    if dist is not None:
-        ex_all = tot[:1].clone()
-        dist.all_reduce(ex_all, op=dist.ReduceOp.SUM)
-        t_max = tot[1:].clone()
-        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
-        exch_total, elapsed_max = float(ex_all.item()), float(t_max.item())
-    else:
-        exch_total, elapsed_max = float(exch), elapsed
+    exch_total, elapsed_max = aggregate(exch, elapsed, dist, dev)
     achieved = c["alg_bytes"] / (kern_ms / 1e3) / 1e9 if kern_ms > 0 else 0.0
     traffic = load_traffic(workload)
     cpu = None

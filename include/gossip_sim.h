@@ -73,9 +73,10 @@ enum gs_region {
     GS_R_MV,          /* u32 [N][NP]   NodeState.max_version */
     GS_R_GC,          /* u32 [N][NP]   NodeState.last_gc_version */
     GS_R_HELD,        /* u8  [N][NP][KP] write ordinal of each key held (0 = absent), KP = K rounded to 4 */
-    GS_R_FD_LAST,     /* u32 [N][NP]   SamplingWindow._last_heartbeat tick, GS_NONE = no window */
-    GS_R_FD_SUM,      /* u32 [N][NP]   BoundedArrayStats._sum in ticks */
-    GS_R_FD_CNT,      /* u32 [N][NP]   intervals appended since the last reset (len = min(cnt, W)) */
+    GS_R_FD,          /* u64 [N][NP]   sampling window: low word = _last_heartbeat tick + 1 (0 = no
+                                        window); high word = _sum in ticks | intervals appended since
+                                        the last reset << sum_bits (len = min(cnt, W)); sum_bits =
+                                        32 - bits(2W) (gs_create rejects W * max_interval >= 2^sum_bits) */
     GS_R_FD_STATE,    /* u32 [N][NP]   0 = unknown, 1 = live, >= 2: dead since tick (v - 2) */
     GS_R_TS,          /* u32 [N][NP][KP] tombstone receive tick, GS_NONE for SET entries (GS_TOMBSTONES) */
     GS_R_RING,        /* u16 [N][NP][W] interval ring in ticks (GS_FD_RING) */
