@@ -45,6 +45,7 @@ constexpr int WAVE = 64;
 constexpr int XB = 128;  // exchange workgroup: 2 waves
 constexpr int LB = 256;  // liveness / elementwise workgroups
 constexpr int NSHARD = 64;
+constexpr uint32_t WIN = 16 * 64;  // positions per packer window (16 per lane)
 constexpr double TICK_S = 1.0 / 64.0;
 
 enum Ctr {
@@ -162,14 +163,14 @@ struct Cand {
 // NodeDelta candidate (state.py:347-390): from_version_excluded, the NodeDeltaPb body without
 // kvs, the DeltaPb bytes of the whole NodeDelta (all kvs with version > from, 392-398) and of
 // its smallest-version kv alone.
-template <int KW>
-__device__ __forceinline__ void eval_cand(const Dev &d, uint32_t s, uint32_t r, const DigestSide &ds, bool genm, uint32_t j,
-                                 uint32_t t, Cand<KW> &c, uint32_t &alg) {
+template <int KW, bool GENM>
+__device__ __forceinline__ void eval_cand(const Dev &d, uint32_t s, uint32_t r, const DigestSide &ds, uint32_t j,
+                                          uint32_t t, Cand<KW> &c, uint32_t &alg) {
     const size_t ps = pix(d, s, j), pr = pix(d, r, j);
     const uint32_t kw = d.KP >> 2;
     // round trip 1
     const uint32_t ms = d.mv[ps], gs = d.gc[ps], mr = d.mv[pr], gr = d.gc[pr];
-    const uint32_t pos_r = genm ? d.pos[pr] : 0u;
+    const uint32_t pos_r = GENM ? d.pos[pr] : 0u;
     const uint32_t fst = ds.sched ? d.fd_state[pr] : 0u;
     const uint32_t *hsp = reinterpret_cast<const uint32_t *>(d.held + ps * d.KP);
     const uint32_t *hrp = reinterpret_cast<const uint32_t *>(d.held + pr * d.KP);
@@ -178,8 +179,8 @@ __device__ __forceinline__ void eval_cand(const Dev &d, uint32_t s, uint32_t r, 
         c.hs[q] = (uint32_t)q < kw ? hsp[q] : 0u;
         c.hr[q] = (uint32_t)q < kw ? hrp[q] : 0u;
     }
-    alg += 16 + 2 * d.KP + (genm ? 4 : 0) + (ds.sched ? 4 : 0);
-    bool in_d = genm ? pos_r < ds.limit : true;
+    alg += 16 + 2 * d.KP + (GENM ? 4 : 0) + (ds.sched ? 4 : 0);
+    bool in_d = GENM ? pos_r < ds.limit : true;
     if (in_d && ds.sched) in_d = !is_sched(fst, t, d.sched_delay);
     const uint32_t dm = in_d ? mr : 0u;
     const uint32_t dg = in_d ? gr : 0u;
@@ -273,32 +274,32 @@ __device__ __forceinline__ void apply_cand(const Dev &d, uint32_t r, const Cand<
 }
 
 // compute_partial_delta_respecting_mtu (state.py:340-415) of sender s for receiver r, fused with
-// r's apply_delta, by one wave.  The sender's dict order is walked in windows of 2048 positions;
+// r's apply_delta, by one wave.  The sender's dict order is walked in windows of 1024 positions;
 // each window's stale owners are compacted (ballot + popcount scan) into a wave-private LDS list
 // and evaluated 64 at a time, one per lane.  Exactness vs the sequential loop: DESIGN.md.
-template <int KW>
-__device__ __forceinline__ void pack_dir(const Dev &d, uint32_t s, uint32_t r, const DigestSide ds, const uint32_t *order,
-                         uint32_t cnt, const uint32_t *bits, uint16_t *wbuf, uint32_t t, bool genm, WStats &st,
-                         bool &tomb) {
+template <int KW, bool GENM>
+__device__ __forceinline__ void pack_dir(const Dev &d, uint32_t s, uint32_t r, const DigestSide ds,
+                                         const uint32_t *order, uint32_t cnt, const uint32_t *bits, uint16_t *wbuf,
+                                         uint32_t t, WStats &st, bool &tomb) {
     const int lane = lane_id();
     const uint32_t mtu = d.mtu;
     uint32_t S = 0;  // DeltaPb bytes committed (wave-uniform)
     bool tail = false, stop = false;
-    for (uint32_t win = 0; win < cnt && !stop; win += 32 * WAVE) {
-        // -- compact this window's stale owners (sender order) into wbuf
+    for (uint32_t win = 0; win < cnt && !stop; win += WIN) {
+        // -- compact this window's stale owners (sender order) into wbuf, 16 positions per lane
         uint32_t m = 0;
-        const uint32_t pb = win + 32u * lane;
+        const uint32_t pb = win + 16u * lane;
         if (pb < cnt) {
-            if (!order) {
-                m = bits[pb >> 5];
+            if (!GENM) {
+                m = (bits[pb >> 5] >> (pb & 16u)) & 0xFFFFu;
             } else {
-                for (uint32_t q = 0; q < 32; q++) {
+                for (uint32_t q = 0; q < 16; q++) {
                     const uint32_t p = pb + q;
                     if (p < cnt && bit(bits, order[p])) m |= 1u << q;
                 }
             }
             const uint32_t lim = cnt - pb;
-            if (lim < 32) m &= (1u << lim) - 1u;
+            if (lim < 16) m &= (1u << lim) - 1u;
         }
         const uint32_t cl = (uint32_t)__popc(m);
         const uint32_t incl = wave_incl_scan(cl);
@@ -309,7 +310,7 @@ __device__ __forceinline__ void pack_dir(const Dev &d, uint32_t s, uint32_t r, c
         while (m) {
             const uint32_t b = (uint32_t)__builtin_ctz(m);
             m &= m - 1u;
-            wbuf[wp++] = (uint16_t)(32u * lane + b);
+            wbuf[wp++] = (uint16_t)(16u * lane + b);
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -321,8 +322,8 @@ __device__ __forceinline__ void pack_dir(const Dev &d, uint32_t s, uint32_t r, c
             c.min1 = 0;
             if (cand) {
                 const uint32_t p = win + wbuf[ci];
-                const uint32_t j = order ? order[p] : p;
-                eval_cand<KW>(d, s, r, ds, genm, j, t, c, st.alg);
+                const uint32_t j = GENM ? order[p] : p;
+                eval_cand<KW, GENM>(d, s, r, ds, j, t, c, st.alg);
                 st.cand++;
             }
             const uint32_t em = cand ? c.emsg : 0u;
@@ -437,8 +438,9 @@ __device__ __forceinline__ void st4w(uint64_t *p, const uint64_t (&v)[4]) {
     reinterpret_cast<ulonglong2 *>(p)[1] = make_ulonglong2(v[2], v[3]);
 }
 
-__device__ __forceinline__ void load_grp(const Dev &d, size_t ra, size_t rb, uint32_t c0, bool genm, bool schA,
-                                         bool schB, Grp &g) {
+template <bool GENM>
+__device__ __forceinline__ void load_grp(const Dev &d, size_t ra, size_t rb, uint32_t c0, bool schA, bool schB,
+                                         Grp &g) {
     ld4(d.hb + ra + c0, g.hA);
     ld4(d.hb + rb + c0, g.hB);
     ld4(d.mv + ra + c0, g.mA);
@@ -449,7 +451,7 @@ __device__ __forceinline__ void load_grp(const Dev &d, size_t ra, size_t rb, uin
     ld4w(d.fd + rb + c0, g.wB);
 #pragma unroll
     for (int i = 0; i < 4; i++) { g.pA[i] = g.pB[i] = g.fA[i] = g.fB[i] = 0u; }
-    if (genm) { ld4(d.pos + ra + c0, g.pA); ld4(d.pos + rb + c0, g.pB); }
+    if (GENM) { ld4(d.pos + ra + c0, g.pA); ld4(d.pos + rb + c0, g.pB); }
     if (schA) ld4(d.fd_state + ra + c0, g.fA);
     if (schB) ld4(d.fd_state + rb + c0, g.fB);
 }
@@ -457,11 +459,12 @@ __device__ __forceinline__ void load_grp(const Dev &d, size_t ra, size_t rb, uin
 // FailureDetector.report_heartbeat -> SamplingWindow.report_heartbeat on prefetched fields
 // (failure_detector.py:79-81, 32-38): the first report only records the time; later intervals
 // <= max_interval go to BoundedArrayStats (139-150).
+template <bool RING>
 __device__ __forceinline__ Fd fd_report_val(const Dev &d, size_t p, uint32_t t, Fd f, uint32_t &alg, uint32_t &ovf) {
     if (f.last != NONE) {
         const uint32_t iv = t - f.last;
         if (iv <= d.max_iv) {
-            if (d.flags & GS_FD_RING) {
+            if (RING) {
                 uint16_t *rg = d.ring + p * d.W;
                 const uint32_t slot = f.cnt % d.W;
                 if (f.cnt >= d.W) f.sum -= rg[slot];  // subtract-then-add (failure_detector.py:140-143)
@@ -483,18 +486,19 @@ __device__ __forceinline__ Fd fd_report_val(const Dev &d, size_t p, uint32_t t, 
     return f;
 }
 
+template <bool GENM, bool RING>
 __device__ __forceinline__ void pass1_grp(const Dev &d, size_t ra, size_t rb, uint32_t c0, uint32_t a, uint32_t b,
-                                          uint32_t t, bool genm, bool schA, bool schB, Grp &g, uint32_t *bBA,
+                                          uint32_t t, bool schA, bool schB, Grp &g, uint32_t *bBA,
                                           uint32_t *bAB, uint32_t *bNB, uint32_t *bNA, uint32_t &alg,
                                           uint32_t &reports, uint32_t &hbw, uint32_t &ovf, bool &anynew) {
     bool dA = false, dB = false, fdA = false, fdB = false;
-    alg += 64 + (genm ? 32 : 0) + (schA ? 16 : 0) + (schB ? 16 : 0);
+    alg += 64 + (GENM ? 32 : 0) + (schA ? 16 : 0) + (schB ? 16 : 0);
 #pragma unroll
     for (int i = 0; i < 4; i++) {
         const uint32_t j = c0 + i;
         if (j < d.N) {
-            const bool pa = genm ? g.pA[i] != NONE : true;
-            const bool pb = genm ? g.pB[i] != NONE : true;
+            const bool pa = GENM ? g.pA[i] != NONE : true;
+            const bool pb = GENM ? g.pB[i] != NONE : true;
             const bool sa = schA && pa && is_sched(g.fA[i], t, d.sched_delay);
             const bool sb = schB && pb && is_sched(g.fB[i], t, d.sched_delay);
             const bool inA = pa && !sa;  // j is in a's digest (compute_digest, state.py:324-331)
@@ -517,12 +521,12 @@ __device__ __forceinline__ void pass1_grp(const Dev &d, size_t ra, size_t rb, ui
             g.hA[i] = hA;
             g.hB[i] = hB;
             if (repB) {
-                g.wB[i] = fd_pack(d, fd_report_val(d, rb + j, t, fd_unpack(d, g.wB[i]), alg, ovf));
+                g.wB[i] = fd_pack(d, fd_report_val<RING>(d, rb + j, t, fd_unpack(d, g.wB[i]), alg, ovf));
                 fdB = true;
                 reports++;
             }
             if (repA) {
-                g.wA[i] = fd_pack(d, fd_report_val(d, ra + j, t, fd_unpack(d, g.wA[i]), alg, ovf));
+                g.wA[i] = fd_pack(d, fd_report_val<RING>(d, ra + j, t, fd_unpack(d, g.wA[i]), alg, ovf));
                 fdA = true;
                 reports++;
             }
@@ -541,7 +545,7 @@ __device__ __forceinline__ void pass1_grp(const Dev &d, size_t ra, size_t rb, ui
     if (fdB) st4w(d.fd + rb + c0, g.wB);
 }
 
-template <int KW>
+template <int KW, bool GENM, bool RING>
 __global__ __launch_bounds__(XB) void k_exchange(Dev d, const int32_t *ini, const int32_t *res, uint32_t n,
                                                  uint32_t t, uint32_t seq) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -555,11 +559,11 @@ __global__ __launch_bounds__(XB) void k_exchange(Dev d, const int32_t *ini, cons
         return;
     }
     const uint32_t a = (uint32_t)ai, b = (uint32_t)bi;
-    const bool genm = !(d.flags & GS_CANONICAL);
+    constexpr bool genm = GENM;
     const uint32_t words = d.NP / 32;
-    // LDS: 2048-entry compaction list per wave, then the stale-owner bitmaps (+ insertion bitmaps)
-    uint16_t *wbuf = reinterpret_cast<uint16_t *>(lds) + wid * (32 * WAVE);
-    uint32_t *bm = lds + 32 * WAVE;  // 2 waves x 2048 x u16 = 8 KB
+    // LDS: WIN-entry compaction list per wave, then the stale-owner bitmaps (+ insertion bitmaps)
+    uint16_t *wbuf = reinterpret_cast<uint16_t *>(lds) + wid * WIN;
+    uint32_t *bm = lds + WIN;  // 2 waves x WIN x u16
     uint32_t *bBA = bm, *bAB = bm + words, *bNB = bm + 2 * words, *bNA = bm + 3 * words;
     for (uint32_t i = tid; i < words * (genm ? 4u : 2u); i += XB) bm[i] = 0u;
     if (tid == 0) {
@@ -577,10 +581,18 @@ __global__ __launch_bounds__(XB) void k_exchange(Dev d, const int32_t *ini, cons
     const size_t ra = (size_t)a * d.NP, rb = (size_t)b * d.NP;
     uint32_t alg = 0, reports = 0, hbw = 0, ovf = 0;
     bool anynew = false;
-    for (uint32_t c0 = (uint32_t)tid * 4u; c0 < d.N; c0 += XB * 4u) {
-        Grp g0;
-        load_grp(d, ra, rb, c0, genm, schA, schB, g0);
-        pass1_grp(d, ra, rb, c0, a, b, t, genm, schA, schB, g0, bBA, bAB, bNB, bNA, alg, reports, hbw, ovf, anynew);
+    // software-pipelined: the next group's loads are in flight while this group computes and stores
+    // (different owners, so the early loads never read a location this group writes)
+    uint32_t c0 = (uint32_t)tid * 4u;
+    Grp g0, g1;
+    if (c0 < d.N) load_grp<GENM>(d, ra, rb, c0, schA, schB, g0);
+    while (c0 < d.N) {
+        const uint32_t c1 = c0 + XB * 4u;
+        if (c1 < d.N) load_grp<GENM>(d, ra, rb, c1, schA, schB, g1);
+        pass1_grp<GENM, RING>(d, ra, rb, c0, a, b, t, schA, schB, g0, bBA, bAB, bNB, bNA, alg, reports, hbw, ovf,
+                              anynew);
+        g0 = g1;
+        c0 = c1;
     }
     if (anynew) s_flag[0] = 1u;
     __syncthreads();
@@ -632,7 +644,7 @@ __global__ __launch_bounds__(XB) void k_exchange(Dev d, const int32_t *ini, cons
         const uint32_t snd = w0 ? b : a, rcv = w0 ? a : b;
         const DigestSide ds{rcv, w0 ? cntA0 : cntB, w0 ? schA : schB};
         const uint32_t *ord = genm ? d.ord + (w0 ? rb : ra) : nullptr;
-        pack_dir<KW>(d, snd, rcv, ds, ord, w0 ? cntB : cntA, w0 ? bBA : bAB, wbuf, t, genm, st, tomb);
+        pack_dir<KW, GENM>(d, snd, rcv, ds, ord, w0 ? cntB : cntA, w0 ? bBA : bAB, wbuf, t, st, tomb);
         if (tomb) d.row[rcv * 4 + 1] = 1u;
     }
 
@@ -923,6 +935,16 @@ int check_bound(gs_handle *h) {
     return GS_OK;
 }
 
+template <int KW, bool GENM, bool RING>
+int launch_exchange(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t n, uint32_t tick, size_t lds) {
+    auto *k = k_exchange<KW, GENM, RING>;
+    if (lds > 64 * 1024)
+        HIPCHK(h, hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    k<<<n, XB, lds, h->stream>>>(h->d, ini, res, n, tick, h->seq);
+    HIPCHK(h, hipGetLastError());
+    return GS_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1086,22 +1108,21 @@ int gs_run_phase(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t 
     if (!n) return GS_OK;
     if (!ini || !res) return GS_E_INVALID;
     const bool genm = !(h->cfg.flags & GS_CANONICAL);
-    const size_t lds = 32 * WAVE * 4 + (size_t)(h->NP / 32) * (genm ? 4 : 2) * 4;
+    const bool ring = (h->cfg.flags & GS_FD_RING) != 0;
+    const size_t lds = WIN * 2 * 2 + (size_t)(h->NP / 32) * (genm ? 4 : 2) * 4;
     if (lds > 160 * 1024) return fail(h, GS_E_UNSUPPORTED, "n_nodes too large for the LDS bitmaps (%zu B)", lds);
     h->seq += 1;
-    if (h->KP <= 16) {
-        if (lds > 64 * 1024)
-            HIPCHK(h, hipFuncSetAttribute((const void *)k_exchange<4>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                          (int)lds));
-        k_exchange<4><<<n, XB, lds, h->stream>>>(h->d, ini, res, n, tick, h->seq);
-    } else {
-        if (lds > 64 * 1024)
-            HIPCHK(h, hipFuncSetAttribute((const void *)k_exchange<16>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                          (int)lds));
-        k_exchange<16><<<n, XB, lds, h->stream>>>(h->d, ini, res, n, tick, h->seq);
+    const bool k16 = h->KP <= 16;
+    if (k16) {
+        if (genm) return ring ? launch_exchange<4, true, true>(h, ini, res, n, tick, lds)
+                              : launch_exchange<4, true, false>(h, ini, res, n, tick, lds);
+        return ring ? launch_exchange<4, false, true>(h, ini, res, n, tick, lds)
+                    : launch_exchange<4, false, false>(h, ini, res, n, tick, lds);
     }
-    HIPCHK(h, hipGetLastError());
-    return GS_OK;
+    if (genm) return ring ? launch_exchange<16, true, true>(h, ini, res, n, tick, lds)
+                          : launch_exchange<16, true, false>(h, ini, res, n, tick, lds);
+    return ring ? launch_exchange<16, false, true>(h, ini, res, n, tick, lds)
+                : launch_exchange<16, false, false>(h, ini, res, n, tick, lds);
 }
 
 int gs_liveness(gs_handle *h, const uint8_t *up, uint32_t tick) {

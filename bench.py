@@ -185,15 +185,17 @@ def aggregate(exchanges: float, elapsed: float, dist=None, dev=None) -> tuple[fl
     return float(ex.item()), float(tm.item())
 
 
-def load_traffic(workload: str):
-    """Per-launch HBM bytes of k_exchange from a committed rocprofv3 PMC summary, if present."""
+def load_traffic(workload: str, exchanges_per_launch: float):
+    """HBM bytes per k_exchange launch from the committed rocprofv3 PMC summary of this workload
+    (tools/profile.sh + tools/pmc_summary.py): measured bytes per exchange x this run's exchanges per launch."""
     path = os.path.join(REPO, "profiles", "pmc_summary.json")
     if not os.path.exists(path):
         return None
     try:
-        d = json.load(open(path))
-        e = d.get(workload)
-        return None if e is None else e.get("k_exchange_bytes_per_launch")
+        e = json.load(open(path)).get(workload)
+        if e is None or e.get("k_exchange_bytes_per_exchange") is None:
+            return None
+        return e["k_exchange_bytes_per_exchange"] * exchanges_per_launch
     except Exception:
         return None
 
@@ -274,7 +276,7 @@ def main():
     launches = len(events)
     exch_total, elapsed_max = aggregate(exch, elapsed, dist, dev)
     achieved = c["alg_bytes"] / (kern_ms / 1e3) / 1e9 if kern_ms > 0 else 0.0
-    traffic = load_traffic(workload)
+    traffic = load_traffic(workload, exch / max(1, len(events)))
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(sim, spec, cfg, plans[args.warmup + args.steps], args.cpu_sample, args.cpu_seconds)
