@@ -30,6 +30,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdarg>
+#include <cstdlib>
 #include <cstdio>
 #include <algorithm>
 #include <cstring>
@@ -58,6 +59,7 @@ static_assert(sizeof(gs_counters) == 32 * 8, "gs_counters layout");
 struct Dev {
     uint32_t N, NP, K, KP, C, mtu, flags, W;
     uint32_t max_iv, tomb_grace, dead_grace, sched_delay, lb_min, sum_bits;
+    uint32_t ablate;  // profiling only (env GS_ABLATE): 1 = skip packing, 2 = skip pass-1 stores; results invalid
     double phi_thr, prior5;
     uint32_t *hb, *mv, *gc;
     uint8_t *held;
@@ -115,6 +117,14 @@ __device__ inline uint64_t fd_pack(const Dev &d, Fd f) {
 }
 
 __device__ inline int lane_id() { return (int)__lane_id(); }
+
+// true in every lane of an aligned group of 4 lanes if it is true in any of them
+__device__ inline bool quad_any(bool x) {
+    uint32_t v = x ? 1u : 0u;
+    v |= __shfl_xor(v, 1, 64);
+    v |= __shfl_xor(v, 2, 64);
+    return v != 0u;
+}
 __device__ inline bool bit(const uint32_t *bm, uint32_t j) { return (bm[j >> 5] >> (j & 31u)) & 1u; }
 
 __device__ inline uint32_t wave_incl_scan(uint32_t x) {
@@ -539,10 +549,11 @@ __device__ __forceinline__ void pass1_grp(const Dev &d, size_t ra, size_t rb, ui
             if (newA) { atomicOr(&bNA[j >> 5], 1u << (j & 31u)); anynew = true; }
         }
     }
-    if (dA) { st4(d.hb + ra + c0, g.hA); alg += 16; }
-    if (dB) { st4(d.hb + rb + c0, g.hB); alg += 16; }
-    if (fdA) st4w(d.fd + ra + c0, g.wA);
-    if (fdB) st4w(d.fd + rb + c0, g.wB);
+    // Whole 64-byte lines are written back when any lane of the line changed (lanes 4q..4q+3 hold one
+    // line of each array): no partial-line writes, which HBM would have to read-modify-write.
+    const bool lA = quad_any(dA || fdA) && !(d.ablate & 2u), lB = quad_any(dB || fdB) && !(d.ablate & 2u);
+    if (lA) { st4(d.hb + ra + c0, g.hA); st4w(d.fd + ra + c0, g.wA); alg += dA ? 16 : 0; }
+    if (lB) { st4(d.hb + rb + c0, g.hB); st4w(d.fd + rb + c0, g.wB); alg += dB ? 16 : 0; }
 }
 
 template <int KW, bool GENM, bool RING>
@@ -639,7 +650,7 @@ __global__ __launch_bounds__(XB) void k_exchange(Dev d, const int32_t *ini, cons
     // ---- pass 3: SynAck delta b -> a (wave 0) and Ack delta a -> b (wave 1), each applied
     WStats st{0, 0, 0, 0, 0};
     bool tomb = false;
-    {
+    if (!(d.ablate & 1u)) {
         const bool w0 = wid == 0;  // wave-uniform: one call site, so pack_dir inlines
         const uint32_t snd = w0 ? b : a, rcv = w0 ? a : b;
         const DigestSide ds{rcv, w0 ? cntA0 : cntB, w0 ? schA : schB};
@@ -1012,6 +1023,7 @@ int gs_create(const gs_config *cfg, gs_handle **out) {
     d.dead_grace = c.dead_grace_ticks;
     d.sched_delay = c.sched_delay_ticks;
     d.sum_bits = sum_bits;
+    if (const char *ab = getenv("GS_ABLATE")) d.ablate = (uint32_t)atoi(ab);
     d.phi_thr = c.phi_threshold;
     d.prior5 = c.prior_weighted;
     *out = h;

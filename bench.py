@@ -316,6 +316,7 @@ def main():
                 "kernel_share_of_step": kern_ms / 1e3 / elapsed,
             },
             "cpu_baseline": cpu,
+            **({"ABLATION_RESULTS_INVALID": os.environ["GS_ABLATE"]} if os.environ.get("GS_ABLATE") else {}),
             "counters": {k: v for k, v in c.items() if not k.startswith("err_")},
         }
         print(json.dumps(line), flush=True)
