@@ -51,7 +51,7 @@ constexpr double TICK_S = 1.0 / 64.0;
 
 enum Ctr {
     C_EXCH = 0, C_REPORTS, C_ND, C_KVS, C_TRUNC, C_DBYTES, C_ALG, C_HBW, C_CAND, C_LIVE, C_TOMBGC,
-    C_E_FDOVF, C_E_HIST, C_E_IDX, C_E_CONFLICT, C_E_FDGC, C_E_INSERT, C_NUM
+    C_E_FDOVF, C_E_HIST, C_E_IDX, C_E_CONFLICT, C_E_FDGC, C_E_INSERT, C_FDGC, C_Q9, C_NUM
 };
 static_assert(C_NUM <= 32, "counter region");
 static_assert(sizeof(gs_counters) == 32 * 8, "gs_counters layout");
@@ -777,8 +777,104 @@ __global__ __launch_bounds__(LB) void k_liveness(Dev d, const uint8_t *up, uint3
     if ((threadIdx.x & 63) == 0) {
         if (minS != NONE) atomicMin(&d.row[o * 4 + 2], minS);
         shard_add(d, C_LIVE, sl);
-        shard_add(d, C_E_FDGC, sg);
+        if (sg) {
+            if (genm) d.row[o * 4 + 3] = 1u;  // k_fd_gc collects this row
+            else shard_add(d, C_E_FDGC, sg);  // removal would break the canonical layout
+        }
     }
+}
+
+// FailureDetector.garbage_collect + ClusterState.remove_node, the tail of _update_node_liveness
+// (failure_detector.py:108-119, server.py:618-620), for rows k_liveness flagged.  The reference walks
+// _dead_nodes in insertion order = (time of death, dict position) and deletes the dead entry, then
+// the sampling window, of each expired target; a target without a window raises KeyError there
+// (SURVEY Q9): earlier targets lose dead entry + window, the failing one its dead entry, later ones
+// nothing, and no node leaves the dict.  Otherwise every expired target leaves the dict (the
+// insertion order of the others is kept: stable compaction of ORD/POS).
+__global__ __launch_bounds__(LB) void k_fd_gc(Dev d, const uint8_t *up, uint32_t t) {
+    __shared__ unsigned long long s_key[LB / WAVE];
+    __shared__ uint32_t s_wsum[LB / WAVE];
+    extern __shared__ __attribute__((aligned(16))) uint32_t rmv[];  // removal bitmap, NP bits
+    const uint32_t o = blockIdx.x;
+    if (!up[o] || !d.row[o * 4 + 3]) return;
+    const int tid = threadIdx.x, lane = tid & (WAVE - 1), wid = tid >> 6;
+    const size_t ro = (size_t)o * d.NP;
+    const uint32_t cnt = d.row[o * 4 + 0];
+    // 1. earliest expired target (in dead-dict order) that has no window
+    unsigned long long fkey = ~0ull;
+    for (uint32_t j = tid; j < d.N; j += LB) {
+        const uint32_t st = d.fd_state[ro + j], pos = d.pos[ro + j];
+        if (st >= 2u && pos != NONE && (uint64_t)t >= (uint64_t)(st - 2u) + d.dead_grace && d.fd[ro + j] == 0ull) {
+            const unsigned long long key = ((unsigned long long)(st - 2u) << 32) | pos;
+            if (key < fkey) fkey = key;
+        }
+    }
+    for (int dd = 32; dd >= 1; dd >>= 1) {
+        const unsigned long long y = __shfl_xor(fkey, dd, WAVE);
+        if (y < fkey) fkey = y;
+    }
+    if (lane == 0) s_key[wid] = fkey;
+    for (uint32_t i = tid; i < d.NP / 32; i += LB) rmv[i] = 0u;
+    __syncthreads();
+    fkey = ~0ull;
+    for (int w = 0; w < LB / WAVE; w++) fkey = s_key[w] < fkey ? s_key[w] : fkey;
+    const bool q9 = fkey != ~0ull;
+    // 2. drop dead entries / windows; mark dict removals
+    uint32_t gcn = 0;
+    for (uint32_t j = tid; j < d.N; j += LB) {
+        const uint32_t st = d.fd_state[ro + j], pos = d.pos[ro + j];
+        if (!(st >= 2u && pos != NONE && (uint64_t)t >= (uint64_t)(st - 2u) + d.dead_grace)) continue;
+        const unsigned long long key = ((unsigned long long)(st - 2u) << 32) | pos;
+        if (q9 && key > fkey) continue;
+        d.fd_state[ro + j] = 0u;  // del self._dead_nodes[gossip_id]
+        if (q9 && key == fkey) continue;
+        d.fd[ro + j] = 0ull;  // del self._node_samples[gossip_id]
+        gcn++;
+        if (!q9) atomicOr(&rmv[j >> 5], 1u << (j & 31u));
+    }
+    __syncthreads();
+    if (!q9) {
+        // 3. remove_node: stable compaction of the dict order, clear the removed views
+        uint32_t base = 0;
+        for (uint32_t p0 = 0; p0 < cnt; p0 += LB) {
+            const uint32_t p = p0 + tid;
+            const uint32_t j = p < cnt ? d.ord[ro + p] : NONE;
+            const bool keep = j != NONE && !bit(rmv, j);
+            const unsigned long long m = __ballot(keep);
+            const uint32_t rk = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+            if (lane == 0) s_wsum[wid] = (uint32_t)__popcll(m);
+            __syncthreads();
+            uint32_t off = base, tot = 0;
+            for (int w = 0; w < LB / WAVE; w++) {
+                if (w < wid) off += s_wsum[w];
+                tot += s_wsum[w];
+            }
+            if (keep) {
+                d.ord[ro + off + rk] = j;
+                d.pos[ro + j] = off + rk;
+            }
+            base += tot;
+            __syncthreads();
+        }
+        for (uint32_t j = tid; j < d.N; j += LB) {
+            if (!bit(rmv, j)) continue;
+            const size_t p = ro + j;
+            d.pos[p] = NONE;
+            d.hb[p] = 0u;
+            d.mv[p] = 0u;
+            d.gc[p] = 0u;
+            for (uint32_t k = 0; k < d.KP; k += 4) *reinterpret_cast<uint32_t *>(d.held + p * d.KP + k) = 0u;
+            if (d.flags & GS_TOMBSTONES)
+                for (uint32_t k = 0; k < d.KP; k++) d.ts[p * d.KP + k] = NONE;
+        }
+        if (tid == 0) d.row[o * 4 + 0] = base;
+    }
+    if (tid == 0) {
+        d.row[o * 4 + 3] = 0u;
+        if (q9) shard_add(d, C_Q9, 1);
+    }
+    const unsigned long long sg = wave_sum(gcn);
+    if (lane == 0) shard_add(d, C_FDGC, sg);
 }
 
 // SamplingWindow.phi (failure_detector.py:43-53) of every target of observer o; NaN for None.
@@ -1144,6 +1240,10 @@ int gs_liveness(gs_handle *h, const uint8_t *up, uint32_t tick) {
     const uint32_t chunks = (h->N + 4 * LB - 1) / (4 * LB);
     k_liveness<<<chunks * h->N, LB, 0, h->stream>>>(h->d, up, tick, chunks);
     HIPCHK(h, hipGetLastError());
+    if (!(h->cfg.flags & GS_CANONICAL)) {
+        k_fd_gc<<<h->N, LB, (h->NP / 32) * 4, h->stream>>>(h->d, up, tick);
+        HIPCHK(h, hipGetLastError());
+    }
     return GS_OK;
 }
 

@@ -104,7 +104,8 @@ class GossipSim:
     def __init__(self, node_ids: list[NodeId], keys: list[str], cfg: dict, init: str = "cold",
                  initial_values: dict[int, list[tuple[int, str]]] | None = None, *, device: str = "cuda:0",
                  tombstones: bool = True, fd_ring: bool | None = None, hist_cap: int = 64,
-                 nid_sizes: list[int] | None = None, initial_ops: list[np.ndarray] | None = None):
+                 nid_sizes: list[int] | None = None, initial_ops: list[np.ndarray] | None = None,
+                 canonical: bool | None = None):
         import torch
 
         if not torch.cuda.is_available():
@@ -122,7 +123,11 @@ class GossipSim:
         self.hist_cap = hist_cap
         self.init = init
         flags = 0
-        if init == "warm":
+        if canonical is None:
+            canonical = init == "warm"
+        if canonical and init != "warm":
+            raise GsError("the canonical layout needs a warm start")
+        if canonical:
             flags |= GS_CANONICAL
         if tombstones:
             flags |= GS_TOMBSTONES
@@ -294,7 +299,8 @@ class GossipSim:
         c = self.counters()
         errs = {k: v for k, v in c.items() if k.startswith("err_") and v}
         if errs.get("err_fd_gc"):
-            raise GsError(f"FailureDetector.garbage_collect is due but not implemented on the device: {errs}")
+            raise GsError(f"FailureDetector.garbage_collect is due in a canonical (warm, index-order) state; "
+                          f"removing nodes needs the general layout (init='cold' or canonical=False): {errs}")
         if errs:
             raise GsError(f"device checks failed: {errs}")
         return c

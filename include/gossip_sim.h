@@ -111,9 +111,11 @@ typedef struct gs_counters {
     uint64_t err_hist_full;    /* a (owner, key) wrote more than hist_cap - 1 times */
     uint64_t err_bad_index;    /* exchange endpoint out of range or a == b */
     uint64_t err_conflict;     /* a node appeared twice in one phase */
-    uint64_t err_fd_gc;        /* a dead target reached dead_node_grace_period (FD GC not implemented) */
+    uint64_t err_fd_gc;        /* a dead target expired in a GS_CANONICAL state (removal needs the general layout) */
     uint64_t err_insert;       /* insertion into a GS_CANONICAL state */
-    uint64_t reserved[15];
+    uint64_t fd_gc;            /* targets removed by FailureDetector.garbage_collect */
+    uint64_t q9;               /* garbage_collect calls that raised KeyError */
+    uint64_t reserved[13];
 } gs_counters;
 
 typedef struct gs_write {   /* one owner write */
@@ -147,7 +149,8 @@ int gs_begin_round(gs_handle *h, const uint8_t *up, uint32_t tick);
  * Syn/SynAck/Ack = server.py:327-376 + 524, i.e. compute_digest, _report_heartbeat,
  * compute_partial_delta_respecting_mtu and apply_delta on both sides. */
 int gs_run_phase(gs_handle *h, const int32_t *initiators, const int32_t *responders, uint32_t n, uint32_t tick);
-/* _update_node_liveness for every up node (server.py:606-620; failure_detector.py:89-128). */
+/* _update_node_liveness for every up node (server.py:606-620; failure_detector.py:89-128),
+ * including garbage_collect + remove_node (general layout only). */
 int gs_liveness(gs_handle *h, const uint8_t *up, uint32_t tick);
 
 /* SamplingWindow.phi (failure_detector.py:43-53) of every target of `observer` at `tick`

@@ -68,6 +68,13 @@ SCENARIOS = {
         {"dead_grace_s": 8.0, "phi_threshold": 2.0, "initial_interval_s": 1.0},
         True,
     ),
+    # FD garbage collection that raises KeyError for windowless dead targets
+    "q9x10": (
+        WorkloadSpec(n=10, k=2, fanout=1, seed=4, init="cold", write_frac=0.2, down_frac=0.5, down_rounds=10),
+        40,
+        {"dead_grace_s": 4.0, "phi_threshold": 1.5, "initial_interval_s": 1.0},
+        True,
+    ),
     # cold start at moderate N with truncation and deletes (hashes per round)
     "cold64": (
         WorkloadSpec(n=64, k=16, fanout=3, seed=5, init="cold", write_frac=0.05, delete_frac=0.1, ttl_frac=0.05),

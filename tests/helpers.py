@@ -7,7 +7,7 @@ import os
 from aiocluster_amd.scenario import initial_by_owner, replay, scenario_node_ids, state_hash
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
-SCENARIOS = ["simple3", "trunc8", "sched16", "fdgc12", "cold64", "warm128"]
+SCENARIOS = ["simple3", "trunc8", "sched16", "fdgc12", "q9x10", "cold64", "warm128"]
 
 
 def load_scenario(name):

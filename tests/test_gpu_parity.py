@@ -24,22 +24,34 @@ pytestmark = pytest.mark.gpu
 PHI_RTOL = 1e-9  # north_star tolerance for phi
 
 
-@pytest.mark.parametrize("name", [s for s in SCENARIOS if s != "fdgc12"])
+@pytest.mark.parametrize("name", SCENARIOS)
 def test_gpu_matches_reference_golden(name):
     scen = load_scenario(name)
     exp = scen["expect"]
     sim = make_backend(GossipSim, scen)
     res = replay_and_compare(sim, scen, exp["states"], exp["hashes"])
     assert res is None, f"{name}: first mismatch at round {res[0]}: {res[1]}"
-    sim.check()
+    c = sim.check()
+    assert c["q9"] == len(exp["q9"])  # garbage_collect KeyErrors
 
 
-def test_fd_garbage_collection_fails_loudly():
-    """FailureDetector.garbage_collect + remove_node are not on the device yet: must raise, never diverge silently."""
-    scen = load_scenario("fdgc12")
+def test_fd_garbage_collection_in_canonical_layout_fails_loudly():
+    """Removing nodes needs the general layout: a canonical (warm, index-order) state must refuse."""
+    spec = WorkloadSpec(n=16, k=2, fanout=2, seed=3, init="warm", write_frac=0.1, down_frac=0.4, down_rounds=12)
+    scen = make_scenario("gcwarm", spec, 30, {"dead_grace_s": 4.0, "phi_threshold": 2.0, "initial_interval_s": 1.0})
     sim = make_backend(GossipSim, scen)
     with pytest.raises(GsError, match="garbage_collect"):
         replay(sim, scen, on_round=lambda r: sim.check())
+
+
+def test_warm_general_layout_with_fd_gc_vs_oracle():
+    """A warm start run in the general layout so FD garbage collection can remove and re-add nodes."""
+    spec = WorkloadSpec(n=48, k=4, fanout=2, seed=21, init="warm", write_frac=0.2, delete_frac=0.2,
+                        down_frac=0.4, down_rounds=10)
+    scen = make_scenario("gcwarm48", spec, 36, {"dead_grace_s": 5.0, "phi_threshold": 2.0,
+                                                 "initial_interval_s": 1.0, "tombstone_grace_s": 3, "mtu": 1500})
+    gpu, orc, c = lockstep_vs_oracle(scen, canonical=False)
+    assert c["fd_gc"] > 0 and c["q9"] == len(orc.q9_events)
 
 
 def lockstep_vs_oracle(scen, every=1, **kw):
