@@ -58,6 +58,7 @@ static_assert(sizeof(gs_counters) == 32 * 8, "gs_counters layout");
 
 struct Dev {
     uint32_t N, NP, K, KP, C, mtu, flags, W;
+    uint32_t col_lo, ncol, shards, shard;  // owner columns [col_lo, col_lo + ncol) of the N x N matrices
     uint32_t max_iv, tomb_grace, dead_grace, sched_delay, lb_min, sum_bits;
     uint32_t ablate;  // profiling only (env GS_ABLATE): 1 = skip packing, 2 = skip pass-1 stores; results invalid
     double phi_thr, prior5;
@@ -118,13 +119,6 @@ __device__ inline uint64_t fd_pack(const Dev &d, Fd f) {
 
 __device__ inline int lane_id() { return (int)__lane_id(); }
 
-// true in every lane of an aligned group of 4 lanes if it is true in any of them
-__device__ inline bool quad_any(bool x) {
-    uint32_t v = x ? 1u : 0u;
-    v |= __shfl_xor(v, 1, 64);
-    v |= __shfl_xor(v, 2, 64);
-    return v != 0u;
-}
 __device__ inline bool bit(const uint32_t *bm, uint32_t j) { return (bm[j >> 5] >> (j & 31u)) & 1u; }
 
 __device__ inline uint32_t wave_incl_scan(uint32_t x) {
@@ -287,14 +281,23 @@ __device__ __forceinline__ void apply_cand(const Dev &d, uint32_t r, const Cand<
 // r's apply_delta, by one wave.  The sender's dict order is walked in windows of 1024 positions;
 // each window's stale owners are compacted (ballot + popcount scan) into a wave-private LDS list
 // and evaluated 64 at a time, one per lane.  Exactness vs the sequential loop: DESIGN.md.
-template <int KW, bool GENM>
+struct PackState {
+    uint32_t S;  // DeltaPb bytes committed so far (wave-uniform)
+    bool tail;   // the budget was exceeded once: first-fit continuation mode
+    bool stop;   // the delta is complete (>= mtu, or less than the smallest NodeDelta left)
+};
+
+// COUNT: only sum the DeltaPb bytes of every candidate (owner-sharded runs: the slice total).
+template <int KW, bool GENM, bool COUNT>
 __device__ __forceinline__ void pack_dir(const Dev &d, uint32_t s, uint32_t r, const DigestSide ds,
                                          const uint32_t *order, uint32_t cnt, const uint32_t *bits, uint16_t *wbuf,
-                                         uint32_t t, WStats &st, bool &tomb) {
+                                         uint32_t t, WStats &st, bool &tomb, PackState &pst) {
     const int lane = lane_id();
     const uint32_t mtu = d.mtu;
-    uint32_t S = 0;  // DeltaPb bytes committed (wave-uniform)
-    bool tail = false, stop = false;
+    const uint32_t S0 = pst.S;
+    uint32_t S = pst.S;
+    bool tail = pst.tail, stop = pst.stop;
+    if (!COUNT && !stop && (S >= mtu || mtu - S < d.lb_min)) stop = true;
     for (uint32_t win = 0; win < cnt && !stop; win += WIN) {
         // -- compact this window's stale owners (sender order) into wbuf, 16 positions per lane
         uint32_t m = 0;
@@ -337,6 +340,10 @@ __device__ __forceinline__ void pack_dir(const Dev &d, uint32_t s, uint32_t r, c
                 st.cand++;
             }
             const uint32_t em = cand ? c.emsg : 0u;
+            if (COUNT) {
+                S += (uint32_t)wave_sum(em);
+                continue;
+            }
             // this lane's NodeDelta: 0 = not sent, NONE = all its kvs, else kvs up to that version
             uint32_t vsel = 0, nsel = 0;
             int cur = 0;
@@ -421,7 +428,10 @@ __device__ __forceinline__ void pack_dir(const Dev &d, uint32_t s, uint32_t r, c
         }
         __builtin_amdgcn_wave_barrier();
     }
-    if (lane == 0) shard_add(d, C_DBYTES, S);  // DeltaPb bytes of this direction
+    pst.S = S;
+    pst.tail = tail;
+    pst.stop = stop;
+    if (!COUNT && lane == 0) shard_add(d, C_DBYTES, S - S0);  // DeltaPb bytes this call added
 }
 
 // ------------------------------------------------------------------ exchange kernel
@@ -549,11 +559,12 @@ __device__ __forceinline__ void pass1_grp(const Dev &d, size_t ra, size_t rb, ui
             if (newA) { atomicOr(&bNA[j >> 5], 1u << (j & 31u)); anynew = true; }
         }
     }
-    // Whole 64-byte lines are written back when any lane of the line changed (lanes 4q..4q+3 hold one
-    // line of each array): no partial-line writes, which HBM would have to read-modify-write.
-    const bool lA = quad_any(dA || fdA) && !(d.ablate & 2u), lB = quad_any(dB || fdB) && !(d.ablate & 2u);
-    if (lA) { st4(d.hb + ra + c0, g.hA); st4w(d.fd + ra + c0, g.wA); alg += dA ? 16 : 0; }
-    if (lB) { st4(d.hb + rb + c0, g.hB); st4w(d.fd + rb + c0, g.wB); alg += dB ? 16 : 0; }
+    // only changed 16/32-byte groups are written back (writing whole lines measured slower: r1c vs r1b)
+    if (d.ablate & 2u) return;
+    if (dA) { st4(d.hb + ra + c0, g.hA); alg += 16; }
+    if (dB) { st4(d.hb + rb + c0, g.hB); alg += 16; }
+    if (fdA) st4w(d.fd + ra + c0, g.wA);
+    if (fdB) st4w(d.fd + rb + c0, g.wB);
 }
 
 template <int KW, bool GENM, bool RING>
@@ -655,7 +666,8 @@ __global__ __launch_bounds__(XB) void k_exchange(Dev d, const int32_t *ini, cons
         const uint32_t snd = w0 ? b : a, rcv = w0 ? a : b;
         const DigestSide ds{rcv, w0 ? cntA0 : cntB, w0 ? schA : schB};
         const uint32_t *ord = genm ? d.ord + (w0 ? rb : ra) : nullptr;
-        pack_dir<KW, GENM>(d, snd, rcv, ds, ord, w0 ? cntB : cntA, w0 ? bBA : bAB, wbuf, t, st, tomb);
+        PackState pst{0u, false, false};
+        pack_dir<KW, GENM, false>(d, snd, rcv, ds, ord, w0 ? cntB : cntA, w0 ? bBA : bAB, wbuf, t, st, tomb, pst);
         if (tomb) d.row[rcv * 4 + 1] = 1u;
     }
 
@@ -1107,6 +1119,10 @@ int gs_create(const gs_config *cfg, gs_handle **out) {
     Dev &d = h->d;
     memset(&d, 0, sizeof d);
     d.N = h->N;
+    d.col_lo = 0;
+    d.ncol = h->N;
+    d.shards = 1;
+    d.shard = 0;
     d.NP = h->NP;
     d.K = h->K;
     d.KP = h->KP;
