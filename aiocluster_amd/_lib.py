@@ -27,6 +27,17 @@ GS_NONE = 0xFFFFFFFF
 TICK_US = 15_625
 
 
+def slice_columns(n: int, shards: int, shard: int) -> tuple[int, int]:
+    """Owner columns ``(col_lo, n_cols)`` of slice ``shard`` of ``shards`` (gs_config.n_shards)."""
+    if shards <= 1:
+        return 0, n
+    blk = (-(-n // shards) + 63) // 64 * 64
+    if (shards - 1) * blk >= n:
+        raise ValueError(f"{shards} slices of {blk} columns leave a slice of a {n}-node cluster empty")
+    lo = shard * blk
+    return lo, min(blk, n - lo)
+
+
 def fd_sum_bits(window: int) -> int:
     """Bits of the packed window's interval sum (include/gossip_sim.h, GS_R_FD)."""
     cnt_bits = 1
@@ -36,7 +47,7 @@ def fd_sum_bits(window: int) -> int:
 
 REGIONS = [
     "HB", "MV", "GC", "HELD", "FD", "FD_STATE", "TS", "RING", "POS", "ORD", "ROW",
-    "LAST_W", "HIST", "HIST_VID", "NID_SIZE", "KEY_LEN", "STAMP", "COUNTERS",
+    "LAST_W", "HIST", "HIST_VID", "NID_SIZE", "KEY_LEN", "STAMP", "COUNTERS", "SLICE_BITS",
 ]
 REGION = {n: i for i, n in enumerate(REGIONS)}
 
@@ -52,8 +63,10 @@ COUNTER_FIELDS = [
 EXPORTS = [
     "gs_create", "gs_destroy", "gs_last_error", "gs_api_version", "gs_region_bytes", "gs_bind", "gs_set_stream",
     "gs_boot", "gs_warm", "gs_owner_writes", "gs_begin_round", "gs_run_phase", "gs_liveness", "gs_phi_row",
-    "gs_read_counters", "gs_reset_counters", "gs_sync",
+    "gs_read_counters", "gs_reset_counters", "gs_sync", "gs_shard_columns", "gs_phase_count", "gs_phase_pack",
 ]
+
+API_VERSION = 2
 
 
 class GsConfig(C.Structure):
@@ -70,6 +83,8 @@ class GsConfig(C.Structure):
         ("sched_delay_ticks", C.c_uint32),
         ("phi_threshold", C.c_double),
         ("prior_weighted", C.c_double),
+        ("n_shards", C.c_uint32),
+        ("shard", C.c_uint32),
     ]
 
 
@@ -123,6 +138,9 @@ def load():
         "gs_read_counters": (C.c_int, [P, C.POINTER(GsCounters)]),
         "gs_reset_counters": (C.c_int, [P]),
         "gs_sync": (C.c_int, [P]),
+        "gs_shard_columns": (C.c_int, [P, C.POINTER(u32), C.POINTER(u32)]),
+        "gs_phase_count": (C.c_int, [P, P, P, u32, u32, P]),
+        "gs_phase_pack": (C.c_int, [P, P, P, u32, u32, u32, P, P, P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

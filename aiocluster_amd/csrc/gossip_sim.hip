@@ -58,7 +58,9 @@ static_assert(sizeof(gs_counters) == 32 * 8, "gs_counters layout");
 
 struct Dev {
     uint32_t N, NP, K, KP, C, mtu, flags, W;
-    uint32_t col_lo, ncol, shards, shard;  // owner columns [col_lo, col_lo + ncol) of the N x N matrices
+    // owner-column slice: this handle holds columns [col_lo, col_lo + ncol) of every observer row
+    // (NP = ncol rounded to 64 is the row stride); shards = 1: the whole matrix
+    uint32_t col_lo, ncol, shards, shard;
     uint32_t max_iv, tomb_grace, dead_grace, sched_delay, lb_min, sum_bits;
     uint32_t ablate;  // profiling only (env GS_ABLATE): 1 = skip packing, 2 = skip pass-1 stores; results invalid
     double phi_thr, prior5;
@@ -75,6 +77,7 @@ struct Dev {
     uint8_t *key_len;
     uint32_t *stamp;
     unsigned long long *ctr;
+    uint32_t *sbits;  // sharded phases: stale-owner bitmaps of both directions per exchange [e][2][NP/32]
 };
 
 // ------------------------------------------------------------------ protobuf sizes
@@ -515,17 +518,17 @@ __device__ __forceinline__ void pass1_grp(const Dev &d, size_t ra, size_t rb, ui
     alg += 64 + (GENM ? 32 : 0) + (schA ? 16 : 0) + (schB ? 16 : 0);
 #pragma unroll
     for (int i = 0; i < 4; i++) {
-        const uint32_t j = c0 + i;
-        if (j < d.N) {
+        const uint32_t j = c0 + i, jg = d.col_lo + j;  // local column, node id
+        if (j < d.ncol) {
             const bool pa = GENM ? g.pA[i] != NONE : true;
             const bool pb = GENM ? g.pB[i] != NONE : true;
             const bool sa = schA && pa && is_sched(g.fA[i], t, d.sched_delay);
             const bool sb = schB && pb && is_sched(g.fB[i], t, d.sched_delay);
             const bool inA = pa && !sa;  // j is in a's digest (compute_digest, state.py:324-331)
             uint32_t hA = g.hA[i], hB = g.hB[i];
-            if (j == b) { hB += 1u; dB = true; hbw++; }  // responder inc_heartbeat (server.py:524)
+            if (jg == b) { hB += 1u; dB = true; hbw++; }  // responder inc_heartbeat (server.py:524)
             bool newB = false, repB = false;
-            if (inA && j != b) {  // b: _report_heartbeat over a's digest (server.py:336-337, 599-604)
+            if (inA && jg != b) {  // b: _report_heartbeat over a's digest (server.py:336-337, 599-604)
                 if (!pb) { newB = true; hB = hA; dB = true; hbw++; }
                 else if (hB == 0u) { if (hA) { hB = hA; dB = true; hbw++; } }
                 else if (hA > hB) { hB = hA; dB = true; hbw++; repB = true; }
@@ -533,7 +536,7 @@ __device__ __forceinline__ void pass1_grp(const Dev &d, size_t ra, size_t rb, ui
             const bool pb2 = pb || newB;
             const bool inB = pb2 && !sb;  // j is in b's digest, computed after the merge (server.py:340)
             bool newA = false, repA = false;
-            if (inB && j != a) {  // a: _report_heartbeat over b's digest (server.py:356-357)
+            if (inB && jg != a) {  // a: _report_heartbeat over b's digest (server.py:356-357)
                 if (!pa) { newA = true; hA = hB; dA = true; hbw++; }
                 else if (hA == 0u) { if (hB) { hA = hB; dA = true; hbw++; } }
                 else if (hB > hA) { hA = hB; dA = true; hbw++; repA = true; }
@@ -567,9 +570,29 @@ __device__ __forceinline__ void pass1_grp(const Dev &d, size_t ra, size_t rb, ui
     if (fdB) st4w(d.fd + rb + c0, g.wB);
 }
 
-template <int KW, bool GENM, bool RING>
+// Owner-column sharded phases ("multi-GPU"): the count pass leaves each exchange's
+// stale-owner bitmaps in GS_R_SLICE_BITS and the DeltaPb bytes of all this slice's candidates per
+// direction in tot[e][dir]; the pack passes resume the sender-order packing where the previous
+// slice left it: chain[e][dir] = S | tail << 32 | stop << 33, or CHAIN_PENDING.
+constexpr uint64_t CHAIN_PENDING = ~0ull;
+struct SliceIO {
+    uint64_t *tot;              // [n][2] count pass output
+    const uint64_t *tot_all;    // [shards][n][2] every slice's totals (gathered)
+    const uint64_t *chain_all;  // [shards][n][2] every slice's chain state after the previous step
+    uint64_t *chain;            // [n][2] this slice's chain state
+    uint32_t step;
+};
+__device__ inline uint64_t chain_pack(const PackState &p) {
+    return (uint64_t)p.S | ((uint64_t)p.tail << 32) | ((uint64_t)p.stop << 33);
+}
+__device__ inline PackState chain_unpack(uint64_t v) {
+    return PackState{(uint32_t)v, ((v >> 32) & 1ull) != 0, ((v >> 33) & 1ull) != 0};
+}
+
+// MODE 0: the whole exchange (one slice).  MODE 1: sharded count pass (pass 1, then the slice totals).
+template <int KW, bool GENM, bool RING, int MODE>
 __global__ __launch_bounds__(XB) void k_exchange(Dev d, const int32_t *ini, const int32_t *res, uint32_t n,
-                                                 uint32_t t, uint32_t seq) {
+                                                 uint32_t t, uint32_t seq, SliceIO io) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     __shared__ uint32_t s_flag[4];
     const uint32_t e = blockIdx.x;
@@ -593,8 +616,8 @@ __global__ __launch_bounds__(XB) void k_exchange(Dev d, const int32_t *ini, cons
         const uint32_t oa = atomicMax(&d.stamp[a], seq), ob = atomicMax(&d.stamp[b], seq);
         if (oa == seq || ob == seq) shard_add(d, C_E_CONFLICT, 1);
     }
-    const uint32_t cntA0 = genm ? d.row[a * 4 + 0] : d.N;
-    const uint32_t cntB0 = genm ? d.row[b * 4 + 0] : d.N;
+    const uint32_t cntA0 = genm ? d.row[a * 4 + 0] : d.ncol;
+    const uint32_t cntB0 = genm ? d.row[b * 4 + 0] : d.ncol;
     const bool schA = t >= d.row[a * 4 + 2];
     const bool schB = t >= d.row[b * 4 + 2];
     __syncthreads();
@@ -607,10 +630,10 @@ __global__ __launch_bounds__(XB) void k_exchange(Dev d, const int32_t *ini, cons
     // (different owners, so the early loads never read a location this group writes)
     uint32_t c0 = (uint32_t)tid * 4u;
     Grp g0, g1;
-    if (c0 < d.N) load_grp<GENM>(d, ra, rb, c0, schA, schB, g0);
-    while (c0 < d.N) {
+    if (c0 < d.ncol) load_grp<GENM>(d, ra, rb, c0, schA, schB, g0);
+    while (c0 < d.ncol) {
         const uint32_t c1 = c0 + XB * 4u;
-        if (c1 < d.N) load_grp<GENM>(d, ra, rb, c1, schA, schB, g1);
+        if (c1 < d.ncol) load_grp<GENM>(d, ra, rb, c1, schA, schB, g1);
         pass1_grp<GENM, RING>(d, ra, rb, c0, a, b, t, schA, schB, g0, bBA, bAB, bNB, bNA, alg, reports, hbw, ovf,
                               anynew);
         g0 = g1;
@@ -618,6 +641,31 @@ __global__ __launch_bounds__(XB) void k_exchange(Dev d, const int32_t *ini, cons
     }
     if (anynew) s_flag[0] = 1u;
     __syncthreads();
+
+    if (MODE == 1) {
+        // ---- sharded count pass: publish the bitmaps, total this slice's candidates per direction
+        if (s_flag[0] && tid == 0) shard_add(d, C_E_INSERT, 1);
+        uint32_t *gb = d.sbits + (size_t)e * 2 * words;
+        for (uint32_t i = tid; i < 2 * words; i += XB) gb[i] = bm[i];
+        const bool w0 = wid == 0;
+        const uint32_t snd = w0 ? b : a, rcv = w0 ? a : b;
+        const DigestSide ds{rcv, d.ncol, w0 ? schA : schB};
+        WStats cs{0, 0, 0, 0, 0};
+        bool ctomb = false;
+        PackState pst{0u, false, false};
+        pack_dir<KW, false, true>(d, snd, rcv, ds, nullptr, d.ncol, w0 ? bBA : bAB, wbuf, t, cs, ctomb, pst);
+        if (lane == 0) io.tot[(size_t)e * 2 + wid] = pst.S;
+        const unsigned long long s_alg = wave_sum(alg), s_rep = wave_sum(reports), s_hbw = wave_sum(hbw);
+        const unsigned long long s_ovf = wave_sum(ovf);
+        if (lane == 0) {
+            shard_add(d, C_ALG, s_alg);
+            shard_add(d, C_REPORTS, s_rep);
+            shard_add(d, C_HBW, s_hbw);
+            shard_add(d, C_E_FDOVF, s_ovf);
+            if (wid == 0 && d.shard == 0) shard_add(d, C_EXCH, 1);
+        }
+        return;
+    }
 
     // ---- pass 2: dict insertions (node_state_or_default appends in digest order)
     uint32_t cntA = cntA0, cntB = cntB0;
@@ -689,17 +737,69 @@ __global__ __launch_bounds__(XB) void k_exchange(Dev d, const int32_t *ini, cons
     }
 }
 
+// Sharded pack pass, step `io.step` (wave 0: b -> a, wave 1: a -> b).  Step 0: a slice whose
+// predecessors' totals fit in the MTU starts at their sum (every one of their candidates is sent
+// whole, state.py:392-398); the others wait.  Step k: a waiting slice whose predecessor has
+// finished continues from the predecessor's state.  Sequential semantics over the slices in
+// column (= canonical dict) order, so the result is the single-slice result bit for bit.
+template <int KW>
+__global__ __launch_bounds__(XB) void k_pack_slice(Dev d, const int32_t *ini, const int32_t *res, uint32_t n,
+                                                   uint32_t t, SliceIO io) {
+    __shared__ __attribute__((aligned(16))) uint16_t s_wbuf[2 * WIN];
+    const uint32_t e = blockIdx.x;
+    if (e >= n) return;
+    const int tid = threadIdx.x, lane = tid & (WAVE - 1), wid = tid >> 6;
+    const int32_t ai = ini[e], bi = res[e];
+    if (ai < 0 || bi < 0 || (uint32_t)ai >= d.N || (uint32_t)bi >= d.N || ai == bi) return;  // counted already
+    const uint32_t a = (uint32_t)ai, b = (uint32_t)bi;
+    const size_t slot = (size_t)e * 2 + wid;
+    PackState pst;
+    if (io.step == 0) {
+        uint64_t P = 0;
+        for (uint32_t g = 0; g < d.shard; g++) P += io.tot_all[(size_t)g * n * 2 + slot];
+        if (P > d.mtu) {
+            if (lane == 0) io.chain[slot] = CHAIN_PENDING;
+            return;
+        }
+        pst = PackState{(uint32_t)P, false, false};
+    } else {
+        if (io.chain[slot] != CHAIN_PENDING) return;
+        const uint64_t prev = io.chain_all[(size_t)(d.shard - 1) * n * 2 + slot];
+        if (prev == CHAIN_PENDING) return;
+        pst = chain_unpack(prev);
+    }
+    const bool w0 = wid == 0;
+    const uint32_t snd = w0 ? b : a, rcv = w0 ? a : b;
+    const DigestSide ds{rcv, d.ncol, t >= d.row[rcv * 4 + 2]};
+    const uint32_t words = d.NP / 32;
+    WStats st{0, 0, 0, 0, 0};
+    bool tomb = false;
+    pack_dir<KW, false, false>(d, snd, rcv, ds, nullptr, d.ncol, d.sbits + (slot * words), s_wbuf + wid * WIN, t,
+                               st, tomb, pst);
+    if (tomb) d.row[rcv * 4 + 1] = 1u;
+    if (lane == 0) io.chain[slot] = chain_pack(pst);
+    const unsigned long long s_alg = wave_sum(st.alg), s_nd = wave_sum(st.nd), s_kv = wave_sum(st.kvs);
+    const unsigned long long s_tr = wave_sum(st.trunc), s_cd = wave_sum(st.cand);
+    if (lane == 0) {
+        shard_add(d, C_ALG, s_alg);
+        shard_add(d, C_ND, s_nd);
+        shard_add(d, C_KVS, s_kv);
+        shard_add(d, C_TRUNC, s_tr);
+        shard_add(d, C_CAND, s_cd);
+    }
+}
+
 // ------------------------------------------------------------------ round start
 // inc_heartbeat + ClusterState.gc_marked_for_deletion (server.py:471-474; state.py:253-274, 333-338)
 __global__ __launch_bounds__(LB) void k_begin_round(Dev d, const uint8_t *up, uint32_t t) {
     const uint32_t o = blockIdx.x;
     if (o >= d.N || !up[o]) return;
-    if (threadIdx.x == 0) d.hb[pix(d, o, o)] += 1u;
+    if (threadIdx.x == 0 && o - d.col_lo < d.ncol) d.hb[pix(d, o, o - d.col_lo)] += 1u;
     if (!(d.flags & GS_TOMBSTONES) || !d.row[o * 4 + 1]) return;
     const bool genm = !(d.flags & GS_CANONICAL);
     bool remaining = false;
     uint32_t gcn = 0;
-    for (uint32_t j = threadIdx.x; j < d.N; j += LB) {
+    for (uint32_t j = threadIdx.x; j < d.ncol; j += LB) {
         const size_t p = pix(d, o, j);
         if (genm && d.pos[p] == NONE) continue;
         uint32_t maxdel = d.gc[p];
@@ -743,7 +843,7 @@ __global__ __launch_bounds__(LB) void k_liveness(Dev d, const uint8_t *up, uint3
     const bool ring = (d.flags & GS_FD_RING) != 0;
     uint32_t minS = NONE, live = 0, gcdue = 0;
     const uint32_t c0 = (cb * LB + threadIdx.x) * 4u;
-    if (c0 < d.N) {
+    if (c0 < d.ncol) {
         const size_t p = pix(d, o, c0);
         uint64_t w[4];
         uint32_t st[4], ps[4] = {0u, 0u, 0u, 0u};
@@ -754,7 +854,7 @@ __global__ __launch_bounds__(LB) void k_liveness(Dev d, const uint8_t *up, uint3
 #pragma unroll
         for (int i = 0; i < 4; i++) {
             const uint32_t j = c0 + i;
-            if (j < d.N && j != o && !(genm && ps[i] == NONE)) {
+            if (j < d.ncol && d.col_lo + j != o && !(genm && ps[i] == NONE)) {
                 live++;
                 const Fd f = fd_unpack(d, w[i]);
                 const bool has = f.last != NONE;
@@ -814,7 +914,7 @@ __global__ __launch_bounds__(LB) void k_fd_gc(Dev d, const uint8_t *up, uint32_t
     const uint32_t cnt = d.row[o * 4 + 0];
     // 1. earliest expired target (in dead-dict order) that has no window
     unsigned long long fkey = ~0ull;
-    for (uint32_t j = tid; j < d.N; j += LB) {
+    for (uint32_t j = tid; j < d.ncol; j += LB) {
         const uint32_t st = d.fd_state[ro + j], pos = d.pos[ro + j];
         if (st >= 2u && pos != NONE && (uint64_t)t >= (uint64_t)(st - 2u) + d.dead_grace && d.fd[ro + j] == 0ull) {
             const unsigned long long key = ((unsigned long long)(st - 2u) << 32) | pos;
@@ -833,7 +933,7 @@ __global__ __launch_bounds__(LB) void k_fd_gc(Dev d, const uint8_t *up, uint32_t
     const bool q9 = fkey != ~0ull;
     // 2. drop dead entries / windows; mark dict removals
     uint32_t gcn = 0;
-    for (uint32_t j = tid; j < d.N; j += LB) {
+    for (uint32_t j = tid; j < d.ncol; j += LB) {
         const uint32_t st = d.fd_state[ro + j], pos = d.pos[ro + j];
         if (!(st >= 2u && pos != NONE && (uint64_t)t >= (uint64_t)(st - 2u) + d.dead_grace)) continue;
         const unsigned long long key = ((unsigned long long)(st - 2u) << 32) | pos;
@@ -868,7 +968,7 @@ __global__ __launch_bounds__(LB) void k_fd_gc(Dev d, const uint8_t *up, uint32_t
             base += tot;
             __syncthreads();
         }
-        for (uint32_t j = tid; j < d.N; j += LB) {
+        for (uint32_t j = tid; j < d.ncol; j += LB) {
             if (!bit(rmv, j)) continue;
             const size_t p = ro + j;
             d.pos[p] = NONE;
@@ -892,7 +992,7 @@ __global__ __launch_bounds__(LB) void k_fd_gc(Dev d, const uint8_t *up, uint32_t
 // SamplingWindow.phi (failure_detector.py:43-53) of every target of observer o; NaN for None.
 __global__ __launch_bounds__(LB) void k_phi_row(Dev d, uint32_t o, uint32_t t, double *out) {
     const uint32_t j = blockIdx.x * LB + threadIdx.x;
-    if (j >= d.N) return;
+    if (j >= d.ncol) return;
     const Fd f = fd_unpack(d, d.fd[pix(d, o, j)]);
     const uint32_t len = (d.flags & GS_FD_RING) ? (f.cnt < d.W ? f.cnt : d.W) : f.cnt;
     double phi = __builtin_nan("");
@@ -910,8 +1010,9 @@ __global__ __launch_bounds__(LB) void k_owner_writes(Dev d, const gs_write *ops,
     if (i >= n) return;
     const gs_write op = ops[i];
     if (op.owner >= d.N || op.key >= d.K || op.op > 3u) { shard_add(d, C_E_IDX, 1); return; }
-    const uint32_t j = op.owner, k = op.key;
-    const size_t pj = pix(d, j, j);
+    const uint32_t j = op.owner - d.col_lo, k = op.key;  // local column of the owner
+    if (j >= d.ncol) return;  // another slice's owner
+    const size_t pj = pix(d, op.owner, j);
     uint8_t *held = d.held + pj * d.KP + k;
     const uint32_t w = *held;
     const uint32_t M = d.mv[pj];
@@ -943,7 +1044,7 @@ __global__ __launch_bounds__(LB) void k_owner_writes(Dev d, const gs_write *ops,
     d.mv[pj] = ver;
     if (d.flags & GS_TOMBSTONES) {
         d.ts[pj * d.KP + k] = st ? t : NONE;
-        if (st) d.row[j * 4 + 1] = 1u;
+        if (st) d.row[op.owner * 4 + 1] = 1u;
     }
 }
 
@@ -951,12 +1052,13 @@ __global__ __launch_bounds__(LB) void k_owner_writes(Dev d, const gs_write *ops,
 __global__ __launch_bounds__(LB) void k_boot_self(Dev d) {
     const uint32_t o = blockIdx.x * LB + threadIdx.x;
     if (o >= d.N) return;
-    const size_t p = pix(d, o, o);
-    d.hb[p] = 1u;  // Cluster.__init__: inc_heartbeat (server.py:95-96)
     d.row[o * 4 + 0] = 1u;
     d.row[o * 4 + 1] = 0u;
     d.row[o * 4 + 2] = NONE;
     d.row[o * 4 + 3] = 0u;
+    if (o - d.col_lo >= d.ncol) return;
+    const size_t p = pix(d, o, o - d.col_lo);
+    d.hb[p] = 1u;  // Cluster.__init__: inc_heartbeat (server.py:95-96)
     if (!(d.flags & GS_CANONICAL)) {
         d.pos[p] = 0u;
         d.ord[(size_t)o * d.NP] = o;
@@ -965,17 +1067,17 @@ __global__ __launch_bounds__(LB) void k_boot_self(Dev d) {
 
 __global__ __launch_bounds__(LB) void k_warm(Dev d) {
     // grid-stride over (observer, owner) pairs: N^2 exceeds one launch's 2^32 work-items at N = 65,536
-    const uint64_t total = (uint64_t)d.N * d.N;
+    const uint64_t total = (uint64_t)d.N * d.ncol;
     for (uint64_t x = (uint64_t)blockIdx.x * LB + threadIdx.x; x < total; x += (uint64_t)gridDim.x * LB) {
-        const uint32_t o = (uint32_t)(x / d.N), j = (uint32_t)(x % d.N);
+        const uint32_t o = (uint32_t)(x / d.ncol), j = (uint32_t)(x % d.ncol), jg = d.col_lo + j;
         const size_t p = pix(d, o, j);
         if (!(d.flags & GS_CANONICAL)) {
             d.pos[p] = j;
             d.ord[p] = j;
             if (j == 0) d.row[o * 4 + 0] = d.N;
         }
-        if (j == o) continue;
-        const size_t q = pix(d, j, j);
+        if (jg == o) continue;
+        const size_t q = pix(d, jg, j);  // the owner's own view
         d.hb[p] = d.hb[q];
         d.mv[p] = d.mv[q];
         d.gc[p] = d.gc[q];
@@ -1001,6 +1103,7 @@ struct gs_handle {
     gs_config cfg;
     Dev d;
     uint32_t N, NP, K, KP, C, W;
+    uint32_t G, shard, col_lo, ncol;  // owner-column slice
     void *reg[GS_NUM_REGIONS];
     uint64_t bytes[GS_NUM_REGIONS];
     hipStream_t stream;
@@ -1051,16 +1154,33 @@ int check_bound(gs_handle *h) {
     d.key_len = (uint8_t *)h->reg[GS_R_KEY_LEN];
     d.stamp = (uint32_t *)h->reg[GS_R_STAMP];
     d.ctr = (unsigned long long *)h->reg[GS_R_COUNTERS];
+    d.sbits = (uint32_t *)h->reg[GS_R_SLICE_BITS];
     return GS_OK;
 }
 
-template <int KW, bool GENM, bool RING>
-int launch_exchange(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t n, uint32_t tick, size_t lds) {
-    auto *k = k_exchange<KW, GENM, RING>;
+template <int KW, bool GENM, bool RING, int MODE>
+int launch_exchange(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t n, uint32_t tick, size_t lds,
+                    const SliceIO &io) {
+    auto *k = k_exchange<KW, GENM, RING, MODE>;
     if (lds > 64 * 1024)
         HIPCHK(h, hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    k<<<n, XB, lds, h->stream>>>(h->d, ini, res, n, tick, h->seq);
+    k<<<n, XB, lds, h->stream>>>(h->d, ini, res, n, tick, h->seq, io);
     HIPCHK(h, hipGetLastError());
+    return GS_OK;
+}
+
+// LDS of k_exchange: two packer windows, then the stale-owner (+ insertion) bitmaps of this slice
+size_t exchange_lds(const gs_handle *h) {
+    const bool genm = !(h->cfg.flags & GS_CANONICAL);
+    return WIN * 2 * 2 + (size_t)(h->NP / 32) * (genm ? 4 : 2) * 4;
+}
+
+int check_phase(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t n) {
+    if (!h || !h->booted) return GS_E_INVALID;
+    if (n && (!ini || !res)) return GS_E_INVALID;
+    if (n > h->N / 2) return fail(h, GS_E_INVALID, "a phase has at most n_nodes/2 exchanges (got %u)", n);
+    if (exchange_lds(h) > 160 * 1024)
+        return fail(h, GS_E_UNSUPPORTED, "slice too wide for the LDS bitmaps (%zu B)", exchange_lds(h));
     return GS_OK;
 }
 
@@ -1077,6 +1197,13 @@ int gs_create(const gs_config *cfg, gs_handle **out) {
     *out = nullptr;
     const gs_config &c = *cfg;
     if (c.n_nodes < 2 || c.n_nodes > (1u << 20)) return GS_E_INVALID;
+    // owner-column slices: blocks of round_up(ceil(N / G), 64) columns, none empty, canonical only
+    const uint32_t G = c.n_shards ? c.n_shards : 1u;
+    if (G > 64 || c.shard >= G) return GS_E_INVALID;
+    const uint32_t blk = round_up((c.n_nodes + G - 1) / G, 64);
+    const uint64_t col_lo = (uint64_t)c.shard * blk;
+    if (G > 1 && (!(c.flags & GS_CANONICAL) || (uint64_t)(G - 1) * blk >= c.n_nodes)) return GS_E_INVALID;
+    const uint32_t ncol = G > 1 ? (uint32_t)std::min<uint64_t>(blk, c.n_nodes - col_lo) : c.n_nodes;
     if (c.n_keys < 1 || c.n_keys > 64) return GS_E_INVALID;
     if (c.hist_cap < 2 || c.hist_cap > 255) return GS_E_INVALID;
     if (c.mtu < 1 || c.window < 1) return GS_E_INVALID;
@@ -1089,7 +1216,11 @@ int gs_create(const gs_config *cfg, gs_handle **out) {
     gs_handle *h = new gs_handle();
     h->cfg = c;
     h->N = c.n_nodes;
-    h->NP = round_up(c.n_nodes, 64);
+    h->G = G;
+    h->shard = c.shard;
+    h->col_lo = G > 1 ? (uint32_t)col_lo : 0u;
+    h->ncol = ncol;
+    h->NP = round_up(ncol, 64);
     h->K = c.n_keys;
     h->KP = round_up(c.n_keys, 4);
     h->C = c.hist_cap;
@@ -1097,7 +1228,8 @@ int gs_create(const gs_config *cfg, gs_handle **out) {
     h->stream = nullptr;
     h->seq = 0;
     h->booted = false;
-    const uint64_t N = h->N, NP = h->NP, KP = h->KP, K = h->K, C = h->C, W = h->W;
+    const uint64_t N = h->N, NP = h->NP, KP = h->KP, K = h->K, C = h->C, W = h->W, NC = h->ncol;
+    const uint64_t NR = round_up(h->N, 64);
     const uint64_t pairs = N * NP;
     const bool genm = !(c.flags & GS_CANONICAL);
     uint64_t *b = h->bytes;
@@ -1109,20 +1241,21 @@ int gs_create(const gs_config *cfg, gs_handle **out) {
     b[GS_R_RING] = (c.flags & GS_FD_RING) ? pairs * W * 2 : 0;
     b[GS_R_POS] = b[GS_R_ORD] = genm ? pairs * 4 : 0;
     b[GS_R_ROW] = N * 16;
-    b[GS_R_LAST_W] = N * KP;
-    b[GS_R_HIST] = N * C * K * 8;
-    b[GS_R_HIST_VID] = N * C * K * 4;
+    b[GS_R_LAST_W] = NC * KP;
+    b[GS_R_HIST] = NC * C * K * 8;
+    b[GS_R_HIST_VID] = NC * C * K * 4;
     b[GS_R_NID_SIZE] = NP * 2;
     b[GS_R_KEY_LEN] = KP;
-    b[GS_R_STAMP] = NP * 4;
+    b[GS_R_STAMP] = NR * 4;
     b[GS_R_COUNTERS] = (uint64_t)NSHARD * 32 * 8;
+    b[GS_R_SLICE_BITS] = G > 1 ? (N / 2) * 2 * (NP / 32) * 4 : 0;
     Dev &d = h->d;
     memset(&d, 0, sizeof d);
     d.N = h->N;
-    d.col_lo = 0;
-    d.ncol = h->N;
-    d.shards = 1;
-    d.shard = 0;
+    d.col_lo = h->col_lo;
+    d.ncol = h->ncol;
+    d.shards = G;
+    d.shard = c.shard;
     d.NP = h->NP;
     d.K = h->K;
     d.KP = h->KP;
@@ -1169,21 +1302,21 @@ int gs_boot(gs_handle *h, const uint16_t *nid_size, const uint8_t *key_len) {
     int rc = check_bound(h);
     if (rc) return rc;
     hipStream_t s = h->stream;
-    const uint64_t pairs = (uint64_t)h->N * h->NP;
     // regions that start at zero
     const int zero[] = {GS_R_HB, GS_R_MV, GS_R_GC, GS_R_HELD, GS_R_FD, GS_R_FD_STATE,
                         GS_R_RING, GS_R_ROW, GS_R_LAST_W, GS_R_HIST, GS_R_HIST_VID,
-                        GS_R_STAMP, GS_R_COUNTERS};
+                        GS_R_STAMP, GS_R_COUNTERS, GS_R_SLICE_BITS};
     for (int r : zero)
         if (h->bytes[r]) HIPCHK(h, hipMemsetAsync(h->reg[r], 0, h->bytes[r], s));
     if (h->bytes[GS_R_TS]) HIPCHK(h, hipMemsetAsync(h->reg[GS_R_TS], 0xFF, h->bytes[GS_R_TS], s));
     if (h->bytes[GS_R_POS]) HIPCHK(h, hipMemsetAsync(h->reg[GS_R_POS], 0xFF, h->bytes[GS_R_POS], s));
     if (h->bytes[GS_R_ORD]) HIPCHK(h, hipMemsetAsync(h->reg[GS_R_ORD], 0xFF, h->bytes[GS_R_ORD], s));
     // tables
+    // nid_size covers all n_nodes (the packer's stop bound must hold across slices); keep this slice's
     std::vector<uint16_t> ns(h->NP, 0);
     uint32_t min_nid = 0xFFFFFFFFu, min_key = 0xFFFFFFFFu;
     for (uint32_t j = 0; j < h->N; j++) {
-        ns[j] = nid_size[j];
+        if (j - h->col_lo < h->ncol) ns[j - h->col_lo] = nid_size[j];
         if (nid_size[j] < min_nid) min_nid = nid_size[j];
     }
     std::vector<uint8_t> kl(h->KP, 0);
@@ -1205,7 +1338,7 @@ int gs_boot(gs_handle *h, const uint16_t *nid_size, const uint8_t *key_len) {
 
 int gs_warm(gs_handle *h) {
     if (!h || !h->booted) return GS_E_INVALID;
-    const uint64_t pairs = (uint64_t)h->N * h->N;
+    const uint64_t pairs = (uint64_t)h->N * h->ncol;
     const uint32_t blocks = (uint32_t)std::min<uint64_t>((pairs + LB - 1) / LB, 1u << 20);
     k_warm<<<blocks, LB, 0, h->stream>>>(h->d);
     HIPCHK(h, hipGetLastError());
@@ -1228,32 +1361,76 @@ int gs_begin_round(gs_handle *h, const uint8_t *up, uint32_t tick) {
 }
 
 int gs_run_phase(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t n, uint32_t tick) {
-    if (!h || !h->booted) return GS_E_INVALID;
+    int rc = check_phase(h, ini, res, n);
+    if (rc) return rc;
+    if (h->G > 1) return fail(h, GS_E_UNSUPPORTED, "sliced handle: use gs_phase_count / gs_phase_pack");
     if (!n) return GS_OK;
-    if (!ini || !res) return GS_E_INVALID;
     const bool genm = !(h->cfg.flags & GS_CANONICAL);
     const bool ring = (h->cfg.flags & GS_FD_RING) != 0;
-    const size_t lds = WIN * 2 * 2 + (size_t)(h->NP / 32) * (genm ? 4 : 2) * 4;
-    if (lds > 160 * 1024) return fail(h, GS_E_UNSUPPORTED, "n_nodes too large for the LDS bitmaps (%zu B)", lds);
+    const size_t lds = exchange_lds(h);
+    const SliceIO io{};
     h->seq += 1;
-    const bool k16 = h->KP <= 16;
-    if (k16) {
-        if (genm) return ring ? launch_exchange<4, true, true>(h, ini, res, n, tick, lds)
-                              : launch_exchange<4, true, false>(h, ini, res, n, tick, lds);
-        return ring ? launch_exchange<4, false, true>(h, ini, res, n, tick, lds)
-                    : launch_exchange<4, false, false>(h, ini, res, n, tick, lds);
+    if (h->KP <= 16) {
+        if (genm) return ring ? launch_exchange<4, true, true, 0>(h, ini, res, n, tick, lds, io)
+                              : launch_exchange<4, true, false, 0>(h, ini, res, n, tick, lds, io);
+        return ring ? launch_exchange<4, false, true, 0>(h, ini, res, n, tick, lds, io)
+                    : launch_exchange<4, false, false, 0>(h, ini, res, n, tick, lds, io);
     }
-    if (genm) return ring ? launch_exchange<16, true, true>(h, ini, res, n, tick, lds)
-                          : launch_exchange<16, true, false>(h, ini, res, n, tick, lds);
-    return ring ? launch_exchange<16, false, true>(h, ini, res, n, tick, lds)
-                : launch_exchange<16, false, false>(h, ini, res, n, tick, lds);
+    if (genm) return ring ? launch_exchange<16, true, true, 0>(h, ini, res, n, tick, lds, io)
+                          : launch_exchange<16, true, false, 0>(h, ini, res, n, tick, lds, io);
+    return ring ? launch_exchange<16, false, true, 0>(h, ini, res, n, tick, lds, io)
+                : launch_exchange<16, false, false, 0>(h, ini, res, n, tick, lds, io);
+}
+
+int gs_shard_columns(const gs_handle *h, uint32_t *col_lo, uint32_t *n_cols) {
+    if (!h || !col_lo || !n_cols) return GS_E_INVALID;
+    *col_lo = h->col_lo;
+    *n_cols = h->ncol;
+    return GS_OK;
+}
+
+int gs_phase_count(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t n, uint32_t tick,
+                   uint64_t *slice_bytes) {
+    int rc = check_phase(h, ini, res, n);
+    if (rc) return rc;
+    if (h->G < 2) return fail(h, GS_E_UNSUPPORTED, "gs_phase_count needs a sliced handle (n_shards > 1)");
+    if (!n) return GS_OK;
+    if (!slice_bytes) return GS_E_INVALID;
+    const bool ring = (h->cfg.flags & GS_FD_RING) != 0;
+    const size_t lds = exchange_lds(h);
+    SliceIO io{};
+    io.tot = slice_bytes;
+    h->seq += 1;
+    if (h->KP <= 16) return ring ? launch_exchange<4, false, true, 1>(h, ini, res, n, tick, lds, io)
+                                 : launch_exchange<4, false, false, 1>(h, ini, res, n, tick, lds, io);
+    return ring ? launch_exchange<16, false, true, 1>(h, ini, res, n, tick, lds, io)
+                : launch_exchange<16, false, false, 1>(h, ini, res, n, tick, lds, io);
+}
+
+int gs_phase_pack(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t n, uint32_t tick, uint32_t step,
+                  const uint64_t *slice_bytes_all, const uint64_t *chain_all, uint64_t *chain) {
+    int rc = check_phase(h, ini, res, n);
+    if (rc) return rc;
+    if (h->G < 2) return fail(h, GS_E_UNSUPPORTED, "gs_phase_pack needs a sliced handle (n_shards > 1)");
+    if (!n) return GS_OK;
+    if (!slice_bytes_all || !chain || step >= h->G || (step && !chain_all)) return GS_E_INVALID;
+    SliceIO io{};
+    io.tot_all = slice_bytes_all;
+    io.chain_all = chain_all;
+    io.chain = chain;
+    io.step = step;
+    if (step && h->shard == 0) return GS_OK;  // slice 0 always finishes at step 0
+    if (h->KP <= 16) k_pack_slice<4><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, io);
+    else k_pack_slice<16><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, io);
+    HIPCHK(h, hipGetLastError());
+    return GS_OK;
 }
 
 int gs_liveness(gs_handle *h, const uint8_t *up, uint32_t tick) {
     if (!h || !h->booted || !up) return GS_E_INVALID;
     k_reset_sched<<<(h->N + LB - 1) / LB, LB, 0, h->stream>>>(h->d, up);
     HIPCHK(h, hipGetLastError());
-    const uint32_t chunks = (h->N + 4 * LB - 1) / (4 * LB);
+    const uint32_t chunks = (h->ncol + 4 * LB - 1) / (4 * LB);
     k_liveness<<<chunks * h->N, LB, 0, h->stream>>>(h->d, up, tick, chunks);
     HIPCHK(h, hipGetLastError());
     if (!(h->cfg.flags & GS_CANONICAL)) {
@@ -1265,7 +1442,7 @@ int gs_liveness(gs_handle *h, const uint8_t *up, uint32_t tick) {
 
 int gs_phi_row(gs_handle *h, uint32_t observer, uint32_t tick, double *out) {
     if (!h || !h->booted || !out || observer >= h->N) return GS_E_INVALID;
-    k_phi_row<<<(h->N + LB - 1) / LB, LB, 0, h->stream>>>(h->d, observer, tick, out);
+    k_phi_row<<<(h->ncol + LB - 1) / LB, LB, 0, h->stream>>>(h->d, observer, tick, out);
     HIPCHK(h, hipGetLastError());
     return GS_OK;
 }

@@ -1,0 +1,201 @@
+"""Owner-column sharding of one simulated cluster (DESIGN.md "multi-GPU").
+
+Every slice holds all N observer rows and a contiguous block of owner columns
+(``gs_config.n_shards``/``shard``).  Heartbeat merges, failure-detector reports,
+digests and stale-owner tests are per column, so they run on each slice with no
+communication.  The only coupling is the MTU budget of each delta:
+``compute_partial_delta_respecting_mtu`` (state.py:340-415) walks the sender's
+stale owners in dict order — index order in the canonical layout, i.e. slice
+order — and stops adding once the DeltaPb is full.  Per phase:
+
+1. ``gs_phase_count`` on every slice: pass 1, plus the DeltaPb bytes of all the
+   slice's stale owners per (exchange, direction) — ``u64 [n][2]``;
+2. all-gather of those totals (16 B per exchange per slice; RCCL over xGMI);
+3. ``gs_phase_pack(step 0)``: each slice packs and applies its owners starting
+   at the byte count its predecessors reach when they all fit whole;
+4. only when some exchange's totals sum past the MTU: G-1 further steps, each an
+   all-gather of the ``u64 [n][2]`` chain states and a ``gs_phase_pack`` that
+   lets the next slice continue where its predecessor's packing stopped.
+
+The result equals ``gs_run_phase`` on a single handle bit for bit (tested on one
+GPU with G in-process slices).  ``comm`` abstracts the gather: ``LocalComm``
+(every slice in this process) or ``DistComm`` (one slice per rank,
+``torch.distributed``: RCCL on GPUs, gloo in the CPU tests).
+"""
+
+from __future__ import annotations
+
+import numpy as np
+
+from ._lib import COUNTER_FIELDS, GsError
+
+CHAIN_PENDING = -1  # u64 ~0 viewed as int64 (gossip_sim.hip CHAIN_PENDING)
+
+
+class LocalComm:
+    """All G slices live in this process (tests; one GPU)."""
+
+    def __init__(self, world: int):
+        self.world = world
+        self.rank = 0
+
+    def gather(self, parts):
+        import torch
+
+        return torch.stack(parts)
+
+    def sum_counters(self, per_slice: list[dict]) -> dict:
+        return {k: sum(c[k] for c in per_slice) for k in COUNTER_FIELDS}
+
+    def any(self, flag: bool) -> bool:
+        return flag
+
+
+class DistComm:
+    """One slice per rank of a ``torch.distributed`` process group."""
+
+    def __init__(self, group=None):
+        import torch.distributed as dist
+
+        self.dist = dist
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+
+    def gather(self, parts):
+        import torch
+
+        (x,) = parts
+        out = torch.empty((self.world,) + tuple(x.shape), dtype=x.dtype, device=x.device)
+        if self.dist.get_backend(self.group) == "gloo":
+            self.dist.all_gather(list(out.unbind(0)), x.contiguous(), group=self.group)
+        else:
+            self.dist.all_gather_into_tensor(out, x.contiguous(), group=self.group)
+        return out
+
+    def sum_counters(self, per_slice: list[dict]) -> dict:
+        import torch
+
+        (c,) = per_slice
+        dev = "cpu" if self.dist.get_backend(self.group) == "gloo" else "cuda"
+        v = torch.tensor([c[k] for k in COUNTER_FIELDS], dtype=torch.int64, device=dev)
+        self.dist.all_reduce(v, group=self.group)
+        return dict(zip(COUNTER_FIELDS, (int(x) for x in v.tolist())))
+
+    def any(self, flag: bool) -> bool:
+        return flag  # decided from gathered data, identical on every rank
+
+
+def run_sliced_phase(slices, comm, mtu: int, t: int, ini, res) -> int:
+    """One phase on the slices this process drives; returns the pack steps taken (1 = no chain).
+
+    ``slices`` expose ``phase_count(t, ini, res) -> [n, 2]`` and
+    ``phase_pack(t, ini, res, step, tot_all, chain_all, chain) -> chain`` (``GossipSim`` does).
+    """
+    import torch
+
+    n = int(ini.numel())
+    if n == 0:
+        return 0
+    tots = [s.phase_count(t, ini, res) for s in slices]
+    tot_all = comm.gather(tots)
+    chains = [torch.empty_like(x) for x in tots]
+    for s, ch in zip(slices, chains):
+        s.phase_pack(t, ini, res, 0, tot_all, None, ch)
+    # every rank holds the same tot_all, so they agree on whether the chain steps run
+    if not bool((tot_all.sum(0) > mtu).any()):
+        return 1
+    for step in range(1, comm.world):
+        chain_all = comm.gather(chains)
+        for s, ch in zip(slices, chains):
+            s.phase_pack(t, ini, res, step, tot_all, chain_all, ch)
+    return comm.world
+
+
+class ShardGroup:
+    """The owner-column slices of one simulated cluster, driven like one ``GossipSim``."""
+
+    def __init__(self, slices, comm, mtu: int):
+        if not slices:
+            raise GsError("ShardGroup needs at least one slice")
+        self.slices = list(slices)
+        self.comm = comm
+        self.mtu = int(mtu)
+        self.n = self.slices[0].n
+        self.chain_phases = 0
+
+    @classmethod
+    def in_process(cls, node_ids, keys, cfg, shards: int, **kw):
+        from .sim import GossipSim
+
+        sl = [GossipSim(node_ids, keys, cfg, shards=shards, shard=g, **kw) for g in range(shards)]
+        return cls(sl, LocalComm(shards), cfg["mtu"])
+
+    @classmethod
+    def distributed(cls, node_ids, keys, cfg, group=None, **kw):
+        from .sim import GossipSim
+
+        comm = DistComm(group)
+        s = GossipSim(node_ids, keys, cfg, shards=comm.world, shard=comm.rank, **kw)
+        return cls([s], comm, cfg["mtu"])
+
+    # -- owner writes / round driver: every slice sees every call (each keeps its own columns)
+    def write(self, t, j, k, op, value):
+        for s in self.slices:
+            s.write(t, j, k, op, value)
+
+    def owner_writes(self, ops: np.ndarray, tick: int):
+        for s in self.slices:
+            s.owner_writes(ops, tick)
+
+    def begin_round(self, t: int, up):
+        for s in self.slices:
+            s.begin_round(t, up)
+
+    def run_phase(self, t: int, pairs):
+        if len(pairs) == 0:
+            return
+        arr = np.asarray(pairs, dtype=np.int32).reshape(-1, 2)
+        self.run_phase_arrays(t, arr[:, 0], arr[:, 1])
+
+    def run_phase_arrays(self, t: int, initiators, responders):
+        s0 = self.slices[0]
+        for s in self.slices:
+            s._flush()
+        ini, res = s0._pairs_dev(initiators, responders)
+        if run_sliced_phase(self.slices, self.comm, self.mtu, t, ini, res) > 1:
+            self.chain_phases += 1
+
+    def update_node_liveness(self, t: int, up):
+        for s in self.slices:
+            s.update_node_liveness(t, up)
+
+    def liveness(self, t: int, up, r: int = -1):
+        self.update_node_liveness(t, up)
+
+    def sync(self):
+        for s in self.slices:
+            s.sync()
+
+    # -- counters / readback
+    def counters(self) -> dict:
+        return self.comm.sum_counters([s.counters() for s in self.slices])
+
+    def reset_counters(self):
+        for s in self.slices:
+            s.reset_counters()
+
+    def check(self) -> dict:
+        c = self.counters()
+        errs = {k: v for k, v in c.items() if k.startswith("err_") and v}
+        if errs:
+            raise GsError(f"device checks failed: {errs}")
+        return c
+
+    def export(self) -> dict:
+        """The slices this process holds, joined along the owner axis (all of them in-process)."""
+        parts = [s.export() for s in self.slices]
+        return {k: np.concatenate([p[k] for p in parts], axis=1) for k in parts[0]}
+
+    def phi_row(self, observer: int, tick: int | None = None) -> np.ndarray:
+        return np.concatenate([s.phi_row(observer, tick) for s in self.slices])

@@ -61,8 +61,11 @@ def sched_delay_ticks(dead_grace_s: float) -> int:
     return -(-half // TICK_US)
 
 
-def make_config(n: int, k: int, cfg: dict, flags: int, hist_cap: int) -> _lib.GsConfig:
+def make_config(n: int, k: int, cfg: dict, flags: int, hist_cap: int, shards: int = 1,
+                shard: int = 0) -> _lib.GsConfig:
     c = _lib.GsConfig()
+    c.n_shards = shards
+    c.shard = shard
     c.n_nodes = n
     c.n_keys = k
     c.hist_cap = hist_cap
@@ -99,13 +102,18 @@ def split_owner_batches(ops: list[tuple]) -> list[list[tuple]]:
 
 
 class GossipSim:
-    """A simulated cluster of ``len(node_ids)`` aiocluster nodes resident on one MI355X."""
+    """A simulated cluster of ``len(node_ids)`` aiocluster nodes resident on one MI355X.
+
+    With ``shards > 1`` this object holds one owner-column slice of the cluster (every
+    observer row, columns ``[col_lo, col_lo + ncol)``); the slices of a cluster are
+    driven together by ``aiocluster_amd.shard.ShardGroup``.
+    """
 
     def __init__(self, node_ids: list[NodeId], keys: list[str], cfg: dict, init: str = "cold",
                  initial_values: dict[int, list[tuple[int, str]]] | None = None, *, device: str = "cuda:0",
                  tombstones: bool = True, fd_ring: bool | None = None, hist_cap: int = 64,
                  nid_sizes: list[int] | None = None, initial_ops: list[np.ndarray] | None = None,
-                 canonical: bool | None = None):
+                 canonical: bool | None = None, shards: int = 1, shard: int = 0):
         import torch
 
         if not torch.cuda.is_available():
@@ -118,7 +126,9 @@ class GossipSim:
         self.keys = list(keys)
         self.k = k = len(keys)
         self.cfg = dict(cfg)
-        self.np_ = (n + 63) // 64 * 64
+        self.shards, self.shard = shards, shard
+        self.col_lo, self.ncol = _lib.slice_columns(n, shards, shard)
+        self.np_ = (self.ncol + 63) // 64 * 64
         self.kp = (k + 3) // 4 * 4
         self.hist_cap = hist_cap
         self.init = init
@@ -133,12 +143,12 @@ class GossipSim:
             flags |= GS_TOMBSTONES
         W = int(cfg["window"])
         if fd_ring is None:
-            fd_ring = n * self.np_ * W * 2 <= (1 << 30)
+            fd_ring = n * ((n + 63) // 64 * 64) * W * 2 <= (1 << 30)  # whole-cluster rule: every slice agrees
         if fd_ring:
             flags |= GS_FD_RING
         self.flags = flags
         self.canonical = bool(flags & GS_CANONICAL)
-        c = make_config(n, k, cfg, flags, hist_cap)
+        c = make_config(n, k, cfg, flags, hist_cap, shards, shard)
         h = C.c_void_p()
         rc = self.L.gs_create(C.byref(c), C.byref(h))
         if rc:
@@ -265,16 +275,41 @@ class GossipSim:
         arr = np.asarray(pairs, dtype=np.int32).reshape(-1, 2)
         self.run_phase_arrays(t, arr[:, 0], arr[:, 1])
 
-    def run_phase_arrays(self, t: int, initiators, responders):
+    def _pairs_dev(self, initiators, responders):
         ini = initiators if hasattr(initiators, "data_ptr") else self._dev(np.asarray(initiators, np.int32),
                                                                            self.torch.int32)
         res = responders if hasattr(responders, "data_ptr") else self._dev(np.asarray(responders, np.int32),
                                                                            self.torch.int32)
+        return ini, res
+
+    def run_phase_arrays(self, t: int, initiators, responders):
+        if self.shards > 1:
+            raise GsError("a column slice runs phases through ShardGroup (gs_phase_count / gs_phase_pack)")
+        ini, res = self._pairs_dev(initiators, responders)
         n = int(ini.numel())
         if n == 0:
             return
         self._chk(self.L.gs_run_phase(self.h, C.c_void_p(ini.data_ptr()), C.c_void_p(res.data_ptr()), n, t),
                   "gs_run_phase")
+
+    # ------------------------------------------------------- sliced phases (shards > 1)
+    def phase_count(self, t: int, ini, res, out=None):
+        """gs_phase_count: pass 1 on this slice; returns the device u64 slice totals [n, 2] (as int64)."""
+        n = int(ini.numel())
+        if out is None:
+            out = self.torch.empty((n, 2), dtype=self.torch.int64, device=self.device)
+        self._chk(self.L.gs_phase_count(self.h, C.c_void_p(ini.data_ptr()), C.c_void_p(res.data_ptr()), n, t,
+                                        C.c_void_p(out.data_ptr())), "gs_phase_count")
+        return out
+
+    def phase_pack(self, t: int, ini, res, step: int, tot_all, chain_all, chain):
+        """gs_phase_pack step ``step``; ``tot_all``/``chain_all`` are the gathered [G, n, 2] tensors."""
+        n = int(ini.numel())
+        ca = C.c_void_p(chain_all.data_ptr()) if chain_all is not None else None
+        self._chk(self.L.gs_phase_pack(self.h, C.c_void_p(ini.data_ptr()), C.c_void_p(res.data_ptr()), n, t, step,
+                                       C.c_void_p(tot_all.data_ptr()), ca, C.c_void_p(chain.data_ptr())),
+                  "gs_phase_pack")
+        return chain
 
     def update_node_liveness(self, t: int, up):
         self._flush()
@@ -318,10 +353,11 @@ class GossipSim:
             g[name] = self.region(name, torch.int32, (n, NP)).cpu().numpy().view(np.uint32)
         g["FD_LAST"], g["FD_SUM"], g["FD_CNT"] = self.unpack_fd(self.region("FD", torch.int64, (n, NP)).cpu().numpy())
         g["HELD"] = self.region("HELD", torch.uint8, (n, NP, KP)).cpu().numpy()
-        hist = self.region("HIST", torch.int64, (n, Cc, K)).cpu().numpy().view(np.uint64)
+        nc = self.ncol
+        hist = self.region("HIST", torch.int64, (nc, Cc, K)).cpu().numpy().view(np.uint64)
         g["HIST_VER"] = (hist & 0xFFFFFFFF).astype(np.uint32)
         g["HIST_META"] = (hist >> 32).astype(np.uint32)
-        g["HIST_VID"] = self.region("HIST_VID", torch.int32, (n, Cc, K)).cpu().numpy().view(np.uint32)
+        g["HIST_VID"] = self.region("HIST_VID", torch.int32, (nc, Cc, K)).cpu().numpy().view(np.uint32)
         g["ROW"] = self.region("ROW", torch.int32, (n, 4)).cpu().numpy().view(np.uint32)
         if "TS" in self.regions:
             g["TS"] = self.region("TS", torch.int32, (n, NP, KP)).cpu().numpy().view(np.uint32)
@@ -330,9 +366,11 @@ class GossipSim:
         return g
 
     def export(self, g=None) -> dict:
-        """All observers as numpy arrays in the oracle's ``export_row`` format (times in ticks)."""
+        """All observers as numpy arrays in the oracle's ``export_row`` format (times in ticks).
+
+        A column slice exports its own owner columns (``ShardGroup.export`` joins them)."""
         g = self._host() if g is None else g
-        n, K = self.n, self.k
+        nr, n, K = self.n, self.ncol, self.k
         held = g["HELD"][:, :n, :K].astype(np.int64)
         jj = np.arange(n)[None, :, None]
         kk = np.arange(K)[None, None, :]
@@ -347,11 +385,11 @@ class GossipSim:
             "kv_value_id": np.where(present, vid, 0).astype(np.uint32),
         }
         if self.canonical:
-            out["pos"] = np.broadcast_to(np.arange(n, dtype=np.int32), (n, n)).copy()
+            out["pos"] = np.broadcast_to(np.arange(self.col_lo, self.col_lo + n, dtype=np.int32), (nr, n)).copy()
         else:
             pos = self.region("POS", self.torch.int32, (n, self.np_)).cpu().numpy()[:, :n]
             out["pos"] = np.where(pos == -1, -1, pos).astype(np.int32)
-        ts = g["TS"][:, :n, :K].astype(np.int64) if "TS" in g else np.zeros((n, n, K), np.int64)
+        ts = g["TS"][:, :n, :K].astype(np.int64) if "TS" in g else np.zeros((nr, n, K), np.int64)
         out["kv_ts"] = np.where(out["kv_status"] != 0, ts, 0)
         last = g["FD_LAST"][:, :n]
         out["fd_last"] = np.where(last == GS_NONE, -1, last.astype(np.int64))
@@ -376,9 +414,13 @@ class GossipSim:
     def phi_row(self, observer: int, tick: int | None = None) -> np.ndarray:
         """Device-computed phi (binary64) of every target of ``observer``; NaN = None."""
         t = self.last_tick if tick is None else tick
-        out = self.torch.empty(self.n, dtype=self.torch.float64, device=self.device)
+        out = self.torch.empty(self.ncol, dtype=self.torch.float64, device=self.device)
         self._chk(self.L.gs_phi_row(self.h, observer, t, C.c_void_p(out.data_ptr())), "gs_phi_row")
         return out.cpu().numpy()
+
+    def _whole(self):
+        if self.shards > 1:
+            raise GsError("per-observer views need the whole matrix (shards == 1); use export() on a slice")
 
     def _order(self, g, o: int) -> list[int]:
         if self.canonical:
@@ -405,6 +447,7 @@ class GossipSim:
 
     def observer_state(self, o: int, g=None) -> dict:
         """Canonical dump, identical in format to ``oracle/refharness.py`` (golden fixtures)."""
+        self._whole()
         g = self._host() if g is None else g
         nodes = []
         for j in self._order(g, o):
@@ -428,6 +471,7 @@ class GossipSim:
     # --------------------------------------------------------------- reference-shaped views
     def node_state(self, observer: int, owner: int) -> NodeState | None:
         """``ClusterState.node_state`` of ``observer`` for ``owner`` (state.py:295-296)."""
+        self._whole()
         g = self._host()
         if owner not in self._order(g, observer):
             return None
@@ -439,10 +483,12 @@ class GossipSim:
                          int(g["GC"][observer, owner]))
 
     def live_nodes(self, observer: int) -> list[NodeId]:
+        self._whole()
         st = self.region("FD_STATE", self.torch.int32, (self.n, self.np_))[observer, : self.n].cpu().numpy()
         return [self.node_ids[j] for j in np.flatnonzero(st == 1)]
 
     def dead_nodes(self, observer: int) -> list[NodeId]:
+        self._whole()
         st = self.region("FD_STATE", self.torch.int32, (self.n, self.np_))[observer, : self.n].cpu().numpy()
         return [self.node_ids[j] for j in np.flatnonzero(st >= 2)]
 

@@ -7,9 +7,12 @@ answer), phi window 1000, mtu 65,507.  One step = one gossip round: owner writes
 heartbeat + tombstone GC, 9 conflict-free exchange phases, liveness sweep.  All
 inputs (schedules, write batches, up masks) are uploaded to HBM before timing.
 
-Multi-GPU: ``--gpus N`` under torch.distributed runs one 65,536-node simulation per
-GPU (independent replicas, seed + rank; observer-row sharding across GPUs is not
-built yet -- DESIGN.md).  ``value`` is the exchanges of all ranks / max rank time.
+Multi-GPU: ``--gpus N`` under torch.distributed splits ONE 65,536-node cluster into N
+owner-column slices, one per GPU (aiocluster_amd/shard.py; strong scaling): every rank
+runs every exchange on its columns, and the ranks exchange only 16 bytes per exchange
+(an RCCL all-gather of per-slice DeltaPb totals, plus chain states when a delta
+overflows the MTU).  ``value`` is the cluster's exchanges / the slowest rank's time.
+``--slices G`` rehearses the same sliced path with G slices in one process on one GPU.
 
 Prints ONE JSON line (rank 0) with the roofline of the dominant kernel (k_exchange,
 HIP-event timed on the library's stream) and the CPU baseline (the C oracle on one
@@ -75,23 +78,33 @@ def prepare(sim, spec, rounds, torch, dev):
     return out
 
 
-def run_round(sim, rd, events=None):
-    L, h = sim.L, sim.h
-    if rd["nops"]:
-        sim._chk(L.gs_owner_writes(h, C.c_void_p(rd["ops"].data_ptr()), rd["nops"], rd["t"]), "gs_owner_writes")
-    sim._chk(L.gs_begin_round(h, C.c_void_p(rd["up"].data_ptr()), rd["t"]), "gs_begin_round")
+def run_round(sims, rd, events=None, group=None):
+    """One gossip round on the slices this process drives (one GossipSim when unsliced)."""
+    from aiocluster_amd.shard import run_sliced_phase
+
+    s0 = sims[0]
+    for sim in sims:
+        if rd["nops"]:
+            sim._chk(sim.L.gs_owner_writes(sim.h, C.c_void_p(rd["ops"].data_ptr()), rd["nops"], rd["t"]),
+                     "gs_owner_writes")
+        sim._chk(sim.L.gs_begin_round(sim.h, C.c_void_p(rd["up"].data_ptr()), rd["t"]), "gs_begin_round")
     for a, b, n, t in rd["phases"]:
         if not n:
             continue
         if events is not None:
-            e0 = sim.torch.cuda.Event(enable_timing=True)
-            e1 = sim.torch.cuda.Event(enable_timing=True)
-            e0.record(sim.stream)
-        sim._chk(L.gs_run_phase(h, C.c_void_p(a.data_ptr()), C.c_void_p(b.data_ptr()), n, t), "gs_run_phase")
+            e0 = s0.torch.cuda.Event(enable_timing=True)
+            e1 = s0.torch.cuda.Event(enable_timing=True)
+            e0.record(s0.stream)
+        if group is None:
+            s0._chk(s0.L.gs_run_phase(s0.h, C.c_void_p(a.data_ptr()), C.c_void_p(b.data_ptr()), n, t),
+                    "gs_run_phase")
+        else:
+            run_sliced_phase(sims, group.comm, group.mtu, t, a, b)
         if events is not None:
-            e1.record(sim.stream)
+            e1.record(s0.stream)
             events.append((e0, e1))
-    sim._chk(L.gs_liveness(h, C.c_void_p(rd["up"].data_ptr()), rd["t_live"]), "gs_liveness")
+    for sim in sims:
+        sim._chk(sim.L.gs_liveness(sim.h, C.c_void_p(rd["up"].data_ptr()), rd["t_live"]), "gs_liveness")
 
 
 def cpu_baseline(sim, spec, cfg, next_plan, sample: int, min_seconds: float = 10.0):
@@ -212,6 +225,7 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=64)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--slices", type=int, default=1, help="owner-column slices in this process (1-GPU rehearsal)")
     args = ap.parse_args()
 
     import torch
@@ -229,12 +243,13 @@ def main():
     torch.cuda.set_device(dev)
 
     from aiocluster_amd.scenario import DEFAULT_CFG
+    from aiocluster_amd.shard import DistComm, LocalComm, ShardGroup
     from aiocluster_amd.sim import GossipSim
     from aiocluster_amd.workload import WorkloadSpec, key_names, synthetic_node_ids
 
     n, K = args.nodes, args.keys
     cfg = dict(DEFAULT_CFG)  # mtu 65507, window 1000, phi 8, max_interval 10 s, prior 5 s
-    spec = WorkloadSpec(n=n, k=K, fanout=args.fanout, seed=args.seed + rank, init="warm", write_frac=0.05,
+    spec = WorkloadSpec(n=n, k=K, fanout=args.fanout, seed=args.seed, init="warm", write_frac=0.05,
                         down_frac=0.05, down_rounds=3)
     workload = f"N={n} K={K} F={args.fanout} warm, 5% writes + 5% down churn/round, window 1000, mtu 65507"
     t_setup = time.perf_counter()
@@ -247,38 +262,54 @@ def main():
         ops[:, 3] = 1 + k * n + np.arange(n)
         ops[:, 4] = 3 + digits(np.arange(n)) + digits(np.full(n, k)) + 1
         boot.append(ops)
-    sim = GossipSim(ids, key_names(K), cfg, init="warm", device=str(dev), tombstones=False, fd_ring=False,
-                    hist_cap=16, initial_ops=boot)
+    kw = dict(init="warm", device=str(dev), tombstones=False, fd_ring=False, hist_cap=16, initial_ops=boot)
+    if world > 1 and args.slices > 1:
+        raise SystemExit("--slices is a one-process rehearsal; with --gpus N each rank holds one slice")
+    group = None
+    if world > 1:
+        sims = [GossipSim(ids, key_names(K), cfg, shards=world, shard=rank, **kw)]
+        group = ShardGroup(sims, DistComm(), cfg["mtu"])
+    elif args.slices > 1:
+        sims = [GossipSim(ids, key_names(K), cfg, shards=args.slices, shard=g, **kw) for g in range(args.slices)]
+        group = ShardGroup(sims, LocalComm(args.slices), cfg["mtu"])
+    else:
+        sims = [GossipSim(ids, key_names(K), cfg, **kw)]
+    sim = sims[0]
     plans = prepare(sim, spec, args.warmup + args.steps + 1, torch, dev)
     torch.cuda.synchronize(dev)
     log(f"setup {time.perf_counter() - t_setup:.1f}s")
 
     for r in range(args.warmup):
-        run_round(sim, plans[r])
+        run_round(sims, plans[r], group=group)
     torch.cuda.synchronize(dev)
-    sim.check()
-    sim.reset_counters()
+    for s_ in sims:
+        s_.check()
+        s_.reset_counters()
     events = []
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for r in range(args.warmup, args.warmup + args.steps):
-        run_round(sim, plans[r], events)
+        run_round(sims, plans[r], events, group)
     torch.cuda.synchronize(dev)
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    c = sim.check()
+    local = [s_.check() for s_ in sims]
+    c = group.comm.sum_counters(local) if group is not None else local[0]
     exch = sum(plans[r]["exchanges"] for r in range(args.warmup, args.warmup + args.steps))
     assert c["exchanges"] == exch, (c["exchanges"], exch)
     kern_ms = sum(e0.elapsed_time(e1) for e0, e1 in events)
     launches = len(events)
-    exch_total, elapsed_max = aggregate(exch, elapsed, dist, dev)
-    achieved = c["alg_bytes"] / (kern_ms / 1e3) / 1e9 if kern_ms > 0 else 0.0
-    traffic = load_traffic(workload, exch / max(1, len(events)))
+    # a sliced cluster: every rank runs the same exchanges on its columns -> count them once
+    exch_total, elapsed_max = aggregate(exch if (group is None or rank == 0) else 0, elapsed, dist, dev)
+    # this process's algorithmic bytes (all its slices) over its phase time
+    alg_local = sum(x["alg_bytes"] for x in local)
+    achieved = alg_local / (kern_ms / 1e3) / 1e9 if kern_ms > 0 else 0.0
+    traffic = load_traffic(workload, exch / max(1, len(events))) if group is None else None
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and group is None and not args.no_cpu_baseline:
         cpu = cpu_baseline(sim, spec, cfg, plans[args.warmup + args.steps], args.cpu_sample, args.cpu_seconds)
     if rank == 0:
         line = {
@@ -290,7 +321,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed_max / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if group is not None else "weak",
             "vs_baseline": None,
             "dtype": "u32",
             "data": "synthetic (seeded workload generator; no dataset)",
@@ -300,17 +331,19 @@ def main():
                 "keys": K,
                 "fanout": args.fanout,
                 "exchanges_per_step": exch / args.steps,
-                "parallelism": f"replicas x{world}" if world > 1 else "1 GPU",
+                "parallelism": (f"owner-column slices x{world} (RCCL all-gather of slice totals)" if world > 1
+                                else f"owner-column slices x{args.slices} in one process" if group is not None
+                                else "1 GPU"),
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "k_exchange",
+                "kernel": "k_exchange" if group is None else "sliced phase (count + gather + pack), per rank",
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBPS,
                 "traffic": traffic,
-                "alg_bytes_per_launch": c["alg_bytes"] / max(1, launches),
+                "alg_bytes_per_launch": alg_local / max(1, launches),
                 "avg_launch_ms": kern_ms / max(1, launches),
                 "launches": launches,
                 "kernel_share_of_step": kern_ms / 1e3 / elapsed,

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define GS_API_VERSION 1
+#define GS_API_VERSION 2
 #define GS_TICK_US 15625u
 #define GS_NONE 0xFFFFFFFFu
 
@@ -65,9 +65,16 @@ typedef struct gs_config {
                                        (failure_detector.py:124-126) */
     double phi_threshold;           /* FailureDetectorConfig.phi_threshhold (entities.py:87) */
     double prior_weighted;          /* 5.0 * initial_interval.total_seconds() (failure_detector.py:22-23,51) */
+    uint32_t n_shards;              /* G owner-column slices of the cluster (0 or 1 = the whole matrix;
+                                       G > 1 needs GS_CANONICAL); one handle per slice, usually one per GPU */
+    uint32_t shard;                 /* this handle's slice: columns [shard*B, min(N, (shard+1)*B)),
+                                       B = ceil(N/G) rounded up to 64 (every slice must be non-empty) */
 } gs_config;
 
-/* device regions (all caller-allocated; row stride NP = n_nodes rounded up to 64) */
+/* device regions (all caller-allocated).  [N][NP] regions hold every observer row o and this
+ * handle's owner columns j = col_lo + jl (gs_shard_columns), row stride NP = n_cols rounded up
+ * to 64; per-owner regions ([NC]..., NC = n_cols) are indexed by the local column jl.  With one
+ * slice col_lo = 0 and n_cols = n_nodes. */
 enum gs_region {
     GS_R_HB = 0,      /* u32 [N][NP]   NodeState.heartbeat of owner j as seen by observer o */
     GS_R_MV,          /* u32 [N][NP]   NodeState.max_version */
@@ -82,16 +89,18 @@ enum gs_region {
     GS_R_RING,        /* u16 [N][NP][W] interval ring in ticks (GS_FD_RING) */
     GS_R_POS,         /* u32 [N][NP]   insertion index of owner j in observer o's dict, GS_NONE = absent (general) */
     GS_R_ORD,         /* u32 [N][NP]   owner at insertion index q (general) */
-    GS_R_ROW,         /* u32 [N][4]    {dict size, tombstone-present flag, first tick a dead target is
-                                        scheduled for deletion, reserved} */
-    GS_R_LAST_W,      /* u8  [N][KP]   owner's latest write ordinal per key */
-    GS_R_HIST,        /* u64 [N][C][K] write w of (owner, key): version | meta << 32, where
+    GS_R_ROW,         /* u32 [N][4]    {dict size, tombstone-present flag, first tick a dead target of
+                                        this slice is scheduled for deletion, FD-GC-due flag} */
+    GS_R_LAST_W,      /* u8  [NC][KP]  owner's latest write ordinal per key */
+    GS_R_HIST,        /* u64 [NC][C][K] write w of (owner, key): version | meta << 32, where
                                         meta = KeyValueUpdatePb size | status << 16 | value bytes << 18 */
-    GS_R_HIST_VID,    /* u32 [N][C][K] interned value id (host string table) */
-    GS_R_NID_SIZE,    /* u16 [NP]      NodeIdPb size per node (entities.py:62-72) */
+    GS_R_HIST_VID,    /* u32 [NC][C][K] interned value id (host string table) */
+    GS_R_NID_SIZE,    /* u16 [NP]      NodeIdPb size per owner column (entities.py:62-72) */
     GS_R_KEY_LEN,     /* u8  [KP]      UTF-8 key length per key index */
-    GS_R_STAMP,       /* u32 [NP]      per-node phase stamp (conflict check) */
+    GS_R_STAMP,       /* u32 [N rounded to 64] per-node phase stamp (conflict check) */
     GS_R_COUNTERS,    /* u64 [64][32]  sharded gs_counters (summed by gs_read_counters) */
+    GS_R_SLICE_BITS,  /* u32 [N/2][2][NP/32] stale-owner bitmaps between gs_phase_count and
+                                        gs_phase_pack (n_shards > 1 only) */
     GS_NUM_REGIONS
 };
 
@@ -149,12 +158,32 @@ int gs_begin_round(gs_handle *h, const uint8_t *up, uint32_t tick);
  * Syn/SynAck/Ack = server.py:327-376 + 524, i.e. compute_digest, _report_heartbeat,
  * compute_partial_delta_respecting_mtu and apply_delta on both sides. */
 int gs_run_phase(gs_handle *h, const int32_t *initiators, const int32_t *responders, uint32_t n, uint32_t tick);
+/* Owner-column sliced phase (n_shards > 1; gs_run_phase refuses sliced handles).  The slices of one
+ * cluster run, per phase, on the same initiators/responders:
+ *   1. gs_phase_count: pass 1 of every exchange on this slice's columns (heartbeats, failure-detector
+ *      reports, stale-owner bitmaps) and, per exchange and direction, the DeltaPb bytes of all this
+ *      slice's stale owners: DEVICE u64 slice_bytes[n][2] (dir 0 = responder -> initiator).
+ *   2. the caller gathers every slice's slice_bytes into slice_bytes_all[G][n][2] (slice order), e.g.
+ *      an RCCL all-gather;
+ *   3. gs_phase_pack(step 0): packing + apply_delta of this slice's owners, resumed at the DeltaPb
+ *      size the earlier slices reach (compute_partial_delta_respecting_mtu walks owners in dict order,
+ *      state.py:392-413); its state goes to chain[n][2];
+ *   4. only if some exchange's slice totals sum past the mtu: for step = 1 .. G-1, gather every
+ *      slice's chain into chain_all[G][n][2], then gs_phase_pack(step).
+ * The result equals gs_run_phase on one handle bit for bit. */
+int gs_shard_columns(const gs_handle *h, uint32_t *col_lo, uint32_t *n_cols);
+int gs_phase_count(gs_handle *h, const int32_t *initiators, const int32_t *responders, uint32_t n, uint32_t tick,
+                   uint64_t *slice_bytes);
+int gs_phase_pack(gs_handle *h, const int32_t *initiators, const int32_t *responders, uint32_t n, uint32_t tick,
+                  uint32_t step, const uint64_t *slice_bytes_all, const uint64_t *chain_all, uint64_t *chain);
+
 /* _update_node_liveness for every up node (server.py:606-620; failure_detector.py:89-128),
  * including garbage_collect + remove_node (general layout only). */
 int gs_liveness(gs_handle *h, const uint8_t *up, uint32_t tick);
 
 /* SamplingWindow.phi (failure_detector.py:43-53) of every target of `observer` at `tick`
- * into the DEVICE array out[n_nodes] (binary64; NaN where the reference returns None). */
+ * into the DEVICE array out[n_cols] (this slice's targets; binary64; NaN where the reference
+ * returns None). */
 int gs_phi_row(gs_handle *h, uint32_t observer, uint32_t tick, double *out);
 
 int gs_read_counters(gs_handle *h, gs_counters *out);

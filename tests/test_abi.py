@@ -28,7 +28,7 @@ def test_library_loads_and_exports_every_symbol():
     for name in header_functions():
         assert hasattr(L, name), name
     lib = _lib.load()
-    assert lib.gs_api_version() == 1
+    assert lib.gs_api_version() == _lib.API_VERSION
 
 
 def test_create_validates_config_without_gpu():
@@ -56,3 +56,42 @@ def test_sched_delay_rounding():
     assert sched_delay_ticks(86400.0) == 43200 * 64
     assert sched_delay_ticks(1 / 64) == 1  # 7812.5 us rounds half-even to 7812 -> 1 tick
     assert sched_delay_ticks(30.0) == 15 * 64
+
+
+def test_slice_columns_and_region_sizes_without_gpu():
+    """Owner-column slices (gs_config.n_shards/shard): the library and the host agree on the split."""
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("library not built")
+    from aiocluster_amd.scenario import DEFAULT_CFG
+    from aiocluster_amd.sim import make_config
+
+    lib = _lib.load()
+    n = 1000
+    seen = []
+    for g in range(3):
+        c = make_config(n, 16, DEFAULT_CFG, _lib.GS_CANONICAL, 32)
+        c.n_shards, c.shard = 3, g
+        h = ctypes.c_void_p()
+        assert lib.gs_create(ctypes.byref(c), ctypes.byref(h)) == 0
+        lo, nc = ctypes.c_uint32(), ctypes.c_uint32()
+        assert lib.gs_shard_columns(h, ctypes.byref(lo), ctypes.byref(nc)) == 0
+        assert (lo.value, nc.value) == _lib.slice_columns(n, 3, g)
+        seen.append((lo.value, nc.value))
+        npad = (nc.value + 63) // 64 * 64
+        nb = ctypes.c_uint64()
+        assert lib.gs_region_bytes(h, _lib.REGION["HB"], ctypes.byref(nb)) == 0 and nb.value == n * npad * 4
+        assert lib.gs_region_bytes(h, _lib.REGION["HIST"], ctypes.byref(nb)) == 0 and nb.value == nc.value * 32 * 16 * 8
+        assert lib.gs_region_bytes(h, _lib.REGION["SLICE_BITS"], ctypes.byref(nb)) == 0
+        assert nb.value == (n // 2) * 2 * (npad // 32) * 4
+        lib.gs_destroy(h)
+    assert seen == [(0, 384), (384, 384), (768, 232)]
+    # slices need the canonical layout, and none may be empty
+    c = make_config(n, 16, DEFAULT_CFG, 0, 32)
+    c.n_shards, c.shard = 2, 0
+    h = ctypes.c_void_p()
+    assert lib.gs_create(ctypes.byref(c), ctypes.byref(h)) == -1
+    c = make_config(100, 16, DEFAULT_CFG, _lib.GS_CANONICAL, 32)
+    c.n_shards, c.shard = 3, 0
+    assert lib.gs_create(ctypes.byref(c), ctypes.byref(h)) == -1
+    with pytest.raises(ValueError):
+        _lib.slice_columns(100, 3, 0)

@@ -1,0 +1,64 @@
+"""Owner-column sharding invariance on one GPU (SURVEY.md §8(c) "config 4 is checked for sharding
+invariance"): G in-process slices driven through gs_phase_count / gs_phase_pack must end every
+round in exactly the state of a single handle (and of the C oracle), including deltas that the MTU
+cuts across slice boundaries (the chain steps).  GPU only.
+"""
+
+import numpy as np
+import pytest
+from helpers import compare_exports, make_backend
+from oracle import OracleSim
+
+from aiocluster_amd.scenario import initial_by_owner, make_scenario, replay_round, scenario_node_ids
+from aiocluster_amd.shard import ShardGroup
+from aiocluster_amd.sim import GossipSim
+from aiocluster_amd.workload import WorkloadSpec
+
+pytestmark = pytest.mark.gpu
+
+
+def sharded(scen, G, **kw):
+    return ShardGroup.in_process(scenario_node_ids(scen), scen["keys"], scen["config"], G, init=scen["init"],
+                                 initial_values=initial_by_owner(scen), **kw)
+
+
+@pytest.mark.parametrize("n,G,mtu,tomb", [(256, 2, 1800, True), (384, 3, 3000, False), (512, 4, 1200, True),
+                                          (200, 2, 65507, True)])
+def test_slices_match_single_handle(n, G, mtu, tomb):
+    spec = WorkloadSpec(n=n, k=8, fanout=3, seed=n + G, init="warm", write_frac=0.3,
+                        delete_frac=0.1 if tomb else 0.0, ttl_frac=0.05 if tomb else 0.0,
+                        down_frac=0.05, down_rounds=2)
+    scen = make_scenario(f"shard{n}x{G}", spec, 8, {"mtu": mtu, "tombstone_grace_s": 2})
+    kw = dict(tombstones=tomb, fd_ring=False)
+    one = make_backend(GossipSim, scen, **kw)
+    grp = sharded(scen, G, **kw)
+    for r in range(len(scen["rounds"])):
+        replay_round(one, scen, r)
+        replay_round(grp, scen, r)
+        diff = compare_exports(grp.export(), one.export())
+        assert diff is None, f"round {r}: {diff}"
+    c1, cg = one.check(), grp.check()
+    for k in ("exchanges", "hb_reports", "node_deltas", "kvs_sent", "truncated", "delta_bytes", "hb_writes",
+              "live_pairs", "tomb_gc"):
+        assert cg[k] == c1[k], (k, cg[k], c1[k])
+    if mtu < 65507:
+        assert c1["truncated"] > 0 and grp.chain_phases > 0  # deltas were cut, chains ran
+    o = n // 3
+    assert np.array_equal(grp.phi_row(o), one.phi_row(o), equal_nan=True)
+
+
+def test_slices_match_oracle_with_ring():
+    spec = WorkloadSpec(n=192, k=16, fanout=3, seed=5, init="warm", write_frac=0.2, delete_frac=0.1,
+                        down_frac=0.1, down_rounds=3)
+    scen = make_scenario("shard192", spec, 10, {"mtu": 2200, "window": 4, "tombstone_grace_s": 3,
+                                                "initial_interval_s": 1.0, "phi_threshold": 3.0})
+    grp = sharded(scen, 3, fd_ring=True)
+    orc = make_backend(OracleSim, scen)
+    for r in range(len(scen["rounds"])):
+        replay_round(grp, scen, r)
+        replay_round(orc, scen, r)
+        diff = compare_exports(grp.export(), orc.export())
+        assert diff is None, f"round {r}: {diff}"
+    s, c = orc.stats(), grp.check()
+    assert c["node_deltas"] == s["node_deltas"] and c["truncated"] == s["truncated"] > 0
+    assert c["delta_bytes"] == s["delta_bytes"] and c["exchanges"] == s["exchanges"]

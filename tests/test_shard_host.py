@@ -1,0 +1,171 @@
+"""Host protocol of owner-column sharding (aiocluster_amd/shard.py), on CPU.
+
+The device kernels are replaced by a toy slice whose packing follows the same
+rules as ``k_pack_slice`` (greedy whole-fit prefix, then first-fit) over a list
+of candidate sizes per (exchange, direction); the protocol must make the
+slices' union equal one sequential pass over all slices in order.  Runs both
+in-process (LocalComm) and as two gloo ranks (DistComm).
+"""
+
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from aiocluster_amd.shard import CHAIN_PENDING, LocalComm, run_sliced_phase
+
+MTU = 100
+
+
+def seq_pack(cands, S=0, tail=False, stop=False, mtu=MTU):
+    """Sequential packing of (id, size) candidates; returns (sent ids, S, tail, stop)."""
+    sent = []
+    for cid, size in cands:
+        if stop:
+            break
+        if not tail:
+            if S + size <= mtu:
+                S += size
+                sent.append(cid)
+            else:
+                tail = True
+        if tail and cid not in sent and size <= mtu - S:
+            S += size
+            sent.append(cid)
+        if S >= mtu:
+            stop = True
+    return sent, S, tail, stop
+
+
+def enc(S, tail, stop):
+    return S | (int(tail) << 32) | (int(stop) << 33)
+
+
+def dec(v):
+    return v & 0xFFFFFFFF, bool((v >> 32) & 1), bool((v >> 33) & 1)
+
+
+class ToySlice:
+    def __init__(self, g, cands):
+        self.g = g
+        self.cands = cands  # cands[e][dir] = [(id, size), ...] of this slice
+        self.sent = {}
+
+    def phase_count(self, t, ini, res):
+        n = int(ini.numel())
+        return torch.tensor([[sum(s for _, s in self.cands[e][d]) for d in range(2)] for e in range(n)],
+                            dtype=torch.int64)
+
+    def phase_pack(self, t, ini, res, step, tot_all, chain_all, chain):
+        n = int(ini.numel())
+        for e in range(n):
+            for d in range(2):
+                if step == 0:
+                    P = int(tot_all[: self.g, e, d].sum()) if self.g else 0
+                    if P > MTU:
+                        chain[e, d] = CHAIN_PENDING
+                        continue
+                    st = (P, False, False)
+                else:
+                    if self.g == 0 or int(chain[e, d]) != CHAIN_PENDING:
+                        continue
+                    prev = int(chain_all[self.g - 1, e, d])
+                    if prev == CHAIN_PENDING:
+                        continue
+                    st = dec(prev)
+                sent, S, tail, stop = seq_pack(self.cands[e][d], *st)
+                self.sent[(e, d)] = sent
+                chain[e, d] = enc(S, tail, stop)
+        return chain
+
+
+def make_cands(rng, G, n, per=6):
+    """cands[g][e][d]: candidate (id, size) lists; ids increase with slice (dict order)."""
+    out = [[[[] for _ in range(2)] for _ in range(n)] for _ in range(G)]
+    for e in range(n):
+        for d in range(2):
+            cid = 0
+            for g in range(G):
+                for _ in range(rng.integers(0, per)):
+                    out[g][e][d].append((cid, int(rng.integers(5, 45))))
+                    cid += 1
+    return out
+
+
+def check(slices, cands, G, n):
+    for e in range(n):
+        for d in range(2):
+            allc = [c for g in range(G) for c in cands[g][e][d]]
+            want = seq_pack(allc)[0]
+            got = [c for s in slices for c in s.sent.get((e, d), [])]
+            assert got == want, (e, d, got, want)
+
+
+@pytest.mark.parametrize("G", [2, 3, 5])
+def test_chain_protocol_in_process(G):
+    rng = np.random.default_rng(G)
+    n = 40
+    cands = make_cands(rng, G, n)
+    slices = [ToySlice(g, cands[g]) for g in range(G)]
+    ini = torch.zeros(n, dtype=torch.int32)
+    steps = run_sliced_phase(slices, LocalComm(G), MTU, 0, ini, ini)
+    assert steps == G  # these inputs overflow the MTU somewhere
+    check(slices, cands, G, n)
+
+
+def test_no_chain_when_everything_fits():
+    G, n = 3, 10
+    cands = [[[[(g, 5)], [(g, 6)]] for _ in range(n)] for g in range(G)]
+    slices = [ToySlice(g, cands[g]) for g in range(G)]
+    ini = torch.zeros(n, dtype=torch.int32)
+    assert run_sliced_phase(slices, LocalComm(G), MTU, 0, ini, ini) == 1
+    check(slices, cands, G, n)
+
+
+def _gloo_worker(rank, world, port, q):
+    import torch.distributed as dist
+
+    from aiocluster_amd.shard import DistComm
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        rng = np.random.default_rng(7)
+        n = 30
+        cands = make_cands(rng, world, n)
+        s = ToySlice(rank, cands[rank])
+        ini = torch.zeros(n, dtype=torch.int32)
+        steps = run_sliced_phase([s], DistComm(), MTU, 0, ini, ini)
+        counters = DistComm().sum_counters([{k: rank + 1 for k in __import__("aiocluster_amd._lib").
+                                             _lib.COUNTER_FIELDS}])
+        q.put((rank, steps, {k: v for k, v in s.sent.items()}, counters["exchanges"]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_chain_protocol_gloo_world2():
+    import socket
+
+    import torch.multiprocessing as mp
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_gloo_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    rng = np.random.default_rng(7)
+    n = 30
+    cands = make_cands(rng, 2, n)
+    slices = [ToySlice(g, cands[g]) for g in range(2)]
+    for (rank, steps, sent, ex), s in zip(res, slices):
+        assert steps == 2 and ex == 3  # 1 + 2 summed over the ranks
+        s.sent = sent
+    check(slices, cands, 2, n)
