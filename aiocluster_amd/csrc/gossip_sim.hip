@@ -192,13 +192,17 @@ __device__ __forceinline__ void eval_cand(const Dev &d, uint32_t s, uint32_t r, 
     const uint32_t dm = in_d ? mr : 0u;
     const uint32_t dg = in_d ? gr : 0u;
     const uint32_t from = (dg < gs && dm < gs) ? 0u : dm;  // should_reset (state.py:359-362)
-    // round trip 2: the sender's kv history entries
+    // round trip 2: the sender's kv history entries.  Every version a view holds is <= its
+    // max_version (apply_delta raises max_version to the NodeDelta's, state.py:232-233), so when
+    // from = the receiver's max_version a key the receiver holds at the sender's write ordinal or a
+    // later one cannot pass version > from: its entry is not needed.
+    const bool all_keys = from != mr || !in_d;
 #pragma unroll
     for (int q = 0; q < 4 * KW; q++) {
         const uint32_t w = byte_of(c.hs, q);
         c.ver[q] = 0u;
         c.km[q] = 0u;
-        if (w && (uint32_t)q < d.K) {
+        if (w && (uint32_t)q < d.K && (all_keys || w > byte_of(c.hr, q))) {
             const uint64_t e = d.hist[hix(d, j, w, q)];
             const uint32_t meta = (uint32_t)(e >> 32);
             c.ver[q] = (uint32_t)e;
@@ -283,7 +287,9 @@ __device__ __forceinline__ void apply_cand(const Dev &d, uint32_t r, const Cand<
 // compute_partial_delta_respecting_mtu (state.py:340-415) of sender s for receiver r, fused with
 // r's apply_delta, by one wave.  The sender's dict order is walked in windows of 1024 positions;
 // each window's stale owners are compacted (ballot + popcount scan) into a wave-private LDS list
-// and evaluated 64 at a time, one per lane.  Exactness vs the sequential loop: DESIGN.md.
+// and evaluated 64 at a time, one candidate per lane.  Fewer than 64 left at the end of a window
+// are carried to the next one in a register (lane i = the i-th), so sparse stale sets still
+// fill whole groups.  Exactness vs the sequential loop: DESIGN.md.
 struct PackState {
     uint32_t S;  // DeltaPb bytes committed so far (wave-uniform)
     bool tail;   // the budget was exceeded once: first-fit continuation mode
@@ -301,6 +307,8 @@ __device__ __forceinline__ void pack_dir(const Dev &d, uint32_t s, uint32_t r, c
     uint32_t S = pst.S;
     bool tail = pst.tail, stop = pst.stop;
     if (!COUNT && !stop && (S >= mtu || mtu - S < d.lb_min)) stop = true;
+    uint32_t pend = 0;  // wave-uniform: candidates carried from earlier windows (< 64), in rv
+    uint32_t rv = 0;    // lane i < pend: the i-th carried candidate's position
     for (uint32_t win = 0; win < cnt && !stop; win += WIN) {
         // -- compact this window's stale owners (sender order) into wbuf, 16 positions per lane
         uint32_t m = 0;
@@ -320,24 +328,30 @@ __device__ __forceinline__ void pack_dir(const Dev &d, uint32_t s, uint32_t r, c
         const uint32_t cl = (uint32_t)__popc(m);
         const uint32_t incl = wave_incl_scan(cl);
         const uint32_t tot = __shfl(incl, WAVE - 1, WAVE);
-        if (tot == 0) continue;
-        __builtin_amdgcn_wave_barrier();
-        uint32_t wp = incl - cl;
-        while (m) {
-            const uint32_t b = (uint32_t)__builtin_ctz(m);
-            m &= m - 1u;
-            wbuf[wp++] = (uint16_t)(16u * lane + b);
+        const bool last = win + WIN >= cnt;
+        if (tot) {
+            __builtin_amdgcn_wave_barrier();
+            uint32_t wp = incl - cl;
+            while (m) {
+                const uint32_t b = (uint32_t)__builtin_ctz(m);
+                m &= m - 1u;
+                wbuf[wp++] = (uint16_t)(16u * lane + b);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            __builtin_amdgcn_wave_barrier();
         }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        for (uint32_t c0 = 0; c0 < tot && !stop; c0 += WAVE) {
+        // list = the carried candidates, then this window's; whole groups of 64 are evaluated now,
+        // the rest with the next window (all of it at the end)
+        const uint32_t total = pend + tot;
+        const uint32_t lim = last ? total : (total & ~(uint32_t)(WAVE - 1));
+        for (uint32_t c0 = 0; c0 < lim && !stop; c0 += WAVE) {
             const uint32_t ci = c0 + lane;
-            const bool cand = ci < tot;
+            const bool cand = ci < lim;
             Cand<KW> c;
             c.emsg = 0;
             c.min1 = 0;
             if (cand) {
-                const uint32_t p = win + wbuf[ci];
+                const uint32_t p = ci < pend ? rv : win + wbuf[ci - pend];
                 const uint32_t j = GENM ? order[p] : p;
                 eval_cand<KW, GENM>(d, s, r, ds, j, t, c, st.alg);
                 st.cand++;
@@ -428,6 +442,13 @@ __device__ __forceinline__ void pack_dir(const Dev &d, uint32_t s, uint32_t r, c
                     st.trunc++;
                 }
             }
+        }
+        if (!last) {  // carry the rest (< 64): entry lim + i to lane i
+            const uint32_t rem = total - lim, idx = lim + lane;
+            uint32_t v = 0;
+            if ((uint32_t)lane < rem) v = idx < pend ? rv : win + wbuf[idx - pend];  // idx < pend only if lim = 0
+            rv = v;
+            pend = rem;
         }
         __builtin_amdgcn_wave_barrier();
     }
@@ -608,7 +629,7 @@ __global__ __launch_bounds__(XB) void k_exchange(Dev d, const int32_t *ini, cons
     const uint32_t words = d.NP / 32;
     // LDS: WIN-entry compaction list per wave, then the stale-owner bitmaps (+ insertion bitmaps)
     uint16_t *wbuf = reinterpret_cast<uint16_t *>(lds) + wid * WIN;
-    uint32_t *bm = lds + WIN;  // 2 waves x WIN x u16
+    uint32_t *bm = lds + WIN;  // after the two waves' WIN x u16 candidate lists
     uint32_t *bBA = bm, *bAB = bm + words, *bNB = bm + 2 * words, *bNA = bm + 3 * words;
     for (uint32_t i = tid; i < words * (genm ? 4u : 2u); i += XB) bm[i] = 0u;
     if (tid == 0) {

@@ -66,11 +66,13 @@ class DistComm:
         import torch
 
         (x,) = parts
+        if self.dist.get_backend(self.group) == "gloo":  # CPU tests / rehearsals: gather through host memory
+            xc = x.detach().to("cpu").contiguous()
+            out = torch.empty((self.world,) + tuple(x.shape), dtype=x.dtype)
+            self.dist.all_gather(list(out.unbind(0)), xc, group=self.group)
+            return out.to(x.device)
         out = torch.empty((self.world,) + tuple(x.shape), dtype=x.dtype, device=x.device)
-        if self.dist.get_backend(self.group) == "gloo":
-            self.dist.all_gather(list(out.unbind(0)), x.contiguous(), group=self.group)
-        else:
-            self.dist.all_gather_into_tensor(out, x.contiguous(), group=self.group)
+        self.dist.all_gather_into_tensor(out, x.contiguous(), group=self.group)
         return out
 
     def sum_counters(self, per_slice: list[dict]) -> dict:

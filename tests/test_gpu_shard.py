@@ -62,3 +62,54 @@ def test_slices_match_oracle_with_ring():
     s, c = orc.stats(), grp.check()
     assert c["node_deltas"] == s["node_deltas"] and c["truncated"] == s["truncated"] > 0
     assert c["delta_bytes"] == s["delta_bytes"] and c["exchanges"] == s["exchanges"]
+
+
+def _dist_worker(rank, world, port, scen, q):
+    import os
+
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        grp = ShardGroup.distributed(scenario_node_ids(scen), scen["keys"], scen["config"], init=scen["init"],
+                                     initial_values=initial_by_owner(scen), fd_ring=False)
+        for r in range(len(scen["rounds"])):
+            replay_round(grp, scen, r)
+        c = grp.check()
+        q.put((rank, grp.export(), c, grp.chain_phases))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_distributed_slices_two_processes_match_single_handle():
+    """DistComm end to end: two processes (gloo for the gather; both slices on cuda:0) vs one handle."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    spec = WorkloadSpec(n=256, k=8, fanout=3, seed=9, init="warm", write_frac=0.3, delete_frac=0.1,
+                        down_frac=0.05, down_rounds=2)
+    scen = make_scenario("dist256", spec, 6, {"mtu": 1500, "tombstone_grace_s": 2})
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_dist_worker, args=(r, 2, port, scen, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted((q.get(timeout=300) for _ in ps), key=lambda x: x[0])
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    one = make_backend(GossipSim, scen, fd_ring=False)
+    for r in range(len(scen["rounds"])):
+        replay_round(one, scen, r)
+    want = one.export()
+    got = {k: np.concatenate([res[0][1][k], res[1][1][k]], axis=1) for k in want}
+    assert compare_exports(got, want) is None
+    c1 = one.check()
+    for k in ("exchanges", "node_deltas", "kvs_sent", "truncated", "delta_bytes", "hb_reports"):
+        assert res[0][2][k] == c1[k], k  # counters summed over the ranks
+    assert c1["truncated"] > 0 and res[0][3] > 0

@@ -69,6 +69,14 @@ def main(root: str, tag: str, workload: str):
             traffic[k] = {"fetch_kib": f, "write_kib": w, "hbm_bytes_per_launch": (2 * f + w) * 1024,
                           "hbm_bytes_per_workgroup": (2 * fetch_u[k] + write_u[k]) * 1024}
     summary = {"tag": tag, "workload": workload, "kernel_stats": ks, "traffic": traffic}
+    sq = {}
+    for name in ("SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU",
+                 "SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_WAVES"):
+        avg, _ = counters(root, "sq", name)
+        for k, v in avg.items():
+            sq.setdefault(k, {})[name] = v
+    if sq:
+        summary["sq_per_launch"] = sq
     os.makedirs(os.path.join(REPO, "profiles"), exist_ok=True)
     with open(os.path.join(REPO, "profiles", f"{tag}_summary.json"), "w") as f:
         json.dump(summary, f, indent=1)

@@ -2,7 +2,8 @@
 # rocprofv3 evidence for bench.py (run on the GPU box via gpurun).
 #   1. kernel trace + stats (per-kernel average duration)
 #   2. PMC FETCH_SIZE and WRITE_SIZE in separate passes (MI355X_MICROARCH.md, HBM section)
-# Usage: tools/profile.sh <tag> [bench args...]
+#   3. (SQ=1) SQ issue/stall counters in a pass of their own
+# Usage: [SQ=1] tools/profile.sh <tag> [bench args...]
 set -eo pipefail
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 TAG=$1; shift
@@ -13,4 +14,7 @@ cd /tmp && export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/kt -o kt --output-format csv -- python3 $R/bench.py $ARGS > $OUT/bench_kt.log 2>&1
 timeout -k 10 900 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $OUT/fetch -o fetch --output-format csv -- python3 $R/bench.py $ARGS > $OUT/bench_fetch.log 2>&1
 timeout -k 10 900 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $OUT/write -o write --output-format csv -- python3 $R/bench.py $ARGS > $OUT/bench_write.log 2>&1
+if [ -n "$SQ" ]; then
+  timeout -k 10 900 rocprofv3 --kernel-trace --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES -d $OUT/sq -o sq --output-format csv -- python3 $R/bench.py $ARGS > $OUT/bench_sq.log 2>&1
+fi
 find $OUT -name "*.csv" | xargs ls -la
