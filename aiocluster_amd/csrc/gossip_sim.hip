@@ -78,6 +78,8 @@ struct Dev {
     uint32_t *stamp;
     unsigned long long *ctr;
     uint32_t *sbits;  // sharded phases: stale-owner bitmaps of both directions per exchange [e][2][NP/32]
+    uint16_t *pend;   // heartbeat reports of the current round not yet applied: bit p = phase tick t_round + 1 + p
+    uint32_t t_round; // tick of the last gs_begin_round
 };
 
 // ------------------------------------------------------------------ protobuf sizes
@@ -463,7 +465,7 @@ __device__ __forceinline__ void pack_dir(const Dev &d, uint32_t s, uint32_t r, c
 // as scalar arrays so every element stays in a register after unrolling.
 struct Grp {
     uint32_t hA[4], hB[4], mA[4], mB[4], pA[4], pB[4], fA[4], fB[4];
-    uint64_t wA[4], wB[4];  // packed sampling windows
+    uint32_t qA[2], qB[2];  // pending-report masks, two u16 per word
 };
 
 __device__ __forceinline__ void ld4(const uint32_t *p, uint32_t (&v)[4]) {
@@ -481,6 +483,13 @@ __device__ __forceinline__ void st4w(uint64_t *p, const uint64_t (&v)[4]) {
     reinterpret_cast<ulonglong2 *>(p)[0] = make_ulonglong2(v[0], v[1]);
     reinterpret_cast<ulonglong2 *>(p)[1] = make_ulonglong2(v[2], v[3]);
 }
+__device__ __forceinline__ void ld4h(const uint16_t *p, uint32_t (&v)[2]) {
+    const uint2 x = *reinterpret_cast<const uint2 *>(p);
+    v[0] = x.x; v[1] = x.y;
+}
+__device__ __forceinline__ void st4h(uint16_t *p, const uint32_t (&v)[2]) {
+    *reinterpret_cast<uint2 *>(p) = make_uint2(v[0], v[1]);
+}
 
 template <bool GENM>
 __device__ __forceinline__ void load_grp(const Dev &d, size_t ra, size_t rb, uint32_t c0, bool schA, bool schB,
@@ -489,10 +498,10 @@ __device__ __forceinline__ void load_grp(const Dev &d, size_t ra, size_t rb, uin
     ld4(d.hb + rb + c0, g.hB);
     ld4(d.mv + ra + c0, g.mA);
     ld4(d.mv + rb + c0, g.mB);
-    // failure-detector fields are prefetched unconditionally: about half the owners report per
-    // exchange, so every 64-byte line of both rows is touched anyway
-    ld4w(d.fd + ra + c0, g.wA);
-    ld4w(d.fd + rb + c0, g.wB);
+    // pending-report masks (2 B per owner): about a third of each row reports per exchange, so
+    // every line is touched anyway
+    ld4h(d.pend + ra + c0, g.qA);
+    ld4h(d.pend + rb + c0, g.qB);
 #pragma unroll
     for (int i = 0; i < 4; i++) { g.pA[i] = g.pB[i] = g.fA[i] = g.fB[i] = 0u; }
     if (GENM) { ld4(d.pos + ra + c0, g.pA); ld4(d.pos + rb + c0, g.pB); }
@@ -500,7 +509,7 @@ __device__ __forceinline__ void load_grp(const Dev &d, size_t ra, size_t rb, uin
     if (schB) ld4(d.fd_state + rb + c0, g.fB);
 }
 
-// FailureDetector.report_heartbeat -> SamplingWindow.report_heartbeat on prefetched fields
+// FailureDetector.report_heartbeat -> SamplingWindow.report_heartbeat on one unpacked window
 // (failure_detector.py:79-81, 32-38): the first report only records the time; later intervals
 // <= max_interval go to BoundedArrayStats (139-150).
 template <bool RING>
@@ -530,13 +539,16 @@ __device__ __forceinline__ Fd fd_report_val(const Dev &d, size_t p, uint32_t t, 
     return f;
 }
 
-template <bool GENM, bool RING>
+// Reports are deferred: the window of (observer, owner) is only read by phi, i.e. by the liveness
+// sweep at the end of the round, so pass 1 records the phase of each report as one bit and
+// k_liveness replays them in tick order before computing phi (same appends, same order).
+template <bool GENM>
 __device__ __forceinline__ void pass1_grp(const Dev &d, size_t ra, size_t rb, uint32_t c0, uint32_t a, uint32_t b,
-                                          uint32_t t, bool schA, bool schB, Grp &g, uint32_t *bBA,
+                                          uint32_t t, uint32_t rbit, bool schA, bool schB, Grp &g, uint32_t *bBA,
                                           uint32_t *bAB, uint32_t *bNB, uint32_t *bNA, uint32_t &alg,
-                                          uint32_t &reports, uint32_t &hbw, uint32_t &ovf, bool &anynew) {
+                                          uint32_t &reports, uint32_t &hbw, bool &anynew) {
     bool dA = false, dB = false, fdA = false, fdB = false;
-    alg += 64 + (GENM ? 32 : 0) + (schA ? 16 : 0) + (schB ? 16 : 0);
+    alg += 64 + 16 + (GENM ? 32 : 0) + (schA ? 16 : 0) + (schB ? 16 : 0);
 #pragma unroll
     for (int i = 0; i < 4; i++) {
         const uint32_t j = c0 + i, jg = d.col_lo + j;  // local column, node id
@@ -565,12 +577,12 @@ __device__ __forceinline__ void pass1_grp(const Dev &d, size_t ra, size_t rb, ui
             g.hA[i] = hA;
             g.hB[i] = hB;
             if (repB) {
-                g.wB[i] = fd_pack(d, fd_report_val<RING>(d, rb + j, t, fd_unpack(d, g.wB[i]), alg, ovf));
+                g.qB[i >> 1] |= rbit << (16 * (i & 1));
                 fdB = true;
                 reports++;
             }
             if (repA) {
-                g.wA[i] = fd_pack(d, fd_report_val<RING>(d, ra + j, t, fd_unpack(d, g.wA[i]), alg, ovf));
+                g.qA[i >> 1] |= rbit << (16 * (i & 1));
                 fdA = true;
                 reports++;
             }
@@ -587,8 +599,8 @@ __device__ __forceinline__ void pass1_grp(const Dev &d, size_t ra, size_t rb, ui
     if (d.ablate & 2u) return;
     if (dA) { st4(d.hb + ra + c0, g.hA); alg += 16; }
     if (dB) { st4(d.hb + rb + c0, g.hB); alg += 16; }
-    if (fdA) st4w(d.fd + ra + c0, g.wA);
-    if (fdB) st4w(d.fd + rb + c0, g.wB);
+    if (fdA) { st4h(d.pend + ra + c0, g.qA); alg += 8; }
+    if (fdB) { st4h(d.pend + rb + c0, g.qB); alg += 8; }
 }
 
 // Owner-column sharded phases ("multi-GPU"): the count pass leaves each exchange's
@@ -611,7 +623,7 @@ __device__ inline PackState chain_unpack(uint64_t v) {
 }
 
 // MODE 0: the whole exchange (one slice).  MODE 1: sharded count pass (pass 1, then the slice totals).
-template <int KW, bool GENM, bool RING, int MODE>
+template <int KW, bool GENM, int MODE>
 __global__ __launch_bounds__(XB) void k_exchange(Dev d, const int32_t *ini, const int32_t *res, uint32_t n,
                                                  uint32_t t, uint32_t seq, SliceIO io) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -645,8 +657,9 @@ __global__ __launch_bounds__(XB) void k_exchange(Dev d, const int32_t *ini, cons
 
     // ---- pass 1: Syn at a, heartbeat merge at b, SynAck digest, heartbeat merge at a
     const size_t ra = (size_t)a * d.NP, rb = (size_t)b * d.NP;
-    uint32_t alg = 0, reports = 0, hbw = 0, ovf = 0;
+    uint32_t alg = 0, reports = 0, hbw = 0;
     bool anynew = false;
+    const uint32_t rbit = 1u << (t - d.t_round - 1u);  // phase of this round (host-checked: < 16)
     // software-pipelined: the next group's loads are in flight while this group computes and stores
     // (different owners, so the early loads never read a location this group writes)
     uint32_t c0 = (uint32_t)tid * 4u;
@@ -655,8 +668,7 @@ __global__ __launch_bounds__(XB) void k_exchange(Dev d, const int32_t *ini, cons
     while (c0 < d.ncol) {
         const uint32_t c1 = c0 + XB * 4u;
         if (c1 < d.ncol) load_grp<GENM>(d, ra, rb, c1, schA, schB, g1);
-        pass1_grp<GENM, RING>(d, ra, rb, c0, a, b, t, schA, schB, g0, bBA, bAB, bNB, bNA, alg, reports, hbw, ovf,
-                              anynew);
+        pass1_grp<GENM>(d, ra, rb, c0, a, b, t, rbit, schA, schB, g0, bBA, bAB, bNB, bNA, alg, reports, hbw, anynew);
         g0 = g1;
         c0 = c1;
     }
@@ -677,12 +689,10 @@ __global__ __launch_bounds__(XB) void k_exchange(Dev d, const int32_t *ini, cons
         pack_dir<KW, false, true>(d, snd, rcv, ds, nullptr, d.ncol, w0 ? bBA : bAB, wbuf, t, cs, ctomb, pst);
         if (lane == 0) io.tot[(size_t)e * 2 + wid] = pst.S;
         const unsigned long long s_alg = wave_sum(alg), s_rep = wave_sum(reports), s_hbw = wave_sum(hbw);
-        const unsigned long long s_ovf = wave_sum(ovf);
         if (lane == 0) {
             shard_add(d, C_ALG, s_alg);
             shard_add(d, C_REPORTS, s_rep);
             shard_add(d, C_HBW, s_hbw);
-            shard_add(d, C_E_FDOVF, s_ovf);
             if (wid == 0 && d.shard == 0) shard_add(d, C_EXCH, 1);
         }
         return;
@@ -742,14 +752,13 @@ __global__ __launch_bounds__(XB) void k_exchange(Dev d, const int32_t *ini, cons
 
     // ---- counters: wave-reduced, sharded atomics
     const unsigned long long s_alg = wave_sum((unsigned long long)alg + st.alg);
-    const unsigned long long s_rep = wave_sum(reports), s_hbw = wave_sum(hbw), s_ovf = wave_sum(ovf);
+    const unsigned long long s_rep = wave_sum(reports), s_hbw = wave_sum(hbw);
     const unsigned long long s_nd = wave_sum(st.nd), s_kv = wave_sum(st.kvs), s_tr = wave_sum(st.trunc);
     const unsigned long long s_cd = wave_sum(st.cand);
     if (lane == 0) {
         shard_add(d, C_ALG, s_alg);
         shard_add(d, C_REPORTS, s_rep);
         shard_add(d, C_HBW, s_hbw);
-        shard_add(d, C_E_FDOVF, s_ovf);
         shard_add(d, C_ND, s_nd);
         shard_add(d, C_KVS, s_kv);
         shard_add(d, C_TRUNC, s_tr);
@@ -854,32 +863,55 @@ __global__ __launch_bounds__(LB) void k_reset_sched(Dev d, const uint8_t *up) {
     if (o < d.N && up[o]) d.row[o * 4 + 2] = NONE;
 }
 
-// Cluster._update_node_liveness -> FailureDetector.update_node_liveness for every known node but
-// self (server.py:606-610; failure_detector.py:89-106), phi in binary64 exactly as
-// SamplingWindow.phi (43-53).  Also folds the earliest "scheduled for deletion" tick per row.
+// First the round's deferred heartbeat reports (pass 1 of k_exchange) are replayed into the
+// sampling windows in tick order (FailureDetector.report_heartbeat, failure_detector.py:79-81),
+// for every row.  Then, for up observers, Cluster._update_node_liveness ->
+// FailureDetector.update_node_liveness for every known node but self (server.py:606-610;
+// failure_detector.py:89-106), phi in binary64 exactly as SamplingWindow.phi (43-53).  Also folds
+// the earliest "scheduled for deletion" tick per row.
+template <bool RING>
 __global__ __launch_bounds__(LB) void k_liveness(Dev d, const uint8_t *up, uint32_t t, uint32_t chunks) {
     const uint32_t o = blockIdx.x / chunks, cb = blockIdx.x % chunks;
-    if (!up[o]) return;
+    const bool upo = up[o] != 0;
     const bool genm = !(d.flags & GS_CANONICAL);
-    const bool ring = (d.flags & GS_FD_RING) != 0;
-    uint32_t minS = NONE, live = 0, gcdue = 0;
+    uint32_t minS = NONE, live = 0, gcdue = 0, ovf = 0, alg = 0;
     const uint32_t c0 = (cb * LB + threadIdx.x) * 4u;
     if (c0 < d.ncol) {
         const size_t p = pix(d, o, c0);
-        uint64_t w[4];
-        uint32_t st[4], ps[4] = {0u, 0u, 0u, 0u};
-        ld4w(d.fd + p, w);
-        ld4(d.fd_state + p, st);
-        if (genm) ld4(d.pos + p, ps);
+        uint32_t q[2];
+        ld4h(d.pend + p, q);
+        const bool rep = (q[0] | q[1]) != 0u;
+        uint64_t w[4] = {0ull, 0ull, 0ull, 0ull};
+        uint32_t st[4] = {0u, 0u, 0u, 0u}, ps[4] = {0u, 0u, 0u, 0u};
+        if (upo || rep) ld4w(d.fd + p, w);
+        if (upo) ld4(d.fd_state + p, st);
+        if (upo && genm) ld4(d.pos + p, ps);
         bool dw = false, ds = false;
+        if (rep) {
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                uint32_t m = (q[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
+                if (!m) continue;
+                Fd f = fd_unpack(d, w[i]);
+                while (m) {
+                    const uint32_t bb = (uint32_t)__builtin_ctz(m);
+                    m &= m - 1u;
+                    f = fd_report_val<RING>(d, p + i, d.t_round + 1u + bb, f, alg, ovf);
+                }
+                w[i] = fd_pack(d, f);
+            }
+            dw = true;
+            const uint32_t z[2] = {0u, 0u};
+            st4h(d.pend + p, z);
+        }
 #pragma unroll
         for (int i = 0; i < 4; i++) {
             const uint32_t j = c0 + i;
-            if (j < d.ncol && d.col_lo + j != o && !(genm && ps[i] == NONE)) {
+            if (upo && j < d.ncol && d.col_lo + j != o && !(genm && ps[i] == NONE)) {
                 live++;
                 const Fd f = fd_unpack(d, w[i]);
                 const bool has = f.last != NONE;
-                const uint32_t len = ring ? (f.cnt < d.W ? f.cnt : d.W) : f.cnt;
+                const uint32_t len = RING ? (f.cnt < d.W ? f.cnt : d.W) : f.cnt;
                 bool alive = false;
                 if (has && len) {
                     const double mean = ((double)f.sum * TICK_S + d.prior5) / ((double)len + 5.0);
@@ -906,10 +938,11 @@ __global__ __launch_bounds__(LB) void k_liveness(Dev d, const uint8_t *up, uint3
         const uint32_t y = __shfl_xor(minS, dd, WAVE);
         if (y < minS) minS = y;
     }
-    const unsigned long long sl = wave_sum(live), sg = wave_sum(gcdue);
+    const unsigned long long sl = wave_sum(live), sg = wave_sum(gcdue), so = wave_sum(ovf);
     if ((threadIdx.x & 63) == 0) {
         if (minS != NONE) atomicMin(&d.row[o * 4 + 2], minS);
         shard_add(d, C_LIVE, sl);
+        shard_add(d, C_E_FDOVF, so);
         if (sg) {
             if (genm) d.row[o * 4 + 3] = 1u;  // k_fd_gc collects this row
             else shard_add(d, C_E_FDGC, sg);  // removal would break the canonical layout
@@ -1125,6 +1158,8 @@ struct gs_handle {
     Dev d;
     uint32_t N, NP, K, KP, C, W;
     uint32_t G, shard, col_lo, ncol;  // owner-column slice
+    bool reports_pending;             // phases ran since the last gs_liveness
+    uint32_t last_phase_tick;
     void *reg[GS_NUM_REGIONS];
     uint64_t bytes[GS_NUM_REGIONS];
     hipStream_t stream;
@@ -1176,13 +1211,14 @@ int check_bound(gs_handle *h) {
     d.stamp = (uint32_t *)h->reg[GS_R_STAMP];
     d.ctr = (unsigned long long *)h->reg[GS_R_COUNTERS];
     d.sbits = (uint32_t *)h->reg[GS_R_SLICE_BITS];
+    d.pend = (uint16_t *)h->reg[GS_R_PEND];
     return GS_OK;
 }
 
-template <int KW, bool GENM, bool RING, int MODE>
+template <int KW, bool GENM, int MODE>
 int launch_exchange(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t n, uint32_t tick, size_t lds,
                     const SliceIO &io) {
-    auto *k = k_exchange<KW, GENM, RING, MODE>;
+    auto *k = k_exchange<KW, GENM, MODE>;
     if (lds > 64 * 1024)
         HIPCHK(h, hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     k<<<n, XB, lds, h->stream>>>(h->d, ini, res, n, tick, h->seq, io);
@@ -1196,8 +1232,10 @@ size_t exchange_lds(const gs_handle *h) {
     return WIN * 2 * 2 + (size_t)(h->NP / 32) * (genm ? 4 : 2) * 4;
 }
 
-int check_phase(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t n) {
+int check_phase(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t n, uint32_t tick) {
     if (!h || !h->booted) return GS_E_INVALID;
+    if (tick <= h->d.t_round || tick - h->d.t_round > 16u)
+        return fail(h, GS_E_INVALID, "phase tick %u outside (round tick %u, round tick + 16]", tick, h->d.t_round);
     if (n && (!ini || !res)) return GS_E_INVALID;
     if (n > h->N / 2) return fail(h, GS_E_INVALID, "a phase has at most n_nodes/2 exchanges (got %u)", n);
     if (exchange_lds(h) > 160 * 1024)
@@ -1270,6 +1308,7 @@ int gs_create(const gs_config *cfg, gs_handle **out) {
     b[GS_R_STAMP] = NR * 4;
     b[GS_R_COUNTERS] = (uint64_t)NSHARD * 32 * 8;
     b[GS_R_SLICE_BITS] = G > 1 ? (N / 2) * 2 * (NP / 32) * 4 : 0;
+    b[GS_R_PEND] = pairs * 2;
     Dev &d = h->d;
     memset(&d, 0, sizeof d);
     d.N = h->N;
@@ -1326,7 +1365,7 @@ int gs_boot(gs_handle *h, const uint16_t *nid_size, const uint8_t *key_len) {
     // regions that start at zero
     const int zero[] = {GS_R_HB, GS_R_MV, GS_R_GC, GS_R_HELD, GS_R_FD, GS_R_FD_STATE,
                         GS_R_RING, GS_R_ROW, GS_R_LAST_W, GS_R_HIST, GS_R_HIST_VID,
-                        GS_R_STAMP, GS_R_COUNTERS, GS_R_SLICE_BITS};
+                        GS_R_STAMP, GS_R_COUNTERS, GS_R_SLICE_BITS, GS_R_PEND};
     for (int r : zero)
         if (h->bytes[r]) HIPCHK(h, hipMemsetAsync(h->reg[r], 0, h->bytes[r], s));
     if (h->bytes[GS_R_TS]) HIPCHK(h, hipMemsetAsync(h->reg[GS_R_TS], 0xFF, h->bytes[GS_R_TS], s));
@@ -1376,31 +1415,30 @@ int gs_owner_writes(gs_handle *h, const gs_write *ops, uint32_t n, uint32_t tick
 
 int gs_begin_round(gs_handle *h, const uint8_t *up, uint32_t tick) {
     if (!h || !h->booted || !up) return GS_E_INVALID;
+    if (h->reports_pending)
+        return fail(h, GS_E_INVALID, "gs_begin_round: the previous round's phases were not closed by gs_liveness");
+    h->d.t_round = tick;
+    h->last_phase_tick = tick;
     k_begin_round<<<h->N, LB, 0, h->stream>>>(h->d, up, tick);
     HIPCHK(h, hipGetLastError());
     return GS_OK;
 }
 
 int gs_run_phase(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t n, uint32_t tick) {
-    int rc = check_phase(h, ini, res, n);
+    int rc = check_phase(h, ini, res, n, tick);
     if (rc) return rc;
     if (h->G > 1) return fail(h, GS_E_UNSUPPORTED, "sliced handle: use gs_phase_count / gs_phase_pack");
     if (!n) return GS_OK;
     const bool genm = !(h->cfg.flags & GS_CANONICAL);
-    const bool ring = (h->cfg.flags & GS_FD_RING) != 0;
     const size_t lds = exchange_lds(h);
     const SliceIO io{};
     h->seq += 1;
-    if (h->KP <= 16) {
-        if (genm) return ring ? launch_exchange<4, true, true, 0>(h, ini, res, n, tick, lds, io)
-                              : launch_exchange<4, true, false, 0>(h, ini, res, n, tick, lds, io);
-        return ring ? launch_exchange<4, false, true, 0>(h, ini, res, n, tick, lds, io)
-                    : launch_exchange<4, false, false, 0>(h, ini, res, n, tick, lds, io);
-    }
-    if (genm) return ring ? launch_exchange<16, true, true, 0>(h, ini, res, n, tick, lds, io)
-                          : launch_exchange<16, true, false, 0>(h, ini, res, n, tick, lds, io);
-    return ring ? launch_exchange<16, false, true, 0>(h, ini, res, n, tick, lds, io)
-                : launch_exchange<16, false, false, 0>(h, ini, res, n, tick, lds, io);
+    h->reports_pending = true;
+    h->last_phase_tick = std::max(h->last_phase_tick, tick);
+    if (h->KP <= 16) return genm ? launch_exchange<4, true, 0>(h, ini, res, n, tick, lds, io)
+                                 : launch_exchange<4, false, 0>(h, ini, res, n, tick, lds, io);
+    return genm ? launch_exchange<16, true, 0>(h, ini, res, n, tick, lds, io)
+                : launch_exchange<16, false, 0>(h, ini, res, n, tick, lds, io);
 }
 
 int gs_shard_columns(const gs_handle *h, uint32_t *col_lo, uint32_t *n_cols) {
@@ -1412,25 +1450,24 @@ int gs_shard_columns(const gs_handle *h, uint32_t *col_lo, uint32_t *n_cols) {
 
 int gs_phase_count(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t n, uint32_t tick,
                    uint64_t *slice_bytes) {
-    int rc = check_phase(h, ini, res, n);
+    int rc = check_phase(h, ini, res, n, tick);
     if (rc) return rc;
     if (h->G < 2) return fail(h, GS_E_UNSUPPORTED, "gs_phase_count needs a sliced handle (n_shards > 1)");
     if (!n) return GS_OK;
     if (!slice_bytes) return GS_E_INVALID;
-    const bool ring = (h->cfg.flags & GS_FD_RING) != 0;
     const size_t lds = exchange_lds(h);
     SliceIO io{};
     io.tot = slice_bytes;
     h->seq += 1;
-    if (h->KP <= 16) return ring ? launch_exchange<4, false, true, 1>(h, ini, res, n, tick, lds, io)
-                                 : launch_exchange<4, false, false, 1>(h, ini, res, n, tick, lds, io);
-    return ring ? launch_exchange<16, false, true, 1>(h, ini, res, n, tick, lds, io)
-                : launch_exchange<16, false, false, 1>(h, ini, res, n, tick, lds, io);
+    h->reports_pending = true;
+    h->last_phase_tick = std::max(h->last_phase_tick, tick);
+    if (h->KP <= 16) return launch_exchange<4, false, 1>(h, ini, res, n, tick, lds, io);
+    return launch_exchange<16, false, 1>(h, ini, res, n, tick, lds, io);
 }
 
 int gs_phase_pack(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t n, uint32_t tick, uint32_t step,
                   const uint64_t *slice_bytes_all, const uint64_t *chain_all, uint64_t *chain) {
-    int rc = check_phase(h, ini, res, n);
+    int rc = check_phase(h, ini, res, n, tick);
     if (rc) return rc;
     if (h->G < 2) return fail(h, GS_E_UNSUPPORTED, "gs_phase_pack needs a sliced handle (n_shards > 1)");
     if (!n) return GS_OK;
@@ -1449,11 +1486,15 @@ int gs_phase_pack(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t
 
 int gs_liveness(gs_handle *h, const uint8_t *up, uint32_t tick) {
     if (!h || !h->booted || !up) return GS_E_INVALID;
+    if (h->reports_pending && tick < h->last_phase_tick)
+        return fail(h, GS_E_INVALID, "gs_liveness at tick %u precedes a phase at tick %u", tick, h->last_phase_tick);
     k_reset_sched<<<(h->N + LB - 1) / LB, LB, 0, h->stream>>>(h->d, up);
     HIPCHK(h, hipGetLastError());
     const uint32_t chunks = (h->ncol + 4 * LB - 1) / (4 * LB);
-    k_liveness<<<chunks * h->N, LB, 0, h->stream>>>(h->d, up, tick, chunks);
+    if (h->cfg.flags & GS_FD_RING) k_liveness<true><<<chunks * h->N, LB, 0, h->stream>>>(h->d, up, tick, chunks);
+    else k_liveness<false><<<chunks * h->N, LB, 0, h->stream>>>(h->d, up, tick, chunks);
     HIPCHK(h, hipGetLastError());
+    h->reports_pending = false;  // replayed
     if (!(h->cfg.flags & GS_CANONICAL)) {
         k_fd_gc<<<h->N, LB, (h->NP / 32) * 4, h->stream>>>(h->d, up, tick);
         HIPCHK(h, hipGetLastError());

@@ -101,6 +101,8 @@ enum gs_region {
     GS_R_COUNTERS,    /* u64 [64][32]  sharded gs_counters (summed by gs_read_counters) */
     GS_R_SLICE_BITS,  /* u32 [N/2][2][NP/32] stale-owner bitmaps between gs_phase_count and
                                         gs_phase_pack (n_shards > 1 only) */
+    GS_R_PEND,        /* u16 [N][NP]   heartbeat reports of the current round, bit p = the phase at
+                                        round tick + 1 + p; replayed into GS_R_FD by gs_liveness */
     GS_NUM_REGIONS
 };
 
@@ -152,11 +154,15 @@ int gs_warm(gs_handle *h);
 /* Owner writes at `tick` (state.py:137-180).  `ops` is a DEVICE array; owners must be distinct. */
 int gs_owner_writes(gs_handle *h, const gs_write *ops, uint32_t n, uint32_t tick);
 /* Round start for every node with up[o] != 0 (DEVICE u8 array): inc_heartbeat +
- * gc_marked_for_deletion (server.py:471-474, state.py:253-274, 333-338). */
+ * gc_marked_for_deletion (server.py:471-474, state.py:253-274, 333-338).  The previous round's
+ * phases must have been closed by gs_liveness. */
 int gs_begin_round(gs_handle *h, const uint8_t *up, uint32_t tick);
 /* One conflict-free phase of exchanges initiators[e] -> responders[e] (DEVICE int32 arrays):
  * Syn/SynAck/Ack = server.py:327-376 + 524, i.e. compute_digest, _report_heartbeat,
- * compute_partial_delta_respecting_mtu and apply_delta on both sides. */
+ * compute_partial_delta_respecting_mtu and apply_delta on both sides.  At most n_nodes/2 exchanges;
+ * `tick` must lie in (round tick, round tick + 16] of the last gs_begin_round.  The failure
+ * detector's report_heartbeat calls are recorded per phase (GS_R_PEND) and applied to the
+ * sampling windows, in tick order, by the next gs_liveness (nothing reads a window in between). */
 int gs_run_phase(gs_handle *h, const int32_t *initiators, const int32_t *responders, uint32_t n, uint32_t tick);
 /* Owner-column sliced phase (n_shards > 1; gs_run_phase refuses sliced handles).  The slices of one
  * cluster run, per phase, on the same initiators/responders:
