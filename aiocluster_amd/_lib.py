@@ -56,7 +56,7 @@ ERRORS = {-1: "GS_E_INVALID", -2: "GS_E_UNBOUND", -3: "GS_E_HIP", -4: "GS_E_DEVI
 COUNTER_FIELDS = [
     "exchanges", "hb_reports", "node_deltas", "kvs_sent", "truncated", "delta_bytes", "alg_bytes", "hb_writes",
     "candidates", "live_pairs", "tomb_gc", "err_fd_overflow", "err_hist_full", "err_bad_index", "err_conflict",
-    "err_fd_gc", "err_insert", "fd_gc", "q9",
+    "err_fd_gc", "err_insert", "fd_gc", "q9", "pack_bytes",
 ]
 
 # Every symbol include/gossip_sim.h declares (checked by tests/test_abi.py).
@@ -89,7 +89,7 @@ class GsConfig(C.Structure):
 
 
 class GsCounters(C.Structure):
-    _fields_ = [(n, C.c_uint64) for n in COUNTER_FIELDS] + [("reserved", C.c_uint64 * 13)]
+    _fields_ = [(n, C.c_uint64) for n in COUNTER_FIELDS] + [("reserved", C.c_uint64 * 12)]
 
 
 class GsError(RuntimeError):

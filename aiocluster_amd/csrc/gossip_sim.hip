@@ -51,7 +51,7 @@ constexpr double TICK_S = 1.0 / 64.0;
 
 enum Ctr {
     C_EXCH = 0, C_REPORTS, C_ND, C_KVS, C_TRUNC, C_DBYTES, C_ALG, C_HBW, C_CAND, C_LIVE, C_TOMBGC,
-    C_E_FDOVF, C_E_HIST, C_E_IDX, C_E_CONFLICT, C_E_FDGC, C_E_INSERT, C_FDGC, C_Q9, C_NUM
+    C_E_FDOVF, C_E_HIST, C_E_IDX, C_E_CONFLICT, C_E_FDGC, C_E_INSERT, C_FDGC, C_Q9, C_PACKB, C_NUM
 };
 static_assert(C_NUM <= 32, "counter region");
 static_assert(sizeof(gs_counters) == 32 * 8, "gs_counters layout");
@@ -178,7 +178,11 @@ __device__ __forceinline__ void eval_cand(const Dev &d, uint32_t s, uint32_t r, 
     const size_t ps = pix(d, s, j), pr = pix(d, r, j);
     const uint32_t kw = d.KP >> 2;
     // round trip 1
-    const uint32_t ms = d.mv[ps], gs = d.gc[ps], mr = d.mv[pr], gr = d.gc[pr];
+    // without GS_TOMBSTONES no tombstone is ever collected, so every last_gc_version stays 0 and the
+    // GC region is not allocated
+    const bool gct = (d.flags & GS_TOMBSTONES) != 0;
+    const uint32_t ms = d.mv[ps], mr = d.mv[pr];
+    const uint32_t gs = gct ? d.gc[ps] : 0u, gr = gct ? d.gc[pr] : 0u;
     const uint32_t pos_r = GENM ? d.pos[pr] : 0u;
     const uint32_t fst = ds.sched ? d.fd_state[pr] : 0u;
     const uint32_t *hsp = reinterpret_cast<const uint32_t *>(d.held + ps * d.KP);
@@ -188,7 +192,7 @@ __device__ __forceinline__ void eval_cand(const Dev &d, uint32_t s, uint32_t r, 
         c.hs[q] = (uint32_t)q < kw ? hsp[q] : 0u;
         c.hr[q] = (uint32_t)q < kw ? hrp[q] : 0u;
     }
-    alg += 16 + 2 * d.KP + (GENM ? 4 : 0) + (ds.sched ? 4 : 0);
+    alg += (gct ? 16 : 8) + 2 * d.KP + (GENM ? 4 : 0) + (ds.sched ? 4 : 0);
     bool in_d = GENM ? pos_r < ds.limit : true;
     if (in_d && ds.sched) in_d = !is_sched(fst, t, d.sched_delay);
     const uint32_t dm = in_d ? mr : 0u;
@@ -751,12 +755,13 @@ __global__ __launch_bounds__(XB) void k_exchange(Dev d, const int32_t *ini, cons
     }
 
     // ---- counters: wave-reduced, sharded atomics
-    const unsigned long long s_alg = wave_sum((unsigned long long)alg + st.alg);
+    const unsigned long long s_alg = wave_sum((unsigned long long)alg + st.alg), s_pk = wave_sum(st.alg);
     const unsigned long long s_rep = wave_sum(reports), s_hbw = wave_sum(hbw);
     const unsigned long long s_nd = wave_sum(st.nd), s_kv = wave_sum(st.kvs), s_tr = wave_sum(st.trunc);
     const unsigned long long s_cd = wave_sum(st.cand);
     if (lane == 0) {
         shard_add(d, C_ALG, s_alg);
+        shard_add(d, C_PACKB, s_pk);
         shard_add(d, C_REPORTS, s_rep);
         shard_add(d, C_HBW, s_hbw);
         shard_add(d, C_ND, s_nd);
@@ -812,6 +817,7 @@ __global__ __launch_bounds__(XB) void k_pack_slice(Dev d, const int32_t *ini, co
     const unsigned long long s_tr = wave_sum(st.trunc), s_cd = wave_sum(st.cand);
     if (lane == 0) {
         shard_add(d, C_ALG, s_alg);
+        shard_add(d, C_PACKB, s_alg);
         shard_add(d, C_ND, s_nd);
         shard_add(d, C_KVS, s_kv);
         shard_add(d, C_TRUNC, s_tr);
@@ -1028,7 +1034,7 @@ __global__ __launch_bounds__(LB) void k_fd_gc(Dev d, const uint8_t *up, uint32_t
             d.pos[p] = NONE;
             d.hb[p] = 0u;
             d.mv[p] = 0u;
-            d.gc[p] = 0u;
+            if (d.flags & GS_TOMBSTONES) d.gc[p] = 0u;
             for (uint32_t k = 0; k < d.KP; k += 4) *reinterpret_cast<uint32_t *>(d.held + p * d.KP + k) = 0u;
             if (d.flags & GS_TOMBSTONES)
                 for (uint32_t k = 0; k < d.KP; k++) d.ts[p * d.KP + k] = NONE;
@@ -1063,7 +1069,11 @@ __global__ __launch_bounds__(LB) void k_owner_writes(Dev d, const gs_write *ops,
     const uint32_t i = blockIdx.x * LB + threadIdx.x;
     if (i >= n) return;
     const gs_write op = ops[i];
-    if (op.owner >= d.N || op.key >= d.K || op.op > 3u) { shard_add(d, C_E_IDX, 1); return; }
+    // deletes and TTL writes leave tombstones, which need GS_TOMBSTONES (receive ticks + GC)
+    if (op.owner >= d.N || op.key >= d.K || op.op > 3u || (op.op != GS_OP_SET && !(d.flags & GS_TOMBSTONES))) {
+        shard_add(d, C_E_IDX, 1);
+        return;
+    }
     const uint32_t j = op.owner - d.col_lo, k = op.key;  // local column of the owner
     if (j >= d.ncol) return;  // another slice's owner
     const size_t pj = pix(d, op.owner, j);
@@ -1134,7 +1144,7 @@ __global__ __launch_bounds__(LB) void k_warm(Dev d) {
         const size_t q = pix(d, jg, j);  // the owner's own view
         d.hb[p] = d.hb[q];
         d.mv[p] = d.mv[q];
-        d.gc[p] = d.gc[q];
+        if (d.flags & GS_TOMBSTONES) d.gc[p] = d.gc[q];
         for (uint32_t k = 0; k < d.KP; k += 4)
             *reinterpret_cast<uint32_t *>(d.held + p * d.KP + k) =
                 *reinterpret_cast<const uint32_t *>(d.held + q * d.KP + k);
@@ -1292,7 +1302,8 @@ int gs_create(const gs_config *cfg, gs_handle **out) {
     const uint64_t pairs = N * NP;
     const bool genm = !(c.flags & GS_CANONICAL);
     uint64_t *b = h->bytes;
-    b[GS_R_HB] = b[GS_R_MV] = b[GS_R_GC] = pairs * 4;
+    b[GS_R_HB] = b[GS_R_MV] = pairs * 4;
+    b[GS_R_GC] = (c.flags & GS_TOMBSTONES) ? pairs * 4 : 0;  // last_gc_version stays 0 without tombstone GC
     b[GS_R_HELD] = pairs * KP;
     b[GS_R_FD] = pairs * 8;
     b[GS_R_FD_STATE] = pairs * 4;

@@ -350,7 +350,10 @@ class GossipSim:
         self.sync()
         g = {}
         for name in ("HB", "MV", "GC", "FD_STATE"):
-            g[name] = self.region(name, torch.int32, (n, NP)).cpu().numpy().view(np.uint32)
+            if name in self.regions:
+                g[name] = self.region(name, torch.int32, (n, NP)).cpu().numpy().view(np.uint32)
+        if "GC" not in g:  # no tombstone GC: last_gc_version is 0 everywhere
+            g["GC"] = np.zeros((n, NP), dtype=np.uint32)
         g["FD_LAST"], g["FD_SUM"], g["FD_CNT"] = self.unpack_fd(self.region("FD", torch.int64, (n, NP)).cpu().numpy())
         g["HELD"] = self.region("HELD", torch.uint8, (n, NP, KP)).cpu().numpy()
         nc = self.ncol

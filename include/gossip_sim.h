@@ -78,7 +78,8 @@ typedef struct gs_config {
 enum gs_region {
     GS_R_HB = 0,      /* u32 [N][NP]   NodeState.heartbeat of owner j as seen by observer o */
     GS_R_MV,          /* u32 [N][NP]   NodeState.max_version */
-    GS_R_GC,          /* u32 [N][NP]   NodeState.last_gc_version */
+    GS_R_GC,          /* u32 [N][NP]   NodeState.last_gc_version (GS_TOMBSTONES only: without tombstone GC
+                                        it is 0 everywhere, and deletes / TTL writes are refused) */
     GS_R_HELD,        /* u8  [N][NP][KP] write ordinal of each key held (0 = absent), KP = K rounded to 4 */
     GS_R_FD,          /* u64 [N][NP]   sampling window: low word = _last_heartbeat tick + 1 (0 = no
                                         window); high word = _sum in ticks | intervals appended since
@@ -126,7 +127,8 @@ typedef struct gs_counters {
     uint64_t err_insert;       /* insertion into a GS_CANONICAL state */
     uint64_t fd_gc;            /* targets removed by FailureDetector.garbage_collect */
     uint64_t q9;               /* garbage_collect calls that raised KeyError */
-    uint64_t reserved[13];
+    uint64_t pack_bytes;       /* the part of alg_bytes moved by delta packing + apply (pass 3) */
+    uint64_t reserved[12];
 } gs_counters;
 
 typedef struct gs_write {   /* one owner write */

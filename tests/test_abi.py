@@ -45,6 +45,13 @@ def test_create_validates_config_without_gpu():
     assert lib.gs_region_bytes(h, _lib.REGION["HB"], ctypes.byref(nb)) == 0
     assert nb.value == 1000 * 1024 * 4
     assert lib.gs_region_bytes(h, _lib.REGION["POS"], ctypes.byref(nb)) == 0 and nb.value == 1000 * 1024 * 4
+    # no tombstone GC: last_gc_version is 0 everywhere and not stored
+    assert lib.gs_region_bytes(h, _lib.REGION["GC"], ctypes.byref(nb)) == 0 and nb.value == 0
+    assert lib.gs_region_bytes(h, _lib.REGION["PEND"], ctypes.byref(nb)) == 0 and nb.value == 1000 * 1024 * 2
+    lib.gs_destroy(h)
+    withgc = make_config(1000, 16, DEFAULT_CFG, _lib.GS_TOMBSTONES, 32)
+    assert lib.gs_create(ctypes.byref(withgc), ctypes.byref(h)) == 0
+    assert lib.gs_region_bytes(h, _lib.REGION["GC"], ctypes.byref(nb)) == 0 and nb.value == 1000 * 1024 * 4
     lib.gs_destroy(h)
     bad = make_config(1000, 65, DEFAULT_CFG, 0, 32)  # K > 64
     assert lib.gs_create(ctypes.byref(bad), ctypes.byref(h)) == -1
