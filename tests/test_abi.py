@@ -102,3 +102,10 @@ def test_slice_columns_and_region_sizes_without_gpu():
     assert lib.gs_create(ctypes.byref(c), ctypes.byref(h)) == -1
     with pytest.raises(ValueError):
         _lib.slice_columns(100, 3, 0)
+
+
+def test_region_enum_matches_binding():
+    src = open(_lib.HEADER).read()
+    body = re.search(r"enum gs_region \{(.*?)GS_NUM_REGIONS", src, re.S).group(1)
+    names = re.findall(r"^\s*GS_R_(\w+)", body, re.M)
+    assert names == _lib.REGIONS
