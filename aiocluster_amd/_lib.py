@@ -47,7 +47,7 @@ def fd_sum_bits(window: int) -> int:
 
 REGIONS = [
     "HB", "MV", "GC", "HELD", "FD", "FD_STATE", "TS", "RING", "POS", "ORD", "ROW",
-    "LAST_W", "HIST", "HIST_VID", "NID_SIZE", "KEY_LEN", "STAMP", "COUNTERS", "SLICE_BITS", "PEND",
+    "LAST_W", "HIST", "HIST_VID", "NID_SIZE", "KEY_LEN", "STAMP", "COUNTERS", "SLICE_BITS", "PEND", "PEND_STAMP",
 ]
 REGION = {n: i for i, n in enumerate(REGIONS)}
 
@@ -66,7 +66,7 @@ EXPORTS = [
     "gs_read_counters", "gs_reset_counters", "gs_sync", "gs_shard_columns", "gs_phase_count", "gs_phase_pack",
 ]
 
-API_VERSION = 2
+API_VERSION = 3
 
 
 class GsConfig(C.Structure):

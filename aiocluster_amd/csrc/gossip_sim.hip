@@ -78,8 +78,13 @@ struct Dev {
     uint32_t *stamp;
     unsigned long long *ctr;
     uint32_t *sbits;  // sharded phases: stale-owner bitmaps of both directions per exchange [e][2][NP/32]
-    uint16_t *pend;   // heartbeat reports of the current round not yet applied: bit p = phase tick t_round + 1 + p
-    uint32_t t_round; // tick of the last gs_begin_round
+    // heartbeat reports of the current round not yet applied to the windows: one bit plane per phase
+    // p (tick t_round + 1 + p) and observer row, [N][16][PW] u64 in quad-interleaved column order
+    // (plane_word/plane_bit); a plane row is valid only if pstamp[o][p] holds that phase's tick
+    uint64_t *pend;
+    uint32_t *pstamp;  // [N][16]
+    uint32_t PW;       // u64 words per plane row: NP rounded up to 256, / 64
+    uint32_t t_round;  // tick of the last gs_begin_round
 };
 
 // ------------------------------------------------------------------ protobuf sizes
@@ -469,8 +474,13 @@ __device__ __forceinline__ void pack_dir(const Dev &d, uint32_t s, uint32_t r, c
 // as scalar arrays so every element stays in a register after unrolling.
 struct Grp {
     uint32_t hA[4], hB[4], mA[4], mB[4], pA[4], pB[4], fA[4], fB[4];
-    uint32_t qA[2], qB[2];  // pending-report masks, two u16 per word
 };
+
+// Report bit planes (Dev::pend): column c of a plane row sits in word (c / 256) * 4 + c % 4, bit
+// (c / 4) % 64 -- the order in which one wave's four ballots over its 64 lanes x 4 consecutive
+// columns come out, so pass 1 stores its ballots as they are and never reads a plane.
+__device__ inline uint32_t plane_word(uint32_t c) { return (c >> 8) * 4u + (c & 3u); }
+__device__ inline uint32_t plane_bit(uint32_t c) { return (c >> 2) & 63u; }
 
 __device__ __forceinline__ void ld4(const uint32_t *p, uint32_t (&v)[4]) {
     const uint4 x = *reinterpret_cast<const uint4 *>(p);
@@ -487,14 +497,6 @@ __device__ __forceinline__ void st4w(uint64_t *p, const uint64_t (&v)[4]) {
     reinterpret_cast<ulonglong2 *>(p)[0] = make_ulonglong2(v[0], v[1]);
     reinterpret_cast<ulonglong2 *>(p)[1] = make_ulonglong2(v[2], v[3]);
 }
-__device__ __forceinline__ void ld4h(const uint16_t *p, uint32_t (&v)[2]) {
-    const uint2 x = *reinterpret_cast<const uint2 *>(p);
-    v[0] = x.x; v[1] = x.y;
-}
-__device__ __forceinline__ void st4h(uint16_t *p, const uint32_t (&v)[2]) {
-    *reinterpret_cast<uint2 *>(p) = make_uint2(v[0], v[1]);
-}
-
 template <bool GENM>
 __device__ __forceinline__ void load_grp(const Dev &d, size_t ra, size_t rb, uint32_t c0, bool schA, bool schB,
                                          Grp &g) {
@@ -502,10 +504,6 @@ __device__ __forceinline__ void load_grp(const Dev &d, size_t ra, size_t rb, uin
     ld4(d.hb + rb + c0, g.hB);
     ld4(d.mv + ra + c0, g.mA);
     ld4(d.mv + rb + c0, g.mB);
-    // pending-report masks (2 B per owner): about a third of each row reports per exchange, so
-    // every line is touched anyway
-    ld4h(d.pend + ra + c0, g.qA);
-    ld4h(d.pend + rb + c0, g.qB);
 #pragma unroll
     for (int i = 0; i < 4; i++) { g.pA[i] = g.pB[i] = g.fA[i] = g.fB[i] = 0u; }
     if (GENM) { ld4(d.pos + ra + c0, g.pA); ld4(d.pos + rb + c0, g.pB); }
@@ -544,15 +542,17 @@ __device__ __forceinline__ Fd fd_report_val(const Dev &d, size_t p, uint32_t t, 
 }
 
 // Reports are deferred: the window of (observer, owner) is only read by phi, i.e. by the liveness
-// sweep at the end of the round, so pass 1 records the phase of each report as one bit and
-// k_liveness replays them in tick order before computing phi (same appends, same order).
+// sweep at the end of the round, so pass 1 records each report as one bit in the phase's bit plane
+// (rmA/rmB: bit i = column c0 + i) and k_liveness replays them in tick order before computing phi
+// (same appends, same order).
 template <bool GENM>
 __device__ __forceinline__ void pass1_grp(const Dev &d, size_t ra, size_t rb, uint32_t c0, uint32_t a, uint32_t b,
-                                          uint32_t t, uint32_t rbit, bool schA, bool schB, Grp &g, uint32_t *bBA,
-                                          uint32_t *bAB, uint32_t *bNB, uint32_t *bNA, uint32_t &alg,
-                                          uint32_t &reports, uint32_t &hbw, bool &anynew) {
-    bool dA = false, dB = false, fdA = false, fdB = false;
-    alg += 64 + 16 + (GENM ? 32 : 0) + (schA ? 16 : 0) + (schB ? 16 : 0);
+                                          uint32_t t, bool schA, bool schB, Grp &g, uint32_t *bBA, uint32_t *bAB,
+                                          uint32_t *bNB, uint32_t *bNA, uint32_t &alg, uint32_t &reports,
+                                          uint32_t &hbw, bool &anynew, uint32_t &rmA, uint32_t &rmB) {
+    bool dA = false, dB = false;
+    rmA = rmB = 0u;
+    alg += 64 + (GENM ? 32 : 0) + (schA ? 16 : 0) + (schB ? 16 : 0);
 #pragma unroll
     for (int i = 0; i < 4; i++) {
         const uint32_t j = c0 + i, jg = d.col_lo + j;  // local column, node id
@@ -580,16 +580,8 @@ __device__ __forceinline__ void pass1_grp(const Dev &d, size_t ra, size_t rb, ui
             }
             g.hA[i] = hA;
             g.hB[i] = hB;
-            if (repB) {
-                g.qB[i >> 1] |= rbit << (16 * (i & 1));
-                fdB = true;
-                reports++;
-            }
-            if (repA) {
-                g.qA[i >> 1] |= rbit << (16 * (i & 1));
-                fdA = true;
-                reports++;
-            }
+            if (repB) { rmB |= 1u << i; reports++; }
+            if (repA) { rmA |= 1u << i; reports++; }
             // stale owners (state.py:347-357): sender's max_version above the digest's
             const uint32_t dmA = inA ? g.mA[i] : 0u;
             if (pb2 && !sb && g.mB[i] > dmA) atomicOr(&bBA[j >> 5], 1u << (j & 31u));
@@ -603,8 +595,19 @@ __device__ __forceinline__ void pass1_grp(const Dev &d, size_t ra, size_t rb, ui
     if (d.ablate & 2u) return;
     if (dA) { st4(d.hb + ra + c0, g.hA); alg += 16; }
     if (dB) { st4(d.hb + rb + c0, g.hB); alg += 16; }
-    if (fdA) { st4h(d.pend + ra + c0, g.qA); alg += 8; }
-    if (fdB) { st4h(d.pend + rb + c0, g.qB); alg += 8; }
+}
+
+// The four ballots of one group step are this wave's 32-byte block of the phase's bit plane
+// (plane_word/plane_bit): stored whole, zeros included, so a plane row written in this phase never
+// needs clearing.  Lane 0 is active whenever any lane of the wave is (it has the lowest column).
+__device__ __forceinline__ void store_plane(uint64_t *plane, uint32_t c0, uint32_t rm, uint32_t &alg) {
+    const uint64_t b0 = __ballot(rm & 1u), b1 = __ballot(rm & 2u), b2 = __ballot(rm & 4u), b3 = __ballot(rm & 8u);
+    if (lane_id() == 0) {
+        ulonglong2 *p = reinterpret_cast<ulonglong2 *>(plane + plane_word(c0));
+        p[0] = make_ulonglong2(b0, b1);
+        p[1] = make_ulonglong2(b2, b3);
+        alg += 32;
+    }
 }
 
 // Owner-column sharded phases ("multi-GPU"): the count pass leaves each exchange's
@@ -663,7 +666,13 @@ __global__ __launch_bounds__(XB) void k_exchange(Dev d, const int32_t *ini, cons
     const size_t ra = (size_t)a * d.NP, rb = (size_t)b * d.NP;
     uint32_t alg = 0, reports = 0, hbw = 0;
     bool anynew = false;
-    const uint32_t rbit = 1u << (t - d.t_round - 1u);  // phase of this round (host-checked: < 16)
+    const uint32_t ph = t - d.t_round - 1u;  // phase of this round (host-checked: < 16)
+    uint64_t *planeA = d.pend + ((size_t)a * 16u + ph) * d.PW;
+    uint64_t *planeB = d.pend + ((size_t)b * 16u + ph) * d.PW;
+    if (tid == 0) {  // both plane rows are rewritten below: valid for this phase
+        d.pstamp[a * 16u + ph] = t;
+        d.pstamp[b * 16u + ph] = t;
+    }
     // software-pipelined: the next group's loads are in flight while this group computes and stores
     // (different owners, so the early loads never read a location this group writes)
     uint32_t c0 = (uint32_t)tid * 4u;
@@ -672,7 +681,13 @@ __global__ __launch_bounds__(XB) void k_exchange(Dev d, const int32_t *ini, cons
     while (c0 < d.ncol) {
         const uint32_t c1 = c0 + XB * 4u;
         if (c1 < d.ncol) load_grp<GENM>(d, ra, rb, c1, schA, schB, g1);
-        pass1_grp<GENM>(d, ra, rb, c0, a, b, t, rbit, schA, schB, g0, bBA, bAB, bNB, bNA, alg, reports, hbw, anynew);
+        uint32_t rmA, rmB;
+        pass1_grp<GENM>(d, ra, rb, c0, a, b, t, schA, schB, g0, bBA, bAB, bNB, bNA, alg, reports, hbw, anynew, rmA,
+                        rmB);
+        if (!(d.ablate & 2u)) {
+            store_plane(planeA, c0, rmA, alg);
+            store_plane(planeB, c0, rmB, alg);
+        }
         g0 = g1;
         c0 = c1;
     }
@@ -876,17 +891,40 @@ __global__ __launch_bounds__(LB) void k_reset_sched(Dev d, const uint8_t *up) {
 // failure_detector.py:89-106), phi in binary64 exactly as SamplingWindow.phi (43-53).  Also folds
 // the earliest "scheduled for deletion" tick per row.
 template <bool RING>
-__global__ __launch_bounds__(LB) void k_liveness(Dev d, const uint8_t *up, uint32_t t, uint32_t chunks) {
+__global__ __launch_bounds__(LB) void k_liveness(Dev d, const uint8_t *up, uint32_t t, uint32_t chunks,
+                                                 bool replay) {
+    __shared__ uint64_t s_pl[16][16];  // [phase][the 16 plane words of this workgroup's 1024 columns]
+    __shared__ uint32_t s_vm;
     const uint32_t o = blockIdx.x / chunks, cb = blockIdx.x % chunks;
     const bool upo = up[o] != 0;
     const bool genm = !(d.flags & GS_CANONICAL);
     uint32_t minS = NONE, live = 0, gcdue = 0, ovf = 0, alg = 0;
+    // phases of the current round in which row o was in an exchange (its plane rows are valid);
+    // replay = false once this round's reports were replayed (the host closes the round)
+    if (threadIdx.x < 64) {
+        const bool v = replay && threadIdx.x < 16 && d.pstamp[o * 16u + threadIdx.x] == d.t_round + 1u + threadIdx.x;
+        const uint32_t m = (uint32_t)__ballot(v);
+        if (threadIdx.x == 0) s_vm = m;
+    }
+    __syncthreads();
+    const uint32_t vm = s_vm;
+    {
+        const uint32_t ph = threadIdx.x >> 4, wi = cb * 16u + (threadIdx.x & 15u);
+        if ((vm >> ph) & 1u) s_pl[ph][threadIdx.x & 15u] = wi < d.PW ? d.pend[((size_t)o * 16u + ph) * d.PW + wi] : 0ull;
+    }
+    __syncthreads();
     const uint32_t c0 = (cb * LB + threadIdx.x) * 4u;
     if (c0 < d.ncol) {
         const size_t p = pix(d, o, c0);
-        uint32_t q[2];
-        ld4h(d.pend + p, q);
-        const bool rep = (q[0] | q[1]) != 0u;
+        // this thread's four columns: bit ph of q[i] = a report in phase ph
+        uint32_t q[4] = {0u, 0u, 0u, 0u};
+        const uint32_t wb = (threadIdx.x >> 6) * 4u, lb = plane_bit(c0);
+        for (uint32_t m = vm; m; m &= m - 1u) {
+            const uint32_t ph = (uint32_t)__builtin_ctz(m);
+#pragma unroll
+            for (int i = 0; i < 4; i++) q[i] |= (uint32_t)((s_pl[ph][wb + i] >> lb) & 1ull) << ph;
+        }
+        const bool rep = (q[0] | q[1] | q[2] | q[3]) != 0u;
         uint64_t w[4] = {0ull, 0ull, 0ull, 0ull};
         uint32_t st[4] = {0u, 0u, 0u, 0u}, ps[4] = {0u, 0u, 0u, 0u};
         if (upo || rep) ld4w(d.fd + p, w);
@@ -896,7 +934,7 @@ __global__ __launch_bounds__(LB) void k_liveness(Dev d, const uint8_t *up, uint3
         if (rep) {
 #pragma unroll
             for (int i = 0; i < 4; i++) {
-                uint32_t m = (q[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
+                uint32_t m = q[i];
                 if (!m) continue;
                 Fd f = fd_unpack(d, w[i]);
                 while (m) {
@@ -907,8 +945,6 @@ __global__ __launch_bounds__(LB) void k_liveness(Dev d, const uint8_t *up, uint3
                 w[i] = fd_pack(d, f);
             }
             dw = true;
-            const uint32_t z[2] = {0u, 0u};
-            st4h(d.pend + p, z);
         }
 #pragma unroll
         for (int i = 0; i < 4; i++) {
@@ -1169,6 +1205,7 @@ struct gs_handle {
     uint32_t N, NP, K, KP, C, W;
     uint32_t G, shard, col_lo, ncol;  // owner-column slice
     bool reports_pending;             // phases ran since the last gs_liveness
+    bool round_open;                  // gs_begin_round ran and gs_liveness has not closed the round yet
     uint32_t last_phase_tick;
     void *reg[GS_NUM_REGIONS];
     uint64_t bytes[GS_NUM_REGIONS];
@@ -1221,7 +1258,8 @@ int check_bound(gs_handle *h) {
     d.stamp = (uint32_t *)h->reg[GS_R_STAMP];
     d.ctr = (unsigned long long *)h->reg[GS_R_COUNTERS];
     d.sbits = (uint32_t *)h->reg[GS_R_SLICE_BITS];
-    d.pend = (uint16_t *)h->reg[GS_R_PEND];
+    d.pend = (uint64_t *)h->reg[GS_R_PEND];
+    d.pstamp = (uint32_t *)h->reg[GS_R_PEND_STAMP];
     return GS_OK;
 }
 
@@ -1244,6 +1282,8 @@ size_t exchange_lds(const gs_handle *h) {
 
 int check_phase(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t n, uint32_t tick) {
     if (!h || !h->booted) return GS_E_INVALID;
+    if (!h->round_open)
+        return fail(h, GS_E_INVALID, "phases run between gs_begin_round and gs_liveness (the round is closed)");
     if (tick <= h->d.t_round || tick - h->d.t_round > 16u)
         return fail(h, GS_E_INVALID, "phase tick %u outside (round tick %u, round tick + 16]", tick, h->d.t_round);
     if (n && (!ini || !res)) return GS_E_INVALID;
@@ -1319,7 +1359,9 @@ int gs_create(const gs_config *cfg, gs_handle **out) {
     b[GS_R_STAMP] = NR * 4;
     b[GS_R_COUNTERS] = (uint64_t)NSHARD * 32 * 8;
     b[GS_R_SLICE_BITS] = G > 1 ? (N / 2) * 2 * (NP / 32) * 4 : 0;
-    b[GS_R_PEND] = pairs * 2;
+    const uint64_t PW = round_up(h->NP, 256) / 64;
+    b[GS_R_PEND] = N * 16 * PW * 8;  // 16 phase bit planes per observer row
+    b[GS_R_PEND_STAMP] = N * 16 * 4;
     Dev &d = h->d;
     memset(&d, 0, sizeof d);
     d.N = h->N;
@@ -1328,6 +1370,7 @@ int gs_create(const gs_config *cfg, gs_handle **out) {
     d.shards = G;
     d.shard = c.shard;
     d.NP = h->NP;
+    d.PW = (uint32_t)PW;
     d.K = h->K;
     d.KP = h->KP;
     d.C = h->C;
@@ -1376,7 +1419,7 @@ int gs_boot(gs_handle *h, const uint16_t *nid_size, const uint8_t *key_len) {
     // regions that start at zero
     const int zero[] = {GS_R_HB, GS_R_MV, GS_R_GC, GS_R_HELD, GS_R_FD, GS_R_FD_STATE,
                         GS_R_RING, GS_R_ROW, GS_R_LAST_W, GS_R_HIST, GS_R_HIST_VID,
-                        GS_R_STAMP, GS_R_COUNTERS, GS_R_SLICE_BITS, GS_R_PEND};
+                        GS_R_STAMP, GS_R_COUNTERS, GS_R_SLICE_BITS, GS_R_PEND, GS_R_PEND_STAMP};
     for (int r : zero)
         if (h->bytes[r]) HIPCHK(h, hipMemsetAsync(h->reg[r], 0, h->bytes[r], s));
     if (h->bytes[GS_R_TS]) HIPCHK(h, hipMemsetAsync(h->reg[GS_R_TS], 0xFF, h->bytes[GS_R_TS], s));
@@ -1432,6 +1475,7 @@ int gs_begin_round(gs_handle *h, const uint8_t *up, uint32_t tick) {
     h->last_phase_tick = tick;
     k_begin_round<<<h->N, LB, 0, h->stream>>>(h->d, up, tick);
     HIPCHK(h, hipGetLastError());
+    h->round_open = true;
     return GS_OK;
 }
 
@@ -1502,10 +1546,14 @@ int gs_liveness(gs_handle *h, const uint8_t *up, uint32_t tick) {
     k_reset_sched<<<(h->N + LB - 1) / LB, LB, 0, h->stream>>>(h->d, up);
     HIPCHK(h, hipGetLastError());
     const uint32_t chunks = (h->ncol + 4 * LB - 1) / (4 * LB);
-    if (h->cfg.flags & GS_FD_RING) k_liveness<true><<<chunks * h->N, LB, 0, h->stream>>>(h->d, up, tick, chunks);
-    else k_liveness<false><<<chunks * h->N, LB, 0, h->stream>>>(h->d, up, tick, chunks);
+    const bool replay = h->reports_pending;
+    if (h->cfg.flags & GS_FD_RING)
+        k_liveness<true><<<chunks * h->N, LB, 0, h->stream>>>(h->d, up, tick, chunks, replay);
+    else
+        k_liveness<false><<<chunks * h->N, LB, 0, h->stream>>>(h->d, up, tick, chunks, replay);
     HIPCHK(h, hipGetLastError());
     h->reports_pending = false;  // replayed
+    h->round_open = false;
     if (!(h->cfg.flags & GS_CANONICAL)) {
         k_fd_gc<<<h->N, LB, (h->NP / 32) * 4, h->stream>>>(h->d, up, tick);
         HIPCHK(h, hipGetLastError());

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define GS_API_VERSION 2
+#define GS_API_VERSION 3
 #define GS_TICK_US 15625u
 #define GS_NONE 0xFFFFFFFFu
 
@@ -102,8 +102,12 @@ enum gs_region {
     GS_R_COUNTERS,    /* u64 [64][32]  sharded gs_counters (summed by gs_read_counters) */
     GS_R_SLICE_BITS,  /* u32 [N/2][2][NP/32] stale-owner bitmaps between gs_phase_count and
                                         gs_phase_pack (n_shards > 1 only) */
-    GS_R_PEND,        /* u16 [N][NP]   heartbeat reports of the current round, bit p = the phase at
-                                        round tick + 1 + p; replayed into GS_R_FD by gs_liveness */
+    GS_R_PEND,        /* u64 [N][16][PW] heartbeat reports of the current round: one bit plane per phase
+                                        p (tick = round tick + 1 + p) and observer row, PW = NP rounded up
+                                        to 256, / 64; column c at word (c/256)*4 + c%4, bit (c/4)%64;
+                                        replayed into GS_R_FD by gs_liveness */
+    GS_R_PEND_STAMP,  /* u32 [N][16]   tick of the phase that last wrote plane row (o, p): the row is
+                                        valid for the current round only if it equals round tick + 1 + p */
     GS_NUM_REGIONS
 };
 
@@ -162,9 +166,11 @@ int gs_begin_round(gs_handle *h, const uint8_t *up, uint32_t tick);
 /* One conflict-free phase of exchanges initiators[e] -> responders[e] (DEVICE int32 arrays):
  * Syn/SynAck/Ack = server.py:327-376 + 524, i.e. compute_digest, _report_heartbeat,
  * compute_partial_delta_respecting_mtu and apply_delta on both sides.  At most n_nodes/2 exchanges;
- * `tick` must lie in (round tick, round tick + 16] of the last gs_begin_round.  The failure
- * detector's report_heartbeat calls are recorded per phase (GS_R_PEND) and applied to the
- * sampling windows, in tick order, by the next gs_liveness (nothing reads a window in between). */
+ * `tick` must lie in (round tick, round tick + 16] of the last gs_begin_round, and the round must
+ * still be open (no gs_liveness since that gs_begin_round).  The failure detector's
+ * report_heartbeat calls are recorded per phase (GS_R_PEND bit planes) and applied to the
+ * sampling windows, in tick order, by the gs_liveness that closes the round (nothing reads a
+ * window in between). */
 int gs_run_phase(gs_handle *h, const int32_t *initiators, const int32_t *responders, uint32_t n, uint32_t tick);
 /* Owner-column sliced phase (n_shards > 1; gs_run_phase refuses sliced handles).  The slices of one
  * cluster run, per phase, on the same initiators/responders:
