@@ -24,6 +24,7 @@ GS_CANONICAL = 1
 GS_TOMBSTONES = 2
 GS_FD_RING = 4
 GS_NONE = 0xFFFFFFFF
+GS_MV_INEXACT = 0x80000000
 TICK_US = 15_625
 
 
@@ -47,7 +48,7 @@ def fd_sum_bits(window: int) -> int:
 
 REGIONS = [
     "HB", "MV", "GC", "HELD", "FD", "FD_STATE", "TS", "RING", "POS", "ORD", "ROW",
-    "LAST_W", "HIST", "HIST_VID", "NID_SIZE", "KEY_LEN", "STAMP", "COUNTERS", "SLICE_BITS", "PEND", "PEND_STAMP",
+    "LAST_W", "HIST", "HIST_VID", "NID_SIZE", "KEY_LEN", "STAMP", "COUNTERS", "SLICE_BITS", "PEND", "PEND_STAMP", "LATEST",
 ]
 REGION = {n: i for i, n in enumerate(REGIONS)}
 
@@ -63,10 +64,10 @@ COUNTER_FIELDS = [
 EXPORTS = [
     "gs_create", "gs_destroy", "gs_last_error", "gs_api_version", "gs_region_bytes", "gs_bind", "gs_set_stream",
     "gs_boot", "gs_warm", "gs_owner_writes", "gs_begin_round", "gs_run_phase", "gs_liveness", "gs_phi_row",
-    "gs_read_counters", "gs_reset_counters", "gs_sync", "gs_shard_columns", "gs_phase_count", "gs_phase_pack",
+    "gs_read_counters", "gs_reset_counters", "gs_sync", "gs_shard_columns", "gs_phase_count", "gs_phase_pack", "gs_materialize_held",
 ]
 
-API_VERSION = 3
+API_VERSION = 4
 
 
 class GsConfig(C.Structure):
@@ -141,6 +142,7 @@ def load():
         "gs_shard_columns": (C.c_int, [P, C.POINTER(u32), C.POINTER(u32)]),
         "gs_phase_count": (C.c_int, [P, P, P, u32, u32, P]),
         "gs_phase_pack": (C.c_int, [P, P, P, u32, u32, u32, P, P, P]),
+        "gs_materialize_held": (C.c_int, [P, u32, u32]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

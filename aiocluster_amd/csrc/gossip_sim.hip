@@ -72,6 +72,7 @@ struct Dev {
     uint32_t *pos, *ord, *row;
     uint8_t *last_w;
     uint64_t *hist;  // version | meta << 32
+    uint64_t *lat;   // [NC][KP] copy of each key's latest HIST entry (prefix views, no GS_TOMBSTONES)
     uint32_t *hist_vid;
     uint16_t *nid_size;
     uint8_t *key_len;
@@ -172,7 +173,42 @@ struct Cand {
     uint32_t hs[KW], hr[KW];  // held write ordinals, 4 keys per word (sender / receiver)
     uint32_t ver[4 * KW];     // version of each key the sender holds (0 = absent)
     uint32_t km[4 * KW];      // DeltaPb bytes of that kv | status << 16
+    bool rx;                  // prefix views (no GS_TOMBSTONES): the receiver's view is S_j(mr)
+    bool fast;                // ... and so is the sender's: hr was not loaded
 };
+
+__device__ inline void set_byte(uint32_t *w, int q, uint32_t v) {
+    const int sh = 8 * (q & 3);
+    w[q >> 2] = (w[q >> 2] & ~(0xFFu << sh)) | (v << sh);
+}
+
+// Prefix views (no GS_TOMBSTONES: no deletes, no GC, every write is version M + 1 of its owner).
+// S_j(M) = for every key, owner j's latest write with version <= M.  A view (o, j) whose
+// max_version word has MV_INEXACT clear IS S_j(M): it never received a truncated NodeDelta nor
+// one from a view with holes, so its held ordinals follow from the owner's write
+// history and GS_R_HELD is not read (nor kept) for it.  Exchanges between two such views need
+// only their max_versions and the owner's latest-write table (a hot 16-entry row per owner).
+constexpr uint32_t MV_INEXACT = 0x80000000u;
+constexpr uint32_t MV_MASK = 0x7FFFFFFFu;
+
+// held ordinals of S_j(M) (local owner column j): start from the owner's latest write of each key
+// and step back while the write is newer than M (versions of one key increase with the ordinal)
+template <int KW>
+__device__ __forceinline__ void derive_held(const Dev &d, uint32_t j, uint32_t M, uint32_t (&h)[KW], uint32_t &alg) {
+    const uint32_t kw = d.KP >> 2;
+    const uint32_t *lwp = reinterpret_cast<const uint32_t *>(d.last_w + (size_t)j * d.KP);
+#pragma unroll
+    for (int q = 0; q < KW; q++) h[q] = (uint32_t)q < kw ? lwp[q] : 0u;
+    alg += d.KP;
+#pragma unroll
+    for (int q = 0; q < 4 * KW; q++) {
+        if ((uint32_t)q >= d.K) continue;
+        uint32_t w = byte_of(h, q);
+        const uint32_t w0 = w;
+        while (w && (uint32_t)d.hist[hix(d, j, w, q)] > M) { w--; alg += 8; }
+        if (w != w0) set_byte(h, q, w);
+    }
+}
 
 // NodeDelta candidate (state.py:347-390): from_version_excluded, the NodeDeltaPb body without
 // kvs, the DeltaPb bytes of the whole NodeDelta (all kvs with version > from, 392-398) and of
@@ -184,41 +220,68 @@ __device__ __forceinline__ void eval_cand(const Dev &d, uint32_t s, uint32_t r, 
     const uint32_t kw = d.KP >> 2;
     // round trip 1
     // without GS_TOMBSTONES no tombstone is ever collected, so every last_gc_version stays 0 and the
-    // GC region is not allocated
+    // GC region is not allocated; views are then tracked as prefixes of the owner's writes (MV_INEXACT)
     const bool gct = (d.flags & GS_TOMBSTONES) != 0;
-    const uint32_t ms = d.mv[ps], mr = d.mv[pr];
+    const uint32_t msw = d.mv[ps], mrw = d.mv[pr];
+    const uint32_t ms = msw & MV_MASK, mr = mrw & MV_MASK;
     const uint32_t gs = gct ? d.gc[ps] : 0u, gr = gct ? d.gc[pr] : 0u;
     const uint32_t pos_r = GENM ? d.pos[pr] : 0u;
     const uint32_t fst = ds.sched ? d.fd_state[pr] : 0u;
-    const uint32_t *hsp = reinterpret_cast<const uint32_t *>(d.held + ps * d.KP);
+    const bool sx = !gct && !(msw & MV_INEXACT), rx = !gct && !(mrw & MV_INEXACT);
+    const uint32_t *hsp = reinterpret_cast<const uint32_t *>((sx ? d.last_w + (size_t)j * d.KP : d.held + ps * d.KP));
     const uint32_t *hrp = reinterpret_cast<const uint32_t *>(d.held + pr * d.KP);
 #pragma unroll
     for (int q = 0; q < KW; q++) {
         c.hs[q] = (uint32_t)q < kw ? hsp[q] : 0u;
-        c.hr[q] = (uint32_t)q < kw ? hrp[q] : 0u;
+        c.hr[q] = ((uint32_t)q < kw && !rx) ? hrp[q] : 0u;
     }
-    alg += (gct ? 16 : 8) + 2 * d.KP + (GENM ? 4 : 0) + (ds.sched ? 4 : 0);
+    alg += (gct ? 16 : 8) + (sx ? 0 : d.KP) + (rx ? 0 : d.KP) + (GENM ? 4 : 0) + (ds.sched ? 4 : 0);
     bool in_d = GENM ? pos_r < ds.limit : true;
     if (in_d && ds.sched) in_d = !is_sched(fst, t, d.sched_delay);
     const uint32_t dm = in_d ? mr : 0u;
     const uint32_t dg = in_d ? gr : 0u;
     const uint32_t from = (dg < gs && dm < gs) ? 0u : dm;  // should_reset (state.py:359-362)
-    // round trip 2: the sender's kv history entries.  Every version a view holds is <= its
-    // max_version (apply_delta raises max_version to the NodeDelta's, state.py:232-233), so when
-    // from = the receiver's max_version a key the receiver holds at the sender's write ordinal or a
-    // later one cannot pass version > from: its entry is not needed.
-    const bool all_keys = from != mr || !in_d;
+    if (sx) {
+        // round trip 2 (owner tables, L2-resident for recently written owners): S_j(ms) from the
+        // latest write of every key, stepping back for the keys written after ms
 #pragma unroll
-    for (int q = 0; q < 4 * KW; q++) {
-        const uint32_t w = byte_of(c.hs, q);
-        c.ver[q] = 0u;
-        c.km[q] = 0u;
-        if (w && (uint32_t)q < d.K && (all_keys || w > byte_of(c.hr, q))) {
-            const uint64_t e = d.hist[hix(d, j, w, q)];
+        for (int q = 0; q < 4 * KW; q++) {
+            c.ver[q] = 0u;
+            c.km[q] = 0u;
+            uint32_t w = byte_of(c.hs, q);
+            if (!w || (uint32_t)q >= d.K) continue;
+            uint64_t e = d.lat[(size_t)j * d.KP + q];  // counted below only for the kvs sent
+            if ((uint32_t)e > ms) {
+                do {
+                    w--;
+                    if (w) { e = d.hist[hix(d, j, w, q)]; alg += 8; }
+                } while (w && (uint32_t)e > ms);
+                set_byte(c.hs, q, w);
+                if (!w) continue;
+            }
             const uint32_t meta = (uint32_t)(e >> 32);
             c.ver[q] = (uint32_t)e;
             c.km[q] = msgf(meta_kvlen(meta)) | (meta_status(meta) << 16);
-            alg += 8;
+        }
+    } else {
+        // round trip 2: the sender's kv history entries.  Every version a view holds is <= its
+        // max_version (apply_delta raises max_version to the NodeDelta's, state.py:232-233), so when
+        // from = the receiver's max_version a key the receiver holds at the sender's write ordinal or a
+        // later one cannot pass version > from: its entry is not needed (a prefix receiver: every key
+        // with version <= from).
+        const bool all_keys = from != mr || !in_d;
+#pragma unroll
+        for (int q = 0; q < 4 * KW; q++) {
+            const uint32_t w = byte_of(c.hs, q);
+            c.ver[q] = 0u;
+            c.km[q] = 0u;
+            if (w && (uint32_t)q < d.K && (all_keys || (rx ? true : w > byte_of(c.hr, q)))) {
+                const uint64_t e = d.hist[hix(d, j, w, q)];
+                const uint32_t meta = (uint32_t)(e >> 32);
+                c.ver[q] = (uint32_t)e;
+                c.km[q] = msgf(meta_kvlen(meta)) | (meta_status(meta) << 16);
+                alg += 8;
+            }
         }
     }
     uint32_t sum = 0, nk = 0, minv = NONE, minkv = 0;
@@ -231,12 +294,15 @@ __device__ __forceinline__ void eval_cand(const Dev &d, uint32_t s, uint32_t r, 
             if (c.ver[q] < minv) { minv = c.ver[q]; minkv = kvm; }
         }
     }
+    if (sx) alg += 8 * nk;  // the history entries of the NodeDelta's kvs
     c.j = j;
     c.from = from;
     c.gs = gs;
     c.ms = ms;
     c.gr = gr;
     c.mr = mr;
+    c.rx = rx;
+    c.fast = sx && rx;
     c.base = msgf(d.nid_size[j]) + ufield(from) + ufield(gs) + 1u + vlen(ms);
     c.nkv = nk;
     c.emsg = nk ? msgf(c.base + sum) : 0u;
@@ -251,6 +317,14 @@ template <int KW>
 __device__ __forceinline__ void apply_cand(const Dev &d, uint32_t r, const Cand<KW> &c, uint32_t vmax, uint32_t t, bool &tomb,
                                   uint32_t &alg) {
     const size_t pr = pix(d, r, c.j);
+    if (c.fast && vmax == NONE) {
+        // prefix sender, prefix receiver, whole NodeDelta: the view becomes S_j(max(mr, ms)) (keys
+        // above mr move to the sender's latest write <= ms, the others already are), still a prefix.
+        // ms <= mr happens when the receiver's digest left j out (scheduled for deletion: from = 0)
+        d.mv[pr] = c.ms > c.mr ? c.ms : c.mr;
+        alg += 4;
+        return;
+    }
     uint32_t g = c.gr;
     const uint32_t m0 = c.mr;
     const bool jump = c.gs > g;  // last_gc_version raised: drop entries <= it (200-207)
@@ -259,8 +333,15 @@ __device__ __forceinline__ void apply_cand(const Dev &d, uint32_t r, const Cand<
     const bool tt = (d.flags & GS_TOMBSTONES) != 0;
     uint32_t *tsr = tt ? d.ts + pr * d.KP : nullptr;
     uint32_t hr[KW];
+    if (c.rx) {
+        derive_held<KW>(d, c.j, c.mr, hr, alg);  // the receiver's held ordinals: S_j(mr)
+    } else {
 #pragma unroll
-    for (int q = 0; q < KW; q++) hr[q] = c.hr[q];
+        for (int q = 0; q < KW; q++) hr[q] = c.hr[q];
+    }
+    uint32_t hr0[KW];
+#pragma unroll
+    for (int q = 0; q < KW; q++) hr0[q] = hr[q];
 #pragma unroll
     for (int q = 0; q < 4 * KW; q++) {
         if ((uint32_t)q >= d.K) continue;
@@ -282,15 +363,25 @@ __device__ __forceinline__ void apply_cand(const Dev &d, uint32_t r, const Cand<
                 if (v > maxv) maxv = v;
             }
         }
-        const int sh = 8 * (q & 3);
-        hr[q >> 2] = (hr[q >> 2] & ~(0xFFu << sh)) | (wr << sh);
+        set_byte(hr, q, wr);
+    }
+    if (c.ms > maxv) maxv = c.ms;  // max_version (232-233)
+    uint32_t mvw = maxv;
+    if (!tt) {
+        // still a prefix view if the held keys are exactly S_j(maxv)
+        uint32_t want[KW];
+        derive_held<KW>(d, c.j, maxv, want, alg);
+        bool same = true;
+#pragma unroll
+        for (int q = 0; q < KW; q++) same = same && want[q] == hr[q];
+        if (!same) mvw |= MV_INEXACT;
     }
     uint32_t *hrp = reinterpret_cast<uint32_t *>(d.held + pr * d.KP);
+    const bool keep_held = tt || (mvw & MV_INEXACT);  // a prefix view's HELD is not kept
 #pragma unroll
     for (int q = 0; q < KW; q++)
-        if (hr[q] != c.hr[q]) { hrp[q] = hr[q]; alg += 4; }
-    if (c.ms > maxv) maxv = c.ms;  // max_version (232-233)
-    d.mv[pr] = maxv;
+        if (keep_held && (hr[q] != hr0[q] || c.rx)) { hrp[q] = hr[q]; alg += 4; }
+    d.mv[pr] = mvw;
     if (g != c.gr) d.gc[pr] = g;
     alg += 8;
 }
@@ -505,6 +596,8 @@ __device__ __forceinline__ void load_grp(const Dev &d, size_t ra, size_t rb, uin
     ld4(d.mv + ra + c0, g.mA);
     ld4(d.mv + rb + c0, g.mB);
 #pragma unroll
+    for (int i = 0; i < 4; i++) { g.mA[i] &= MV_MASK; g.mB[i] &= MV_MASK; }  // drop the prefix-view flag
+#pragma unroll
     for (int i = 0; i < 4; i++) { g.pA[i] = g.pB[i] = g.fA[i] = g.fB[i] = 0u; }
     if (GENM) { ld4(d.pos + ra + c0, g.pA); ld4(d.pos + rb + c0, g.pB); }
     if (schA) ld4(d.fd_state + ra + c0, g.fA);
@@ -694,11 +787,22 @@ __global__ __launch_bounds__(XB) void k_exchange(Dev d, const int32_t *ini, cons
     if (anynew) s_flag[0] = 1u;
     __syncthreads();
 
-    if (MODE == 1) {
+    if (MODE >= 1) {
         // ---- sharded count pass: publish the bitmaps, total this slice's candidates per direction
+        // (MODE 2: publish only; one slice, packed by a separate k_pack_slice launch)
         if (s_flag[0] && tid == 0) shard_add(d, C_E_INSERT, 1);
         uint32_t *gb = d.sbits + (size_t)e * 2 * words;
         for (uint32_t i = tid; i < 2 * words; i += XB) gb[i] = bm[i];
+        if (MODE == 2) {
+            const unsigned long long s_alg = wave_sum(alg), s_rep = wave_sum(reports), s_hbw = wave_sum(hbw);
+            if (lane == 0) {
+                shard_add(d, C_ALG, s_alg);
+                shard_add(d, C_REPORTS, s_rep);
+                shard_add(d, C_HBW, s_hbw);
+                if (wid == 0) shard_add(d, C_EXCH, 1);
+            }
+            return;
+        }
         const bool w0 = wid == 0;
         const uint32_t snd = w0 ? b : a, rcv = w0 ? a : b;
         const DigestSide ds{rcv, d.ncol, w0 ? schA : schB};
@@ -827,7 +931,7 @@ __global__ __launch_bounds__(XB) void k_pack_slice(Dev d, const int32_t *ini, co
     pack_dir<KW, false, false>(d, snd, rcv, ds, nullptr, d.ncol, d.sbits + (slot * words), s_wbuf + wid * WIN, t,
                                st, tomb, pst);
     if (tomb) d.row[rcv * 4 + 1] = 1u;
-    if (lane == 0) io.chain[slot] = chain_pack(pst);
+    if (lane == 0 && io.chain) io.chain[slot] = chain_pack(pst);
     const unsigned long long s_alg = wave_sum(st.alg), s_nd = wave_sum(st.nd), s_kv = wave_sum(st.kvs);
     const unsigned long long s_tr = wave_sum(st.trunc), s_cd = wave_sum(st.cand);
     if (lane == 0) {
@@ -1135,10 +1239,12 @@ __global__ __launch_bounds__(LB) void k_owner_writes(Dev d, const gs_write *ops,
     const uint32_t nw = (uint32_t)d.last_w[(size_t)j * d.KP + k] + 1u;
     if (nw >= d.C || vl >= (1u << 14)) { shard_add(d, C_E_HIST, 1); return; }
     const uint32_t ver = M + 1u;
+    if (ver > MV_MASK) { shard_add(d, C_E_HIST, 1); return; }
     const size_t h = hix(d, j, nw, k);
     d.hist[h] = (uint64_t)ver |
                 ((uint64_t)make_meta(sfield(d.key_len[k]) + sfield(vl) + ufield(ver) + ufield(st), st, vl) << 32);
     d.hist_vid[h] = vid;
+    if (d.lat) d.lat[(size_t)j * d.KP + k] = d.hist[h];
     d.last_w[(size_t)j * d.KP + k] = (uint8_t)nw;
     *held = (uint8_t)nw;
     d.mv[pj] = ver;
@@ -1196,6 +1302,21 @@ __global__ __launch_bounds__(LB) void k_warm(Dev d) {
     }
 }
 
+// Fill GS_R_HELD for the prefix views of rows [r0, r1) (MV_INEXACT clear: HELD not kept by the
+// exchange kernel), so a reader sees every view's held ordinals.  Readback only.
+__global__ __launch_bounds__(LB) void k_materialize(Dev d, uint32_t r0, uint32_t r1) {
+    const uint64_t total = (uint64_t)(r1 - r0) * d.ncol;
+    for (uint64_t x = (uint64_t)blockIdx.x * LB + threadIdx.x; x < total; x += (uint64_t)gridDim.x * LB) {
+        const uint32_t o = r0 + (uint32_t)(x / d.ncol), j = (uint32_t)(x % d.ncol);
+        const size_t p = pix(d, o, j);
+        const uint32_t mv = d.mv[p];
+        if (mv & MV_INEXACT) continue;
+        uint32_t h[16], alg = 0;
+        derive_held<16>(d, j, mv, h, alg);
+        for (uint32_t q = 0; q < d.KP / 4; q++) reinterpret_cast<uint32_t *>(d.held + p * d.KP)[q] = h[q];
+    }
+}
+
 }  // namespace
 
 // ====================================================================== C ABI
@@ -1206,6 +1327,7 @@ struct gs_handle {
     uint32_t G, shard, col_lo, ncol;  // owner-column slice
     bool reports_pending;             // phases ran since the last gs_liveness
     bool round_open;                  // gs_begin_round ran and gs_liveness has not closed the round yet
+    bool split;                       // GS_SPLIT experiment (canonical, one slice)
     uint32_t last_phase_tick;
     void *reg[GS_NUM_REGIONS];
     uint64_t bytes[GS_NUM_REGIONS];
@@ -1252,6 +1374,7 @@ int check_bound(gs_handle *h) {
     d.row = (uint32_t *)h->reg[GS_R_ROW];
     d.last_w = (uint8_t *)h->reg[GS_R_LAST_W];
     d.hist = (uint64_t *)h->reg[GS_R_HIST];
+    d.lat = (uint64_t *)h->reg[GS_R_LATEST];
     d.hist_vid = (uint32_t *)h->reg[GS_R_HIST_VID];
     d.nid_size = (uint16_t *)h->reg[GS_R_NID_SIZE];
     d.key_len = (uint8_t *)h->reg[GS_R_KEY_LEN];
@@ -1354,11 +1477,14 @@ int gs_create(const gs_config *cfg, gs_handle **out) {
     b[GS_R_LAST_W] = NC * KP;
     b[GS_R_HIST] = NC * C * K * 8;
     b[GS_R_HIST_VID] = NC * C * K * 4;
+    b[GS_R_LATEST] = (c.flags & GS_TOMBSTONES) ? 0 : NC * KP * 8;
     b[GS_R_NID_SIZE] = NP * 2;
     b[GS_R_KEY_LEN] = KP;
     b[GS_R_STAMP] = NR * 4;
     b[GS_R_COUNTERS] = (uint64_t)NSHARD * 32 * 8;
-    b[GS_R_SLICE_BITS] = G > 1 ? (N / 2) * 2 * (NP / 32) * 4 : 0;
+    // GS_SPLIT (profiling experiment): one-slice phases as pass 1 + a separate packing launch
+    h->split = G == 1 && (c.flags & GS_CANONICAL) && getenv("GS_SPLIT") && atoi(getenv("GS_SPLIT"));
+    b[GS_R_SLICE_BITS] = (G > 1 || h->split) ? (N / 2) * 2 * (NP / 32) * 4 : 0;
     const uint64_t PW = round_up(h->NP, 256) / 64;
     b[GS_R_PEND] = N * 16 * PW * 8;  // 16 phase bit planes per observer row
     b[GS_R_PEND_STAMP] = N * 16 * 4;
@@ -1419,7 +1545,7 @@ int gs_boot(gs_handle *h, const uint16_t *nid_size, const uint8_t *key_len) {
     // regions that start at zero
     const int zero[] = {GS_R_HB, GS_R_MV, GS_R_GC, GS_R_HELD, GS_R_FD, GS_R_FD_STATE,
                         GS_R_RING, GS_R_ROW, GS_R_LAST_W, GS_R_HIST, GS_R_HIST_VID,
-                        GS_R_STAMP, GS_R_COUNTERS, GS_R_SLICE_BITS, GS_R_PEND, GS_R_PEND_STAMP};
+                        GS_R_STAMP, GS_R_COUNTERS, GS_R_SLICE_BITS, GS_R_PEND, GS_R_PEND_STAMP, GS_R_LATEST};
     for (int r : zero)
         if (h->bytes[r]) HIPCHK(h, hipMemsetAsync(h->reg[r], 0, h->bytes[r], s));
     if (h->bytes[GS_R_TS]) HIPCHK(h, hipMemsetAsync(h->reg[GS_R_TS], 0xFF, h->bytes[GS_R_TS], s));
@@ -1459,6 +1585,16 @@ int gs_warm(gs_handle *h) {
     return GS_OK;
 }
 
+int gs_materialize_held(gs_handle *h, uint32_t row_lo, uint32_t row_hi) {
+    if (!h || !h->booted || row_lo > row_hi || row_hi > h->N) return GS_E_INVALID;
+    if ((h->cfg.flags & GS_TOMBSTONES) || row_lo == row_hi) return GS_OK;  // every view's HELD is kept
+    const uint64_t pairs = (uint64_t)(row_hi - row_lo) * h->ncol;
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>((pairs + LB - 1) / LB, 1u << 16);
+    k_materialize<<<blocks, LB, 0, h->stream>>>(h->d, row_lo, row_hi);
+    HIPCHK(h, hipGetLastError());
+    return GS_OK;
+}
+
 int gs_owner_writes(gs_handle *h, const gs_write *ops, uint32_t n, uint32_t tick) {
     if (!h || !h->booted) return GS_E_INVALID;
     if (!n) return GS_OK;
@@ -1490,6 +1626,15 @@ int gs_run_phase(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t 
     h->seq += 1;
     h->reports_pending = true;
     h->last_phase_tick = std::max(h->last_phase_tick, tick);
+    if (h->split) {
+        int rc2 = h->KP <= 16 ? launch_exchange<4, false, 2>(h, ini, res, n, tick, lds, io)
+                              : launch_exchange<16, false, 2>(h, ini, res, n, tick, lds, io);
+        if (rc2) return rc2;
+        if (h->KP <= 16) k_pack_slice<4><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, io);
+        else k_pack_slice<16><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, io);
+        HIPCHK(h, hipGetLastError());
+        return GS_OK;
+    }
     if (h->KP <= 16) return genm ? launch_exchange<4, true, 0>(h, ini, res, n, tick, lds, io)
                                  : launch_exchange<4, false, 0>(h, ini, res, n, tick, lds, io);
     return genm ? launch_exchange<16, true, 0>(h, ini, res, n, tick, lds, io)

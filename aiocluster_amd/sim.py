@@ -343,15 +343,28 @@ class GossipSim:
     def sync(self):
         self._chk(self.L.gs_sync(self.h), "gs_sync")
 
+    def materialize_held(self, row_lo: int = 0, row_hi: int | None = None):
+        """Write out GS_R_HELD for the prefix views of rows [row_lo, row_hi) (readback only)."""
+        hi = self.n if row_hi is None else row_hi
+        self._chk(self.L.gs_materialize_held(self.h, row_lo, hi), "gs_materialize_held")
+
+    def inexact_views(self) -> int:
+        """Views with holes (GS_MV_INEXACT set): those whose HELD row the exchange kernel keeps."""
+        mv = self.region("MV", self.torch.int32, (self.n, self.np_))[:, : self.ncol]
+        return int((mv < 0).sum().item())
+
     # --------------------------------------------------------------- readback
     def _host(self):
         n, NP, KP, K, Cc = self.n, self.np_, self.kp, self.k, self.hist_cap
         torch = self.torch
+        self.materialize_held()
         self.sync()
         g = {}
         for name in ("HB", "MV", "GC", "FD_STATE"):
             if name in self.regions:
                 g[name] = self.region(name, torch.int32, (n, NP)).cpu().numpy().view(np.uint32)
+        g["MV_INEXACT"] = (g["MV"] >> np.uint32(31)).astype(np.uint8)  # prefix-view flag (GS_MV_INEXACT)
+        g["MV"] = g["MV"] & np.uint32(0x7FFFFFFF)
         if "GC" not in g:  # no tombstone GC: last_gc_version is 0 everywhere
             g["GC"] = np.zeros((n, NP), dtype=np.uint32)
         g["FD_LAST"], g["FD_SUM"], g["FD_CNT"] = self.unpack_fd(self.region("FD", torch.int64, (n, NP)).cpu().numpy())

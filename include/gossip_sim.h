@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define GS_API_VERSION 3
+#define GS_API_VERSION 4
 #define GS_TICK_US 15625u
 #define GS_NONE 0xFFFFFFFFu
 
@@ -77,10 +77,11 @@ typedef struct gs_config {
  * slice col_lo = 0 and n_cols = n_nodes. */
 enum gs_region {
     GS_R_HB = 0,      /* u32 [N][NP]   NodeState.heartbeat of owner j as seen by observer o */
-    GS_R_MV,          /* u32 [N][NP]   NodeState.max_version */
+    GS_R_MV,          /* u32 [N][NP]   NodeState.max_version (| GS_MV_INEXACT, see below) */
     GS_R_GC,          /* u32 [N][NP]   NodeState.last_gc_version (GS_TOMBSTONES only: without tombstone GC
                                         it is 0 everywhere, and deletes / TTL writes are refused) */
-    GS_R_HELD,        /* u8  [N][NP][KP] write ordinal of each key held (0 = absent), KP = K rounded to 4 */
+    GS_R_HELD,        /* u8  [N][NP][KP] write ordinal of each key held (0 = absent), KP = K rounded to 4;
+                                        kept only for views with GS_MV_INEXACT or with GS_TOMBSTONES */
     GS_R_FD,          /* u64 [N][NP]   sampling window: low word = _last_heartbeat tick + 1 (0 = no
                                         window); high word = _sum in ticks | intervals appended since
                                         the last reset << sum_bits (len = min(cnt, W)); sum_bits =
@@ -108,8 +109,17 @@ enum gs_region {
                                         replayed into GS_R_FD by gs_liveness */
     GS_R_PEND_STAMP,  /* u32 [N][16]   tick of the phase that last wrote plane row (o, p): the row is
                                         valid for the current round only if it equals round tick + 1 + p */
+    GS_R_LATEST,      /* u64 [NC][KP]  the HIST entry of each key's latest write (no GS_TOMBSTONES only) */
     GS_NUM_REGIONS
 };
+
+/* Prefix views (no GS_TOMBSTONES: no deletes, no tombstone GC).  Bit 31 of a GS_R_MV word
+ * (GS_MV_INEXACT) is set iff the view is NOT S_j(max_version) = owner j's latest write of every
+ * key with version <= max_version, i.e. iff it has holes (a truncated NodeDelta, or a delta
+ * from a view with holes).  GS_R_HELD is kept only for those views; the others
+ * follow from the owner's history (gs_materialize_held writes them out for readers).  With
+ * GS_TOMBSTONES bit 31 is always 0 and GS_R_HELD always kept. */
+#define GS_MV_INEXACT 0x80000000u
 
 typedef struct gs_counters {
     uint64_t exchanges;     /* exchanges executed */
@@ -156,6 +166,10 @@ int gs_set_stream(gs_handle *h, void *hip_stream);
 int gs_boot(gs_handle *h, const uint16_t *nid_size, const uint8_t *key_len);
 /* Warm start: every observer learns every owner's current state, in index order. */
 int gs_warm(gs_handle *h);
+
+/* Fill GS_R_HELD of observer rows [row_lo, row_hi) for the views it is not kept for (see
+ * GS_MV_INEXACT).  Readback only; no-op with GS_TOMBSTONES. */
+int gs_materialize_held(gs_handle *h, uint32_t row_lo, uint32_t row_hi);
 
 /* Owner writes at `tick` (state.py:137-180).  `ops` is a DEVICE array; owners must be distinct. */
 int gs_owner_writes(gs_handle *h, const gs_write *ops, uint32_t n, uint32_t tick);
