@@ -787,22 +787,11 @@ __global__ __launch_bounds__(XB) void k_exchange(Dev d, const int32_t *ini, cons
     if (anynew) s_flag[0] = 1u;
     __syncthreads();
 
-    if (MODE >= 1) {
+    if (MODE == 1) {
         // ---- sharded count pass: publish the bitmaps, total this slice's candidates per direction
-        // (MODE 2: publish only; one slice, packed by a separate k_pack_slice launch)
         if (s_flag[0] && tid == 0) shard_add(d, C_E_INSERT, 1);
         uint32_t *gb = d.sbits + (size_t)e * 2 * words;
         for (uint32_t i = tid; i < 2 * words; i += XB) gb[i] = bm[i];
-        if (MODE == 2) {
-            const unsigned long long s_alg = wave_sum(alg), s_rep = wave_sum(reports), s_hbw = wave_sum(hbw);
-            if (lane == 0) {
-                shard_add(d, C_ALG, s_alg);
-                shard_add(d, C_REPORTS, s_rep);
-                shard_add(d, C_HBW, s_hbw);
-                if (wid == 0) shard_add(d, C_EXCH, 1);
-            }
-            return;
-        }
         const bool w0 = wid == 0;
         const uint32_t snd = w0 ? b : a, rcv = w0 ? a : b;
         const DigestSide ds{rcv, d.ncol, w0 ? schA : schB};
@@ -1327,7 +1316,6 @@ struct gs_handle {
     uint32_t G, shard, col_lo, ncol;  // owner-column slice
     bool reports_pending;             // phases ran since the last gs_liveness
     bool round_open;                  // gs_begin_round ran and gs_liveness has not closed the round yet
-    bool split;                       // GS_SPLIT experiment (canonical, one slice)
     uint32_t last_phase_tick;
     void *reg[GS_NUM_REGIONS];
     uint64_t bytes[GS_NUM_REGIONS];
@@ -1482,9 +1470,7 @@ int gs_create(const gs_config *cfg, gs_handle **out) {
     b[GS_R_KEY_LEN] = KP;
     b[GS_R_STAMP] = NR * 4;
     b[GS_R_COUNTERS] = (uint64_t)NSHARD * 32 * 8;
-    // GS_SPLIT (profiling experiment): one-slice phases as pass 1 + a separate packing launch
-    h->split = G == 1 && (c.flags & GS_CANONICAL) && getenv("GS_SPLIT") && atoi(getenv("GS_SPLIT"));
-    b[GS_R_SLICE_BITS] = (G > 1 || h->split) ? (N / 2) * 2 * (NP / 32) * 4 : 0;
+    b[GS_R_SLICE_BITS] = G > 1 ? (N / 2) * 2 * (NP / 32) * 4 : 0;
     const uint64_t PW = round_up(h->NP, 256) / 64;
     b[GS_R_PEND] = N * 16 * PW * 8;  // 16 phase bit planes per observer row
     b[GS_R_PEND_STAMP] = N * 16 * 4;
@@ -1626,15 +1612,6 @@ int gs_run_phase(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t 
     h->seq += 1;
     h->reports_pending = true;
     h->last_phase_tick = std::max(h->last_phase_tick, tick);
-    if (h->split) {
-        int rc2 = h->KP <= 16 ? launch_exchange<4, false, 2>(h, ini, res, n, tick, lds, io)
-                              : launch_exchange<16, false, 2>(h, ini, res, n, tick, lds, io);
-        if (rc2) return rc2;
-        if (h->KP <= 16) k_pack_slice<4><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, io);
-        else k_pack_slice<16><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, io);
-        HIPCHK(h, hipGetLastError());
-        return GS_OK;
-    }
     if (h->KP <= 16) return genm ? launch_exchange<4, true, 0>(h, ini, res, n, tick, lds, io)
                                  : launch_exchange<4, false, 0>(h, ini, res, n, tick, lds, io);
     return genm ? launch_exchange<16, true, 0>(h, ini, res, n, tick, lds, io)
