@@ -64,7 +64,7 @@ COUNTER_FIELDS = [
 EXPORTS = [
     "gs_create", "gs_destroy", "gs_last_error", "gs_api_version", "gs_region_bytes", "gs_bind", "gs_set_stream",
     "gs_boot", "gs_warm", "gs_owner_writes", "gs_begin_round", "gs_run_phase", "gs_liveness", "gs_phi_row",
-    "gs_read_counters", "gs_reset_counters", "gs_sync", "gs_shard_columns", "gs_phase_count", "gs_phase_pack", "gs_materialize_held",
+    "gs_read_counters", "gs_reset_counters", "gs_sync", "gs_shard_columns", "gs_phase_count", "gs_phase_pack", "gs_materialize_held", "gs_fd_census",
 ]
 
 API_VERSION = 4
@@ -91,6 +91,13 @@ class GsConfig(C.Structure):
 
 class GsCounters(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in COUNTER_FIELDS] + [("reserved", C.c_uint64 * 12)]
+
+
+CENSUS_FIELDS = ["up_pairs", "up_dead", "up_live", "down_pairs", "down_live"]
+
+
+class GsCensus(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in CENSUS_FIELDS]
 
 
 class GsError(RuntimeError):
@@ -143,6 +150,7 @@ def load():
         "gs_phase_count": (C.c_int, [P, P, P, u32, u32, P]),
         "gs_phase_pack": (C.c_int, [P, P, P, u32, u32, u32, P, P, P]),
         "gs_materialize_held": (C.c_int, [P, u32, u32]),
+        "gs_fd_census": (C.c_int, [P, P, C.POINTER(GsCensus)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

@@ -51,7 +51,8 @@ constexpr double TICK_S = 1.0 / 64.0;
 
 enum Ctr {
     C_EXCH = 0, C_REPORTS, C_ND, C_KVS, C_TRUNC, C_DBYTES, C_ALG, C_HBW, C_CAND, C_LIVE, C_TOMBGC,
-    C_E_FDOVF, C_E_HIST, C_E_IDX, C_E_CONFLICT, C_E_FDGC, C_E_INSERT, C_FDGC, C_Q9, C_PACKB, C_NUM
+    C_E_FDOVF, C_E_HIST, C_E_IDX, C_E_CONFLICT, C_E_FDGC, C_E_INSERT, C_FDGC, C_Q9, C_PACKB,
+    C_CEN0 = 24, C_NUM = C_CEN0 + 6  // gs_fd_census scratch slots (not part of gs_counters)
 };
 static_assert(C_NUM <= 32, "counter region");
 static_assert(sizeof(gs_counters) == 32 * 8, "gs_counters layout");
@@ -1178,6 +1179,36 @@ __global__ __launch_bounds__(LB) void k_fd_gc(Dev d, const uint8_t *up, uint32_t
     if (lane == 0) shard_add(d, C_FDGC, sg);
 }
 
+// Membership census over (observer, target) pairs, observer up and target != observer, from the
+// failure detector's live / dead sets (failure_detector.py:60-67): by whether the target is up
+// {up pairs, up and dead-marked (false positives), up and live, down pairs, down and live}.
+__global__ __launch_bounds__(LB) void k_fd_census(Dev d, const uint8_t *up) {
+    const uint32_t o = blockIdx.y;
+    const uint32_t j = blockIdx.x * LB + threadIdx.x;
+    uint32_t c[5] = {0u, 0u, 0u, 0u, 0u};
+    if (up[o] && j < d.ncol && d.col_lo + j != o) {
+        const uint32_t st = d.fd_state[pix(d, o, j)];
+        if (up[d.col_lo + j]) {
+            c[0] = 1u;
+            c[1] = st >= 2u;
+            c[2] = st == 1u;
+        } else {
+            c[3] = 1u;
+            c[4] = st == 1u;
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 5; i++) {
+        const unsigned long long v = wave_sum(c[i]);
+        if ((threadIdx.x & 63) == 0) shard_add(d, C_CEN0 + i, v);
+    }
+}
+
+__global__ void k_zero_slots(Dev d, uint32_t lo, uint32_t n) {
+    const uint32_t i = threadIdx.x;
+    if (i < NSHARD * n) d.ctr[(i / n) * 32 + lo + i % n] = 0ull;
+}
+
 // SamplingWindow.phi (failure_detector.py:43-53) of every target of observer o; NaN for None.
 __global__ __launch_bounds__(LB) void k_phi_row(Dev d, uint32_t o, uint32_t t, double *out) {
     const uint32_t j = blockIdx.x * LB + threadIdx.x;
@@ -1705,6 +1736,27 @@ int gs_read_counters(gs_handle *h, gs_counters *out) {
 int gs_reset_counters(gs_handle *h) {
     if (!h || !h->reg[GS_R_COUNTERS]) return GS_E_INVALID;
     HIPCHK(h, hipMemsetAsync(h->reg[GS_R_COUNTERS], 0, h->bytes[GS_R_COUNTERS], h->stream));
+    return GS_OK;
+}
+
+int gs_fd_census(gs_handle *h, const uint8_t *up, gs_census *out) {
+    if (!h || !h->booted || !up || !out) return GS_E_INVALID;
+    k_zero_slots<<<1, NSHARD * 8, 0, h->stream>>>(h->d, C_CEN0, 5);
+    HIPCHK(h, hipGetLastError());
+    dim3 grid((h->ncol + LB - 1) / LB, h->N);
+    k_fd_census<<<grid, LB, 0, h->stream>>>(h->d, up);
+    HIPCHK(h, hipGetLastError());
+    std::vector<unsigned long long> buf((size_t)NSHARD * 32);
+    HIPCHK(h, hipMemcpyAsync(buf.data(), h->reg[GS_R_COUNTERS], buf.size() * 8, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    uint64_t acc[5] = {0, 0, 0, 0, 0};
+    for (int sh = 0; sh < NSHARD; sh++)
+        for (int i = 0; i < 5; i++) acc[i] += buf[(size_t)sh * 32 + C_CEN0 + i];
+    out->up_pairs = acc[0];
+    out->up_dead = acc[1];
+    out->up_live = acc[2];
+    out->down_pairs = acc[3];
+    out->down_live = acc[4];
     return GS_OK;
 }
 

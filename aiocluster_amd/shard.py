@@ -194,6 +194,20 @@ class ShardGroup:
             raise GsError(f"device checks failed: {errs}")
         return c
 
+    def fd_census(self, up) -> dict:
+        parts = [s.fd_census(up) for s in self.slices]
+        local = {k: sum(p[k] for p in parts) for k in parts[0]}
+        if isinstance(self.comm, DistComm):
+            import torch
+
+            from ._lib import CENSUS_FIELDS
+
+            dev = "cpu" if self.comm.dist.get_backend(self.comm.group) == "gloo" else "cuda"
+            v = torch.tensor([local[k] for k in CENSUS_FIELDS], dtype=torch.int64, device=dev)
+            self.comm.dist.all_reduce(v, group=self.comm.group)
+            local = dict(zip(CENSUS_FIELDS, (int(x) for x in v.tolist())))
+        return local
+
     def export(self) -> dict:
         """The slices this process holds, joined along the owner axis (all of them in-process)."""
         parts = [s.export() for s in self.slices]

@@ -343,6 +343,14 @@ class GossipSim:
     def sync(self):
         self._chk(self.L.gs_sync(self.h), "gs_sync")
 
+    def fd_census(self, up) -> dict:
+        """gs_fd_census: live / dead sets of every up observer against the up mask (config 5's
+        false-positive rate = up_dead / up_pairs)."""
+        u = up if hasattr(up, "data_ptr") else self._dev(np.asarray(up, dtype=np.uint8), self.torch.uint8)
+        c = _lib.GsCensus()
+        self._chk(self.L.gs_fd_census(self.h, C.c_void_p(u.data_ptr()), C.byref(c)), "gs_fd_census")
+        return {n: int(getattr(c, n)) for n in _lib.CENSUS_FIELDS}
+
     def materialize_held(self, row_lo: int = 0, row_hi: int | None = None):
         """Write out GS_R_HELD for the prefix views of rows [row_lo, row_hi) (readback only)."""
         hi = self.n if row_hi is None else row_hi

@@ -145,6 +145,17 @@ typedef struct gs_counters {
     uint64_t reserved[12];
 } gs_counters;
 
+/* Failure-detector membership census (gs_fd_census): (observer, target) pairs with the observer up and
+ * target != observer, split by whether the target is up (BASELINE config 5: false-positive rate =
+ * up_dead / up_pairs). */
+typedef struct gs_census {
+    uint64_t up_pairs;    /* target up */
+    uint64_t up_dead;     /* ... and in the observer's dead set (false positive) */
+    uint64_t up_live;     /* ... and in the observer's live set */
+    uint64_t down_pairs;  /* target down */
+    uint64_t down_live;   /* ... but still in the observer's live set (not yet detected) */
+} gs_census;
+
 typedef struct gs_write {   /* one owner write */
     uint32_t owner, key, op, value_id, value_len;
 } gs_write;
@@ -213,6 +224,10 @@ int gs_liveness(gs_handle *h, const uint8_t *up, uint32_t tick);
  * into the DEVICE array out[n_cols] (this slice's targets; binary64; NaN where the reference
  * returns None). */
 int gs_phi_row(gs_handle *h, uint32_t observer, uint32_t tick, double *out);
+
+/* FailureDetector.live_nodes / dead_nodes of every up observer (failure_detector.py:63-67) counted
+ * against the DEVICE up mask; blocking.  Sliced handles count their own target columns. */
+int gs_fd_census(gs_handle *h, const uint8_t *up, gs_census *out);
 
 int gs_read_counters(gs_handle *h, gs_counters *out);
 int gs_reset_counters(gs_handle *h);

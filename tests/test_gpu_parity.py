@@ -140,3 +140,34 @@ def test_config2_cold_1024x64_converges_bit_exact():
     owner_mv = np.diag(ex["mv"])
     assert np.all(ex["mv"] <= owner_mv[None, :])
     assert np.all(ex["mv"] == owner_mv[None, :]), "version matrix did not converge"
+
+
+def test_config5_partition_heal_small_vs_oracle():
+    """BASELINE config 5 in miniature: MTU-truncated deltas, deletes + tombstone GC, a partition into
+    halves that heals; every round vs the oracle, and the device's failure-detector census (false-
+    positive rate) vs the one counted from the oracle's live / dead sets."""
+    spec = WorkloadSpec(n=256, k=8, fanout=3, seed=55, init="warm", write_frac=0.1, delete_frac=0.1,
+                        partition=(6, 22))
+    scen = make_scenario("c5_256", spec, 30, {"mtu": 1400, "tombstone_grace_s": 4, "initial_interval_s": 1.0,
+                                               "phi_threshold": 3.0})
+    gpu = make_backend(GossipSim, scen, fd_ring=False)
+    orc = make_backend(OracleSim, scen)
+    saw_fp = False
+    for r in range(len(scen["rounds"])):
+        replay_round(gpu, scen, r)
+        replay_round(orc, scen, r)
+        ex = orc.export()
+        diff = compare_exports(gpu.export(), ex)
+        assert diff is None, f"round {r}: {diff}"
+        up = np.asarray(scen["rounds"][r]["up"], dtype=bool)
+        off = ~np.eye(256, dtype=bool) & up[:, None]
+        tu = up[None, :]
+        want = {"up_pairs": int((off & tu).sum()), "up_dead": int((off & tu & (ex["tod"] >= 0)).sum()),
+                "up_live": int((off & tu & (ex["live"] == 1)).sum()), "down_pairs": int((off & ~tu).sum()),
+                "down_live": int((off & ~tu & (ex["live"] == 1)).sum())}
+        got = gpu.fd_census(scen["rounds"][r]["up"])
+        assert got == want, (r, got, want)
+        saw_fp |= got["up_dead"] > 0
+    c = gpu.check()
+    assert saw_fp and c["truncated"] > 0 and c["tomb_gc"] > 0
+    assert got["up_dead"] == 0  # healed: nobody is dead any more
