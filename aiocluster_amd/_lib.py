@@ -23,6 +23,7 @@ HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-ffp-contract=off", "-std=c++17"
 GS_CANONICAL = 1
 GS_TOMBSTONES = 2
 GS_FD_RING = 4
+GS_NO_HELD = 8
 GS_NONE = 0xFFFFFFFF
 GS_MV_INEXACT = 0x80000000
 TICK_US = 15_625
@@ -57,7 +58,7 @@ ERRORS = {-1: "GS_E_INVALID", -2: "GS_E_UNBOUND", -3: "GS_E_HIP", -4: "GS_E_DEVI
 COUNTER_FIELDS = [
     "exchanges", "hb_reports", "node_deltas", "kvs_sent", "truncated", "delta_bytes", "alg_bytes", "hb_writes",
     "candidates", "live_pairs", "tomb_gc", "err_fd_overflow", "err_hist_full", "err_bad_index", "err_conflict",
-    "err_fd_gc", "err_insert", "fd_gc", "q9", "pack_bytes",
+    "err_fd_gc", "err_insert", "fd_gc", "q9", "pack_bytes", "err_holes",
 ]
 
 # Every symbol include/gossip_sim.h declares (checked by tests/test_abi.py).
@@ -90,7 +91,7 @@ class GsConfig(C.Structure):
 
 
 class GsCounters(C.Structure):
-    _fields_ = [(n, C.c_uint64) for n in COUNTER_FIELDS] + [("reserved", C.c_uint64 * 12)]
+    _fields_ = [(n, C.c_uint64) for n in COUNTER_FIELDS] + [("reserved", C.c_uint64 * 11)]
 
 
 CENSUS_FIELDS = ["up_pairs", "up_dead", "up_live", "down_pairs", "down_live"]

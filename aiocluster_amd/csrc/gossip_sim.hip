@@ -51,7 +51,7 @@ constexpr double TICK_S = 1.0 / 64.0;
 
 enum Ctr {
     C_EXCH = 0, C_REPORTS, C_ND, C_KVS, C_TRUNC, C_DBYTES, C_ALG, C_HBW, C_CAND, C_LIVE, C_TOMBGC,
-    C_E_FDOVF, C_E_HIST, C_E_IDX, C_E_CONFLICT, C_E_FDGC, C_E_INSERT, C_FDGC, C_Q9, C_PACKB,
+    C_E_FDOVF, C_E_HIST, C_E_IDX, C_E_CONFLICT, C_E_FDGC, C_E_INSERT, C_FDGC, C_Q9, C_PACKB, C_E_HOLES,
     C_CEN0 = 24, C_NUM = C_CEN0 + 6  // gs_fd_census scratch slots (not part of gs_counters)
 };
 static_assert(C_NUM <= 32, "counter region");
@@ -229,8 +229,10 @@ __device__ __forceinline__ void eval_cand(const Dev &d, uint32_t s, uint32_t r, 
     const uint32_t pos_r = GENM ? d.pos[pr] : 0u;
     const uint32_t fst = ds.sched ? d.fd_state[pr] : 0u;
     const bool sx = !gct && !(msw & MV_INEXACT), rx = !gct && !(mrw & MV_INEXACT);
-    const uint32_t *hsp = reinterpret_cast<const uint32_t *>((sx ? d.last_w + (size_t)j * d.KP : d.held + ps * d.KP));
-    const uint32_t *hrp = reinterpret_cast<const uint32_t *>(d.held + pr * d.KP);
+    // GS_NO_HELD: no view may have holes (counted as err_holes when one would); never read HELD
+    const uint32_t *hsp = reinterpret_cast<const uint32_t *>(
+        (sx || !d.held) ? d.last_w + (size_t)j * d.KP : d.held + ps * d.KP);
+    const uint32_t *hrp = d.held ? reinterpret_cast<const uint32_t *>(d.held + pr * d.KP) : hsp;
 #pragma unroll
     for (int q = 0; q < KW; q++) {
         c.hs[q] = (uint32_t)q < kw ? hsp[q] : 0u;
@@ -377,8 +379,13 @@ __device__ __forceinline__ void apply_cand(const Dev &d, uint32_t r, const Cand<
         for (int q = 0; q < KW; q++) same = same && want[q] == hr[q];
         if (!same) mvw |= MV_INEXACT;
     }
-    uint32_t *hrp = reinterpret_cast<uint32_t *>(d.held + pr * d.KP);
     const bool keep_held = tt || (mvw & MV_INEXACT);  // a prefix view's HELD is not kept
+    if (keep_held && !d.held) {  // GS_NO_HELD: a view with holes cannot be represented
+        shard_add(d, C_E_HOLES, 1);
+        d.mv[pr] = mvw;
+        return;
+    }
+    uint32_t *hrp = reinterpret_cast<uint32_t *>(d.held + pr * d.KP);
 #pragma unroll
     for (int q = 0; q < KW; q++)
         if (keep_held && (hr[q] != hr0[q] || c.rx)) { hrp[q] = hr[q]; alg += 4; }
@@ -1165,7 +1172,8 @@ __global__ __launch_bounds__(LB) void k_fd_gc(Dev d, const uint8_t *up, uint32_t
             d.hb[p] = 0u;
             d.mv[p] = 0u;
             if (d.flags & GS_TOMBSTONES) d.gc[p] = 0u;
-            for (uint32_t k = 0; k < d.KP; k += 4) *reinterpret_cast<uint32_t *>(d.held + p * d.KP + k) = 0u;
+            if (d.held)
+                for (uint32_t k = 0; k < d.KP; k += 4) *reinterpret_cast<uint32_t *>(d.held + p * d.KP + k) = 0u;
             if (d.flags & GS_TOMBSTONES)
                 for (uint32_t k = 0; k < d.KP; k++) d.ts[p * d.KP + k] = NONE;
         }
@@ -1237,7 +1245,9 @@ __global__ __launch_bounds__(LB) void k_owner_writes(Dev d, const gs_write *ops,
     const uint32_t j = op.owner - d.col_lo, k = op.key;  // local column of the owner
     if (j >= d.ncol) return;  // another slice's owner
     const size_t pj = pix(d, op.owner, j);
-    uint8_t *held = d.held + pj * d.KP + k;
+    // the owner's own view holds every latest write (no GC of its own keys without tombstones);
+    // with GS_NO_HELD its held ordinals are the latest-write table
+    uint8_t *held = d.held ? d.held + pj * d.KP + k : d.last_w + (size_t)j * d.KP + k;
     const uint32_t w = *held;
     const uint32_t M = d.mv[pj];
     uint32_t st, vid, vl;
@@ -1307,9 +1317,10 @@ __global__ __launch_bounds__(LB) void k_warm(Dev d) {
         d.hb[p] = d.hb[q];
         d.mv[p] = d.mv[q];
         if (d.flags & GS_TOMBSTONES) d.gc[p] = d.gc[q];
-        for (uint32_t k = 0; k < d.KP; k += 4)
-            *reinterpret_cast<uint32_t *>(d.held + p * d.KP + k) =
-                *reinterpret_cast<const uint32_t *>(d.held + q * d.KP + k);
+        if (d.held)
+            for (uint32_t k = 0; k < d.KP; k += 4)
+                *reinterpret_cast<uint32_t *>(d.held + p * d.KP + k) =
+                    *reinterpret_cast<const uint32_t *>(d.held + q * d.KP + k);
         if (d.flags & GS_TOMBSTONES) {
             bool tb = false;
             for (uint32_t k = 0; k < d.KP; k++) {
@@ -1456,6 +1467,7 @@ int gs_create(const gs_config *cfg, gs_handle **out) {
     if (G > 1 && (!(c.flags & GS_CANONICAL) || (uint64_t)(G - 1) * blk >= c.n_nodes)) return GS_E_INVALID;
     const uint32_t ncol = G > 1 ? (uint32_t)std::min<uint64_t>(blk, c.n_nodes - col_lo) : c.n_nodes;
     if (c.n_keys < 1 || c.n_keys > 64) return GS_E_INVALID;
+    if ((c.flags & GS_NO_HELD) && (c.flags & GS_TOMBSTONES)) return GS_E_INVALID;  // prefix views need no GC
     if (c.hist_cap < 2 || c.hist_cap > 255) return GS_E_INVALID;
     if (c.mtu < 1 || c.window < 1) return GS_E_INVALID;
     if ((c.flags & GS_FD_RING) && (c.window > (1u << 20) || c.max_interval_ticks > 0xFFFFu)) return GS_E_INVALID;
@@ -1486,7 +1498,7 @@ int gs_create(const gs_config *cfg, gs_handle **out) {
     uint64_t *b = h->bytes;
     b[GS_R_HB] = b[GS_R_MV] = pairs * 4;
     b[GS_R_GC] = (c.flags & GS_TOMBSTONES) ? pairs * 4 : 0;  // last_gc_version stays 0 without tombstone GC
-    b[GS_R_HELD] = pairs * KP;
+    b[GS_R_HELD] = (c.flags & GS_NO_HELD) ? 0 : pairs * KP;
     b[GS_R_FD] = pairs * 8;
     b[GS_R_FD_STATE] = pairs * 4;
     b[GS_R_TS] = (c.flags & GS_TOMBSTONES) ? pairs * KP * 4 : 0;
@@ -1604,7 +1616,7 @@ int gs_warm(gs_handle *h) {
 
 int gs_materialize_held(gs_handle *h, uint32_t row_lo, uint32_t row_hi) {
     if (!h || !h->booted || row_lo > row_hi || row_hi > h->N) return GS_E_INVALID;
-    if ((h->cfg.flags & GS_TOMBSTONES) || row_lo == row_hi) return GS_OK;  // every view's HELD is kept
+    if ((h->cfg.flags & (GS_TOMBSTONES | GS_NO_HELD)) || row_lo == row_hi) return GS_OK;  // kept / not stored
     const uint64_t pairs = (uint64_t)(row_hi - row_lo) * h->ncol;
     const uint32_t blocks = (uint32_t)std::min<uint64_t>((pairs + LB - 1) / LB, 1u << 16);
     k_materialize<<<blocks, LB, 0, h->stream>>>(h->d, row_lo, row_hi);

@@ -34,7 +34,7 @@ from datetime import timedelta
 import numpy as np
 
 from . import _lib
-from ._lib import GS_CANONICAL, GS_FD_RING, GS_NONE, GS_TOMBSTONES, REGION, TICK_US, GsError
+from ._lib import GS_CANONICAL, GS_FD_RING, GS_NO_HELD, GS_NONE, GS_TOMBSTONES, REGION, TICK_US, GsError
 from .entities import NodeId, NodeState, VersionedValue, VersionStatusEnum
 from .pbsize import nodeid_size
 
@@ -113,7 +113,7 @@ class GossipSim:
                  initial_values: dict[int, list[tuple[int, str]]] | None = None, *, device: str = "cuda:0",
                  tombstones: bool = True, fd_ring: bool | None = None, hist_cap: int = 64,
                  nid_sizes: list[int] | None = None, initial_ops: list[np.ndarray] | None = None,
-                 canonical: bool | None = None, shards: int = 1, shard: int = 0):
+                 canonical: bool | None = None, shards: int = 1, shard: int = 0, held: bool = True):
         import torch
 
         if not torch.cuda.is_available():
@@ -141,6 +141,10 @@ class GossipSim:
             flags |= GS_CANONICAL
         if tombstones:
             flags |= GS_TOMBSTONES
+        if not held:  # version-only: every view must stay a prefix S_j(max_version) (GS_NO_HELD)
+            if tombstones:
+                raise GsError("held=False (GS_NO_HELD) needs tombstones=False")
+            flags |= GS_NO_HELD
         W = int(cfg["window"])
         if fd_ring is None:
             fd_ring = n * ((n + 63) // 64 * 64) * W * 2 <= (1 << 30)  # whole-cluster rule: every slice agrees
@@ -376,10 +380,19 @@ class GossipSim:
         if "GC" not in g:  # no tombstone GC: last_gc_version is 0 everywhere
             g["GC"] = np.zeros((n, NP), dtype=np.uint32)
         g["FD_LAST"], g["FD_SUM"], g["FD_CNT"] = self.unpack_fd(self.region("FD", torch.int64, (n, NP)).cpu().numpy())
-        g["HELD"] = self.region("HELD", torch.uint8, (n, NP, KP)).cpu().numpy()
         nc = self.ncol
         hist = self.region("HIST", torch.int64, (nc, Cc, K)).cpu().numpy().view(np.uint64)
         g["HIST_VER"] = (hist & 0xFFFFFFFF).astype(np.uint32)
+        if "HELD" in self.regions:
+            g["HELD"] = self.region("HELD", torch.uint8, (n, NP, KP)).cpu().numpy()
+        else:  # GS_NO_HELD: every view is S_j(max_version); count each key's writes <= max_version
+            last_w = self.region("LAST_W", torch.uint8, (nc, KP)).cpu().numpy()[:, :K].astype(np.int64)
+            M = g["MV"][:, :nc].astype(np.int64)
+            held = np.zeros((n, NP, KP), dtype=np.uint8)
+            for w in range(1, Cc):
+                ok = (w <= last_w) & (g["HIST_VER"][:, w, :] > 0)  # [nc, K]
+                held[:, :nc, :K] += (ok[None, :, :] & (g["HIST_VER"][None, :, w, :] <= M[:, :, None])).astype(np.uint8)
+            g["HELD"] = held
         g["HIST_META"] = (hist >> 32).astype(np.uint32)
         g["HIST_VID"] = self.region("HIST_VID", torch.int32, (nc, Cc, K)).cpu().numpy().view(np.uint32)
         g["ROW"] = self.region("ROW", torch.int32, (n, 4)).cpu().numpy().view(np.uint32)

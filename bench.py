@@ -190,6 +190,28 @@ def cpu_baseline(sim, spec, cfg, next_plan, sample: int, min_seconds: float = 10
     }
 
 
+class RehearsalComm:
+    """One slice of a G-slice cluster on this GPU (``--rehearse-slices G``): the other slices' gathered
+    totals are zeros, so the packing is NOT the cluster's -- a timing rehearsal of one GPU's share of a
+    G-GPU run (memory footprint, kernel times), never a result."""
+
+    def __init__(self, world: int):
+        self.world = world
+        self.rank = 0
+
+    def gather(self, parts):
+        import torch
+
+        (x,) = parts
+        return torch.cat([x[None], torch.zeros((self.world - 1,) + tuple(x.shape), dtype=x.dtype, device=x.device)])
+
+    def sum_counters(self, per_slice):
+        return per_slice[0]
+
+    def any(self, flag):
+        return flag
+
+
 def aggregate(exchanges: float, elapsed: float, dist=None, dev=None) -> tuple[float, float]:
     """Whole-job totals: exchanges summed over ranks, time = the slowest rank's."""
     if dist is None:
@@ -231,6 +253,11 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--slices", type=int, default=1, help="owner-column slices in this process (1-GPU rehearsal)")
+    ap.add_argument("--mtu", type=int, default=65507)
+    ap.add_argument("--rehearse-slices", type=int, default=0,
+                    help="hold only slice 0 of G owner-column slices (one GPU's share of a G-GPU run; timing only)")
+    ap.add_argument("--no-held", action="store_true",
+                    help="version-only layout (GS_NO_HELD, config 4): needs an mtu no delta reaches")
     args = ap.parse_args()
 
     import torch
@@ -254,9 +281,11 @@ def main():
 
     n, K = args.nodes, args.keys
     cfg = dict(DEFAULT_CFG)  # mtu 65507, window 1000, phi 8, max_interval 10 s, prior 5 s
+    cfg["mtu"] = args.mtu
     spec = WorkloadSpec(n=n, k=K, fanout=args.fanout, seed=args.seed, init="warm", write_frac=0.05,
                         down_frac=0.05, down_rounds=3)
-    workload = f"N={n} K={K} F={args.fanout} warm, 5% writes + 5% down churn/round, window 1000, mtu 65507"
+    workload = (f"N={n} K={K} F={args.fanout} warm, 5% writes + 5% down churn/round, window 1000, mtu {args.mtu}"
+                + (", version-only views (GS_NO_HELD)" if args.no_held else ""))
     t_setup = time.perf_counter()
     ids = synthetic_node_ids(n)
     boot = []  # Cluster(initial_key_values): key k of owner j = "v{j}.{k}.i", as K batches of distinct owners
@@ -267,13 +296,17 @@ def main():
         ops[:, 3] = 1 + k * n + np.arange(n)
         ops[:, 4] = 3 + digits(np.arange(n)) + digits(np.full(n, k)) + 1
         boot.append(ops)
-    kw = dict(init="warm", device=str(dev), tombstones=False, fd_ring=False, hist_cap=16, initial_ops=boot)
+    kw = dict(init="warm", device=str(dev), tombstones=False, fd_ring=False, hist_cap=16, initial_ops=boot,
+              held=not args.no_held)
     if world > 1 and args.slices > 1:
         raise SystemExit("--slices is a one-process rehearsal; with --gpus N each rank holds one slice")
     group = None
     if world > 1:
         sims = [GossipSim(ids, key_names(K), cfg, shards=world, shard=rank, **kw)]
         group = ShardGroup(sims, DistComm(), cfg["mtu"])
+    elif args.rehearse_slices > 1:
+        sims = [GossipSim(ids, key_names(K), cfg, shards=args.rehearse_slices, shard=0, **kw)]
+        group = ShardGroup(sims, RehearsalComm(args.rehearse_slices), cfg["mtu"])
     elif args.slices > 1:
         sims = [GossipSim(ids, key_names(K), cfg, shards=args.slices, shard=g, **kw) for g in range(args.slices)]
         group = ShardGroup(sims, LocalComm(args.slices), cfg["mtu"])
@@ -325,7 +358,9 @@ def main():
         cpu = cpu_baseline(sim, spec, cfg, plans[args.warmup + args.steps], args.cpu_sample, args.cpu_seconds)
     if rank == 0:
         line = {
-            "metric": "simulated gossip exchanges/sec at 65,536 nodes, 1-8 GPUs; % HBM peak",
+            "metric": ("REHEARSAL (one GPU's slice of a %d-GPU run, packing not the cluster's): exchanges/s"
+                       % args.rehearse_slices if args.rehearse_slices > 1 else
+                       "simulated gossip exchanges/sec at 65,536 nodes, 1-8 GPUs; % HBM peak"),
             "value": exch_total / elapsed_max,
             "unit": "exchanges/s",
             "n_gpus": world,
@@ -344,6 +379,7 @@ def main():
                 "fanout": args.fanout,
                 "exchanges_per_step": exch / args.steps,
                 "parallelism": (f"owner-column slices x{world} (RCCL all-gather of slice totals)" if world > 1
+                                else f"slice 0 of {args.rehearse_slices} (rehearsal)" if args.rehearse_slices > 1
                                 else f"owner-column slices x{args.slices} in one process" if group is not None
                                 else "1 GPU"),
             },

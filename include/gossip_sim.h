@@ -44,6 +44,9 @@ extern "C" {
 #define GS_CANONICAL 1u   /* every observer knows every node in index order (warm start, no removals) */
 #define GS_TOMBSTONES 2u  /* track tombstone receive ticks (needed when deletes/TTL writes occur) */
 #define GS_FD_RING 4u     /* keep each sampling window's ring (exact eviction once a window is full) */
+#define GS_NO_HELD 8u     /* no GS_R_HELD at all (needs !GS_TOMBSTONES): exact only while every view is a
+                             prefix S_j(max_version), i.e. no NodeDelta is ever truncated; a view that would
+                             get holes is counted in err_holes.  16 B less per pair at K = 16 (config 4) */
 
 /* owner write ops (NodeState.set/delete/set_with_ttl/delete_after_ttl, state.py:137-180) */
 #define GS_OP_SET 0u
@@ -81,7 +84,8 @@ enum gs_region {
     GS_R_GC,          /* u32 [N][NP]   NodeState.last_gc_version (GS_TOMBSTONES only: without tombstone GC
                                         it is 0 everywhere, and deletes / TTL writes are refused) */
     GS_R_HELD,        /* u8  [N][NP][KP] write ordinal of each key held (0 = absent), KP = K rounded to 4;
-                                        kept only for views with GS_MV_INEXACT or with GS_TOMBSTONES */
+                                        kept only for views with GS_MV_INEXACT or with GS_TOMBSTONES;
+                                        not allocated with GS_NO_HELD */
     GS_R_FD,          /* u64 [N][NP]   sampling window: low word = _last_heartbeat tick + 1 (0 = no
                                         window); high word = _sum in ticks | intervals appended since
                                         the last reset << sum_bits (len = min(cnt, W)); sum_bits =
@@ -142,7 +146,8 @@ typedef struct gs_counters {
     uint64_t fd_gc;            /* targets removed by FailureDetector.garbage_collect */
     uint64_t q9;               /* garbage_collect calls that raised KeyError */
     uint64_t pack_bytes;       /* the part of alg_bytes moved by delta packing + apply (pass 3) */
-    uint64_t reserved[12];
+    uint64_t err_holes;        /* GS_NO_HELD: a view got holes (a truncated NodeDelta); result inexact */
+    uint64_t reserved[11];
 } gs_counters;
 
 /* Failure-detector membership census (gs_fd_census): (observer, target) pairs with the observer up and

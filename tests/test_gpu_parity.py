@@ -171,3 +171,29 @@ def test_config5_partition_heal_small_vs_oracle():
     c = gpu.check()
     assert saw_fp and c["truncated"] > 0 and c["tomb_gc"] > 0
     assert got["up_dead"] == 0  # healed: nobody is dead any more
+
+
+@pytest.mark.parametrize("name", ["fdgc12", "q9x10"])
+def test_version_only_layout_matches_reference_golden(name):
+    """GS_NO_HELD (config 4's layout): no HELD region at all; exact while no NodeDelta is truncated."""
+    scen = load_scenario(name)
+    exp = scen["expect"]
+    sim = make_backend(GossipSim, scen, tombstones=False, held=False)
+    assert "HELD" not in sim.regions
+    res = replay_and_compare(sim, scen, exp["states"], exp["hashes"])
+    assert res is None, f"{name}: first mismatch at round {res[0]}: {res[1]}"
+    c = sim.check()
+    assert c["err_holes"] == 0 and c["truncated"] == 0
+
+
+def test_version_only_layout_vs_oracle_and_refuses_holes():
+    spec = WorkloadSpec(n=384, k=16, fanout=3, seed=17, init="warm", write_frac=0.2, down_frac=0.05,
+                        down_rounds=3)
+    scen = make_scenario("vo384", spec, 10, {"mtu": 1 << 30})
+    gpu, orc, c = lockstep_vs_oracle(scen, tombstones=False, held=False, fd_ring=False)
+    assert c["err_holes"] == 0 and c["node_deltas"] > 0
+    # the same cluster with a small mtu truncates NodeDeltas: views get holes, which this layout refuses
+    scen2 = make_scenario("vo384t", spec, 10, {"mtu": 1500})
+    sim = make_backend(GossipSim, scen2, tombstones=False, held=False, fd_ring=False)
+    with pytest.raises(GsError, match="err_holes"):
+        replay(sim, scen2, on_round=lambda r: sim.check())

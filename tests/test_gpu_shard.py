@@ -113,3 +113,22 @@ def test_distributed_slices_two_processes_match_single_handle():
     for k in ("exchanges", "node_deltas", "kvs_sent", "truncated", "delta_bytes", "hb_reports"):
         assert res[0][2][k] == c1[k], k  # counters summed over the ranks
     assert c1["truncated"] > 0 and res[0][3] > 0
+
+
+def test_version_only_slices_match_single_handle():
+    """Config 4's layout (GS_NO_HELD, owner-column slices, mtu above every delta) at a size one GPU holds."""
+    spec = WorkloadSpec(n=512, k=16, fanout=3, seed=44, init="warm", write_frac=0.1, down_frac=0.05,
+                        down_rounds=3)
+    scen = make_scenario("vo512x4", spec, 8, {"mtu": 1 << 30})
+    kw = dict(tombstones=False, fd_ring=False, held=False)
+    one = make_backend(GossipSim, scen, **kw)
+    grp = sharded(scen, 4, **kw)
+    for r in range(len(scen["rounds"])):
+        replay_round(one, scen, r)
+        replay_round(grp, scen, r)
+        diff = compare_exports(grp.export(), one.export())
+        assert diff is None, f"round {r}: {diff}"
+    c1, cg = one.check(), grp.check()
+    assert c1["err_holes"] == cg["err_holes"] == 0
+    for k in ("exchanges", "node_deltas", "kvs_sent", "delta_bytes", "hb_reports"):
+        assert cg[k] == c1[k], k
