@@ -1348,6 +1348,234 @@ __global__ __launch_bounds__(LB) void k_materialize(Dev d, uint32_t r0, uint32_t
     }
 }
 
+// ------------------------------------------------------------------ peer selection
+// select_nodes_for_gossip (server.py:656-717) for every up node from its failure detector's
+// live / dead sets and its known peers, as _gossip_multiple uses them at round start
+// (server.py:442-469): F distinct peers sampled uniformly from the live set (from all known
+// peers while the live set is empty), one dead node with probability dead / (live + 1), and one
+// seed when no selected peer is a seed or live < seeds, with probability seeds / (live + dead)
+// (1 if both are empty; always when live = 0).  Random numbers: Philox4x32-10 keyed by the run
+// seed, counter (round, node, slot) -- reproducible, where the reference's Random() over set
+// iteration order is not.  Slots 0..F-1 feed Floyd's sample, SEL_DEAD and SEL_SEED
+// the two probes.  Restated on the CPU by oracle/peer_select.py.
+constexpr uint32_t SEL_DEAD = 14, SEL_SEED = 15;
+
+__host__ __device__ inline void philox4x32(uint32_t (&c)[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c[0], p1 = (uint64_t)0xCD9E8D57u * c[2];
+        const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0, hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+        c[0] = hi1 ^ c[1] ^ k0;
+        c[1] = lo1;
+        c[2] = hi0 ^ c[3] ^ k1;
+        c[3] = lo0;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+}
+__host__ __device__ inline void sel_rand(uint64_t seed, uint32_t round, uint32_t node, uint32_t slot, uint32_t (&c)[4]) {
+    c[0] = round; c[1] = node; c[2] = slot; c[3] = 0u;
+    philox4x32(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+}
+__host__ __device__ inline uint32_t below(uint32_t x, uint32_t n) { return (uint32_t)(((uint64_t)x * n) >> 32); }
+__host__ __device__ inline double unit53(uint32_t a, uint32_t b) {
+    return (double)(((uint64_t)a << 21) ^ (uint64_t)(b >> 11)) * (1.0 / 9007199254740992.0);
+}
+
+// per row: live / dead / known-peer counts (observer up); SCNT[o] = {live, dead, peers, 0}
+__global__ __launch_bounds__(LB) void k_sel_count(Dev d, const uint8_t *up, uint32_t *scnt) {
+    const uint32_t o = blockIdx.x;
+    if (!up[o]) return;
+    const bool genm = !(d.flags & GS_CANONICAL);
+    uint32_t L = 0, D = 0, P = 0;
+    for (uint32_t j = threadIdx.x; j < d.ncol; j += LB) {
+        const size_t p = pix(d, o, j);
+        if (j == o || (genm && d.pos[p] == NONE)) continue;
+        const uint32_t st = d.fd_state[p];
+        P++;
+        L += st == 1u;
+        D += st >= 2u;
+    }
+    __shared__ uint32_t s3[3][LB / WAVE];
+    const uint32_t w = threadIdx.x >> 6;
+    const unsigned long long l = wave_sum(L), dd = wave_sum(D), pp = wave_sum(P);
+    if ((threadIdx.x & 63) == 0) { s3[0][w] = (uint32_t)l; s3[1][w] = (uint32_t)dd; s3[2][w] = (uint32_t)pp; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t a = 0, b = 0, c = 0;
+        for (int i = 0; i < LB / WAVE; i++) { a += s3[0][i]; b += s3[1][i]; c += s3[2][i]; }
+        scnt[o * 4 + 0] = a; scnt[o * 4 + 1] = b; scnt[o * 4 + 2] = c;
+    }
+}
+
+// Floyd's sample of k distinct ranks of [0, n) and the dead probe, by rank; targets resolved next.
+// sel[o][0..F) = live (or peer) ranks, sel[o][F] = dead rank, NONE where absent.
+__global__ __launch_bounds__(LB) void k_sel_pick(Dev d, const uint8_t *up, const uint32_t *scnt, uint32_t F,
+                                                 uint64_t seed, uint32_t round, uint32_t *sel) {
+    const uint32_t o = blockIdx.x * LB + threadIdx.x;
+    if (o >= d.N) return;
+    uint32_t *so = sel + (size_t)o * (F + 2);
+    for (uint32_t i = 0; i < F + 2; i++) so[i] = NONE;
+    if (!up[o]) return;
+    const uint32_t L = scnt[o * 4 + 0], D = scnt[o * 4 + 1], P = scnt[o * 4 + 2];
+    const uint32_t n = L ? L : P, k = F < n ? F : n;
+    uint32_t c[4];
+    for (uint32_t i = 0; i < k; i++) {
+        const uint32_t t = n - k + i;
+        sel_rand(seed, round, o, i, c);
+        uint32_t r = below(c[0], t + 1);
+        for (uint32_t q = 0; q < i; q++)
+            if (so[q] == r) { r = t; break; }
+        so[i] = r;
+    }
+    if (D) {
+        sel_rand(seed, round, o, SEL_DEAD, c);
+        const double pd = (double)D / (double)(L + 1u);
+        if (pd > unit53(c[0], c[1])) so[F] = below(c[2], D);
+    }
+}
+
+// Resolve ranks to node ids in column order (one workgroup per row), then the seed probe.
+// out[o][0..F) live picks, out[o][F] dead pick, out[o][F+1] seed pick (NONE = none).
+__global__ __launch_bounds__(LB) void k_sel_resolve(Dev d, const uint8_t *up, const uint32_t *scnt, uint32_t F,
+                                                    uint64_t seed, uint32_t round, const int32_t *seeds,
+                                                    uint32_t n_seeds, const uint32_t *sel, int32_t *out) {
+    __shared__ uint32_t s_w[LB / WAVE][2];
+    __shared__ uint32_t s_rank[10], s_hit[10];
+    const uint32_t o = blockIdx.x;
+    int32_t *oo = out + (size_t)o * (F + 2);
+    if (!up[o]) {
+        for (uint32_t i = threadIdx.x; i < F + 2; i += LB) oo[i] = -1;
+        return;
+    }
+    const bool genm = !(d.flags & GS_CANONICAL);
+    const uint32_t L = scnt[o * 4 + 0];
+    const bool from_live = L != 0;
+    if (threadIdx.x < F + 1) {
+        s_rank[threadIdx.x] = sel[(size_t)o * (F + 2) + threadIdx.x];
+        s_hit[threadIdx.x] = NONE;
+    }
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    uint32_t base_pool = 0, base_dead = 0;
+    for (uint32_t j0 = 0; j0 < d.ncol; j0 += LB) {
+        const uint32_t j = j0 + threadIdx.x;
+        bool known = false, live = false, dead = false;
+        if (j < d.ncol && j != o) {
+            const size_t p = pix(d, o, j);
+            known = !genm || d.pos[p] != NONE;
+            if (known) {
+                const uint32_t st = d.fd_state[p];
+                live = st == 1u;
+                dead = st >= 2u;
+            }
+        }
+        const bool inpool = from_live ? live : known;
+        const unsigned long long mp = __ballot(inpool), md = __ballot(dead);
+        if (lane == 0) { s_w[w][0] = (uint32_t)__popcll(mp); s_w[w][1] = (uint32_t)__popcll(md); }
+        __syncthreads();
+        uint32_t op = base_pool, od = base_dead, tp = 0, td = 0;
+        for (uint32_t i = 0; i < LB / WAVE; i++) {
+            if (i < w) { op += s_w[i][0]; od += s_w[i][1]; }
+            tp += s_w[i][0];
+            td += s_w[i][1];
+        }
+        const uint64_t lm = (1ull << lane) - 1ull;
+        const uint32_t rp = op + (uint32_t)__popcll(mp & lm), rd = od + (uint32_t)__popcll(md & lm);
+        for (uint32_t i = 0; i < F; i++)
+            if (inpool && s_rank[i] == rp) s_hit[i] = j;
+        if (dead && s_rank[F] == rd) s_hit[F] = j;
+        base_pool += tp;
+        base_dead += td;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        bool has_seed = false;
+        uint32_t S = 0;
+        for (uint32_t q = 0; q < n_seeds; q++) {
+            if ((uint32_t)seeds[q] == o) continue;
+            S++;
+            for (uint32_t i = 0; i < F; i++) has_seed |= s_hit[i] == (uint32_t)seeds[q];
+        }
+        const uint32_t D = scnt[o * 4 + 1];
+        uint32_t pick = NONE;
+        if (S && (!has_seed || L < S)) {
+            uint32_t c[4];
+            sel_rand(seed, round, o, SEL_SEED, c);
+            const double ps = (L + D) == 0u ? 1.0 : (double)S / (double)(L + D);
+            if (L == 0u || unit53(c[0], c[1]) <= ps) {
+                uint32_t k = below(c[2], S);
+                for (uint32_t q = 0; q < n_seeds; q++) {
+                    if ((uint32_t)seeds[q] == o) continue;
+                    if (k-- == 0) { pick = (uint32_t)seeds[q]; break; }
+                }
+            }
+        }
+        for (uint32_t i = 0; i < F + 1; i++) oo[i] = s_hit[i] == NONE ? -1 : (int32_t)(d.col_lo + s_hit[i]);
+        oo[F + 1] = pick == NONE ? -1 : (int32_t)pick;
+    }
+}
+
+// Conflict-free phases for the round's exchanges e = o * (F + 2) + slot (initiator o, responder
+// out[e]; exchanges whose responder is down fail before any state change, as a refused
+// connection does, and are not scheduled).  Per phase p, IT rounds of a deterministic Luby
+// matching: an unscheduled exchange whose two endpoints are free in p takes p if its priority
+// key is the smallest at both endpoints.  Exchanges left after 16 phases are dropped.
+__device__ inline uint32_t fmix32(uint32_t h) {
+    h ^= h >> 16; h *= 0x85EBCA6Bu; h ^= h >> 13; h *= 0xC2B2AE35u; h ^= h >> 16;
+    return h;
+}
+__device__ inline bool luby_active(const int32_t *out, const uint8_t *up, const uint32_t *eph, const uint32_t *busy,
+                                   uint32_t e, uint32_t F, uint32_t p, uint32_t &a, uint32_t &b) {
+    if (eph[e] != NONE) return false;
+    const int32_t t = out[e];
+    if (t < 0 || !up[t]) return false;
+    a = e / (F + 2);
+    b = (uint32_t)t;
+    return !((busy[a] >> p) & 1u) && !((busy[b] >> p) & 1u);
+}
+__device__ inline unsigned long long luby_key(uint64_t seed, uint32_t round, uint32_t e, uint32_t p, uint32_t it) {
+    const uint32_t h = fmix32(e ^ fmix32((uint32_t)seed ^ fmix32(round * 0x9E3779B9u + p * 0x632BE5ABu + it)));
+    return ((unsigned long long)h << 32) | e;
+}
+__global__ __launch_bounds__(LB) void k_luby_min(const int32_t *out, const uint8_t *up, const uint32_t *eph,
+                                                 const uint32_t *busy, unsigned long long *best, uint32_t E,
+                                                 uint32_t F, uint64_t seed, uint32_t round, uint32_t p, uint32_t it) {
+    const uint32_t e = blockIdx.x * LB + threadIdx.x;
+    uint32_t a, b;
+    if (e >= E || !luby_active(out, up, eph, busy, e, F, p, a, b)) return;
+    const unsigned long long k = luby_key(seed, round, e, p, it);
+    atomicMin(&best[a], k);
+    atomicMin(&best[b], k);
+}
+__global__ __launch_bounds__(LB) void k_luby_pick(const int32_t *out, const uint8_t *up, uint32_t *eph, uint32_t *busy,
+                                                  const unsigned long long *best, unsigned long long *best_next,
+                                                  uint32_t E, uint32_t N, uint32_t F, uint64_t seed, uint32_t round,
+                                                  uint32_t p, uint32_t it, uint32_t *pcount) {
+    const uint32_t x = blockIdx.x * LB + threadIdx.x;
+    if (x < N) best_next[x] = ~0ull;
+    uint32_t a, b;
+    if (x >= E || !luby_active(out, up, eph, busy, x, F, p, a, b)) return;
+    const unsigned long long k = luby_key(seed, round, x, p, it);
+    if (best[a] == k && best[b] == k) {
+        eph[x] = p;
+        atomicOr(&busy[a], 1u << p);
+        atomicOr(&busy[b], 1u << p);
+        atomicAdd(&pcount[p], 1u);
+    }
+}
+// scatter the scheduled exchanges into per-phase (initiator, responder) arrays
+__global__ __launch_bounds__(LB) void k_luby_scatter(const int32_t *out, const uint32_t *eph, uint32_t E, uint32_t F,
+                                                     const uint32_t *poff, uint32_t *pfill, int32_t *ini,
+                                                     int32_t *res) {
+    const uint32_t e = blockIdx.x * LB + threadIdx.x;
+    if (e >= E || eph[e] == NONE) return;
+    const uint32_t p = eph[e];
+    const uint32_t slot = poff[p] + atomicAdd(&pfill[p], 1u);
+    ini[slot] = (int32_t)(e / (F + 2));
+    res[slot] = out[e];
+}
+
 }  // namespace
 
 // ====================================================================== C ABI
@@ -1748,6 +1976,62 @@ int gs_read_counters(gs_handle *h, gs_counters *out) {
 int gs_reset_counters(gs_handle *h) {
     if (!h || !h->reg[GS_R_COUNTERS]) return GS_E_INVALID;
     HIPCHK(h, hipMemsetAsync(h->reg[GS_R_COUNTERS], 0, h->bytes[GS_R_COUNTERS], h->stream));
+    return GS_OK;
+}
+
+int gs_select_peers(gs_handle *h, const uint8_t *up, uint32_t fanout, const int32_t *seeds, uint32_t n_seeds,
+                    uint64_t seed, uint32_t round, int32_t *targets, void *scratch) {
+    if (!h || !h->booted || !up || !targets || !scratch || fanout < 1 || fanout > 8 || (n_seeds && !seeds))
+        return GS_E_INVALID;
+    if (h->G > 1) return fail(h, GS_E_UNSUPPORTED, "gs_select_peers needs the whole matrix (one slice)");
+    uint32_t *scnt = (uint32_t *)scratch;
+    uint32_t *sel = scnt + (size_t)h->N * 4;
+    k_sel_count<<<h->N, LB, 0, h->stream>>>(h->d, up, scnt);
+    HIPCHK(h, hipGetLastError());
+    k_sel_pick<<<(h->N + LB - 1) / LB, LB, 0, h->stream>>>(h->d, up, scnt, fanout, seed, round, sel);
+    HIPCHK(h, hipGetLastError());
+    k_sel_resolve<<<h->N, LB, 0, h->stream>>>(h->d, up, scnt, fanout, seed, round, seeds, n_seeds, sel, targets);
+    HIPCHK(h, hipGetLastError());
+    return GS_OK;
+}
+
+int gs_schedule_phases(gs_handle *h, const uint8_t *up, uint32_t fanout, const int32_t *targets, uint64_t seed,
+                       uint32_t round, uint32_t iters, void *scratch, int32_t *initiators, int32_t *responders,
+                       uint32_t *phase_offsets) {
+    if (!h || !up || !targets || !scratch || !initiators || !responders || !phase_offsets || fanout < 1 ||
+        fanout > 8 || iters < 1)
+        return GS_E_INVALID;
+    const uint32_t N = h->N, E = N * (fanout + 2);
+    // scratch: eph[E] | busy[N] | pcount[16] | pfill[16] | poff[16] | pad | best[2][N] (u64)
+    uint32_t *eph = (uint32_t *)scratch;
+    uint32_t *busy = eph + E;
+    uint32_t *pcount = busy + N;
+    uint32_t *pfill = pcount + 16;
+    uint32_t *poff = pfill + 16;
+    unsigned long long *best = (unsigned long long *)(((uintptr_t)(poff + 16) + 15) & ~(uintptr_t)15);
+    hipStream_t s = h->stream;
+    HIPCHK(h, hipMemsetAsync(eph, 0xFF, (size_t)E * 4, s));
+    HIPCHK(h, hipMemsetAsync(busy, 0, (size_t)(N + 48) * 4, s));
+    HIPCHK(h, hipMemsetAsync(best, 0xFF, (size_t)N * 16, s));
+    const uint32_t gE = (std::max(E, N) + LB - 1) / LB;
+    for (uint32_t p = 0; p < 16; p++)
+        for (uint32_t it = 0; it < iters; it++) {
+            unsigned long long *b0 = best + (size_t)(it & 1) * N, *b1 = best + (size_t)((it + 1) & 1) * N;
+            k_luby_min<<<(E + LB - 1) / LB, LB, 0, s>>>(targets, up, eph, busy, b0, E, fanout, seed, round, p, it);
+            k_luby_pick<<<gE, LB, 0, s>>>(targets, up, eph, busy, b0, b1, E, N, fanout, seed, round, p, it, pcount);
+        }
+    HIPCHK(h, hipGetLastError());
+    uint32_t cnt[16];
+    HIPCHK(h, hipMemcpyAsync(cnt, pcount, sizeof cnt, hipMemcpyDeviceToHost, s));
+    HIPCHK(h, hipStreamSynchronize(s));
+    uint32_t off[17];
+    off[0] = 0;
+    for (int p = 0; p < 16; p++) off[p + 1] = off[p] + cnt[p];
+    HIPCHK(h, hipMemcpyAsync(poff, off, 16 * 4, hipMemcpyHostToDevice, s));
+    k_luby_scatter<<<(E + LB - 1) / LB, LB, 0, s>>>(targets, eph, E, fanout, poff, pfill, initiators, responders);
+    HIPCHK(h, hipGetLastError());
+    HIPCHK(h, hipStreamSynchronize(s));
+    memcpy(phase_offsets, off, sizeof off);
     return GS_OK;
 }
 

@@ -269,7 +269,7 @@ class GossipSim:
     # --------------------------------------------------------------- round driver
     def begin_round(self, t: int, up):
         self._flush()
-        u = self._dev(np.asarray(up, dtype=np.uint8), self.torch.uint8)
+        u = up if hasattr(up, "data_ptr") else self._dev(np.asarray(up, dtype=np.uint8), self.torch.uint8)
         self._chk(self.L.gs_begin_round(self.h, C.c_void_p(u.data_ptr()), t), "gs_begin_round")
 
     def run_phase(self, t: int, pairs):

@@ -230,6 +230,27 @@ int gs_liveness(gs_handle *h, const uint8_t *up, uint32_t tick);
  * returns None). */
 int gs_phi_row(gs_handle *h, uint32_t observer, uint32_t tick, double *out);
 
+/* select_nodes_for_gossip (server.py:656-717) for every up node at round start (server.py:442-469),
+ * from its failure detector's live / dead sets and known peers: `fanout` distinct peers uniformly from
+ * the live set (all known peers while it is empty), a dead node with probability dead / (live + 1),
+ * a seed (from the DEVICE list seeds[n_seeds], self excluded) when no selected peer is a seed or
+ * live < seeds, with probability seeds / (live + dead) (1 when both are 0; always when live = 0).
+ * Random numbers: Philox4x32-10 keyed by `seed`, counter (round, node, slot).  Output DEVICE
+ * targets[N][fanout + 2] = fanout peers, the dead pick, the seed pick (-1 = none).  DEVICE scratch of
+ * 4 * N * (fanout + 6) bytes.  1 <= fanout <= 8; one slice only. */
+int gs_select_peers(gs_handle *h, const uint8_t *up, uint32_t fanout, const int32_t *seeds, uint32_t n_seeds,
+                    uint64_t seed, uint32_t round, int32_t *targets, void *scratch);
+/* The round's exchanges (initiator o, responder targets[o][s], responder up) in <= 16 conflict-free
+ * phases: per phase `iters` rounds of a deterministic Luby matching (an exchange whose endpoints are
+ * free in that phase takes it if its priority key is the smallest at both).  Writes the exchanges of
+ * phase p to DEVICE initiators/responders[phase_offsets[p] .. phase_offsets[p+1]) (order within a
+ * phase unspecified: exchanges of one phase commute) and the host array phase_offsets[17]; exchanges
+ * left after 16 phases are not scheduled (N * (fanout + 2) - phase_offsets[16] minus the empty and
+ * down-responder slots).  DEVICE scratch of 4 * (N * (fanout + 6) + 64) + 16 * N bytes.  Blocking. */
+int gs_schedule_phases(gs_handle *h, const uint8_t *up, uint32_t fanout, const int32_t *targets, uint64_t seed,
+                       uint32_t round, uint32_t iters, void *scratch, int32_t *initiators, int32_t *responders,
+                       uint32_t *phase_offsets);
+
 /* FailureDetector.live_nodes / dead_nodes of every up observer (failure_detector.py:63-67) counted
  * against the DEVICE up mask; blocking.  Sliced handles count their own target columns. */
 int gs_fd_census(gs_handle *h, const uint8_t *up, gs_census *out);

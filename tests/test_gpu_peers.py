@@ -1,0 +1,123 @@
+"""Device peer selection (gs_select_peers, gs_schedule_phases) vs its CPU restatement
+(oracle/peer_select.py), and rounds driven by it vs the C oracle.  GPU only.
+
+select_nodes_for_gossip (aiocluster/server.py:656-717) draws from random.Random over set order
+(SURVEY Q11): parity is exact against the restatement of the same Philox draws, distributional
+against the reference's probabilities (dead probe p = dead / (live + 1), F distinct live peers).
+"""
+
+import numpy as np
+import pytest
+import peer_select
+from helpers import compare_exports, make_backend
+from oracle import OracleSim
+
+from aiocluster_amd.peers import PeerSelector, run_selected_round
+from aiocluster_amd.scenario import make_scenario, replay_round
+from aiocluster_amd.sim import GossipSim
+from aiocluster_amd.workload import WorkloadSpec, liveness_tick, phase_tick, round_tick
+
+pytestmark = pytest.mark.gpu
+
+
+def _state(orc):
+    ex = orc.export()
+    return ex["live"], ex["tod"], (ex["pos"] >= 0)
+
+
+def _warm_cluster(n=160, rounds=8, seed=3, init="warm"):
+    spec = WorkloadSpec(n=n, k=4, fanout=3, seed=seed, init=init, write_frac=0.1, down_frac=0.15, down_rounds=4)
+    scen = make_scenario(f"sel{n}", spec, rounds + 1, {"initial_interval_s": 1.0, "phi_threshold": 3.0})
+    gpu = make_backend(GossipSim, scen, fd_ring=False)
+    orc = make_backend(OracleSim, scen)
+    for r in range(rounds):
+        replay_round(gpu, scen, r)
+        replay_round(orc, scen, r)
+    assert compare_exports(gpu.export(), orc.export()) is None
+    return scen, gpu, orc
+
+
+@pytest.mark.parametrize("init", ["warm", "cold"])
+def test_selection_and_schedule_match_restatement(init):
+    scen, gpu, orc = _warm_cluster(init=init)
+    up = np.asarray(scen["rounds"][-1]["up"], dtype=np.uint8)
+    seeds = [0, 5, 77]
+    sel = PeerSelector(gpu, fanout=3, seeds=seeds, seed=1234)
+    up_dev = gpu._dev(up, gpu.torch.uint8)
+    got = sel.select(up_dev, 9).cpu().numpy()
+    live, tod, known = _state(orc)
+    want = peer_select.select_peers(live, tod, known, up, 3, seeds, 1234, 9)
+    assert np.array_equal(got, want)
+    assert (got[:, 3] >= 0).any() and (got[:, 4] >= 0).any()  # dead probes and seed probes happened
+    phases, offs = sel.schedule(up_dev, 9)
+    eph = peer_select.schedule_phases(want, up, 1234, 9, 4)
+    W = want.shape[1]
+    want_sets = [set() for _ in range(16)]
+    for e in np.flatnonzero(eph >= 0):
+        want_sets[eph[e]].add((int(e // W), int(want.reshape(-1)[e])))
+    got_sets = sel.scheduled_pairs(phases)
+    assert got_sets == [x for x in want_sets if x]
+    for ph in got_sets:  # conflict-free
+        nodes = [x for pr in ph for x in pr]
+        assert len(nodes) == len(set(nodes))
+    valid = sum(1 for e in range(want.size) if want.reshape(-1)[e] >= 0 and up[want.reshape(-1)[e]])
+    assert offs[16] == int((eph >= 0).sum()) and offs[16] >= valid - 2  # (almost) nothing dropped
+
+
+def test_rounds_with_device_peer_selection_match_oracle():
+    """Whole rounds whose schedule comes from gs_select_peers / gs_schedule_phases: the oracle replays
+    the same phases and must end every round in the same state."""
+    scen, gpu, orc = _warm_cluster(n=128, rounds=3, seed=9)
+    sel = PeerSelector(gpu, fanout=3, seeds=[1, 2], seed=77)
+    rng = np.random.default_rng(5)
+    for r in range(3, 12):
+        up = (rng.random(128) > 0.1).astype(np.uint8)
+        t = round_tick(r)
+        up_dev = gpu._dev(up, gpu.torch.uint8)
+        gpu.begin_round(t, up_dev)
+        orc.begin_round(t, up)
+        sel.select(up_dev, r)
+        phases, _ = sel.schedule(up_dev, r)
+        sets = sel.scheduled_pairs(phases)
+        for p, (a, b, n) in enumerate(phases):
+            gpu.run_phase_arrays(phase_tick(r, p), a, b)
+            orc.run_phase(phase_tick(r, p), sorted(sets[p]))
+        gpu.update_node_liveness(liveness_tick(r, len(phases)), up_dev)
+        orc.liveness(liveness_tick(r, len(phases)), up, r)
+        diff = compare_exports(gpu.export(), orc.export())
+        assert diff is None, f"round {r}: {diff}"
+    assert gpu.check()["exchanges"] > 0
+
+
+def test_dead_probe_and_sample_distribution():
+    """Frequencies of the device draws against select_nodes_for_gossip's probabilities."""
+    scen, gpu, orc = _warm_cluster(n=256, rounds=8, seed=4)
+    up = np.asarray(scen["rounds"][-1]["up"], dtype=np.uint8)
+    live, tod, known = _state(orc)
+    sel = PeerSelector(gpu, fanout=3, seeds=[], seed=99)
+    up_dev = gpu._dev(up, gpu.torch.uint8)
+    hits, expect, picks = 0, 0.0, 0
+    for r in range(40):
+        tg = sel.select(up_dev, 100 + r).cpu().numpy()
+        for o in np.flatnonzero(up):
+            kn = known[o].copy()
+            kn[o] = False
+            L = int((kn & (live[o] == 1)).sum())
+            D = int((kn & (tod[o] >= 0)).sum())
+            expect += min(1.0, D / (L + 1))
+            hits += tg[o, 3] >= 0
+            row = tg[o, :3]
+            assert len(set(row[row >= 0])) == (row >= 0).sum() == min(3, L if L else int(kn.sum()))
+            assert all(live[o, x] == 1 for x in row[row >= 0]) if L else True
+            picks += 1
+    assert abs(hits - expect) < 4 * np.sqrt(expect) + 1, (hits, expect)
+    assert expect > 20
+
+
+def test_run_selected_round_helper():
+    scen, gpu, orc = _warm_cluster(n=96, rounds=2, seed=12)
+    sel = PeerSelector(gpu, fanout=2, seeds=[0], seed=5)
+    for r in range(2, 6):
+        info = run_selected_round(gpu, sel, r, np.ones(96, dtype=np.uint8))
+        assert 1 <= info["phases"] <= 16 and info["exchanges"] > 0
+    gpu.check()
