@@ -78,9 +78,12 @@ def prepare(sim, spec, rounds, torch, dev):
     return out
 
 
-def run_round(sims, rd, events=None, group=None):
-    """One gossip round on the slices this process drives (one GossipSim when unsliced)."""
+def run_round(sims, rd, events=None, group=None, sel=None):
+    """One gossip round on the slices this process drives (one GossipSim when unsliced).  With ``sel``
+    (a PeerSelector) the round's exchanges come from the device's select_nodes_for_gossip + phase
+    schedule instead of the workload's explicit schedule."""
     from aiocluster_amd.shard import run_sliced_phase
+    from aiocluster_amd.workload import phase_tick
 
     s0 = sims[0]
     for sim in sims:
@@ -88,7 +91,14 @@ def run_round(sims, rd, events=None, group=None):
             sim._chk(sim.L.gs_owner_writes(sim.h, C.c_void_p(rd["ops"].data_ptr()), rd["nops"], rd["t"]),
                      "gs_owner_writes")
         sim._chk(sim.L.gs_begin_round(sim.h, C.c_void_p(rd["up"].data_ptr()), rd["t"]), "gs_begin_round")
-    for a, b, n, t in rd["phases"]:
+    phases = rd["phases"]
+    if sel is not None:
+        sel.select(rd["up"], rd["r"])
+        ph, offs = sel.schedule(rd["up"], rd["r"])
+        phases = [(a, b, n, phase_tick(rd["r"], p)) for p, (a, b, n) in enumerate(ph)]
+        rd["exchanges"] = offs[16]
+        rd["t_live"] = rd["t"] + 1 + len(phases)
+    for a, b, n, t in phases:
         if not n:
             continue
         if events is not None:
@@ -254,6 +264,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--slices", type=int, default=1, help="owner-column slices in this process (1-GPU rehearsal)")
     ap.add_argument("--mtu", type=int, default=65507)
+    ap.add_argument("--peer-select", action="store_true",
+                    help="schedule each round with the device's select_nodes_for_gossip (gs_select_peers) and "
+                         "Luby phases (gs_schedule_phases) instead of the workload's permutation schedule")
     ap.add_argument("--rehearse-slices", type=int, default=0,
                     help="hold only slice 0 of G owner-column slices (one GPU's share of a G-GPU run; timing only)")
     ap.add_argument("--no-held", action="store_true",
@@ -285,7 +298,9 @@ def main():
     spec = WorkloadSpec(n=n, k=K, fanout=args.fanout, seed=args.seed, init="warm", write_frac=0.05,
                         down_frac=0.05, down_rounds=3)
     workload = (f"N={n} K={K} F={args.fanout} warm, 5% writes + 5% down churn/round, window 1000, mtu {args.mtu}"
-                + (", version-only views (GS_NO_HELD)" if args.no_held else ""))
+                + (", version-only views (GS_NO_HELD)" if args.no_held else "")
+                + (", device peer selection (select_nodes_for_gossip, 8 seeds) + Luby phases" if args.peer_select
+                   else ""))
     t_setup = time.perf_counter()
     ids = synthetic_node_ids(n)
     boot = []  # Cluster(initial_key_values): key k of owner j = "v{j}.{k}.i", as K batches of distinct owners
@@ -314,11 +329,18 @@ def main():
         sims = [GossipSim(ids, key_names(K), cfg, **kw)]
     sim = sims[0]
     plans = prepare(sim, spec, args.warmup + args.steps + 1, torch, dev)
+    sel = None
+    if args.peer_select:
+        from aiocluster_amd.peers import PeerSelector
+
+        if group is not None:
+            raise SystemExit("--peer-select needs the whole matrix on one GPU")
+        sel = PeerSelector(sim, fanout=args.fanout, seeds=list(range(0, n, max(1, n // 8))), seed=args.seed)
     torch.cuda.synchronize(dev)
     log(f"setup {time.perf_counter() - t_setup:.1f}s")
 
     for r in range(args.warmup):
-        run_round(sims, plans[r], group=group)
+        run_round(sims, plans[r], group=group, sel=sel)
     torch.cuda.synchronize(dev)
     for s_ in sims:
         s_.check()
@@ -329,7 +351,7 @@ def main():
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for r in range(args.warmup, args.warmup + args.steps):
-        run_round(sims, plans[r], events, group)
+        run_round(sims, plans[r], events, group, sel)
     torch.cuda.synchronize(dev)
     if dist is not None:
         dist.barrier()
