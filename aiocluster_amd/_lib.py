@@ -66,7 +66,7 @@ EXPORTS = [
     "gs_create", "gs_destroy", "gs_last_error", "gs_api_version", "gs_region_bytes", "gs_bind", "gs_set_stream",
     "gs_boot", "gs_warm", "gs_owner_writes", "gs_begin_round", "gs_run_phase", "gs_liveness", "gs_phi_row",
     "gs_read_counters", "gs_reset_counters", "gs_sync", "gs_shard_columns", "gs_phase_count", "gs_phase_pack", "gs_materialize_held", "gs_fd_census",
-    "gs_select_peers", "gs_schedule_phases",
+    "gs_select_peers", "gs_schedule_phases", "gs_set_events",
 ]
 
 API_VERSION = 4
@@ -153,6 +153,7 @@ def load():
         "gs_phase_pack": (C.c_int, [P, P, P, u32, u32, u32, P, P, P]),
         "gs_materialize_held": (C.c_int, [P, u32, u32]),
         "gs_fd_census": (C.c_int, [P, P, C.POINTER(GsCensus)]),
+        "gs_set_events": (C.c_int, [P, P, u32, P]),
         "gs_select_peers": (C.c_int, [P, P, u32, P, u32, C.c_uint64, u32, P, P]),
         "gs_schedule_phases": (C.c_int, [P, P, u32, P, C.c_uint64, u32, u32, P, P, P, C.POINTER(u32)]),
     }

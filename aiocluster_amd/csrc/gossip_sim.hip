@@ -87,6 +87,10 @@ struct Dev {
     uint32_t *pstamp;  // [N][16]
     uint32_t PW;       // u64 words per plane row: NP rounded up to 256, / 64
     uint32_t t_round;  // tick of the last gs_begin_round
+    // event stream (gs_set_events): records {observer, owner, key | kind << 8, old version, new version,
+    // tick}; kind 0 = on_key_change, 1 = node join, 2 = node leave.  ev == nullptr: off
+    uint32_t *ev, *ev_count;
+    uint32_t ev_cap;
 };
 
 // ------------------------------------------------------------------ protobuf sizes
@@ -151,6 +155,15 @@ __device__ inline unsigned long long wave_sum(unsigned long long x) {
 
 __device__ inline void shard_add(const Dev &d, int c, unsigned long long v) {
     if (v) atomicAdd(&d.ctr[(blockIdx.x % NSHARD) * 32 + c], v);
+}
+
+enum EvKind { EV_KEY = 0, EV_JOIN = 1, EV_LEAVE = 2 };
+__device__ inline void emit_event(const Dev &d, uint32_t o, uint32_t j, uint32_t kk, uint32_t v_old, uint32_t v_new,
+                                  uint32_t t) {
+    const uint32_t i = atomicAdd(d.ev_count, 1u);
+    if (i >= d.ev_cap) return;  // overflow: the count says how many were lost
+    uint32_t *r = d.ev + (size_t)i * 6;
+    r[0] = o; r[1] = j; r[2] = kk; r[3] = v_old; r[4] = v_new; r[5] = t;
 }
 
 // ------------------------------------------------------------------ packing / apply
@@ -320,7 +333,7 @@ template <int KW>
 __device__ __forceinline__ void apply_cand(const Dev &d, uint32_t r, const Cand<KW> &c, uint32_t vmax, uint32_t t, bool &tomb,
                                   uint32_t &alg) {
     const size_t pr = pix(d, r, c.j);
-    if (c.fast && vmax == NONE) {
+    if (c.fast && vmax == NONE && !d.ev) {
         // prefix sender, prefix receiver, whole NodeDelta: the view becomes S_j(max(mr, ms)) (keys
         // above mr move to the sender's latest write <= ms, the others already are), still a prefix.
         // ms <= mr happens when the receiver's digest left j out (scheduled for deletion: from = 0)
@@ -360,6 +373,10 @@ __device__ __forceinline__ void apply_cand(const Dev &d, uint32_t r, const Cand<
         if (ws && v > c.from && v <= vmax && v > m0 && wr < ws) {
             const uint32_t st = c.km[q] >> 16;
             if (!(st != 0u && v <= g)) {
+                // on_key_change(node, key, existing, new) for every stored kv (state.py:228-231)
+                if (d.ev)
+                    emit_event(d, r, d.col_lo + c.j, (uint32_t)q | (EV_KEY << 8),
+                               wr ? (uint32_t)d.hist[hix(d, c.j, wr, q)] : 0u, v, t);
                 wr = ws;
                 if (tt) { tsr[q] = st ? t : NONE; alg += 4; }
                 if (st) tomb = true;
@@ -1061,6 +1078,9 @@ __global__ __launch_bounds__(LB) void k_liveness(Dev d, const uint8_t *up, uint3
                     const double phi = ((double)(t - f.last) * TICK_S) / mean;
                     alive = phi <= d.phi_thr;
                 }
+                // node join / leave: the live set against the previous call's (server.py:611-616)
+                if (d.ev && alive != (st[i] == 1u))
+                    emit_event(d, o, d.col_lo + j, (alive ? EV_JOIN : EV_LEAVE) << 8, 0u, 0u, t);
                 if (alive) {
                     if (st[i] != 1u) { st[i] = 1u; ds = true; }
                 } else {
@@ -1278,6 +1298,11 @@ __global__ __launch_bounds__(LB) void k_owner_writes(Dev d, const gs_write *ops,
     d.last_w[(size_t)j * d.KP + k] = (uint8_t)nw;
     *held = (uint8_t)nw;
     d.mv[pj] = ver;
+    // Cluster.set / set_with_ttl emit on_key_change (server.py:193-215, 238-252); delete and
+    // delete_after_ttl mutate the stored VersionedValue in place, so old and new are the same
+    // object and nothing is emitted (server.py:199-203, 211-215)
+    if (d.ev && (op.op == GS_OP_SET || op.op == GS_OP_SET_WITH_TTL))
+        emit_event(d, op.owner, op.owner, k | (EV_KEY << 8), w ? (uint32_t)d.hist[hix(d, j, w, k)] : 0u, ver, t);
     if (d.flags & GS_TOMBSTONES) {
         d.ts[pj * d.KP + k] = st ? t : NONE;
         if (st) d.row[op.owner * 4 + 1] = 1u;
@@ -1976,6 +2001,14 @@ int gs_read_counters(gs_handle *h, gs_counters *out) {
 int gs_reset_counters(gs_handle *h) {
     if (!h || !h->reg[GS_R_COUNTERS]) return GS_E_INVALID;
     HIPCHK(h, hipMemsetAsync(h->reg[GS_R_COUNTERS], 0, h->bytes[GS_R_COUNTERS], h->stream));
+    return GS_OK;
+}
+
+int gs_set_events(gs_handle *h, uint32_t *records, uint32_t capacity, uint32_t *count) {
+    if (!h || (records && !count)) return GS_E_INVALID;
+    h->d.ev = records;
+    h->d.ev_count = records ? count : nullptr;
+    h->d.ev_cap = records ? capacity : 0u;
     return GS_OK;
 }
 

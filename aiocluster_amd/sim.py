@@ -347,6 +347,31 @@ class GossipSim:
     def sync(self):
         self._chk(self.L.gs_sync(self.h), "gs_sync")
 
+    # --------------------------------------------------------------- hook events
+    def enable_events(self, capacity: int = 1 << 20):
+        """gs_set_events: record on_key_change / on_node_join / on_node_leave (see drain_events)."""
+        torch = self.torch
+        self._ev = torch.empty((capacity, 6), dtype=torch.int32, device=self.device)
+        self._ev_count = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self._chk(self.L.gs_set_events(self.h, C.c_void_p(self._ev.data_ptr()), capacity,
+                                       C.c_void_p(self._ev_count.data_ptr())), "gs_set_events")
+
+    def disable_events(self):
+        self._chk(self.L.gs_set_events(self.h, None, 0, None), "gs_set_events")
+        self._ev = self._ev_count = None
+
+    def drain_events(self) -> np.ndarray:
+        """The events since the last drain, uint32 [n, 6] = observer, owner (node index), key | kind << 8,
+        old version (0 = none), new version, tick; sorted.  Raises if the buffer overflowed."""
+        self.sync()
+        n = int(self._ev_count.item())
+        if n > self._ev.shape[0]:
+            raise GsError(f"event buffer overflow: {n} events, capacity {self._ev.shape[0]}")
+        ev = self._ev[:n].cpu().numpy().view(np.uint32)
+        self._ev_count.zero_()
+        order = np.lexsort(ev.T[::-1])
+        return ev[order]
+
     def fd_census(self, up) -> dict:
         """gs_fd_census: live / dead sets of every up observer against the up mask (config 5's
         false-positive rate = up_dead / up_pairs)."""

@@ -230,6 +230,17 @@ int gs_liveness(gs_handle *h, const uint8_t *up, uint32_t tick);
  * returns None). */
 int gs_phi_row(gs_handle *h, uint32_t observer, uint32_t tick, double *out);
 
+/* Batched hook events (Cluster.on_key_change / on_node_join / on_node_leave, server.py:217-257).
+ * When enabled, every kernel that changes what a hook reports appends 6 x u32 records
+ * {observer, owner, key | kind << 8, old version (0 = none), new version, tick} to the DEVICE array
+ * records[capacity][6], counting in the DEVICE u32 *count (records beyond capacity are dropped but
+ * counted; the caller resets *count).  kind 0 = on_key_change: a kv stored by apply_delta
+ * (state.py:228-231) or an owner set / set_with_ttl (owner deletes mutate the stored value in
+ * place and emit nothing, server.py:199-215); 1 = node join, 2 = node leave: the live set of
+ * _update_node_liveness against the previous one (server.py:611-616).  Order is unspecified.
+ * Exchanges between prefix views take the per-key apply path while enabled.  records = NULL: off. */
+int gs_set_events(gs_handle *h, uint32_t *records, uint32_t capacity, uint32_t *count);
+
 /* select_nodes_for_gossip (server.py:656-717) for every up node at round start (server.py:442-469),
  * from its failure detector's live / dead sets and known peers: `fanout` distinct peers uniformly from
  * the live set (all known peers while it is empty), a dead node with probability dead / (live + 1),

@@ -103,7 +103,30 @@ struct orc {
     uint32_t *tmp_from;
     int32_t *tmp_keys;
     orc_stats st;
+    /* hook events (server.py:217-257): {observer, owner, key | kind << 8, old version, new version, now} */
+    int32_t ev_on, ev_n, ev_cap;
+    int64_t *ev;
 };
+
+static void emit(orc *o, int32_t obs, int32_t owner, int32_t kk, uint32_t v_old, uint32_t v_new, int64_t now) {
+    if (!o->ev_on) return;
+    if (o->ev_n == o->ev_cap) {
+        o->ev_cap = o->ev_cap ? 2 * o->ev_cap : 1024;
+        o->ev = realloc(o->ev, sizeof(int64_t) * 6 * (size_t)o->ev_cap);
+        if (!o->ev) abort();
+    }
+    int64_t *r = o->ev + (size_t)o->ev_n * 6;
+    r[0] = obs; r[1] = owner; r[2] = kk; r[3] = v_old; r[4] = v_new; r[5] = now;
+    o->ev_n++;
+}
+
+void orc_enable_events(orc *o, int32_t on) { o->ev_on = on; o->ev_n = 0; }
+int32_t orc_drain_events(orc *o, int64_t *out, int32_t cap) {
+    int32_t n = o->ev_n;
+    if (out) memcpy(out, o->ev, sizeof(int64_t) * 6 * (size_t)(n < cap ? n : cap));
+    o->ev_n = 0;
+    return n;
+}
 
 /* ------------------------------------------------------------ pb sizes */
 static int vlen(uint64_t x) { int n = 1; while (x >= 0x80) { x >>= 7; n++; } return n; }
@@ -262,12 +285,14 @@ void orc_write(orc *o, int32_t owner, int32_t key, int32_t op, uint32_t value_id
     case 0: /* set (state.py:137-142) */
         if (slot->present && slot->value_id == value_id && slot->status == ST_SET) return;
         nv.value_id = value_id; nv.value_len = value_len; nv.version = v->mv + 1; nv.status = ST_SET; nv.ts = now;
+        emit(o, owner, owner, key, slot->present ? slot->version : 0u, nv.version, now); /* server.py:193-197 */
         set_versioned(slot, &v->mv, &nv);
         return;
     case 2: /* set_with_ttl (state.py:144-159) */
         if (slot->present && slot->value_id == value_id && slot->status == ST_DELETE_AFTER_TTL) return;
         nv.value_id = value_id; nv.value_len = value_len; nv.version = v->mv + 1;
         nv.status = ST_DELETE_AFTER_TTL; nv.ts = now;
+        emit(o, owner, owner, key, slot->present ? slot->version : 0u, nv.version, now); /* server.py:205-209 */
         set_versioned(slot, &v->mv, &nv);
         return;
     case 1: /* delete (state.py:161-171): in-place mutation, value cleared */
@@ -533,6 +558,7 @@ static void apply_delta(orc *o, int32_t self, const odelta *dl, int64_t now) {
             okv nv;
             nv.present = 1; nv.status = (uint8_t)u->status; nv.value_len = u->value_len;
             nv.value_id = u->value_id; nv.version = u->version; nv.ts = now;
+            emit(o, self, nd->node, u->key, e->present ? e->version : 0u, u->version, now); /* 228-231 */
             set_versioned(e, &v->mv, &nv);
         }
         if (nd->mv > v->mv) v->mv = nd->mv;                          /* 232-233 */
@@ -569,7 +595,12 @@ int32_t orc_liveness(orc *o, int32_t node, int64_t now) {
     int32_t *snap = xcalloc(cnt, sizeof(int32_t));
     memcpy(snap, b->order, sizeof(int32_t) * cnt);                   /* nodes() is a tuple */
     for (int32_t q = 0; q < cnt; q++)
-        if (snap[q] != node) fd_update(o, b, snap[q], now);
+        if (snap[q] != node) {
+            const int32_t j = snap[q];
+            const int was = b->live[j];
+            fd_update(o, b, j, now);
+            if (b->live[j] != was) emit(o, node, j, (b->live[j] ? 1 : 2) << 8, 0u, 0u, now); /* 611-616 */
+        }
     free(snap);
     /* FailureDetector.garbage_collect (108-119) */
     int32_t *res = xcalloc(b->ndead + 1, sizeof(int32_t));

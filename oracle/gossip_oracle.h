@@ -85,6 +85,10 @@ int32_t orc_fd_phi(const orc *o, int32_t obs, int32_t target, int64_t now_us, do
 int32_t orc_fd_live(const orc *o, int32_t obs, int32_t target);
 int64_t orc_fd_dead_since(const orc *o, int32_t obs, int32_t target);
 void    orc_get_stats(const orc *o, orc_stats *out);
+/* hook events (Cluster.on_key_change / on_node_join / on_node_leave): records of 6 int64
+ * {observer, owner, key | kind << 8, old version, new version, now_us}, kind 0/1/2 = key/join/leave */
+void    orc_enable_events(orc *o, int32_t on);
+int32_t orc_drain_events(orc *o, int64_t *out, int32_t cap);
 /* Bulk export of one observer row (arrays sized N, or N*K for per-key fields):
  * present[j] = dict position or -1; per-key version/status/value_id/ts (version 0 = absent);
  * FD: window last (-1 = no window), len, sum; live flag; time of death (-1 = not dead). */

@@ -75,6 +75,8 @@ def lib():
             "orc_fd_live": (i32, [P, i32, i32]),
             "orc_fd_dead_since": (i64, [P, i32, i32]),
             "orc_get_stats": (None, [P, C.POINTER(_Stats)]),
+            "orc_enable_events": (None, [P, i32]),
+            "orc_drain_events": (i32, [P, P, i32]),
             "orc_export_row": (None, [P, i32] + [P] * 13),
             "orc_load_row": (None, [P, i32, i32, P, P, P, P, P, i32, P, P, P, P, P, P, P, P, i64]),
             "orc_snapshot_row": (None, [P, i32]),
@@ -186,6 +188,19 @@ class OracleSim:
                 q = self.L.orc_liveness(self.h, o, t * TICK_US)
                 if q >= 0:
                     self.q9_events.append([r, o, q])
+
+    def enable_events(self):
+        self.L.orc_enable_events(self.h, 1)
+
+    def drain_events(self) -> np.ndarray:
+        """Events since the last drain in the device's format (times in ticks), sorted."""
+        buf = np.zeros((1 << 22, 6), dtype=np.int64)
+        n = self.L.orc_drain_events(self.h, buf.ctypes.data_as(C.c_void_p), buf.shape[0])
+        assert n <= buf.shape[0]
+        ev = buf[:n].copy()
+        ev[:, 5] //= TICK_US
+        ev = ev.astype(np.uint32)
+        return ev[np.lexsort(ev.T[::-1])]
 
     def stats(self) -> dict:
         s = _Stats()
