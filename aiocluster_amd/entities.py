@@ -135,3 +135,14 @@ class NodeState:
 
     def digest(self) -> NodeDigest:
         return NodeDigest(self.node, self.heartbeat, self.last_gc_version, self.max_version)
+
+
+@dataclass(frozen=True, slots=True)
+class ClusterSnapshot:
+    """``aiocluster/server.py:65-71`` (``Cluster.snapshot``, ``server.py:168-175``)."""
+
+    cluster_id: str
+    self_node_id: NodeId
+    node_states: dict[NodeId, NodeState]
+    live_nodes: list[NodeId]
+    dead_nodes: list[NodeId]

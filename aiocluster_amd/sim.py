@@ -35,7 +35,7 @@ import numpy as np
 
 from . import _lib
 from ._lib import GS_CANONICAL, GS_FD_RING, GS_NO_HELD, GS_NONE, GS_TOMBSTONES, REGION, TICK_US, GsError
-from .entities import NodeId, NodeState, VersionedValue, VersionStatusEnum
+from .entities import ClusterSnapshot, NodeId, NodeState, VersionedValue, VersionStatusEnum
 from .pbsize import nodeid_size
 
 OPS = {"set": 0, "delete": 1, "set_with_ttl": 2, "delete_after_ttl": 3}
@@ -543,6 +543,57 @@ class GossipSim:
         }
         return NodeState(self.node_ids[owner], int(g["HB"][observer, owner]), kvs, int(g["MV"][observer, owner]),
                          int(g["GC"][observer, owner]))
+
+    def snapshot(self, observer: int, cluster_id: str = "default") -> ClusterSnapshot:
+        """``Cluster.snapshot`` of node ``observer`` (server.py:168-175), read from its rows only: its
+        dict in insertion order, each NodeState with its key-values, the failure detector's live and
+        dead nodes (live in target order; dead in time-of-death order, as the reference's dict)."""
+        self._whole()
+        torch, n, K, KP, Cc = self.torch, self.n, self.k, self.kp, self.hist_cap
+        o = int(observer)
+        self.materialize_held(o, o + 1)
+        self.sync()
+
+        def row(name, dt=torch.int32):
+            return self.region(name, dt, (n, self.np_))[o, :n].cpu().numpy()
+
+        hb = row("HB").view(np.uint32)
+        mv = row("MV").view(np.uint32) & np.uint32(0x7FFFFFFF)
+        gc = row("GC").view(np.uint32) if "GC" in self.regions else np.zeros(n, np.uint32)
+        st = row("FD_STATE").view(np.uint32)
+        if "HELD" in self.regions:
+            held = self.region("HELD", torch.uint8, (n, self.np_, KP))[o, :n, :K].cpu().numpy()
+        else:  # GS_NO_HELD: every view is S_j(max_version)
+            held = self._host()["HELD"][o, :n, :K]
+        ts = self.region("TS", torch.int32, (n, self.np_, KP))[o, :n, :K].cpu().numpy().view(np.uint32) \
+            if "TS" in self.regions else None
+        hist = self.region("HIST", torch.int64, (n, Cc, K)).cpu().numpy().view(np.uint64)
+        hvid = self.region("HIST_VID", torch.int32, (n, Cc, K)).cpu().numpy().view(np.uint32)
+        if self.canonical:
+            order = range(n)
+        else:
+            cnt = int(self.region("ROW", torch.int32, (n, 4))[o, 0].item())
+            order = [int(x) for x in self.region("ORD", torch.int32, (n, self.np_))[o, :cnt].cpu().numpy()]
+        states = {}
+        for j in order:
+            kvs = {}
+            for k in range(K):
+                w = int(held[j, k])
+                if not w:
+                    continue
+                e = int(hist[j, w, k])
+                status = VersionStatusEnum((e >> 48) & 3)
+                kvs[self.keys[k]] = VersionedValue(self.values[int(hvid[j, w, k])], e & 0xFFFFFFFF, status,
+                                                   int(ts[j, k]) if (status and ts is not None) else None)
+            states[self.node_ids[j]] = NodeState(self.node_ids[j], int(hb[j]), kvs, int(mv[j]), int(gc[j]))
+        live = [self.node_ids[j] for j in np.flatnonzero(st == 1)]
+        dead_j = np.flatnonzero(st >= 2)
+        if self.canonical:
+            dead_j = sorted(dead_j.tolist(), key=lambda j: (int(st[j]), j))
+        else:
+            pos = row("POS").view(np.uint32)
+            dead_j = sorted(dead_j.tolist(), key=lambda j: (int(st[j]), int(pos[j])))
+        return ClusterSnapshot(cluster_id, self.node_ids[o], states, live, [self.node_ids[j] for j in dead_j])
 
     def live_nodes(self, observer: int) -> list[NodeId]:
         self._whole()

@@ -197,3 +197,26 @@ def test_version_only_layout_vs_oracle_and_refuses_holes():
     sim = make_backend(GossipSim, scen2, tombstones=False, held=False, fd_ring=False)
     with pytest.raises(GsError, match="err_holes"):
         replay(sim, scen2, on_round=lambda r: sim.check())
+
+
+@pytest.mark.parametrize("name", ["trunc8", "fdgc12", "warm128"])
+def test_snapshot_matches_reference_golden(name):
+    """Cluster.snapshot (server.py:168-175) of every node, read from its device rows, against the
+    reference's states after the last round."""
+    scen = load_scenario(name)
+    exp = scen["expect"]
+    sim = make_backend(GossipSim, scen)
+    replay(sim, scen)
+    last = exp["states"][-1] if exp["states"] else exp["final"]
+    idx = {nid: j for j, nid in enumerate(sim.node_ids)}
+    for o in range(scen["n"]):
+        snap = sim.snapshot(o)
+        assert snap.self_node_id == sim.node_ids[o]
+        nodes = []
+        for nid, ns in snap.node_states.items():
+            kvs = sorted([k, v.value, v.version, int(v.status), v.status_change_ts]
+                         for k, v in ns.key_values.items())
+            nodes.append([idx[nid], ns.heartbeat, ns.max_version, ns.last_gc_version, kvs])
+        assert nodes == last[o]["nodes"], (o, nodes[:3], last[o]["nodes"][:3])
+        assert sorted(idx[x] for x in snap.live_nodes) == last[o]["live"]
+        assert sorted(idx[x] for x in snap.dead_nodes) == [d[0] for d in last[o]["dead"]]
