@@ -25,7 +25,7 @@ GS_TOMBSTONES = 2
 GS_FD_RING = 4
 GS_NO_HELD = 8
 GS_NONE = 0xFFFFFFFF
-GS_MV_INEXACT = 0x80000000
+GS_MV_INEXACT = 0x8000
 TICK_US = 15_625
 
 
@@ -69,7 +69,7 @@ EXPORTS = [
     "gs_select_peers", "gs_schedule_phases", "gs_set_events",
 ]
 
-API_VERSION = 4
+API_VERSION = 5
 
 
 class GsConfig(C.Structure):

@@ -65,7 +65,8 @@ struct Dev {
     uint32_t max_iv, tomb_grace, dead_grace, sched_delay, lb_min, sum_bits;
     uint32_t ablate;  // profiling only (env GS_ABLATE): 1 = skip packing, 2 = skip pass-1 stores; results invalid
     double phi_thr, prior5;
-    uint32_t *hb, *mv, *gc;
+    uint32_t *hb, *gc;
+    uint16_t *mv;  // max_version | MV_INEXACT (u16: versions <= K * (C - 1) <= 16,256)
     uint8_t *held;
     uint64_t *fd;  // sampling window: (last tick + 1) | (sum | cnt << sum_bits) << 32; 0 = no window
     uint32_t *fd_state, *ts;
@@ -202,8 +203,8 @@ __device__ inline void set_byte(uint32_t *w, int q, uint32_t v) {
 // one from a view with holes, so its held ordinals follow from the owner's write
 // history and GS_R_HELD is not read (nor kept) for it.  Exchanges between two such views need
 // only their max_versions and the owner's latest-write table (a hot 16-entry row per owner).
-constexpr uint32_t MV_INEXACT = 0x80000000u;
-constexpr uint32_t MV_MASK = 0x7FFFFFFFu;
+constexpr uint32_t MV_INEXACT = GS_MV_INEXACT;
+constexpr uint32_t MV_MASK = GS_MV_INEXACT - 1u;
 
 // held ordinals of S_j(M) (local owner column j): start from the owner's latest write of each key
 // and step back while the write is newer than M (versions of one key increase with the ordinal)
@@ -337,7 +338,7 @@ __device__ __forceinline__ void apply_cand(const Dev &d, uint32_t r, const Cand<
         // prefix sender, prefix receiver, whole NodeDelta: the view becomes S_j(max(mr, ms)) (keys
         // above mr move to the sender's latest write <= ms, the others already are), still a prefix.
         // ms <= mr happens when the receiver's digest left j out (scheduled for deletion: from = 0)
-        d.mv[pr] = c.ms > c.mr ? c.ms : c.mr;
+        d.mv[pr] = (uint16_t)(c.ms > c.mr ? c.ms : c.mr);
         alg += 4;
         return;
     }
@@ -399,14 +400,14 @@ __device__ __forceinline__ void apply_cand(const Dev &d, uint32_t r, const Cand<
     const bool keep_held = tt || (mvw & MV_INEXACT);  // a prefix view's HELD is not kept
     if (keep_held && !d.held) {  // GS_NO_HELD: a view with holes cannot be represented
         shard_add(d, C_E_HOLES, 1);
-        d.mv[pr] = mvw;
+        d.mv[pr] = (uint16_t)mvw;
         return;
     }
     uint32_t *hrp = reinterpret_cast<uint32_t *>(d.held + pr * d.KP);
 #pragma unroll
     for (int q = 0; q < KW; q++)
         if (keep_held && (hr[q] != hr0[q] || c.rx)) { hrp[q] = hr[q]; alg += 4; }
-    d.mv[pr] = mvw;
+    d.mv[pr] = (uint16_t)mvw;
     if (g != c.gr) d.gc[pr] = g;
     alg += 8;
 }
@@ -602,6 +603,10 @@ __device__ __forceinline__ void ld4(const uint32_t *p, uint32_t (&v)[4]) {
     const uint4 x = *reinterpret_cast<const uint4 *>(p);
     v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
 }
+__device__ __forceinline__ void ld4h(const uint16_t *p, uint32_t (&v)[4]) {
+    const uint2 x = *reinterpret_cast<const uint2 *>(p);
+    v[0] = x.x & 0xFFFFu; v[1] = x.x >> 16; v[2] = x.y & 0xFFFFu; v[3] = x.y >> 16;
+}
 __device__ __forceinline__ void st4(uint32_t *p, const uint32_t (&v)[4]) {
     *reinterpret_cast<uint4 *>(p) = make_uint4(v[0], v[1], v[2], v[3]);
 }
@@ -618,8 +623,8 @@ __device__ __forceinline__ void load_grp(const Dev &d, size_t ra, size_t rb, uin
                                          Grp &g) {
     ld4(d.hb + ra + c0, g.hA);
     ld4(d.hb + rb + c0, g.hB);
-    ld4(d.mv + ra + c0, g.mA);
-    ld4(d.mv + rb + c0, g.mB);
+    ld4h(d.mv + ra + c0, g.mA);
+    ld4h(d.mv + rb + c0, g.mB);
 #pragma unroll
     for (int i = 0; i < 4; i++) { g.mA[i] &= MV_MASK; g.mB[i] &= MV_MASK; }  // drop the prefix-view flag
 #pragma unroll
@@ -1297,7 +1302,7 @@ __global__ __launch_bounds__(LB) void k_owner_writes(Dev d, const gs_write *ops,
     if (d.lat) d.lat[(size_t)j * d.KP + k] = d.hist[h];
     d.last_w[(size_t)j * d.KP + k] = (uint8_t)nw;
     *held = (uint8_t)nw;
-    d.mv[pj] = ver;
+    d.mv[pj] = (uint16_t)ver;
     // Cluster.set / set_with_ttl emit on_key_change (server.py:193-215, 238-252); delete and
     // delete_after_ttl mutate the stored VersionedValue in place, so old and new are the same
     // object and nothing is emitted (server.py:199-203, 211-215)
@@ -1645,7 +1650,7 @@ int check_bound(gs_handle *h) {
         if (h->bytes[r] && !h->reg[r]) return fail(h, GS_E_UNBOUND, "region %d not bound", r);
     Dev &d = h->d;
     d.hb = (uint32_t *)h->reg[GS_R_HB];
-    d.mv = (uint32_t *)h->reg[GS_R_MV];
+    d.mv = (uint16_t *)h->reg[GS_R_MV];
     d.gc = (uint32_t *)h->reg[GS_R_GC];
     d.held = (uint8_t *)h->reg[GS_R_HELD];
     d.fd = (uint64_t *)h->reg[GS_R_FD];
@@ -1749,7 +1754,8 @@ int gs_create(const gs_config *cfg, gs_handle **out) {
     const uint64_t pairs = N * NP;
     const bool genm = !(c.flags & GS_CANONICAL);
     uint64_t *b = h->bytes;
-    b[GS_R_HB] = b[GS_R_MV] = pairs * 4;
+    b[GS_R_HB] = pairs * 4;
+    b[GS_R_MV] = pairs * 2;
     b[GS_R_GC] = (c.flags & GS_TOMBSTONES) ? pairs * 4 : 0;  // last_gc_version stays 0 without tombstone GC
     b[GS_R_HELD] = (c.flags & GS_NO_HELD) ? 0 : pairs * KP;
     b[GS_R_FD] = pairs * 8;

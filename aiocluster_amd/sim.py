@@ -387,8 +387,13 @@ class GossipSim:
 
     def inexact_views(self) -> int:
         """Views with holes (GS_MV_INEXACT set): those whose HELD row the exchange kernel keeps."""
-        mv = self.region("MV", self.torch.int32, (self.n, self.np_))[:, : self.ncol]
+        mv = self.region("MV", self.torch.int16, (self.n, self.np_))[:, : self.ncol]
         return int((mv < 0).sum().item())
+
+    def max_versions(self):
+        """Device int32 [N, NP] NodeState.max_version of every view (GS_R_MV is u16 | GS_MV_INEXACT)."""
+        mv = self.region("MV", self.torch.int16, (self.n, self.np_))
+        return mv.to(self.torch.int32) & 0x7FFF
 
     # --------------------------------------------------------------- readback
     def _host(self):
@@ -397,11 +402,12 @@ class GossipSim:
         self.materialize_held()
         self.sync()
         g = {}
-        for name in ("HB", "MV", "GC", "FD_STATE"):
+        for name in ("HB", "GC", "FD_STATE"):
             if name in self.regions:
                 g[name] = self.region(name, torch.int32, (n, NP)).cpu().numpy().view(np.uint32)
-        g["MV_INEXACT"] = (g["MV"] >> np.uint32(31)).astype(np.uint8)  # prefix-view flag (GS_MV_INEXACT)
-        g["MV"] = g["MV"] & np.uint32(0x7FFFFFFF)
+        mv = self.region("MV", torch.int16, (n, NP)).cpu().numpy().view(np.uint16).astype(np.uint32)
+        g["MV_INEXACT"] = (mv >> np.uint32(15)).astype(np.uint8)  # prefix-view flag (GS_MV_INEXACT)
+        g["MV"] = mv & np.uint32(0x7FFF)
         if "GC" not in g:  # no tombstone GC: last_gc_version is 0 everywhere
             g["GC"] = np.zeros((n, NP), dtype=np.uint32)
         g["FD_LAST"], g["FD_SUM"], g["FD_CNT"] = self.unpack_fd(self.region("FD", torch.int64, (n, NP)).cpu().numpy())
@@ -558,7 +564,7 @@ class GossipSim:
             return self.region(name, dt, (n, self.np_))[o, :n].cpu().numpy()
 
         hb = row("HB").view(np.uint32)
-        mv = row("MV").view(np.uint32) & np.uint32(0x7FFFFFFF)
+        mv = row("MV", torch.int16).view(np.uint16).astype(np.uint32) & np.uint32(0x7FFF)
         gc = row("GC").view(np.uint32) if "GC" in self.regions else np.zeros(n, np.uint32)
         st = row("FD_STATE").view(np.uint32)
         if "HELD" in self.regions:

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define GS_API_VERSION 4
+#define GS_API_VERSION 5
 #define GS_TICK_US 15625u
 #define GS_NONE 0xFFFFFFFFu
 
@@ -80,7 +80,8 @@ typedef struct gs_config {
  * slice col_lo = 0 and n_cols = n_nodes. */
 enum gs_region {
     GS_R_HB = 0,      /* u32 [N][NP]   NodeState.heartbeat of owner j as seen by observer o */
-    GS_R_MV,          /* u32 [N][NP]   NodeState.max_version (| GS_MV_INEXACT, see below) */
+    GS_R_MV,          /* u16 [N][NP]   NodeState.max_version (| GS_MV_INEXACT, see below); versions are
+                                        bounded by K * (C - 1) <= 16,256, so 15 bits always suffice */
     GS_R_GC,          /* u32 [N][NP]   NodeState.last_gc_version (GS_TOMBSTONES only: without tombstone GC
                                         it is 0 everywhere, and deletes / TTL writes are refused) */
     GS_R_HELD,        /* u8  [N][NP][KP] write ordinal of each key held (0 = absent), KP = K rounded to 4;
@@ -117,13 +118,13 @@ enum gs_region {
     GS_NUM_REGIONS
 };
 
-/* Prefix views (no GS_TOMBSTONES: no deletes, no tombstone GC).  Bit 31 of a GS_R_MV word
+/* Prefix views (no GS_TOMBSTONES: no deletes, no tombstone GC).  Bit 15 of a GS_R_MV word
  * (GS_MV_INEXACT) is set iff the view is NOT S_j(max_version) = owner j's latest write of every
  * key with version <= max_version, i.e. iff it has holes (a truncated NodeDelta, or a delta
  * from a view with holes).  GS_R_HELD is kept only for those views; the others
  * follow from the owner's history (gs_materialize_held writes them out for readers).  With
- * GS_TOMBSTONES bit 31 is always 0 and GS_R_HELD always kept. */
-#define GS_MV_INEXACT 0x80000000u
+ * GS_TOMBSTONES bit 15 is always 0 and GS_R_HELD always kept. */
+#define GS_MV_INEXACT 0x8000u
 
 typedef struct gs_counters {
     uint64_t exchanges;     /* exchanges executed */

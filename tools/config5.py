@@ -93,7 +93,7 @@ def main():
         print(f"r{r:3d} {stage:9s} {dt * 1e3:7.1f} ms  fp {fp:.4f}  nd {d['node_deltas']}  trunc {d['truncated']}"
               f"  tombgc {d['tomb_gc']}", file=sys.stderr, flush=True)
     # version-matrix convergence: every observer's max_version of every owner = the owner's own
-    mv = sim.region("MV", torch.int32, (n, sim.np_))[:, :n]
+    mv = sim.max_versions()[:, :n]
     own = torch.diagonal(mv).clone()
     lag_views = int((mv != own[None, :]).sum().item())
     part = [x for x in per_round if x["stage"] == "partition"]
