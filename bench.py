@@ -260,6 +260,10 @@ def main():
     ap.add_argument("--keys", type=int, default=16)
     ap.add_argument("--fanout", type=int, default=3)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--settle", type=int, default=20,
+                    help="untimed rounds run as part of setup, before the warmup: the warm start has every view "
+                         "equal to its owner, and the heartbeat / version lags reach their steady-state spread "
+                         "only after ~15 rounds (SURVEY 8(d): time 20+ rounds after warm-up)")
     ap.add_argument("--cpu-sample", type=int, default=64)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -329,7 +333,8 @@ def main():
     else:
         sims = [GossipSim(ids, key_names(K), cfg, **kw)]
     sim = sims[0]
-    plans = prepare(sim, spec, args.warmup + args.steps + 1, torch, dev)
+    R0 = args.settle + args.warmup  # first timed round
+    plans = prepare(sim, spec, R0 + args.steps + 1, torch, dev)
     sel = None
     if args.peer_select:
         from aiocluster_amd.peers import PeerSelector
@@ -340,7 +345,12 @@ def main():
     torch.cuda.synchronize(dev)
     log(f"setup {time.perf_counter() - t_setup:.1f}s")
 
-    for r in range(args.warmup):
+    for r in range(args.settle):
+        ts = time.perf_counter()
+        run_round(sims, plans[r], group=group, sel=sel)
+        torch.cuda.synchronize(dev)
+        log(f"settle round {r}: {(time.perf_counter() - ts) * 1e3:.1f} ms, {plans[r]['exchanges']} exchanges")
+    for r in range(args.settle, R0):
         run_round(sims, plans[r], group=group, sel=sel)
     torch.cuda.synchronize(dev)
     for s_ in sims:
@@ -351,7 +361,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for r in range(args.warmup, args.warmup + args.steps):
+    for r in range(R0, R0 + args.steps):
         run_round(sims, plans[r], events, group, sel)
     torch.cuda.synchronize(dev)
     if dist is not None:
@@ -360,7 +370,7 @@ def main():
     local = [s_.check() for s_ in sims]
     inexact = sum(s_.inexact_views() for s_ in sims)  # views with holes (HELD kept), GS_MV_INEXACT
     c = group.comm.sum_counters(local) if group is not None else local[0]
-    exch = sum(plans[r]["exchanges"] for r in range(args.warmup, args.warmup + args.steps))
+    exch = sum(plans[r]["exchanges"] for r in range(R0, R0 + args.steps))
     assert c["exchanges"] == exch, (c["exchanges"], exch)
     kern_ms = sum(e0.elapsed_time(e1) for e0, e1 in events)
     launches = len(events)
@@ -378,7 +388,7 @@ def main():
     traffic = load_traffic(workload, exch / max(1, len(events))) if group is None else None
     cpu = None
     if rank == 0 and group is None and not args.no_cpu_baseline:
-        cpu = cpu_baseline(sim, spec, cfg, plans[args.warmup + args.steps], args.cpu_sample, args.cpu_seconds)
+        cpu = cpu_baseline(sim, spec, cfg, plans[R0 + args.steps], args.cpu_sample, args.cpu_seconds)
     if rank == 0:
         line = {
             "metric": ("REHEARSAL (one GPU's slice of a %d-GPU run, packing not the cluster's): exchanges/s"
