@@ -50,6 +50,7 @@ def fd_sum_bits(window: int) -> int:
 REGIONS = [
     "HB", "MV", "GC", "HELD", "FD", "FD_STATE", "TS", "RING", "POS", "ORD", "ROW",
     "LAST_W", "HIST", "HIST_VID", "NID_SIZE", "KEY_LEN", "STAMP", "COUNTERS", "SLICE_BITS", "PEND", "PEND_STAMP", "LATEST",
+    "SELF_HB",
 ]
 REGION = {n: i for i, n in enumerate(REGIONS)}
 
@@ -69,7 +70,7 @@ EXPORTS = [
     "gs_select_peers", "gs_schedule_phases", "gs_set_events",
 ]
 
-API_VERSION = 5
+API_VERSION = 6
 
 
 class GsConfig(C.Structure):

@@ -65,7 +65,9 @@ struct Dev {
     uint32_t max_iv, tomb_grace, dead_grace, sched_delay, lb_min, sum_bits;
     uint32_t ablate;  // profiling only (env GS_ABLATE): 1 = skip packing, 2 = skip pass-1 stores; results invalid
     double phi_thr, prior5;
-    uint32_t *hb, *gc;
+    uint16_t *hb;       // heartbeat mod 2^16 (hb_dec: exact while a view lags its owner by < 2^16)
+    uint32_t *self_hb;  // [NP] each owner column's own heartbeat, full width
+    uint32_t *gc;
     uint16_t *mv;  // max_version | MV_INEXACT (u16: versions <= K * (C - 1) <= 16,256)
     uint8_t *held;
     uint64_t *fd;  // sampling window: (last tick + 1) | (sum | cnt << sum_bits) << 32; 0 = no window
@@ -603,6 +605,12 @@ __device__ __forceinline__ void ld4(const uint32_t *p, uint32_t (&v)[4]) {
     const uint4 x = *reinterpret_cast<const uint4 *>(p);
     v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
 }
+// Heartbeats are stored mod 2^16 and decoded against the owner's own heartbeat R (every view of
+// owner j is <= R, and views lag R by < 2^16: DESIGN.md §3), so H = R - ((R - s) mod 2^16).
+__device__ __forceinline__ uint32_t hb_dec(uint32_t s, uint32_t R) { return R - ((R - s) & 0xFFFFu); }
+__device__ __forceinline__ void st4h(uint16_t *p, const uint32_t (&v)[4]) {
+    *reinterpret_cast<uint2 *>(p) = make_uint2((v[0] & 0xFFFFu) | (v[1] << 16), (v[2] & 0xFFFFu) | (v[3] << 16));
+}
 __device__ __forceinline__ void ld4h(const uint16_t *p, uint32_t (&v)[4]) {
     const uint2 x = *reinterpret_cast<const uint2 *>(p);
     v[0] = x.x & 0xFFFFu; v[1] = x.x >> 16; v[2] = x.y & 0xFFFFu; v[3] = x.y >> 16;
@@ -621,8 +629,12 @@ __device__ __forceinline__ void st4w(uint64_t *p, const uint64_t (&v)[4]) {
 template <bool GENM>
 __device__ __forceinline__ void load_grp(const Dev &d, size_t ra, size_t rb, uint32_t c0, bool schA, bool schB,
                                          Grp &g) {
-    ld4(d.hb + ra + c0, g.hA);
-    ld4(d.hb + rb + c0, g.hB);
+    uint32_t R[4];
+    ld4(d.self_hb + c0, R);
+    ld4h(d.hb + ra + c0, g.hA);
+    ld4h(d.hb + rb + c0, g.hB);
+#pragma unroll
+    for (int i = 0; i < 4; i++) { g.hA[i] = hb_dec(g.hA[i], R[i]); g.hB[i] = hb_dec(g.hB[i], R[i]); }
     ld4h(d.mv + ra + c0, g.mA);
     ld4h(d.mv + rb + c0, g.mB);
 #pragma unroll
@@ -675,7 +687,7 @@ __device__ __forceinline__ void pass1_grp(const Dev &d, size_t ra, size_t rb, ui
                                           uint32_t &hbw, bool &anynew, uint32_t &rmA, uint32_t &rmB) {
     bool dA = false, dB = false;
     rmA = rmB = 0u;
-    alg += 64 + (GENM ? 32 : 0) + (schA ? 16 : 0) + (schB ? 16 : 0);
+    alg += 48 + (GENM ? 32 : 0) + (schA ? 16 : 0) + (schB ? 16 : 0);
 #pragma unroll
     for (int i = 0; i < 4; i++) {
         const uint32_t j = c0 + i, jg = d.col_lo + j;  // local column, node id
@@ -686,7 +698,7 @@ __device__ __forceinline__ void pass1_grp(const Dev &d, size_t ra, size_t rb, ui
             const bool sb = schB && pb && is_sched(g.fB[i], t, d.sched_delay);
             const bool inA = pa && !sa;  // j is in a's digest (compute_digest, state.py:324-331)
             uint32_t hA = g.hA[i], hB = g.hB[i];
-            if (jg == b) { hB += 1u; dB = true; hbw++; }  // responder inc_heartbeat (server.py:524)
+            if (jg == b) { hB += 1u; dB = true; hbw++; d.self_hb[j] = hB; }  // responder inc_heartbeat (server.py:524)
             bool newB = false, repB = false;
             if (inA && jg != b) {  // b: _report_heartbeat over a's digest (server.py:336-337, 599-604)
                 if (!pb) { newB = true; hB = hA; dB = true; hbw++; }
@@ -716,8 +728,8 @@ __device__ __forceinline__ void pass1_grp(const Dev &d, size_t ra, size_t rb, ui
     }
     // only changed 16/32-byte groups are written back (writing whole lines measured slower: r1c vs r1b)
     if (d.ablate & 2u) return;
-    if (dA) { st4(d.hb + ra + c0, g.hA); alg += 16; }
-    if (dB) { st4(d.hb + rb + c0, g.hB); alg += 16; }
+    if (dA) { st4h(d.hb + ra + c0, g.hA); alg += 8; }
+    if (dB) { st4h(d.hb + rb + c0, g.hB); alg += 8; }
 }
 
 // The four ballots of one group step are this wave's 32-byte block of the phase's bit plane
@@ -968,7 +980,11 @@ __global__ __launch_bounds__(XB) void k_pack_slice(Dev d, const int32_t *ini, co
 __global__ __launch_bounds__(LB) void k_begin_round(Dev d, const uint8_t *up, uint32_t t) {
     const uint32_t o = blockIdx.x;
     if (o >= d.N || !up[o]) return;
-    if (threadIdx.x == 0 && o - d.col_lo < d.ncol) d.hb[pix(d, o, o - d.col_lo)] += 1u;
+    if (threadIdx.x == 0 && o - d.col_lo < d.ncol) {
+        const uint32_t R = d.self_hb[o - d.col_lo] + 1u;
+        d.self_hb[o - d.col_lo] = R;
+        d.hb[pix(d, o, o - d.col_lo)] = (uint16_t)R;
+    }
     if (!(d.flags & GS_TOMBSTONES) || !d.row[o * 4 + 1]) return;
     const bool genm = !(d.flags & GS_CANONICAL);
     bool remaining = false;
@@ -1325,6 +1341,7 @@ __global__ __launch_bounds__(LB) void k_boot_self(Dev d) {
     if (o - d.col_lo >= d.ncol) return;
     const size_t p = pix(d, o, o - d.col_lo);
     d.hb[p] = 1u;  // Cluster.__init__: inc_heartbeat (server.py:95-96)
+    d.self_hb[o - d.col_lo] = 1u;
     if (!(d.flags & GS_CANONICAL)) {
         d.pos[p] = 0u;
         d.ord[(size_t)o * d.NP] = o;
@@ -1649,7 +1666,8 @@ int check_bound(gs_handle *h) {
     for (int r = 0; r < GS_NUM_REGIONS; r++)
         if (h->bytes[r] && !h->reg[r]) return fail(h, GS_E_UNBOUND, "region %d not bound", r);
     Dev &d = h->d;
-    d.hb = (uint32_t *)h->reg[GS_R_HB];
+    d.hb = (uint16_t *)h->reg[GS_R_HB];
+    d.self_hb = (uint32_t *)h->reg[GS_R_SELF_HB];
     d.mv = (uint16_t *)h->reg[GS_R_MV];
     d.gc = (uint32_t *)h->reg[GS_R_GC];
     d.held = (uint8_t *)h->reg[GS_R_HELD];
@@ -1754,7 +1772,8 @@ int gs_create(const gs_config *cfg, gs_handle **out) {
     const uint64_t pairs = N * NP;
     const bool genm = !(c.flags & GS_CANONICAL);
     uint64_t *b = h->bytes;
-    b[GS_R_HB] = pairs * 4;
+    b[GS_R_HB] = pairs * 2;
+    b[GS_R_SELF_HB] = NP * 4;
     b[GS_R_MV] = pairs * 2;
     b[GS_R_GC] = (c.flags & GS_TOMBSTONES) ? pairs * 4 : 0;  // last_gc_version stays 0 without tombstone GC
     b[GS_R_HELD] = (c.flags & GS_NO_HELD) ? 0 : pairs * KP;
@@ -1831,7 +1850,7 @@ int gs_boot(gs_handle *h, const uint16_t *nid_size, const uint8_t *key_len) {
     if (rc) return rc;
     hipStream_t s = h->stream;
     // regions that start at zero
-    const int zero[] = {GS_R_HB, GS_R_MV, GS_R_GC, GS_R_HELD, GS_R_FD, GS_R_FD_STATE,
+    const int zero[] = {GS_R_HB, GS_R_SELF_HB, GS_R_MV, GS_R_GC, GS_R_HELD, GS_R_FD, GS_R_FD_STATE,
                         GS_R_RING, GS_R_ROW, GS_R_LAST_W, GS_R_HIST, GS_R_HIST_VID,
                         GS_R_STAMP, GS_R_COUNTERS, GS_R_SLICE_BITS, GS_R_PEND, GS_R_PEND_STAMP, GS_R_LATEST};
     for (int r : zero)

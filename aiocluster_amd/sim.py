@@ -390,6 +390,13 @@ class GossipSim:
         mv = self.region("MV", self.torch.int16, (self.n, self.np_))[:, : self.ncol]
         return int((mv < 0).sum().item())
 
+    def decode_heartbeats(self, hb16: np.ndarray) -> np.ndarray:
+        """NodeState.heartbeat of host rows of GS_R_HB (u16, any leading shape [..., NP]): the stored
+        value is the heartbeat mod 2^16, decoded against the owner's own heartbeat R (GS_R_SELF_HB)."""
+        R = self.region("SELF_HB", self.torch.int32, (self.np_,)).cpu().numpy().view(np.uint32)
+        s = np.asarray(hb16).view(np.uint16).astype(np.uint32)
+        return (R - ((R - s) & np.uint32(0xFFFF))).astype(np.uint32)
+
     def max_versions(self):
         """Device int32 [N, NP] NodeState.max_version of every view (GS_R_MV is u16 | GS_MV_INEXACT)."""
         mv = self.region("MV", self.torch.int16, (self.n, self.np_))
@@ -402,7 +409,8 @@ class GossipSim:
         self.materialize_held()
         self.sync()
         g = {}
-        for name in ("HB", "GC", "FD_STATE"):
+        g["HB"] = self.decode_heartbeats(self.region("HB", torch.int16, (n, NP)).cpu().numpy())
+        for name in ("GC", "FD_STATE"):
             if name in self.regions:
                 g[name] = self.region(name, torch.int32, (n, NP)).cpu().numpy().view(np.uint32)
         mv = self.region("MV", torch.int16, (n, NP)).cpu().numpy().view(np.uint16).astype(np.uint32)
@@ -563,7 +571,7 @@ class GossipSim:
         def row(name, dt=torch.int32):
             return self.region(name, dt, (n, self.np_))[o, :n].cpu().numpy()
 
-        hb = row("HB").view(np.uint32)
+        hb = self.decode_heartbeats(self.region("HB", torch.int16, (n, self.np_))[o].cpu().numpy())[:n]
         mv = row("MV", torch.int16).view(np.uint16).astype(np.uint32) & np.uint32(0x7FFF)
         gc = row("GC").view(np.uint32) if "GC" in self.regions else np.zeros(n, np.uint32)
         st = row("FD_STATE").view(np.uint32)

@@ -154,7 +154,8 @@ def cpu_baseline(sim, spec, cfg, next_plan, sample: int, min_seconds: float = 10
     for a, b in pairs:  # prefix views keep no HELD row on the device: write them out for these rows
         sim.materialize_held(a, a + 1)
         sim.materialize_held(b, b + 1)
-    hb, fst = (rows(x, torch.int32, (n, NP)) for x in ("HB", "FD_STATE"))
+    hb16 = rows("HB", torch.int16, (n, NP))  # heartbeat mod 2^16 (decoded per row below)
+    fst = rows("FD_STATE", torch.int32, (n, NP))
     mv16 = rows("MV", torch.int16, (n, NP))  # u16 max_version | GS_MV_INEXACT
     gc = rows("GC", torch.int32, (n, NP)) if "GC" in sim.regions else torch.zeros((n, NP), dtype=torch.int32)
     fdw = rows("FD", torch.int64, (n, NP))
@@ -164,10 +165,11 @@ def cpu_baseline(sim, spec, cfg, next_plan, sample: int, min_seconds: float = 10
         for o in (a, b):
             def g(x):
                 return np.ascontiguousarray(x[o, :n].cpu().numpy().view(np.uint32))
+            hb = np.ascontiguousarray(sim.decode_heartbeats(hb16[o].cpu().numpy())[:n])
             mv = np.ascontiguousarray((mv16[o, :n].cpu().numpy().view(np.uint16) & 0x7FFF).astype(np.uint32))
             fl, fs, fc = (np.ascontiguousarray(x) for x in sim.unpack_fd(fdw[o, :n].cpu().numpy()))
             hw = np.ascontiguousarray(held[o, :n, :K].cpu().numpy())
-            L.orc_load_row(h, o, n, order.ctypes.data_as(P), g(hb).ctypes.data_as(P), mv.ctypes.data_as(P),
+            L.orc_load_row(h, o, n, order.ctypes.data_as(P), hb.ctypes.data_as(P), mv.ctypes.data_as(P),
                            g(gc).ctypes.data_as(P), hw.ctypes.data_as(P), Cc, hist_ver.ctypes.data_as(P),
                            hist_vid.ctypes.data_as(P), hist_vlen.ctypes.data_as(P), hist_st.ctypes.data_as(P),
                            fl.ctypes.data_as(P), fs.ctypes.data_as(P), fc.ctypes.data_as(P),

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define GS_API_VERSION 5
+#define GS_API_VERSION 6
 #define GS_TICK_US 15625u
 #define GS_NONE 0xFFFFFFFFu
 
@@ -79,7 +79,9 @@ typedef struct gs_config {
  * to 64; per-owner regions ([NC]..., NC = n_cols) are indexed by the local column jl.  With one
  * slice col_lo = 0 and n_cols = n_nodes. */
 enum gs_region {
-    GS_R_HB = 0,      /* u32 [N][NP]   NodeState.heartbeat of owner j as seen by observer o */
+    GS_R_HB = 0,      /* u16 [N][NP]   NodeState.heartbeat of owner j as seen by observer o, mod 2^16: decoded
+                                        against GS_R_SELF_HB as R - ((R - s) mod 2^16), exact while every view
+                                        lags its owner's own heartbeat by less than 2^16 */
     GS_R_MV,          /* u16 [N][NP]   NodeState.max_version (| GS_MV_INEXACT, see below); versions are
                                         bounded by K * (C - 1) <= 16,256, so 15 bits always suffice */
     GS_R_GC,          /* u32 [N][NP]   NodeState.last_gc_version (GS_TOMBSTONES only: without tombstone GC
@@ -115,6 +117,7 @@ enum gs_region {
     GS_R_PEND_STAMP,  /* u32 [N][16]   tick of the phase that last wrote plane row (o, p): the row is
                                         valid for the current round only if it equals round tick + 1 + p */
     GS_R_LATEST,      /* u64 [NC][KP]  the HIST entry of each key's latest write (no GS_TOMBSTONES only) */
+    GS_R_SELF_HB,     /* u32 [NP]      each owner column's own heartbeat (the diagonal of GS_R_HB, full width) */
     GS_NUM_REGIONS
 };
 

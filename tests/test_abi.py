@@ -43,7 +43,7 @@ def test_create_validates_config_without_gpu():
     assert lib.gs_create(ctypes.byref(good), ctypes.byref(h)) == 0
     nb = ctypes.c_uint64()
     assert lib.gs_region_bytes(h, _lib.REGION["HB"], ctypes.byref(nb)) == 0
-    assert nb.value == 1000 * 1024 * 4
+    assert nb.value == 1000 * 1024 * 2
     assert lib.gs_region_bytes(h, _lib.REGION["POS"], ctypes.byref(nb)) == 0 and nb.value == 1000 * 1024 * 4
     # no tombstone GC: last_gc_version is 0 everywhere and not stored
     assert lib.gs_region_bytes(h, _lib.REGION["GC"], ctypes.byref(nb)) == 0 and nb.value == 0
@@ -86,7 +86,7 @@ def test_slice_columns_and_region_sizes_without_gpu():
         seen.append((lo.value, nc.value))
         npad = (nc.value + 63) // 64 * 64
         nb = ctypes.c_uint64()
-        assert lib.gs_region_bytes(h, _lib.REGION["HB"], ctypes.byref(nb)) == 0 and nb.value == n * npad * 4
+        assert lib.gs_region_bytes(h, _lib.REGION["HB"], ctypes.byref(nb)) == 0 and nb.value == n * npad * 2
         assert lib.gs_region_bytes(h, _lib.REGION["HIST"], ctypes.byref(nb)) == 0 and nb.value == nc.value * 32 * 16 * 8
         assert lib.gs_region_bytes(h, _lib.REGION["SLICE_BITS"], ctypes.byref(nb)) == 0
         assert nb.value == (n // 2) * 2 * (npad // 32) * 4

@@ -1,0 +1,54 @@
+"""Heartbeats past 2^16 (GPU only).
+
+GS_R_HB holds each view's heartbeat mod 2^16, decoded against the owner's own heartbeat
+(GS_R_SELF_HB): exact while no view lags its owner by 2^16 or more.  Here
+eight nodes gossip every round for ~34,000 rounds, so every heartbeat crosses 65,536 while
+the views stay close behind; the device must match the C oracle (unbounded heartbeats)
+array for array, heartbeats, failure-detector windows and live sets included.
+"""
+
+import numpy as np
+import pytest
+from helpers import compare_exports
+from oracle import OracleSim
+
+from aiocluster_amd.scenario import DEFAULT_CFG
+from aiocluster_amd.sim import GossipSim
+from aiocluster_amd.workload import key_names, liveness_tick, phase_tick, round_tick, synthetic_node_ids
+
+pytestmark = pytest.mark.gpu
+
+SCHED = [[(0, 1), (2, 3), (4, 5), (6, 7)], [(1, 2), (3, 4), (5, 6), (7, 0)], [(0, 4), (1, 5), (2, 6), (3, 7)],
+         [(5, 0), (6, 1), (7, 2), (4, 3)]]
+
+
+def test_heartbeats_past_2_16_match_oracle():
+    import torch
+
+    n, rounds = 8, 34000
+    ids, keys = synthetic_node_ids(n), key_names(2)
+    init = {j: [(0, f"v{j}")] for j in range(n)}
+    gpu = GossipSim(ids, keys, dict(DEFAULT_CFG), "warm", init, tombstones=False, fd_ring=True, hist_cap=8)
+    orc = OracleSim(ids, keys, dict(DEFAULT_CFG), "warm", init)
+    up = np.ones(n, np.uint8)
+    up_dev = torch.from_numpy(up).to(gpu.device)
+    dev_sched = [(torch.tensor([a for a, _ in s], dtype=torch.int32, device=gpu.device),
+                  torch.tensor([b for _, b in s], dtype=torch.int32, device=gpu.device)) for s in SCHED]
+    for r in range(rounds):
+        t = round_tick(r)
+        gpu.begin_round(t, up_dev)
+        orc.begin_round(t, up)
+        for p in range(2):
+            i = (r + p) % len(SCHED)
+            gpu.run_phase_arrays(phase_tick(r, p), *dev_sched[i])
+            orc.run_phase(phase_tick(r, p), SCHED[i])
+        gpu.liveness(liveness_tick(r, 2), up_dev)
+        orc.liveness(liveness_tick(r, 2), up)
+        if r in (100, rounds // 2, rounds - 1):
+            want = orc.export()
+            diff = compare_exports(gpu.export(), want)
+            assert diff is None, f"round {r}: {diff}"
+    hb = np.asarray(want["hb"])
+    assert hb.min() > 65536, "every heartbeat must have crossed 2^16"
+    c = gpu.check()
+    assert c["exchanges"] == rounds * 8
