@@ -25,6 +25,7 @@ GS_TOMBSTONES = 2
 GS_FD_RING = 4
 GS_NO_HELD = 8
 GS_NONE = 0xFFFFFFFF
+GS_E_INVALID = -1
 GS_MV_INEXACT = 0x8000
 TICK_US = 15_625
 
@@ -67,10 +68,10 @@ EXPORTS = [
     "gs_create", "gs_destroy", "gs_last_error", "gs_api_version", "gs_region_bytes", "gs_bind", "gs_set_stream",
     "gs_boot", "gs_warm", "gs_owner_writes", "gs_begin_round", "gs_run_phase", "gs_liveness", "gs_phi_row",
     "gs_read_counters", "gs_reset_counters", "gs_sync", "gs_shard_columns", "gs_phase_count", "gs_phase_pack", "gs_materialize_held", "gs_fd_census",
-    "gs_select_peers", "gs_schedule_phases", "gs_set_events",
+    "gs_select_peers", "gs_schedule_phases", "gs_set_events", "gs_emit_scratch_bytes", "gs_emit_digest", "gs_emit_delta",
 ]
 
-API_VERSION = 6
+API_VERSION = 7
 
 
 class GsConfig(C.Structure):
@@ -101,6 +102,10 @@ CENSUS_FIELDS = ["up_pairs", "up_dead", "up_live", "down_pairs", "down_live"]
 
 class GsCensus(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in CENSUS_FIELDS]
+
+
+class GsWire(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in ("node_ids", "node_id_off", "keys", "key_off", "values", "value_off")]
 
 
 class GsError(RuntimeError):
@@ -157,6 +162,9 @@ def load():
         "gs_set_events": (C.c_int, [P, P, u32, P]),
         "gs_select_peers": (C.c_int, [P, P, u32, P, u32, C.c_uint64, u32, P, P]),
         "gs_schedule_phases": (C.c_int, [P, P, u32, P, C.c_uint64, u32, u32, P, P, P, C.POINTER(u32)]),
+        "gs_emit_scratch_bytes": (C.c_int, [P, C.POINTER(u64)]),
+        "gs_emit_digest": (C.c_int, [P, C.POINTER(GsWire), u32, u32, P, u64, C.POINTER(u64), P]),
+        "gs_emit_delta": (C.c_int, [P, C.POINTER(GsWire), u32, u32, u32, P, u64, C.POINTER(u64), P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

@@ -427,16 +427,20 @@ struct PackState {
 };
 
 // COUNT: only sum the DeltaPb bytes of every candidate (owner-sharded runs: the slice total).
-template <int KW, bool GENM, bool COUNT>
+// REC: record the selected NodeDeltas {owner, vsel} in sender order into rec[] (*nrec of them)
+// instead of applying them (the wire-format emitter, gs_emit_delta).
+template <int KW, bool GENM, bool COUNT, bool REC = false>
 __device__ __forceinline__ void pack_dir(const Dev &d, uint32_t s, uint32_t r, const DigestSide ds,
                                          const uint32_t *order, uint32_t cnt, const uint32_t *bits, uint16_t *wbuf,
-                                         uint32_t t, WStats &st, bool &tomb, PackState &pst) {
+                                         uint32_t t, WStats &st, bool &tomb, PackState &pst, uint2 *rec = nullptr,
+                                         uint32_t *nrec = nullptr) {
     const int lane = lane_id();
     const uint32_t mtu = d.mtu;
     const uint32_t S0 = pst.S;
     uint32_t S = pst.S;
     bool tail = pst.tail, stop = pst.stop;
     if (!COUNT && !stop && (S >= mtu || mtu - S < d.lb_min)) stop = true;
+    uint32_t nr = 0;    // REC: NodeDeltas recorded so far (wave-uniform)
     uint32_t pend = 0;  // wave-uniform: candidates carried from earlier windows (< 64), in rv
     uint32_t rv = 0;    // lane i < pend: the i-th carried candidate's position
     for (uint32_t win = 0; win < cnt && !stop; win += WIN) {
@@ -561,6 +565,12 @@ __device__ __forceinline__ void pack_dir(const Dev &d, uint32_t s, uint32_t r, c
                 cur = x + 1;
             }
             if (tail && mtu - S < d.lb_min) stop = true;
+            if (REC) {  // lanes hold candidates in sender order: rank by lane
+                const unsigned long long sm = __ballot(vsel != 0u);
+                if (vsel) rec[nr + (uint32_t)__popcll(sm & ((1ull << lane) - 1ull))] = make_uint2(c.j, vsel);
+                nr += (uint32_t)__popcll(sm);
+                continue;
+            }
             // apply_delta at the receiver: one lane per NodeDelta, distinct owners, any order
             if (vsel) {
                 apply_cand<KW>(d, r, c, vsel, t, tomb, st.alg);
@@ -585,6 +595,10 @@ __device__ __forceinline__ void pack_dir(const Dev &d, uint32_t s, uint32_t r, c
     pst.S = S;
     pst.tail = tail;
     pst.stop = stop;
+    if (REC) {
+        if (lane == 0) *nrec = nr;
+        return;
+    }
     if (!COUNT && lane == 0) shard_add(d, C_DBYTES, S - S0);  // DeltaPb bytes this call added
 }
 
@@ -1395,6 +1409,204 @@ __global__ __launch_bounds__(LB) void k_materialize(Dev d, uint32_t r0, uint32_t
     }
 }
 
+// ------------------------------------------------------------------ wire-format emitter
+// The bytes the reference's SerializeToString gives for DigestPb / DeltaPb (messages.proto:46-74,
+// built at state.py:56-58, 74-81, 98-99 and entities.py:62-72, 125-131): fields in field-number
+// order, proto3 scalars only when non-zero, NodeDeltaPb.max_version always (it is `optional`).
+// String tables (NodeIdPb bytes per node, key names, interned values) are caller-owned device arrays.
+struct Wire {
+    const uint8_t *nid;
+    const uint32_t *nid_off;  // [n_nodes + 1]
+    const uint8_t *key;
+    const uint32_t *key_off;  // [K + 1]
+    const uint8_t *val;
+    const uint64_t *val_off;  // [values + 1], indexed by value id
+};
+__device__ inline uint8_t *put_var(uint8_t *p, uint32_t x) {
+    while (x >= 0x80u) { *p++ = (uint8_t)(x | 0x80u); x >>= 7; }
+    *p++ = (uint8_t)x;
+    return p;
+}
+__device__ inline uint8_t *put_bytes(uint8_t *p, const uint8_t *src, uint32_t n) {
+    for (uint32_t i = 0; i < n; i++) p[i] = src[i];
+    return p + n;
+}
+__device__ inline uint8_t *put_u(uint8_t *p, uint32_t tag, uint32_t x) {
+    if (x) { *p++ = (uint8_t)tag; p = put_var(p, x); }
+    return p;
+}
+
+// Entry q of observer o's digest (compute_digest, state.py:324-331: dict order minus the targets
+// scheduled for deletion): the owner's local column, or NONE.
+__device__ inline uint32_t digest_owner(const Dev &d, uint32_t o, uint32_t q, uint32_t t, bool sch) {
+    const uint32_t j = (d.flags & GS_CANONICAL) ? q : d.ord[(size_t)o * d.NP + q];
+    if (j == NONE) return NONE;
+    if (sch && is_sched(d.fd_state[pix(d, o, j)], t, d.sched_delay)) return NONE;
+    return j;
+}
+__device__ inline void view_hgm(const Dev &d, uint32_t o, uint32_t j, uint32_t &H, uint32_t &G, uint32_t &M) {
+    const size_t p = pix(d, o, j);
+    H = hb_dec(d.hb[p], d.self_hb[j]);
+    G = (d.flags & GS_TOMBSTONES) ? d.gc[p] : 0u;
+    M = d.mv[p] & MV_MASK;
+}
+__global__ __launch_bounds__(LB) void k_digest_size(Dev d, Wire w, uint32_t o, uint32_t t, bool sch, uint32_t cnt,
+                                                    uint64_t *sz) {
+    const uint32_t q = blockIdx.x * LB + threadIdx.x;
+    if (q >= cnt) return;
+    const uint32_t j = digest_owner(d, o, q, t, sch);
+    uint64_t n = 0;
+    if (j != NONE) {
+        uint32_t H, G, M;
+        view_hgm(d, o, j, H, G, M);
+        const uint32_t jg = d.col_lo + j, nl = w.nid_off[jg + 1] - w.nid_off[jg];
+        n = msgf(msgf(nl) + ufield(H) + ufield(G) + ufield(M));
+    }
+    sz[q] = n;
+}
+__global__ __launch_bounds__(LB) void k_digest_write(Dev d, Wire w, uint32_t o, uint32_t t, bool sch, uint32_t cnt,
+                                                     const uint64_t *off, uint8_t *out) {
+    const uint32_t q = blockIdx.x * LB + threadIdx.x;
+    if (q >= cnt) return;
+    const uint32_t j = digest_owner(d, o, q, t, sch);
+    if (j == NONE) return;
+    uint32_t H, G, M;
+    view_hgm(d, o, j, H, G, M);
+    const uint32_t jg = d.col_lo + j, nl = w.nid_off[jg + 1] - w.nid_off[jg];
+    uint8_t *p = out + off[q];
+    *p++ = 0x0Au;  // DigestPb.node_digests (1)
+    p = put_var(p, msgf(nl) + ufield(H) + ufield(G) + ufield(M));
+    *p++ = 0x0Au;  // NodeDigestPb.node_id (1)
+    p = put_var(p, nl);
+    p = put_bytes(p, w.nid + w.nid_off[jg], nl);
+    p = put_u(p, 0x10u, H);  // heartbeat (2)
+    p = put_u(p, 0x18u, G);  // last_gc_version (3)
+    put_u(p, 0x20u, M);      // max_version (4)
+}
+
+// exclusive prefix sum of n u64 sizes into off[0..n] (one workgroup; the emitter's n <= n_cols)
+__global__ __launch_bounds__(1024) void k_scan_sizes(const uint64_t *in, uint32_t n, uint64_t *off) {
+    __shared__ uint64_t part[1024];
+    const uint32_t tid = threadIdx.x, per = (n + 1023u) / 1024u;
+    const uint32_t lo = min(n, tid * per), hi = min(n, lo + per);
+    uint64_t acc = 0;
+    for (uint32_t i = lo; i < hi; i++) acc += in[i];
+    part[tid] = acc;
+    __syncthreads();
+    for (uint32_t k = 1; k < 1024u; k <<= 1) {
+        const uint64_t v = tid >= k ? part[tid - k] : 0ull;
+        __syncthreads();
+        part[tid] += v;
+        __syncthreads();
+    }
+    uint64_t base = tid ? part[tid - 1] : 0ull;
+    for (uint32_t i = lo; i < hi; i++) { off[i] = base; base += in[i]; }
+    if (tid == 1023u) off[n] = part[1023];
+}
+
+// compute_partial_delta_respecting_mtu(r's digest, mtu, s's scheduled_for_deletion) of sender s
+// (state.py:340-415), without applying it: one wave builds the stale-owner bitmap of the direction
+// s -> r (as pass 1 does) and runs the packer in record mode: rec[] = {owner, vsel} in s's dict order.
+template <int KW, bool GENM>
+__global__ __launch_bounds__(WAVE) void k_delta_plan(Dev d, uint32_t s, uint32_t r, uint32_t t, uint2 *rec,
+                                                     uint32_t *nrec) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    uint16_t *wbuf = reinterpret_cast<uint16_t *>(lds);
+    uint32_t *bits = lds + WIN / 2;
+    const int lane = lane_id();
+    const bool schS = t >= d.row[s * 4 + 2], schR = t >= d.row[r * 4 + 2];
+    const uint32_t cntS = GENM ? d.row[s * 4 + 0] : d.ncol, cntR = GENM ? d.row[r * 4 + 0] : d.ncol;
+    for (uint32_t j0 = 0; j0 < d.NP; j0 += WAVE) {
+        const uint32_t j = j0 + (uint32_t)lane;
+        bool stale = false;
+        if (j < d.ncol) {
+            const size_t ps = pix(d, s, j), pr = pix(d, r, j);
+            const bool has = GENM ? d.pos[ps] != NONE : true;
+            if (has && !(schS && is_sched(d.fd_state[ps], t, d.sched_delay))) {
+                bool in_d = GENM ? d.pos[pr] < cntR : true;
+                if (in_d && schR && is_sched(d.fd_state[pr], t, d.sched_delay)) in_d = false;
+                const uint32_t dm = in_d ? (d.mv[pr] & MV_MASK) : 0u;
+                stale = (d.mv[ps] & MV_MASK) > dm;  // state.py:347-357
+            }
+        }
+        const unsigned long long m = __ballot(stale);
+        if (lane == 0) { bits[j0 >> 5] = (uint32_t)m; bits[(j0 >> 5) + 1] = (uint32_t)(m >> 32); }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const DigestSide ds{r, cntR, schR};
+    WStats st{0, 0, 0, 0, 0};
+    bool tomb = false;
+    PackState pst{0u, false, false};
+    pack_dir<KW, GENM, false, true>(d, s, r, ds, GENM ? d.ord + (size_t)s * d.NP : nullptr, cntS, bits, wbuf, t, st,
+                                    tomb, pst, rec, nrec);
+}
+
+// one recorded NodeDelta: the sender's candidate (eval_cand) and its NodeDeltaPb body size
+template <int KW, bool GENM>
+__device__ inline uint32_t nd_eval(const Dev &d, uint32_t s, uint32_t r, uint32_t t, uint2 rc, Cand<KW> &c) {
+    const bool schR = t >= d.row[r * 4 + 2];
+    const DigestSide ds{r, GENM ? d.row[r * 4 + 0] : d.ncol, schR};
+    uint32_t alg = 0;
+    eval_cand<KW, GENM>(d, s, r, ds, rc.x, t, c, alg);
+    uint32_t sum = 0;
+#pragma unroll
+    for (int q = 0; q < 4 * KW; q++)
+        if (c.ver[q] > c.from && c.ver[q] <= rc.y) sum += c.km[q] & 0xFFFFu;
+    return c.base + sum;
+}
+template <int KW, bool GENM>
+__global__ __launch_bounds__(LB) void k_delta_size(Dev d, uint32_t s, uint32_t r, uint32_t t, const uint2 *rec,
+                                                   uint32_t n, uint64_t *sz) {
+    const uint32_t i = blockIdx.x * LB + threadIdx.x;
+    if (i >= n) return;
+    Cand<KW> c;
+    sz[i] = msgf(nd_eval<KW, GENM>(d, s, r, t, rec[i], c));
+}
+template <int KW, bool GENM>
+__global__ __launch_bounds__(LB) void k_delta_write(Dev d, Wire w, uint32_t s, uint32_t r, uint32_t t,
+                                                    const uint2 *rec, uint32_t n, const uint64_t *off, uint8_t *out) {
+    const uint32_t i = blockIdx.x * LB + threadIdx.x;
+    if (i >= n) return;
+    Cand<KW> c;
+    const uint2 rc = rec[i];
+    const uint32_t body = nd_eval<KW, GENM>(d, s, r, t, rc, c);
+    const uint32_t j = rc.x, jg = d.col_lo + j, nl = w.nid_off[jg + 1] - w.nid_off[jg];
+    uint8_t *p = out + off[i];
+    *p++ = 0x0Au;  // DeltaPb.node_deltas (1)
+    p = put_var(p, body);
+    *p++ = 0x0Au;  // NodeDeltaPb.node_id (1)
+    p = put_var(p, nl);
+    p = put_bytes(p, w.nid + w.nid_off[jg], nl);
+    p = put_u(p, 0x10u, c.from);  // from_version_excluded (2)
+    p = put_u(p, 0x18u, c.gs);    // last_gc_version (3)
+    // key_values (4), increasing version (state.py:373-374); versions of one owner are distinct
+    uint32_t last = c.from;
+    for (;;) {
+        int qm = -1;
+        uint32_t vm = NONE;
+        for (int q = 0; q < 4 * KW; q++)
+            if (c.ver[q] > last && c.ver[q] <= rc.y && c.ver[q] < vm) { vm = c.ver[q]; qm = q; }
+        if (qm < 0) break;
+        last = vm;
+        const size_t hx = hix(d, j, byte_of(c.hs, qm), (uint32_t)qm);
+        const uint32_t meta = (uint32_t)(d.hist[hx] >> 32), vl = meta_vlen(meta), st = meta_status(meta);
+        const uint32_t kl = w.key_off[qm + 1] - w.key_off[qm];
+        *p++ = 0x22u;
+        p = put_var(p, meta_kvlen(meta));
+        if (kl) { *p++ = 0x0Au; p = put_var(p, kl); p = put_bytes(p, w.key + w.key_off[qm], kl); }  // key (1)
+        if (vl) {  // value (2)
+            *p++ = 0x12u;
+            p = put_var(p, vl);
+            p = put_bytes(p, w.val + w.val_off[d.hist_vid[hx]], vl);
+        }
+        p = put_u(p, 0x18u, vm);  // version (3)
+        p = put_u(p, 0x20u, st);  // status (4)
+    }
+    *p++ = 0x28u;  // max_version (5), explicit presence
+    put_var(p, c.ms);
+}
+
 // ------------------------------------------------------------------ peer selection
 // select_nodes_for_gossip (server.py:656-717) for every up node from its failure detector's
 // live / dead sets and its known peers, as _gossip_multiple uses them at round start
@@ -2009,6 +2221,121 @@ int gs_phi_row(gs_handle *h, uint32_t observer, uint32_t tick, double *out) {
     k_phi_row<<<(h->ncol + LB - 1) / LB, LB, 0, h->stream>>>(h->d, observer, tick, out);
     HIPCHK(h, hipGetLastError());
     return GS_OK;
+}
+
+// ---- wire-format emitter (blocking)
+extern "C++" {
+namespace {
+struct EmitScratch {
+    uint64_t *sz, *off;
+    uint2 *rec;
+    uint32_t *nrec;
+};
+EmitScratch emit_scratch(const gs_handle *h, void *scratch) {
+    uint8_t *b = (uint8_t *)scratch;
+    const uint64_t NP = h->NP;
+    EmitScratch e;
+    e.sz = (uint64_t *)b;
+    e.off = (uint64_t *)(b + NP * 8);
+    e.rec = (uint2 *)(b + NP * 16 + 64);
+    e.nrec = (uint32_t *)(b + NP * 24 + 64);
+    return e;
+}
+Wire to_wire(const gs_wire *w) {
+    return Wire{w->node_ids, w->node_id_off, w->keys, w->key_off, w->values, w->value_off};
+}
+int emit_check(gs_handle *h, const gs_wire *w, uint8_t *out, uint64_t *len, void *scratch) {
+    if (!h || !h->booted || !w || !len || !scratch || !w->node_ids || !w->node_id_off || !w->keys || !w->key_off)
+        return GS_E_INVALID;
+    if (h->G > 1) return fail(h, GS_E_UNSUPPORTED, "the wire emitter needs the whole matrix (one slice)");
+    (void)out;
+    return GS_OK;
+}
+// copy the total back, check the capacity, then write
+int emit_finish(gs_handle *h, const uint64_t *off_total, uint64_t cap, uint64_t *len, uint8_t *out, bool &go) {
+    uint64_t total = 0;
+    HIPCHK(h, hipMemcpyAsync(&total, off_total, 8, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    *len = total;
+    go = total > 0 && total <= cap && out != nullptr;
+    if (total > cap) return fail(h, GS_E_INVALID, "output buffer of %llu bytes < %llu needed",
+                                 (unsigned long long)cap, (unsigned long long)total);
+    return GS_OK;
+}
+template <int KW, bool GENM>
+int emit_delta(gs_handle *h, const Wire &w, uint32_t s, uint32_t r, uint32_t t, uint8_t *out, uint64_t cap,
+               uint64_t *len, const EmitScratch &e) {
+    hipStream_t st = h->stream;
+    const size_t lds = WIN * 2 + (size_t)(h->NP / 32) * 4;
+    HIPCHK(h, hipMemsetAsync(e.nrec, 0, 4, st));
+    k_delta_plan<KW, GENM><<<1, WAVE, lds, st>>>(h->d, s, r, t, e.rec, e.nrec);
+    HIPCHK(h, hipGetLastError());
+    uint32_t n = 0;
+    HIPCHK(h, hipMemcpyAsync(&n, e.nrec, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(h, hipStreamSynchronize(st));
+    if (n > h->ncol) return fail(h, GS_E_DEVICE, "delta plan recorded %u NodeDeltas", n);
+    if (n == 0) { *len = 0; return GS_OK; }
+    const uint32_t nb = (n + LB - 1) / LB;
+    k_delta_size<KW, GENM><<<nb, LB, 0, st>>>(h->d, s, r, t, e.rec, n, e.sz);
+    k_scan_sizes<<<1, 1024, 0, st>>>(e.sz, n, e.off);
+    HIPCHK(h, hipGetLastError());
+    bool go = false;
+    int rc = emit_finish(h, e.off + n, cap, len, out, go);
+    if (rc || !go) return rc;
+    k_delta_write<KW, GENM><<<nb, LB, 0, st>>>(h->d, w, s, r, t, e.rec, n, e.off, out);
+    HIPCHK(h, hipGetLastError());
+    HIPCHK(h, hipStreamSynchronize(st));
+    return GS_OK;
+}
+}  // namespace
+}  // extern "C++"
+
+int gs_emit_scratch_bytes(const gs_handle *h, uint64_t *bytes) {
+    if (!h || !bytes) return GS_E_INVALID;
+    *bytes = (uint64_t)h->NP * 24 + 128;
+    return GS_OK;
+}
+
+int gs_emit_digest(gs_handle *h, const gs_wire *w, uint32_t observer, uint32_t tick, uint8_t *out, uint64_t cap,
+                   uint64_t *len, void *scratch) {
+    int rc = emit_check(h, w, out, len, scratch);
+    if (rc) return rc;
+    if (observer >= h->N) return GS_E_INVALID;
+    const EmitScratch e = emit_scratch(h, scratch);
+    const Wire wr = to_wire(w);
+    uint32_t row[4];
+    HIPCHK(h, hipMemcpyAsync(row, h->d.row + observer * 4, 16, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    const uint32_t cnt = (h->cfg.flags & GS_CANONICAL) ? h->ncol : row[0];
+    const bool sch = tick >= row[2];
+    if (cnt == 0) { *len = 0; return GS_OK; }
+    const uint32_t nb = (cnt + LB - 1) / LB;
+    k_digest_size<<<nb, LB, 0, h->stream>>>(h->d, wr, observer, tick, sch, cnt, e.sz);
+    k_scan_sizes<<<1, 1024, 0, h->stream>>>(e.sz, cnt, e.off);
+    HIPCHK(h, hipGetLastError());
+    bool go = false;
+    rc = emit_finish(h, e.off + cnt, cap, len, out, go);
+    if (rc || !go) return rc;
+    k_digest_write<<<nb, LB, 0, h->stream>>>(h->d, wr, observer, tick, sch, cnt, e.off, out);
+    HIPCHK(h, hipGetLastError());
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return GS_OK;
+}
+
+int gs_emit_delta(gs_handle *h, const gs_wire *w, uint32_t sender, uint32_t receiver, uint32_t tick, uint8_t *out,
+                  uint64_t cap, uint64_t *len, void *scratch) {
+    int rc = emit_check(h, w, out, len, scratch);
+    if (rc) return rc;
+    if (sender >= h->N || receiver >= h->N || sender == receiver) return GS_E_INVALID;
+    if (!w->values || !w->value_off) return GS_E_INVALID;
+    const EmitScratch e = emit_scratch(h, scratch);
+    const Wire wr = to_wire(w);
+    const bool genm = !(h->cfg.flags & GS_CANONICAL);
+    if (h->KP <= 16)
+        return genm ? emit_delta<4, true>(h, wr, sender, receiver, tick, out, cap, len, e)
+                    : emit_delta<4, false>(h, wr, sender, receiver, tick, out, cap, len, e);
+    return genm ? emit_delta<16, true>(h, wr, sender, receiver, tick, out, cap, len, e)
+                : emit_delta<16, false>(h, wr, sender, receiver, tick, out, cap, len, e);
 }
 
 int gs_read_counters(gs_handle *h, gs_counters *out) {

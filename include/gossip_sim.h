@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define GS_API_VERSION 6
+#define GS_API_VERSION 7
 #define GS_TICK_US 15625u
 #define GS_NONE 0xFFFFFFFFu
 
@@ -269,6 +269,33 @@ int gs_schedule_phases(gs_handle *h, const uint8_t *up, uint32_t fanout, const i
 /* FailureDetector.live_nodes / dead_nodes of every up observer (failure_detector.py:63-67) counted
  * against the DEVICE up mask; blocking.  Sliced handles count their own target columns. */
 int gs_fd_census(gs_handle *h, const uint8_t *up, gs_census *out);
+
+/* Wire-format emitter: the protobuf bytes the reference's SerializeToString gives, from device state,
+ * so a simulated cluster can talk to real aiocluster nodes (messages.proto:46-74).  String tables are
+ * DEVICE arrays owned by the caller: NodeIdPb bytes of every node (entities.py:62-72; node i at
+ * node_ids[node_id_off[i] .. node_id_off[i + 1])), the UTF-8 key names (key_off[K + 1]) and the
+ * interned values by value id (value_off[n_values + 1]; value ids as passed to gs_owner_writes).
+ *   gs_emit_digest: DigestPb of observer's compute_digest at `tick` (state.py:324-331, 56-58; what
+ *                   _make_syn_msg sends, server.py:327-332);
+ *   gs_emit_delta:  DeltaPb of sender's compute_partial_delta_respecting_mtu(receiver's digest at `tick`,
+ *                   mtu, sender's scheduled_for_deletion) (state.py:340-415, 98-99; the SynAck delta,
+ *                   server.py:339-346), without applying it.
+ * `out` is a DEVICE buffer of `cap` bytes; *len (host) receives the message size.  A size above `cap`
+ * returns GS_E_INVALID with *len set and nothing written (out = NULL: size query).  DEVICE scratch of
+ * gs_emit_scratch_bytes.  Blocking; one slice only. */
+typedef struct gs_wire {
+    const uint8_t *node_ids;
+    const uint32_t *node_id_off;
+    const uint8_t *keys;
+    const uint32_t *key_off;
+    const uint8_t *values;
+    const uint64_t *value_off;
+} gs_wire;
+int gs_emit_scratch_bytes(const gs_handle *h, uint64_t *bytes);
+int gs_emit_digest(gs_handle *h, const gs_wire *w, uint32_t observer, uint32_t tick, uint8_t *out, uint64_t cap,
+                   uint64_t *len, void *scratch);
+int gs_emit_delta(gs_handle *h, const gs_wire *w, uint32_t sender, uint32_t receiver, uint32_t tick, uint8_t *out,
+                  uint64_t cap, uint64_t *len, void *scratch);
 
 int gs_read_counters(gs_handle *h, gs_counters *out);
 int gs_reset_counters(gs_handle *h);
