@@ -44,6 +44,9 @@ namespace {
 constexpr uint32_t NONE = GS_NONE;
 constexpr int WAVE = 64;
 constexpr int XB = 128;  // exchange workgroup: 2 waves
+#ifndef XB_WAVES
+#define XB_WAVES 4  // waves per SIMD k_exchange is compiled for (VGPR budget 512 / 4 = 128)
+#endif
 constexpr int LB = 256;  // liveness / elementwise workgroups
 constexpr int NSHARD = 64;
 constexpr uint32_t WIN = 16 * 64;  // positions per packer window (16 per lane)
@@ -780,10 +783,9 @@ __device__ inline PackState chain_unpack(uint64_t v) {
 
 // MODE 0: the whole exchange (one slice).  MODE 1: sharded count pass (pass 1, then the slice totals).
 template <int KW, bool GENM, int MODE>
-__global__ __launch_bounds__(XB) void k_exchange(Dev d, const int32_t *ini, const int32_t *res, uint32_t n,
+__global__ __launch_bounds__(XB, (KW == 4 ? XB_WAVES : 1)) void k_exchange(Dev d, const int32_t *ini, const int32_t *res, uint32_t n,
                                                  uint32_t t, uint32_t seq, SliceIO io) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    __shared__ uint32_t s_flag[4];
     const uint32_t e = blockIdx.x;
     if (e >= n) return;
     const int tid = threadIdx.x, lane = tid & (WAVE - 1), wid = tid >> 6;
@@ -800,8 +802,11 @@ __global__ __launch_bounds__(XB) void k_exchange(Dev d, const int32_t *ini, cons
     uint32_t *bm = lds + WIN;  // after the two waves' WIN x u16 candidate lists
     uint32_t *bBA = bm, *bAB = bm + words, *bNB = bm + 2 * words, *bNA = bm + 3 * words;
     for (uint32_t i = tid; i < words * (genm ? 4u : 2u); i += XB) bm[i] = 0u;
+    // pass 1's "some owner is new to a side" flag: the last word of wave 1's candidate list, which
+    // wave 1 only writes in pass 3, after reading the flag (no static LDS: see below)
+    uint32_t *s_new = lds + WIN - 1;
     if (tid == 0) {
-        s_flag[0] = 0;
+        *s_new = 0u;
         const uint32_t oa = atomicMax(&d.stamp[a], seq), ob = atomicMax(&d.stamp[b], seq);
         if (oa == seq || ob == seq) shard_add(d, C_E_CONFLICT, 1);
     }
@@ -840,12 +845,15 @@ __global__ __launch_bounds__(XB) void k_exchange(Dev d, const int32_t *ini, cons
         g0 = g1;
         c0 = c1;
     }
-    if (anynew) s_flag[0] = 1u;
+    // no static LDS: the 20 KB of dynamic LDS per workgroup (N = 65,536, canonical) then fits 8
+    // workgroups = 4 waves per SIMD
+    if (anynew) *s_new = 1u;
     __syncthreads();
+    const bool any_new = *s_new != 0u;
 
     if (MODE == 1) {
         // ---- sharded count pass: publish the bitmaps, total this slice's candidates per direction
-        if (s_flag[0] && tid == 0) shard_add(d, C_E_INSERT, 1);
+        if (any_new && tid == 0) shard_add(d, C_E_INSERT, 1);
         uint32_t *gb = d.sbits + (size_t)e * 2 * words;
         for (uint32_t i = tid; i < 2 * words; i += XB) gb[i] = bm[i];
         const bool w0 = wid == 0;
@@ -868,7 +876,7 @@ __global__ __launch_bounds__(XB) void k_exchange(Dev d, const int32_t *ini, cons
 
     // ---- pass 2: dict insertions (node_state_or_default appends in digest order)
     uint32_t cntA = cntA0, cntB = cntB0;
-    if (s_flag[0]) {
+    if (any_new) {
         if (!genm) {
             if (tid == 0) shard_add(d, C_E_INSERT, 1);
         } else if (wid == 0) {
@@ -896,13 +904,11 @@ __global__ __launch_bounds__(XB) void k_exchange(Dev d, const int32_t *ini, cons
             if (lane == 0) {
                 d.row[b * 4 + 0] = baseB;
                 d.row[a * 4 + 0] = baseA;
-                s_flag[1] = baseB;
-                s_flag[2] = baseA;
             }
             __threadfence_block();
         }
         __syncthreads();
-        if (genm) { cntB = s_flag[1]; cntA = s_flag[2]; }
+        if (genm) { cntB = d.row[b * 4 + 0]; cntA = d.row[a * 4 + 0]; }  // wave 0's counts (fenced above)
     }
 
     // ---- pass 3: SynAck delta b -> a (wave 0) and Ack delta a -> b (wave 1), each applied

@@ -43,32 +43,66 @@ def kernel_stats(root: str) -> dict:
     return out
 
 
-def counters(root: str, sub: str, name: str) -> tuple[dict, dict]:
-    """Average counter value per launch, and per work-item-group unit (k_exchange: per exchange)."""
-    per = defaultdict(list)
-    units = defaultdict(float)
+def timed_launches(root: str, sub: str = "kt") -> int | None:
+    """k_exchange launches inside bench.py's timed region (its JSON line's roofline.launches): the
+    trace's LAST that many k_exchange launches, so settle/warmup rounds are not averaged in."""
+    path = os.path.join(root, f"bench_{sub}.log")
+    if not os.path.exists(path):
+        return None
+    for line in open(path):
+        if line.startswith("{"):
+            return json.loads(line)["roofline"]["launches"]
+    return None
+
+
+def trace_avg(root: str, last: int | None) -> dict:
+    """Average k_exchange duration (ms) over the last `last` launches of the kernel trace."""
+    d = []
+    for path in glob.glob(os.path.join(root, "kt", "**", "*kernel_trace.csv"), recursive=True):
+        for row in csv.DictReader(open(path)):
+            if "k_exchange" in row["Kernel_Name"]:
+                d.append((int(row["Start_Timestamp"]), (int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) / 1e6))
+    d.sort()
+    tail = d[-last:] if last else d
+    return {"launches": len(tail), "avg_ms": sum(x for _, x in tail) / max(1, len(tail))} if tail else {}
+
+
+def counters(root: str, sub: str, name: str, last: int | None = None) -> tuple[dict, dict]:
+    """Average counter value per launch, and per work-item-group unit (k_exchange: per exchange); with
+    `last`, over each kernel's last `last` dispatches only (the timed region)."""
+    rows = defaultdict(list)
     for path in glob.glob(os.path.join(root, sub, "**", "*counter_collection.csv"), recursive=True):
         for row in csv.DictReader(open(path)):
             if row.get("Counter_Name") == name:
                 k = short(row["Kernel_Name"])
-                per[k].append(float(row["Counter_Value"]))
-                units[k] += float(row.get("Grid_Size", 0) or 0) / max(1.0, float(row.get("Workgroup_Size", 1) or 1))
-    avg = {k: sum(v) / len(v) for k, v in per.items()}
-    per_unit = {k: sum(v) / units[k] for k, v in per.items() if units[k] > 0}
+                wg = float(row.get("Grid_Size", 0) or 0) / max(1.0, float(row.get("Workgroup_Size", 1) or 1))
+                rows[k].append((int(row.get("Dispatch_Id", 0) or 0), float(row["Counter_Value"]), wg))
+    avg, per_unit = {}, {}
+    for k, v in rows.items():
+        v.sort()
+        if last and k == "k_exchange":
+            v = v[-last:]
+        avg[k] = sum(x[1] for x in v) / len(v)
+        u = sum(x[2] for x in v)
+        if u > 0:
+            per_unit[k] = sum(x[1] for x in v) / u
     return avg, per_unit
 
 
 def main(root: str, tag: str, workload: str):
     ks = kernel_stats(root)
-    fetch, fetch_u = counters(root, "fetch", "FETCH_SIZE")
-    write, write_u = counters(root, "write", "WRITE_SIZE")
+    lastn = timed_launches(root)
+    timed = trace_avg(root, lastn)
+    fetch, fetch_u = counters(root, "fetch", "FETCH_SIZE", timed_launches(root, "fetch"))
+    write, write_u = counters(root, "write", "WRITE_SIZE", timed_launches(root, "write"))
     traffic = {}
     for k in set(fetch) | set(write):
         f, w = fetch.get(k), write.get(k)
         if f is not None and w is not None:
             traffic[k] = {"fetch_kib": f, "write_kib": w, "hbm_bytes_per_launch": (2 * f + w) * 1024,
                           "hbm_bytes_per_workgroup": (2 * fetch_u[k] + write_u[k]) * 1024}
-    summary = {"tag": tag, "workload": workload, "kernel_stats": ks, "traffic": traffic}
+    summary = {"tag": tag, "workload": workload, "kernel_stats": ks, "k_exchange_timed_region": timed,
+               "traffic": traffic}
     sq = {}
     for name in ("SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU",
                  "SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_WAVES"):
@@ -86,7 +120,7 @@ def main(root: str, tag: str, workload: str):
     if "k_exchange" in traffic:
         agg[workload] = {"tag": tag, "k_exchange_bytes_per_launch": traffic["k_exchange"]["hbm_bytes_per_launch"],
                          "k_exchange_bytes_per_exchange": traffic["k_exchange"]["hbm_bytes_per_workgroup"],
-                         "k_exchange_avg_ms": ks.get("k_exchange", {}).get("avg_ms")}
+                         "k_exchange_avg_ms": timed.get("avg_ms", ks.get("k_exchange", {}).get("avg_ms"))}
         with open(agg_path, "w") as f:
             json.dump(agg, f, indent=1)
     print(json.dumps(summary, indent=1))
