@@ -48,6 +48,9 @@ constexpr int XB = 128;  // exchange workgroup: 2 waves
 #define XB_WAVES 4  // waves per SIMD k_exchange is compiled for (VGPR budget 512 / 4 = 128)
 #endif
 constexpr int LB = 256;  // liveness / elementwise workgroups
+#ifndef LIVE_PER
+#define LIVE_PER 8  // 1024-column chunks per k_liveness workgroup
+#endif
 constexpr int NSHARD = 64;
 constexpr uint32_t WIN = 16 * 64;  // positions per packer window (16 per lane)
 constexpr double TICK_S = 1.0 / 64.0;
@@ -1050,11 +1053,14 @@ __global__ __launch_bounds__(LB) void k_reset_sched(Dev d, const uint8_t *up) {
 // failure_detector.py:89-106), phi in binary64 exactly as SamplingWindow.phi (43-53).  Also folds
 // the earliest "scheduled for deletion" tick per row.
 template <bool RING>
+// One workgroup sweeps `per` consecutive 1024-column chunks of one row (fewer, longer workgroups:
+// the per-workgroup plane staging, stamp check and counter atomics are paid once per `per` chunks).
 __global__ __launch_bounds__(LB) void k_liveness(Dev d, const uint8_t *up, uint32_t t, uint32_t chunks,
-                                                 bool replay) {
-    __shared__ uint64_t s_pl[16][16];  // [phase][the 16 plane words of this workgroup's 1024 columns]
+                                                 uint32_t per, bool replay) {
+    __shared__ uint64_t s_pl[16][16];  // [phase][the 16 plane words of this chunk's 1024 columns]
     __shared__ uint32_t s_vm;
-    const uint32_t o = blockIdx.x / chunks, cb = blockIdx.x % chunks;
+    const uint32_t groups = (chunks + per - 1) / per;
+    const uint32_t o = blockIdx.x / groups, cb0 = (blockIdx.x % groups) * per;
     const bool upo = up[o] != 0;
     const bool genm = !(d.flags & GS_CANONICAL);
     uint32_t minS = NONE, live = 0, gcdue = 0, ovf = 0, alg = 0;
@@ -1067,11 +1073,14 @@ __global__ __launch_bounds__(LB) void k_liveness(Dev d, const uint8_t *up, uint3
     }
     __syncthreads();
     const uint32_t vm = s_vm;
-    {
+    const uint32_t cb1 = min(chunks, cb0 + per);
+    for (uint32_t cb = cb0; cb < cb1; cb++) {
+    if (vm) {
+        if (cb != cb0) __syncthreads();  // every thread is done with the previous chunk's planes
         const uint32_t ph = threadIdx.x >> 4, wi = cb * 16u + (threadIdx.x & 15u);
         if ((vm >> ph) & 1u) s_pl[ph][threadIdx.x & 15u] = wi < d.PW ? d.pend[((size_t)o * 16u + ph) * d.PW + wi] : 0ull;
+        __syncthreads();
     }
-    __syncthreads();
     const uint32_t c0 = (cb * LB + threadIdx.x) * 4u;
     if (c0 < d.ncol) {
         const size_t p = pix(d, o, c0);
@@ -1137,6 +1146,7 @@ __global__ __launch_bounds__(LB) void k_liveness(Dev d, const uint8_t *up, uint3
         if (dw) st4w(d.fd + p, w);
         if (ds) st4(d.fd_state + p, st);
     }
+    }
     // earliest scheduled-for-deletion tick of this row
     for (int dd = 32; dd >= 1; dd >>= 1) {
         const uint32_t y = __shfl_xor(minS, dd, WAVE);
@@ -1145,8 +1155,8 @@ __global__ __launch_bounds__(LB) void k_liveness(Dev d, const uint8_t *up, uint3
     const unsigned long long sl = wave_sum(live), sg = wave_sum(gcdue), so = wave_sum(ovf);
     if ((threadIdx.x & 63) == 0) {
         if (minS != NONE) atomicMin(&d.row[o * 4 + 2], minS);
-        shard_add(d, C_LIVE, sl);
-        shard_add(d, C_E_FDOVF, so);
+        if (sl) shard_add(d, C_LIVE, sl);
+        if (so) shard_add(d, C_E_FDOVF, so);
         if (sg) {
             if (genm) d.row[o * 4 + 3] = 1u;  // k_fd_gc collects this row
             else shard_add(d, C_E_FDGC, sg);  // removal would break the canonical layout
@@ -2207,11 +2217,12 @@ int gs_liveness(gs_handle *h, const uint8_t *up, uint32_t tick) {
     k_reset_sched<<<(h->N + LB - 1) / LB, LB, 0, h->stream>>>(h->d, up);
     HIPCHK(h, hipGetLastError());
     const uint32_t chunks = (h->ncol + 4 * LB - 1) / (4 * LB);
+    const uint32_t per = LIVE_PER, groups = (chunks + per - 1) / per;
     const bool replay = h->reports_pending;
     if (h->cfg.flags & GS_FD_RING)
-        k_liveness<true><<<chunks * h->N, LB, 0, h->stream>>>(h->d, up, tick, chunks, replay);
+        k_liveness<true><<<groups * h->N, LB, 0, h->stream>>>(h->d, up, tick, chunks, per, replay);
     else
-        k_liveness<false><<<chunks * h->N, LB, 0, h->stream>>>(h->d, up, tick, chunks, replay);
+        k_liveness<false><<<groups * h->N, LB, 0, h->stream>>>(h->d, up, tick, chunks, per, replay);
     HIPCHK(h, hipGetLastError());
     h->reports_pending = false;  // replayed
     h->round_open = false;
