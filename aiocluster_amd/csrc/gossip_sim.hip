@@ -245,6 +245,18 @@ __device__ __forceinline__ void eval_cand(const Dev &d, uint32_t s, uint32_t r, 
     // without GS_TOMBSTONES no tombstone is ever collected, so every last_gc_version stays 0 and the
     // GC region is not allocated; views are then tracked as prefixes of the owner's writes (MV_INEXACT)
     const bool gct = (d.flags & GS_TOMBSTONES) != 0;
+    // prefix views: the owner's latest write of every key is loaded with round trip 1, before it is
+    // known whether the sender's view is a prefix, so a prefix sender costs one round trip, not two
+    uint64_t lat[4 * KW];
+    if (!gct) {
+        const ulonglong2 *lp = reinterpret_cast<const ulonglong2 *>(d.lat + (size_t)j * d.KP);
+#pragma unroll
+        for (int q = 0; q < 2 * KW; q++) {
+            const ulonglong2 v = (uint32_t)(2 * q) < d.KP ? lp[q] : make_ulonglong2(0ull, 0ull);
+            lat[2 * q] = v.x;
+            lat[2 * q + 1] = v.y;
+        }
+    }
     const uint32_t msw = d.mv[ps], mrw = d.mv[pr];
     const uint32_t ms = msw & MV_MASK, mr = mrw & MV_MASK;
     const uint32_t gs = gct ? d.gc[ps] : 0u, gr = gct ? d.gc[pr] : 0u;
@@ -275,7 +287,7 @@ __device__ __forceinline__ void eval_cand(const Dev &d, uint32_t s, uint32_t r, 
             c.km[q] = 0u;
             uint32_t w = byte_of(c.hs, q);
             if (!w || (uint32_t)q >= d.K) continue;
-            uint64_t e = d.lat[(size_t)j * d.KP + q];  // counted below only for the kvs sent
+            uint64_t e = lat[q];  // counted below only for the kvs sent
             if ((uint32_t)e > ms) {
                 do {
                     w--;
