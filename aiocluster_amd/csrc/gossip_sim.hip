@@ -1087,13 +1087,24 @@ __global__ __launch_bounds__(LB) void k_liveness(Dev d, const uint8_t *up, uint3
     const uint32_t vm = s_vm;
     const uint32_t cb1 = min(chunks, cb0 + per);
     for (uint32_t cb = cb0; cb < cb1; cb++) {
+    // this chunk's windows and states are loaded before the plane staging (they do not depend on
+    // it), so the two global round trips of a chunk overlap; a down row has no valid planes (its
+    // node was in no exchange), so it loads windows only for up observers, as before
+    const uint32_t c0 = (cb * LB + threadIdx.x) * 4u;
+    uint64_t w[4] = {0ull, 0ull, 0ull, 0ull};
+    uint32_t st[4] = {0u, 0u, 0u, 0u}, ps[4] = {0u, 0u, 0u, 0u};
+    if (c0 < d.ncol) {
+        const size_t p = pix(d, o, c0);
+        if (upo || vm) ld4w(d.fd + p, w);
+        if (upo) ld4(d.fd_state + p, st);
+        if (upo && genm) ld4(d.pos + p, ps);
+    }
     if (vm) {
         if (cb != cb0) __syncthreads();  // every thread is done with the previous chunk's planes
         const uint32_t ph = threadIdx.x >> 4, wi = cb * 16u + (threadIdx.x & 15u);
         if ((vm >> ph) & 1u) s_pl[ph][threadIdx.x & 15u] = wi < d.PW ? d.pend[((size_t)o * 16u + ph) * d.PW + wi] : 0ull;
         __syncthreads();
     }
-    const uint32_t c0 = (cb * LB + threadIdx.x) * 4u;
     if (c0 < d.ncol) {
         const size_t p = pix(d, o, c0);
         // this thread's four columns: bit ph of q[i] = a report in phase ph
@@ -1104,12 +1115,7 @@ __global__ __launch_bounds__(LB) void k_liveness(Dev d, const uint8_t *up, uint3
 #pragma unroll
             for (int i = 0; i < 4; i++) q[i] |= (uint32_t)((s_pl[ph][wb + i] >> lb) & 1ull) << ph;
         }
-        const bool rep = (q[0] | q[1] | q[2] | q[3]) != 0u;
-        uint64_t w[4] = {0ull, 0ull, 0ull, 0ull};
-        uint32_t st[4] = {0u, 0u, 0u, 0u}, ps[4] = {0u, 0u, 0u, 0u};
-        if (upo || rep) ld4w(d.fd + p, w);
-        if (upo) ld4(d.fd_state + p, st);
-        if (upo && genm) ld4(d.pos + p, ps);
+        const bool rep = (q[0] | q[1] | q[2] | q[3]) != 0u;  // only if vm != 0: then w was loaded
         bool dw = false, ds = false;
         if (rep) {
 #pragma unroll
