@@ -238,6 +238,24 @@ def aggregate(exchanges: float, elapsed: float, dist=None, dev=None) -> tuple[fl
     return float(ex.item()), float(tm.item())
 
 
+def copy_ceiling(torch, dev, nbytes: int = 1 << 30, reps: int = 20) -> float:
+    """Measured streaming-copy ceiling: read + write bytes of a 1 GiB
+    device-to-device copy over its HIP-event time, in GB/s."""
+    src = torch.empty(nbytes // 4, dtype=torch.int32, device=dev).fill_(1)
+    dst = torch.empty_like(src)
+    dst.copy_(src)
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        dst.copy_(src)
+    e1.record()
+    torch.cuda.synchronize(dev)
+    gbs = 2.0 * nbytes * reps / (e0.elapsed_time(e1) / 1e3) / 1e9
+    del src, dst
+    return gbs
+
+
 def load_traffic(workload: str, exchanges_per_launch: float):
     """HBM bytes per k_exchange launch from the committed rocprofv3 PMC summary of this workload
     (tools/profile.sh + tools/pmc_summary.py): measured bytes per exchange x this run's exchanges per launch."""
@@ -388,6 +406,7 @@ def main():
     achieved = alg_survey / (kern_ms / 1e3) / 1e9 if kern_ms > 0 else 0.0
     achieved_in_kernel = alg_local / (kern_ms / 1e3) / 1e9 if kern_ms > 0 else 0.0
     traffic = load_traffic(workload, exch / max(1, len(events))) if group is None else None
+    copy_gbs = copy_ceiling(torch, dev) if rank == 0 else None
     cpu = None
     if rank == 0 and group is None and not args.no_cpu_baseline:
         cpu = cpu_baseline(sim, spec, cfg, plans[R0 + args.steps], args.cpu_sample, args.cpu_seconds)
@@ -426,6 +445,8 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBPS,
                 "traffic": traffic,
+                "measured_copy_ceiling": copy_gbs,
+                "frac_of_copy_ceiling": achieved / copy_gbs if copy_gbs else None,
                 "alg_bytes_per_launch": alg_survey / max(1, launches),
                 "alg_bytes_formula": "exchanges x 32 x N + pack_bytes (SURVEY 8(d) minus the FD term, see DESIGN.md)",
                 "in_kernel_bytes_per_launch": alg_local / max(1, launches),
