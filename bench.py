@@ -446,7 +446,11 @@ def main():
                 "frac": achieved / HBM_PEAK_GBPS,
                 "traffic": traffic,
                 "measured_copy_ceiling": copy_gbs,
-                "frac_of_copy_ceiling": achieved / copy_gbs if copy_gbs else None,
+                # the PMC-measured HBM bytes of one launch over its HIP-event time, against the copy
+                # ceiling ("achieved" prices the SURVEY formula's u32 rows; this layout moves fewer bytes)
+                "traffic_gbs": traffic / (kern_ms / max(1, launches) / 1e3) / 1e9 if traffic and kern_ms else None,
+                "traffic_frac_of_copy_ceiling": (traffic / (kern_ms / max(1, launches) / 1e3) / 1e9 / copy_gbs
+                                                 if traffic and kern_ms and copy_gbs else None),
                 "alg_bytes_per_launch": alg_survey / max(1, launches),
                 "alg_bytes_formula": "exchanges x 32 x N + pack_bytes (SURVEY 8(d) minus the FD term, see DESIGN.md)",
                 "in_kernel_bytes_per_launch": alg_local / max(1, launches),
