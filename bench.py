@@ -117,8 +117,8 @@ def run_round(sims, rd, events=None, group=None, sel=None):
         sim._chk(sim.L.gs_liveness(sim.h, C.c_void_p(rd["up"].data_ptr()), rd["t_live"]), "gs_liveness")
 
 
-def cpu_baseline(sim, spec, cfg, next_plan, sample: int, min_seconds: float = 10.0):
-    """The C oracle (one host core) on `sample` exchanges whose two rows are copied from the device."""
+def cpu_baseline(sim, spec, cfg, next_plan, sample: int, min_seconds: float = 10.0, threads: int = 1):
+    """The C oracle (`threads` host cores) on `sample` exchanges whose two rows are copied from the device."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle as orc_mod  # test infrastructure: the checker, timed here as the CPU baseline
 
@@ -135,17 +135,21 @@ def cpu_baseline(sim, spec, cfg, next_plan, sample: int, min_seconds: float = 10
     oc = orc_mod._Cfg(n, K, int(cfg["mtu"]), orc_mod.us(cfg["tombstone_grace_s"]), float(cfg["phi_threshold"]),
                       int(cfg["window"]), orc_mod.us(cfg["max_interval_s"]), orc_mod.us(cfg["initial_interval_s"]),
                       orc_mod.us(cfg["dead_grace_s"]))
-    h = L.orc_create(C.byref(oc), ns, kl)
+    # disjoint pairs from the first phase of the next round; `threads` host cores, one oracle handle
+    # each (the oracle keeps per-handle scratch), pairs dealt round-robin (one
+    # thread and threads over a phase, core count stated)
+    a_all, b_all, _, t = next_plan["phases"][0]
+    a_all, b_all = a_all.cpu().numpy(), b_all.cpu().numpy()
+    pairs = list(zip(a_all[:sample].tolist(), b_all[:sample].tolist()))
+    T = max(1, min(threads, len(pairs)))
+    hs = [L.orc_create(C.byref(oc), ns, kl) for _ in range(T)]
+    mine = [pairs[i::T] for i in range(T)]
     hist = sim.region("HIST", torch.int64, (n, Cc, K)).cpu().numpy().view(np.uint64)
     hist_ver = np.ascontiguousarray((hist & 0xFFFFFFFF).astype(np.uint32))
     hist_vid = sim.region("HIST_VID", torch.int32, (n, Cc, K)).cpu().numpy().view(np.uint32).copy()
     meta = (hist >> 32).astype(np.uint32)
     hist_vlen = (meta >> 18).astype(np.int32)
     hist_st = ((meta >> 16) & 3).astype(np.uint8)
-    # disjoint pairs from the first phase of the next round
-    a_all, b_all, _, t = next_plan["phases"][0]
-    a_all, b_all = a_all.cpu().numpy(), b_all.cpu().numpy()
-    pairs = list(zip(a_all[:sample].tolist(), b_all[:sample].tolist()))
     order = np.arange(n, dtype=np.int32)
 
     def rows(name, dt, shape):
@@ -161,45 +165,90 @@ def cpu_baseline(sim, spec, cfg, next_plan, sample: int, min_seconds: float = 10
     fdw = rows("FD", torch.int64, (n, NP))
     held = rows("HELD", torch.uint8, (n, NP, KP))
     P = C.c_void_p
-    for a, b in pairs:
-        for o in (a, b):
-            def g(x):
-                return np.ascontiguousarray(x[o, :n].cpu().numpy().view(np.uint32))
-            hb = np.ascontiguousarray(sim.decode_heartbeats(hb16[o].cpu().numpy())[:n])
-            mv = np.ascontiguousarray((mv16[o, :n].cpu().numpy().view(np.uint16) & 0x7FFF).astype(np.uint32))
-            fl, fs, fc = (np.ascontiguousarray(x) for x in sim.unpack_fd(fdw[o, :n].cpu().numpy()))
-            hw = np.ascontiguousarray(held[o, :n, :K].cpu().numpy())
-            L.orc_load_row(h, o, n, order.ctypes.data_as(P), hb.ctypes.data_as(P), mv.ctypes.data_as(P),
-                           g(gc).ctypes.data_as(P), hw.ctypes.data_as(P), Cc, hist_ver.ctypes.data_as(P),
-                           hist_vid.ctypes.data_as(P), hist_vlen.ctypes.data_as(P), hist_st.ctypes.data_as(P),
-                           fl.ctypes.data_as(P), fs.ctypes.data_as(P), fc.ctypes.data_as(P),
-                           g(fst).ctypes.data_as(P), 15625)
-    for a, b in pairs:
-        L.orc_snapshot_row(h, a)
-        L.orc_snapshot_row(h, b)
-    # repeat the same exchanges on restored rows until ~min_seconds of CPU work are timed
-    dt, reps = 0.0, 0
-    while dt < min_seconds or reps == 0:
-        if reps:
-            for a, b in pairs:
-                L.orc_restore_row(h, a)
-                L.orc_restore_row(h, b)
+    for h, prs in zip(hs, mine):
+        for a, b in prs:
+            for o in (a, b):
+                def g(x):
+                    return np.ascontiguousarray(x[o, :n].cpu().numpy().view(np.uint32))
+                hb = np.ascontiguousarray(sim.decode_heartbeats(hb16[o].cpu().numpy())[:n])
+                mv = np.ascontiguousarray((mv16[o, :n].cpu().numpy().view(np.uint16) & 0x7FFF).astype(np.uint32))
+                fl, fs, fc = (np.ascontiguousarray(x) for x in sim.unpack_fd(fdw[o, :n].cpu().numpy()))
+                hw = np.ascontiguousarray(held[o, :n, :K].cpu().numpy())
+                L.orc_load_row(h, o, n, order.ctypes.data_as(P), hb.ctypes.data_as(P), mv.ctypes.data_as(P),
+                               g(gc).ctypes.data_as(P), hw.ctypes.data_as(P), Cc, hist_ver.ctypes.data_as(P),
+                               hist_vid.ctypes.data_as(P), hist_vlen.ctypes.data_as(P), hist_st.ctypes.data_as(P),
+                               fl.ctypes.data_as(P), fs.ctypes.data_as(P), fc.ctypes.data_as(P),
+                               g(fst).ctypes.data_as(P), 15625)
+        for a, b in prs:
+            L.orc_snapshot_row(h, a)
+            L.orc_snapshot_row(h, b)
+
+    def restore(i):
+        for a, b in mine[i]:
+            L.orc_restore_row(hs[i], a)
+            L.orc_restore_row(hs[i], b)
+
+    def run(i):
+        for a, b in mine[i]:
+            L.orc_exchange(hs[i], a, b, t * 15625)
+
+    # one thread: every handle's pairs in turn, on restored rows, until ~min_seconds/3 are timed
+    dt1, reps1 = 0.0, 0
+    while dt1 < min_seconds / 3 or reps1 == 0:
+        if reps1:
+            for i in range(T):
+                restore(i)
         t0 = time.perf_counter()
-        for a, b in pairs:
-            L.orc_exchange(h, a, b, t * 15625)
-        dt += time.perf_counter() - t0
-        reps += 1
-    st = orc_mod._Stats()
-    L.orc_get_stats(h, C.byref(st))
-    L.orc_destroy(h)
+        for i in range(T):
+            run(i)
+        dt1 += time.perf_counter() - t0
+        reps1 += 1
+    # T threads (ctypes drops the GIL during each oracle call), a barrier around every timed pass
+    import threading
+    bar = threading.Barrier(T + 1)
+    stop = [False]
+
+    def worker(i):
+        while True:
+            bar.wait()  # restore
+            if stop[0]:
+                return
+            restore(i)
+            bar.wait()  # go
+            run(i)
+            bar.wait()  # done
+
+    ths = [threading.Thread(target=worker, args=(i,), daemon=True) for i in range(T)]
+    for th in ths:
+        th.start()
+    dtT, repsT = 0.0, 0
+    while dtT < min_seconds or repsT == 0:
+        bar.wait()
+        bar.wait()
+        t0 = time.perf_counter()
+        bar.wait()
+        dtT += time.perf_counter() - t0
+        repsT += 1
+    stop[0] = True
+    bar.wait()
+    for th in ths:
+        th.join()
+    nd = 0
+    for h in hs:
+        st = orc_mod._Stats()
+        L.orc_get_stats(h, C.byref(st))
+        nd += st.node_deltas
+        L.orc_destroy(h)
     return {
-        "value": len(pairs) * reps / dt,
+        "value": len(pairs) * repsT / dtT,
         "unit": "exchanges/s",
-        "cores": 1,
+        "cores": T,
         "kind": "port",
+        "single_core_value": len(pairs) * reps1 / dt1,
         "sample": f"{len(pairs)} exchanges (disjoint pairs of the next round's first phase) at N={n}, K={K} on "
-                  f"oracle rows copied from the device state after the timed rounds, run {reps}x on restored rows: "
-                  f"{dt:.1f} s of single-core CPU work, {st.node_deltas // reps} NodeDeltas per pass",
+                  f"oracle rows copied from the device state after the timed rounds, dealt to {T} host threads "
+                  f"(one oracle handle each) and run {repsT}x on restored rows ({dtT:.1f} s wall); one thread: "
+                  f"{reps1}x ({dt1:.1f} s); {nd // (reps1 + repsT)} NodeDeltas per pass",
     }
 
 
@@ -286,6 +335,8 @@ def main():
                          "only after ~15 rounds (SURVEY 8(d): time 20+ rounds after warm-up)")
     ap.add_argument("--cpu-sample", type=int, default=64)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-threads", type=int, default=min(16, len(os.sched_getaffinity(0))),
+                    help="host threads for the CPU baseline (the GPU box's CPU share is 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--slices", type=int, default=1, help="owner-column slices in this process (1-GPU rehearsal)")
     ap.add_argument("--mtu", type=int, default=65507)
@@ -409,7 +460,8 @@ def main():
     copy_gbs = copy_ceiling(torch, dev) if rank == 0 else None
     cpu = None
     if rank == 0 and group is None and not args.no_cpu_baseline:
-        cpu = cpu_baseline(sim, spec, cfg, plans[R0 + args.steps], args.cpu_sample, args.cpu_seconds)
+        cpu = cpu_baseline(sim, spec, cfg, plans[R0 + args.steps], args.cpu_sample, args.cpu_seconds,
+                           args.cpu_threads)
     if rank == 0:
         line = {
             "metric": ("REHEARSAL (one GPU's slice of a %d-GPU run, packing not the cluster's): exchanges/s"
