@@ -132,9 +132,11 @@ def load():
     global _LIB
     if _LIB is not None:
         return _LIB
-    if not os.path.exists(LIB_PATH):
-        raise GsError(f"{LIB_PATH} missing: run __graft_entry__.build() (hipcc, gfx950)")
-    L = C.CDLL(LIB_PATH)
+    # GS_LIB: an in-tree build variant (tuning sweeps); still the HIP library, never a fallback
+    path = os.environ.get("GS_LIB") or LIB_PATH
+    if not os.path.exists(path):
+        raise GsError(f"{path} missing: run __graft_entry__.build() (hipcc, gfx950)")
+    L = C.CDLL(path)
     P, u32, i32, u64 = C.c_void_p, C.c_uint32, C.c_int32, C.c_uint64
     sig = {
         "gs_api_version": (C.c_int, []),
