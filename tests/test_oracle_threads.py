@@ -1,0 +1,42 @@
+"""The C oracle keeps all of its state per handle, so bench.py's CPU baseline may run one
+handle per host thread: two handles replayed concurrently on two threads end bit-identical
+to a third replayed alone (CPU only; the oracle is test infrastructure, see oracle/oracle.py)."""
+
+import threading
+
+from helpers import compare_exports, make_backend
+from oracle import OracleSim
+
+from aiocluster_amd.scenario import make_scenario, replay
+from aiocluster_amd.workload import WorkloadSpec
+
+
+def test_oracle_handles_are_independent_across_threads():
+    spec = WorkloadSpec(n=96, k=8, fanout=3, seed=13, init="warm", write_frac=0.2, delete_frac=0.1,
+                        down_frac=0.1, down_rounds=3)
+    scen = make_scenario("thr96", spec, 12, {"mtu": 700, "window": 4, "tombstone_grace_s": 3,
+                                             "initial_interval_s": 1.0, "phi_threshold": 3.0})
+    alone = make_backend(OracleSim, scen)
+    replay(alone, scen)
+    want = alone.export()
+    pair = [make_backend(OracleSim, scen) for _ in range(2)]
+    errs = []
+
+    def run(b):
+        try:
+            replay(b, scen)
+        except Exception as e:  # surfaced below
+            errs.append(e)
+
+    ths = [threading.Thread(target=run, args=(b,)) for b in pair]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    assert not errs, errs
+    for b in pair:
+        assert compare_exports(b.export(), want) is None
+    st = alone.stats()
+    assert st["exchanges"] > 1000 and st["truncated"] > 0, st
+    for b in (alone, *pair):
+        b.close()
