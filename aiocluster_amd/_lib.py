@@ -60,7 +60,7 @@ ERRORS = {-1: "GS_E_INVALID", -2: "GS_E_UNBOUND", -3: "GS_E_HIP", -4: "GS_E_DEVI
 COUNTER_FIELDS = [
     "exchanges", "hb_reports", "node_deltas", "kvs_sent", "truncated", "delta_bytes", "alg_bytes", "hb_writes",
     "candidates", "live_pairs", "tomb_gc", "err_fd_overflow", "err_hist_full", "err_bad_index", "err_conflict",
-    "err_fd_gc", "err_insert", "fd_gc", "q9", "pack_bytes", "err_holes",
+    "err_fd_gc", "err_insert", "fd_gc", "q9", "pack_bytes", "err_holes", "err_hb_lag", "plane_flushes",
 ]
 
 # Every symbol include/gossip_sim.h declares (checked by tests/test_abi.py).
@@ -69,9 +69,11 @@ EXPORTS = [
     "gs_boot", "gs_warm", "gs_owner_writes", "gs_begin_round", "gs_run_phase", "gs_liveness", "gs_phi_row",
     "gs_read_counters", "gs_reset_counters", "gs_sync", "gs_shard_columns", "gs_phase_count", "gs_phase_pack", "gs_materialize_held", "gs_fd_census",
     "gs_select_peers", "gs_schedule_phases", "gs_set_events", "gs_emit_scratch_bytes", "gs_emit_digest", "gs_emit_delta",
+    "gs_check_heartbeat_lag", "gs_stream_copy", "gs_stream_read",
 ]
 
-API_VERSION = 7
+API_VERSION = 8
+MAX_PHASES = 64  # GS_MAX_PHASES
 
 
 class GsConfig(C.Structure):
@@ -94,7 +96,7 @@ class GsConfig(C.Structure):
 
 
 class GsCounters(C.Structure):
-    _fields_ = [(n, C.c_uint64) for n in COUNTER_FIELDS] + [("reserved", C.c_uint64 * 11)]
+    _fields_ = [(n, C.c_uint64) for n in COUNTER_FIELDS] + [("reserved", C.c_uint64 * (32 - len(COUNTER_FIELDS)))]
 
 
 CENSUS_FIELDS = ["up_pairs", "up_dead", "up_live", "down_pairs", "down_live"]
@@ -163,7 +165,11 @@ def load():
         "gs_fd_census": (C.c_int, [P, P, C.POINTER(GsCensus)]),
         "gs_set_events": (C.c_int, [P, P, u32, P]),
         "gs_select_peers": (C.c_int, [P, P, u32, P, u32, C.c_uint64, u32, P, P]),
-        "gs_schedule_phases": (C.c_int, [P, P, u32, P, C.c_uint64, u32, u32, P, P, P, C.POINTER(u32)]),
+        "gs_schedule_phases": (C.c_int, [P, P, u32, P, C.c_uint64, u32, u32, u32, P, P, P, C.POINTER(u32),
+                                         C.POINTER(u32)]),
+        "gs_check_heartbeat_lag": (C.c_int, [P]),
+        "gs_stream_copy": (C.c_int, [P, P, u64, P]),
+        "gs_stream_read": (C.c_int, [P, u64, u32, P, P]),
         "gs_emit_scratch_bytes": (C.c_int, [P, C.POINTER(u64)]),
         "gs_emit_digest": (C.c_int, [P, C.POINTER(GsWire), u32, u32, P, u64, C.POINTER(u64), P]),
         "gs_emit_delta": (C.c_int, [P, C.POINTER(GsWire), u32, u32, u32, P, u64, C.POINTER(u64), P]),

@@ -54,10 +54,12 @@ constexpr int LB = 256;  // liveness / elementwise workgroups
 constexpr int NSHARD = 64;
 constexpr uint32_t WIN = 16 * 64;  // positions per packer window (16 per lane)
 constexpr double TICK_S = 1.0 / 64.0;
+constexpr uint32_t HB_LAG_CHECK_EVERY = 1u << 14;  // round starts + phases between heartbeat-lag sweeps
 
 enum Ctr {
     C_EXCH = 0, C_REPORTS, C_ND, C_KVS, C_TRUNC, C_DBYTES, C_ALG, C_HBW, C_CAND, C_LIVE, C_TOMBGC,
     C_E_FDOVF, C_E_HIST, C_E_IDX, C_E_CONFLICT, C_E_FDGC, C_E_INSERT, C_FDGC, C_Q9, C_PACKB, C_E_HOLES,
+    C_E_HBLAG, C_FLUSH /* host-side: plane_flushes */,
     C_CEN0 = 24, C_NUM = C_CEN0 + 6  // gs_fd_census scratch slots (not part of gs_counters)
 };
 static_assert(C_NUM <= 32, "counter region");
@@ -95,7 +97,10 @@ struct Dev {
     uint64_t *pend;
     uint32_t *pstamp;  // [N][16]
     uint32_t PW;       // u64 words per plane row: NP rounded up to 256, / 64
-    uint32_t t_round;  // tick of the last gs_begin_round
+    // plane base: the tick of the last gs_begin_round, or, once a round has run phases more than 16
+    // ticks after it (the planes were replayed into the windows mid-round), the tick before the
+    // first phase after that replay; plane p holds the phase at tick t_round + 1 + p
+    uint32_t t_round;
     // event stream (gs_set_events): records {observer, owner, key | kind << 8, old version, new version,
     // tick}; kind 0 = on_key_change, 1 = node join, 2 = node leave.  ev == nullptr: off
     uint32_t *ev, *ev_count;
@@ -1067,13 +1072,15 @@ __global__ __launch_bounds__(LB) void k_reset_sched(Dev d, const uint8_t *up) {
 template <bool RING>
 // One workgroup sweeps `per` consecutive 1024-column chunks of one row (fewer, longer workgroups:
 // the per-workgroup plane staging, stamp check and counter atomics are paid once per `per` chunks).
+// decide = false: only replay the pending reports into the windows, for every row (a round with phases
+// more than 16 ticks after its plane base: the planes are emptied mid-round)
 __global__ __launch_bounds__(LB) void k_liveness(Dev d, const uint8_t *up, uint32_t t, uint32_t chunks,
-                                                 uint32_t per, bool replay) {
+                                                 uint32_t per, bool replay, bool decide) {
     __shared__ uint64_t s_pl[16][16];  // [phase][the 16 plane words of this chunk's 1024 columns]
     __shared__ uint32_t s_vm;
     const uint32_t groups = (chunks + per - 1) / per;
     const uint32_t o = blockIdx.x / groups, cb0 = (blockIdx.x % groups) * per;
-    const bool upo = up[o] != 0;
+    const bool upo = decide && up[o] != 0;
     const bool genm = !(d.flags & GS_CANONICAL);
     uint32_t minS = NONE, live = 0, gcdue = 0, ovf = 0, alg = 0;
     // phases of the current round in which row o was in an exchange (its plane rows are valid);
@@ -1318,6 +1325,26 @@ __global__ __launch_bounds__(LB) void k_phi_row(Dev d, uint32_t o, uint32_t t, d
         phi = ((double)(t - f.last) * TICK_S) / mean;
     }
     out[j] = phi;
+}
+
+// 16-bit heartbeats (hb_dec) are exact while every view lags its owner's own heartbeat by < 2^16.  An
+// owner's heartbeat grows by at most one per round start or phase, and the host runs this sweep at
+// least every 2^14 of those: if every decoded lag was < 2^15 at the previous sweep (and so exact), every
+// lag is < 2^15 + 2^14 < 2^16 until this one, so every decode in between was exact and this sweep's
+// decoded lags are the true ones -- a view at >= 2^15 is counted in err_hb_lag (the run is reported
+// inexact) before any decode can go wrong.
+__global__ __launch_bounds__(LB) void k_hb_lag(Dev d) {
+    const bool genm = !(d.flags & GS_CANONICAL);
+    const uint64_t total = (uint64_t)d.N * d.ncol;
+    uint32_t bad = 0;
+    for (uint64_t x = (uint64_t)blockIdx.x * LB + threadIdx.x; x < total; x += (uint64_t)gridDim.x * LB) {
+        const uint32_t o = (uint32_t)(x / d.ncol), j = (uint32_t)(x % d.ncol);
+        const size_t p = pix(d, o, j);
+        if (genm && d.pos[p] == NONE) continue;
+        if (((d.self_hb[j] - (uint32_t)d.hb[p]) & 0xFFFFu) >= 0x8000u) bad++;
+    }
+    const unsigned long long s = wave_sum(bad);
+    if ((threadIdx.x & 63) == 0) shard_add(d, C_E_HBLAG, s);
 }
 
 // ------------------------------------------------------------------ owner writes
@@ -1813,26 +1840,33 @@ __global__ __launch_bounds__(LB) void k_sel_resolve(Dev d, const uint8_t *up, co
 // out[e]; exchanges whose responder is down fail before any state change, as a refused
 // connection does, and are not scheduled).  Per phase p, IT rounds of a deterministic Luby
 // matching: an unscheduled exchange whose two endpoints are free in p takes p if its priority
-// key is the smallest at both endpoints.  Exchanges left after 16 phases are dropped.
+// key is the smallest at both endpoints.  Up to 64 phases (busy = one bit per phase and node);
+// exchanges left after the last phase are counted, not run.
 __device__ inline uint32_t fmix32(uint32_t h) {
     h ^= h >> 16; h *= 0x85EBCA6Bu; h ^= h >> 13; h *= 0xC2B2AE35u; h ^= h >> 16;
     return h;
 }
-__device__ inline bool luby_active(const int32_t *out, const uint8_t *up, const uint32_t *eph, const uint32_t *busy,
-                                   uint32_t e, uint32_t F, uint32_t p, uint32_t &a, uint32_t &b) {
-    if (eph[e] != NONE) return false;
+__device__ inline bool luby_valid(const int32_t *out, const uint8_t *up, uint32_t e, uint32_t F, uint32_t &a,
+                                  uint32_t &b) {
     const int32_t t = out[e];
     if (t < 0 || !up[t]) return false;
     a = e / (F + 2);
     b = (uint32_t)t;
-    return !((busy[a] >> p) & 1u) && !((busy[b] >> p) & 1u);
+    return true;
+}
+__device__ inline bool luby_active(const int32_t *out, const uint8_t *up, const uint32_t *eph,
+                                   const unsigned long long *busy, uint32_t e, uint32_t F, uint32_t p, uint32_t &a,
+                                   uint32_t &b) {
+    if (eph[e] != NONE) return false;
+    if (!luby_valid(out, up, e, F, a, b)) return false;
+    return !((busy[a] >> p) & 1ull) && !((busy[b] >> p) & 1ull);
 }
 __device__ inline unsigned long long luby_key(uint64_t seed, uint32_t round, uint32_t e, uint32_t p, uint32_t it) {
     const uint32_t h = fmix32(e ^ fmix32((uint32_t)seed ^ fmix32(round * 0x9E3779B9u + p * 0x632BE5ABu + it)));
     return ((unsigned long long)h << 32) | e;
 }
 __global__ __launch_bounds__(LB) void k_luby_min(const int32_t *out, const uint8_t *up, const uint32_t *eph,
-                                                 const uint32_t *busy, unsigned long long *best, uint32_t E,
+                                                 const unsigned long long *busy, unsigned long long *best, uint32_t E,
                                                  uint32_t F, uint64_t seed, uint32_t round, uint32_t p, uint32_t it) {
     const uint32_t e = blockIdx.x * LB + threadIdx.x;
     uint32_t a, b;
@@ -1841,10 +1875,11 @@ __global__ __launch_bounds__(LB) void k_luby_min(const int32_t *out, const uint8
     atomicMin(&best[a], k);
     atomicMin(&best[b], k);
 }
-__global__ __launch_bounds__(LB) void k_luby_pick(const int32_t *out, const uint8_t *up, uint32_t *eph, uint32_t *busy,
-                                                  const unsigned long long *best, unsigned long long *best_next,
-                                                  uint32_t E, uint32_t N, uint32_t F, uint64_t seed, uint32_t round,
-                                                  uint32_t p, uint32_t it, uint32_t *pcount) {
+__global__ __launch_bounds__(LB) void k_luby_pick(const int32_t *out, const uint8_t *up, uint32_t *eph,
+                                                  unsigned long long *busy, const unsigned long long *best,
+                                                  unsigned long long *best_next, uint32_t E, uint32_t N, uint32_t F,
+                                                  uint64_t seed, uint32_t round, uint32_t p, uint32_t it,
+                                                  uint32_t *pcount) {
     const uint32_t x = blockIdx.x * LB + threadIdx.x;
     if (x < N) best_next[x] = ~0ull;
     uint32_t a, b;
@@ -1852,10 +1887,19 @@ __global__ __launch_bounds__(LB) void k_luby_pick(const int32_t *out, const uint
     const unsigned long long k = luby_key(seed, round, x, p, it);
     if (best[a] == k && best[b] == k) {
         eph[x] = p;
-        atomicOr(&busy[a], 1u << p);
-        atomicOr(&busy[b], 1u << p);
+        atomicOr(&busy[a], 1ull << p);
+        atomicOr(&busy[b], 1ull << p);
         atomicAdd(&pcount[p], 1u);
     }
+}
+// valid exchanges not scheduled yet (pcount[64])
+__global__ __launch_bounds__(LB) void k_luby_left(const int32_t *out, const uint8_t *up, const uint32_t *eph,
+                                                  uint32_t E, uint32_t F, uint32_t *left) {
+    const uint32_t e = blockIdx.x * LB + threadIdx.x;
+    uint32_t a, b;
+    const bool l = e < E && eph[e] == NONE && luby_valid(out, up, e, F, a, b);
+    const unsigned long long m = __ballot(l);
+    if ((threadIdx.x & 63) == 0 && m) atomicAdd(left, (uint32_t)__popcll(m));
 }
 // scatter the scheduled exchanges into per-phase (initiator, responder) arrays
 __global__ __launch_bounds__(LB) void k_luby_scatter(const int32_t *out, const uint32_t *eph, uint32_t E, uint32_t F,
@@ -1869,6 +1913,35 @@ __global__ __launch_bounds__(LB) void k_luby_scatter(const int32_t *out, const u
     res[slot] = out[e];
 }
 
+// ------------------------------------------------------------------ measurement kernels
+// Streaming copy at 16 B per lane (4 loads in flight per lane, then 4 stores): the measured HBM
+// ceiling bench.py prices k_exchange against.  And a read-only stream at 8 or 16 B per lane whose
+// known byte count calibrates rocprofv3's FETCH_SIZE for the widths the exchange kernel uses.
+__global__ __launch_bounds__(256) void k_copy16(uint4 *__restrict__ dst, const uint4 *__restrict__ src, uint64_t n16) {
+    const uint64_t stride = (uint64_t)gridDim.x * 256u;
+    uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    for (; i + 3 * stride < n16; i += 4 * stride) {
+        const uint4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], e = src[i + 3 * stride];
+        dst[i] = a;
+        dst[i + stride] = b;
+        dst[i + 2 * stride] = c;
+        dst[i + 3 * stride] = e;
+    }
+    for (; i < n16; i += stride) dst[i] = src[i];
+}
+template <typename V>
+__global__ __launch_bounds__(256) void k_read(const V *__restrict__ src, uint64_t n, unsigned long long *sink) {
+    const uint64_t stride = (uint64_t)gridDim.x * 256u;
+    uint32_t acc = 0;
+    uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    for (; i + 3 * stride < n; i += 4 * stride) {
+        const V a = src[i], b = src[i + stride], c = src[i + 2 * stride], e = src[i + 3 * stride];
+        acc ^= a.x ^ b.x ^ c.x ^ e.x ^ a.y ^ b.y ^ c.y ^ e.y;
+    }
+    for (; i < n; i += stride) acc ^= src[i].x ^ src[i].y;
+    if (acc == 0x9E3779B9u) atomicAdd(sink, 1ull);  // keeps the loads; practically never taken
+}
+
 }  // namespace
 
 // ====================================================================== C ABI
@@ -1880,6 +1953,8 @@ struct gs_handle {
     bool reports_pending;             // phases ran since the last gs_liveness
     bool round_open;                  // gs_begin_round ran and gs_liveness has not closed the round yet
     uint32_t last_phase_tick;
+    uint64_t plane_flushes;           // mid-round report replays (rounds with phases > 16 ticks after the base)
+    uint32_t hb_incs;                 // rounds + phases since the last heartbeat-lag check (gs_check_heartbeat_lag)
     void *reg[GS_NUM_REGIONS];
     uint64_t bytes[GS_NUM_REGIONS];
     hipStream_t stream;
@@ -1955,12 +2030,40 @@ size_t exchange_lds(const gs_handle *h) {
     return WIN * 2 * 2 + (size_t)(h->NP / 32) * (genm ? 4 : 2) * 4;
 }
 
-int check_phase(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t n, uint32_t tick) {
+int launch_liveness(gs_handle *h, const uint8_t *up, uint32_t tick, bool replay, bool decide) {
+    const uint32_t chunks = (h->ncol + 4 * LB - 1) / (4 * LB);
+    const uint32_t per = LIVE_PER, groups = (chunks + per - 1) / per;
+    if (h->cfg.flags & GS_FD_RING)
+        k_liveness<true><<<groups * h->N, LB, 0, h->stream>>>(h->d, up, tick, chunks, per, replay, decide);
+    else
+        k_liveness<false><<<groups * h->N, LB, 0, h->stream>>>(h->d, up, tick, chunks, per, replay, decide);
+    HIPCHK(h, hipGetLastError());
+    return GS_OK;
+}
+
+// A phase more than 16 ticks after the plane base: replay the pending report planes into the sampling
+// windows now (nothing reads a window before the round's liveness sweep, and the replay applies the
+// same reports in the same tick order), then start a new plane base just before this phase.
+int advance_planes(gs_handle *h, uint32_t tick) {
+    if (tick - h->d.t_round <= 16u) return GS_OK;
+    if (h->reports_pending) {
+        int rc = launch_liveness(h, nullptr, tick, true, false);
+        if (rc) return rc;
+        h->plane_flushes++;
+    }
+    h->d.t_round = tick - 1u;
+    return GS_OK;
+}
+
+// pack = true: gs_phase_pack, which completes the phase gs_phase_count started at the same tick
+int check_phase(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t n, uint32_t tick, bool pack = false) {
     if (!h || !h->booted) return GS_E_INVALID;
     if (!h->round_open)
         return fail(h, GS_E_INVALID, "phases run between gs_begin_round and gs_liveness (the round is closed)");
-    if (tick <= h->d.t_round || tick - h->d.t_round > 16u)
-        return fail(h, GS_E_INVALID, "phase tick %u outside (round tick %u, round tick + 16]", tick, h->d.t_round);
+    if (pack ? tick != h->last_phase_tick : tick <= h->last_phase_tick)
+        return fail(h, GS_E_INVALID, "phase tick %u %s (tick %u)", tick,
+                    pack ? "is not the tick of the last gs_phase_count" : "not after the round start / previous phase",
+                    h->last_phase_tick);
     if (n && (!ini || !res)) return GS_E_INVALID;
     if (n > h->N / 2) return fail(h, GS_E_INVALID, "a phase has at most n_nodes/2 exchanges (got %u)", n);
     if (exchange_lds(h) > 160 * 1024)
@@ -2160,11 +2263,26 @@ int gs_begin_round(gs_handle *h, const uint8_t *up, uint32_t tick) {
     if (!h || !h->booted || !up) return GS_E_INVALID;
     if (h->reports_pending)
         return fail(h, GS_E_INVALID, "gs_begin_round: the previous round's phases were not closed by gs_liveness");
+    if (h->hb_incs >= HB_LAG_CHECK_EVERY) {
+        int rc = gs_check_heartbeat_lag(h);
+        if (rc) return rc;
+    }
     h->d.t_round = tick;
     h->last_phase_tick = tick;
     k_begin_round<<<h->N, LB, 0, h->stream>>>(h->d, up, tick);
     HIPCHK(h, hipGetLastError());
     h->round_open = true;
+    h->hb_incs++;
+    return GS_OK;
+}
+
+int gs_check_heartbeat_lag(gs_handle *h) {
+    if (!h || !h->booted) return GS_E_INVALID;
+    const uint64_t pairs = (uint64_t)h->N * h->ncol;
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>((pairs + LB - 1) / LB, 1u << 16);
+    k_hb_lag<<<blocks, LB, 0, h->stream>>>(h->d);
+    HIPCHK(h, hipGetLastError());
+    h->hb_incs = 0;
     return GS_OK;
 }
 
@@ -2173,12 +2291,14 @@ int gs_run_phase(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t 
     if (rc) return rc;
     if (h->G > 1) return fail(h, GS_E_UNSUPPORTED, "sliced handle: use gs_phase_count / gs_phase_pack");
     if (!n) return GS_OK;
+    if ((rc = advance_planes(h, tick))) return rc;
     const bool genm = !(h->cfg.flags & GS_CANONICAL);
     const size_t lds = exchange_lds(h);
     const SliceIO io{};
     h->seq += 1;
     h->reports_pending = true;
-    h->last_phase_tick = std::max(h->last_phase_tick, tick);
+    h->last_phase_tick = tick;
+    h->hb_incs++;
     if (h->KP <= 16) return genm ? launch_exchange<4, true, 0>(h, ini, res, n, tick, lds, io)
                                  : launch_exchange<4, false, 0>(h, ini, res, n, tick, lds, io);
     return genm ? launch_exchange<16, true, 0>(h, ini, res, n, tick, lds, io)
@@ -2199,19 +2319,22 @@ int gs_phase_count(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_
     if (h->G < 2) return fail(h, GS_E_UNSUPPORTED, "gs_phase_count needs a sliced handle (n_shards > 1)");
     if (!n) return GS_OK;
     if (!slice_bytes) return GS_E_INVALID;
+    if ((rc = advance_planes(h, tick))) return rc;
     const size_t lds = exchange_lds(h);
     SliceIO io{};
     io.tot = slice_bytes;
     h->seq += 1;
     h->reports_pending = true;
-    h->last_phase_tick = std::max(h->last_phase_tick, tick);
+    h->last_phase_tick = tick;
+    h->hb_incs++;
     if (h->KP <= 16) return launch_exchange<4, false, 1>(h, ini, res, n, tick, lds, io);
     return launch_exchange<16, false, 1>(h, ini, res, n, tick, lds, io);
 }
 
 int gs_phase_pack(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t n, uint32_t tick, uint32_t step,
                   const uint64_t *slice_bytes_all, const uint64_t *chain_all, uint64_t *chain) {
-    int rc = check_phase(h, ini, res, n, tick);
+    if (h && !n) return GS_OK;
+    int rc = check_phase(h, ini, res, n, tick, true);
     if (rc) return rc;
     if (h->G < 2) return fail(h, GS_E_UNSUPPORTED, "gs_phase_pack needs a sliced handle (n_shards > 1)");
     if (!n) return GS_OK;
@@ -2234,14 +2357,8 @@ int gs_liveness(gs_handle *h, const uint8_t *up, uint32_t tick) {
         return fail(h, GS_E_INVALID, "gs_liveness at tick %u precedes a phase at tick %u", tick, h->last_phase_tick);
     k_reset_sched<<<(h->N + LB - 1) / LB, LB, 0, h->stream>>>(h->d, up);
     HIPCHK(h, hipGetLastError());
-    const uint32_t chunks = (h->ncol + 4 * LB - 1) / (4 * LB);
-    const uint32_t per = LIVE_PER, groups = (chunks + per - 1) / per;
-    const bool replay = h->reports_pending;
-    if (h->cfg.flags & GS_FD_RING)
-        k_liveness<true><<<groups * h->N, LB, 0, h->stream>>>(h->d, up, tick, chunks, per, replay);
-    else
-        k_liveness<false><<<groups * h->N, LB, 0, h->stream>>>(h->d, up, tick, chunks, per, replay);
-    HIPCHK(h, hipGetLastError());
+    int rc = launch_liveness(h, up, tick, h->reports_pending, true);
+    if (rc) return rc;
     h->reports_pending = false;  // replayed
     h->round_open = false;
     if (!(h->cfg.flags & GS_CANONICAL)) {
@@ -2381,6 +2498,8 @@ int gs_read_counters(gs_handle *h, gs_counters *out) {
     uint64_t acc[32] = {0};
     for (int s = 0; s < NSHARD; s++)
         for (int c = 0; c < 32; c++) acc[c] += buf[(size_t)s * 32 + c];
+    acc[C_FLUSH] = h->plane_flushes;
+    for (int c = C_CEN0; c < 32; c++) acc[c] = 0;  // census scratch, not counters
     memcpy(out, acc, sizeof acc);
     return GS_OK;
 }
@@ -2388,6 +2507,7 @@ int gs_read_counters(gs_handle *h, gs_counters *out) {
 int gs_reset_counters(gs_handle *h) {
     if (!h || !h->reg[GS_R_COUNTERS]) return GS_E_INVALID;
     HIPCHK(h, hipMemsetAsync(h->reg[GS_R_COUNTERS], 0, h->bytes[GS_R_COUNTERS], h->stream));
+    h->plane_flushes = 0;
     return GS_OK;
 }
 
@@ -2416,42 +2536,59 @@ int gs_select_peers(gs_handle *h, const uint8_t *up, uint32_t fanout, const int3
 }
 
 int gs_schedule_phases(gs_handle *h, const uint8_t *up, uint32_t fanout, const int32_t *targets, uint64_t seed,
-                       uint32_t round, uint32_t iters, void *scratch, int32_t *initiators, int32_t *responders,
-                       uint32_t *phase_offsets) {
-    if (!h || !up || !targets || !scratch || !initiators || !responders || !phase_offsets || fanout < 1 ||
-        fanout > 8 || iters < 1)
+                       uint32_t round, uint32_t iters, uint32_t max_phases, void *scratch, int32_t *initiators,
+                       int32_t *responders, uint32_t *phase_offsets, uint32_t *unscheduled) {
+    if (!h || !up || !targets || !scratch || !initiators || !responders || !phase_offsets || !unscheduled ||
+        fanout < 1 || fanout > 8 || iters < 1 || max_phases < 1 || max_phases > GS_MAX_PHASES)
         return GS_E_INVALID;
     const uint32_t N = h->N, E = N * (fanout + 2);
-    // scratch: eph[E] | busy[N] | pcount[16] | pfill[16] | poff[16] | pad | best[2][N] (u64)
+    // scratch: eph[E] | pcount[64] | pfill[64] | poff[64] | left[64] | busy[N] (u64) | best[2][N] (u64)
     uint32_t *eph = (uint32_t *)scratch;
-    uint32_t *busy = eph + E;
-    uint32_t *pcount = busy + N;
-    uint32_t *pfill = pcount + 16;
-    uint32_t *poff = pfill + 16;
-    unsigned long long *best = (unsigned long long *)(((uintptr_t)(poff + 16) + 15) & ~(uintptr_t)15);
+    uint32_t *pcount = eph + E;
+    uint32_t *pfill = pcount + 64;
+    uint32_t *poff = pfill + 64;
+    uint32_t *left = poff + 64;
+    unsigned long long *busy = (unsigned long long *)(((uintptr_t)(left + 64) + 15) & ~(uintptr_t)15);
+    unsigned long long *best = busy + N;
     hipStream_t s = h->stream;
     HIPCHK(h, hipMemsetAsync(eph, 0xFF, (size_t)E * 4, s));
-    HIPCHK(h, hipMemsetAsync(busy, 0, (size_t)(N + 48) * 4, s));
+    HIPCHK(h, hipMemsetAsync(pcount, 0, 4 * 64 * 4, s));
+    HIPCHK(h, hipMemsetAsync(busy, 0, (size_t)N * 8, s));
     HIPCHK(h, hipMemsetAsync(best, 0xFF, (size_t)N * 16, s));
     const uint32_t gE = (std::max(E, N) + LB - 1) / LB;
-    for (uint32_t p = 0; p < 16; p++)
-        for (uint32_t it = 0; it < iters; it++) {
-            unsigned long long *b0 = best + (size_t)(it & 1) * N, *b1 = best + (size_t)((it + 1) & 1) * N;
-            k_luby_min<<<(E + LB - 1) / LB, LB, 0, s>>>(targets, up, eph, busy, b0, E, fanout, seed, round, p, it);
-            k_luby_pick<<<gE, LB, 0, s>>>(targets, up, eph, busy, b0, b1, E, N, fanout, seed, round, p, it, pcount);
-        }
-    HIPCHK(h, hipGetLastError());
-    uint32_t cnt[16];
+    // the two minimum buffers alternate by the GLOBAL iteration index, so each pick resets exactly
+    // the buffer the next iteration (of this phase or the next) reduces into, whatever iters is
+    uint32_t g = 0, nleft = 0;
+    for (uint32_t p0 = 0; p0 < max_phases; p0 += 16) {
+        const uint32_t p1 = std::min(max_phases, p0 + 16u);
+        for (uint32_t p = p0; p < p1; p++)
+            for (uint32_t it = 0; it < iters; it++, g++) {
+                unsigned long long *b0 = best + (size_t)(g & 1) * N, *b1 = best + (size_t)((g + 1) & 1) * N;
+                k_luby_min<<<(E + LB - 1) / LB, LB, 0, s>>>(targets, up, eph, busy, b0, E, fanout, seed, round, p,
+                                                            it);
+                k_luby_pick<<<gE, LB, 0, s>>>(targets, up, eph, busy, b0, b1, E, N, fanout, seed, round, p, it,
+                                              pcount);
+            }
+        // after every 16 phases: stop once every valid exchange has a phase
+        HIPCHK(h, hipMemsetAsync(left + p0 / 16, 0, 4, s));
+        k_luby_left<<<(E + LB - 1) / LB, LB, 0, s>>>(targets, up, eph, E, fanout, left + p0 / 16);
+        HIPCHK(h, hipGetLastError());
+        HIPCHK(h, hipMemcpyAsync(&nleft, left + p0 / 16, 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(h, hipStreamSynchronize(s));
+        if (!nleft) break;
+    }
+    uint32_t cnt[GS_MAX_PHASES];
     HIPCHK(h, hipMemcpyAsync(cnt, pcount, sizeof cnt, hipMemcpyDeviceToHost, s));
     HIPCHK(h, hipStreamSynchronize(s));
-    uint32_t off[17];
+    std::vector<uint32_t> off(max_phases + 1);
     off[0] = 0;
-    for (int p = 0; p < 16; p++) off[p + 1] = off[p] + cnt[p];
-    HIPCHK(h, hipMemcpyAsync(poff, off, 16 * 4, hipMemcpyHostToDevice, s));
+    for (uint32_t p = 0; p < max_phases; p++) off[p + 1] = off[p] + cnt[p];
+    HIPCHK(h, hipMemcpyAsync(poff, off.data(), max_phases * 4, hipMemcpyHostToDevice, s));
     k_luby_scatter<<<(E + LB - 1) / LB, LB, 0, s>>>(targets, eph, E, fanout, poff, pfill, initiators, responders);
     HIPCHK(h, hipGetLastError());
     HIPCHK(h, hipStreamSynchronize(s));
-    memcpy(phase_offsets, off, sizeof off);
+    memcpy(phase_offsets, off.data(), (max_phases + 1) * 4);
+    *unscheduled = nleft;
     return GS_OK;
 }
 
@@ -2474,6 +2611,24 @@ int gs_fd_census(gs_handle *h, const uint8_t *up, gs_census *out) {
     out->down_pairs = acc[3];
     out->down_live = acc[4];
     return GS_OK;
+}
+
+int gs_stream_copy(void *dst, const void *src, uint64_t bytes, void *stream) {
+    if (!dst || !src || (bytes & 15u) || ((uintptr_t)dst & 15u) || ((uintptr_t)src & 15u)) return GS_E_INVALID;
+    k_copy16<<<2048, 256, 0, (hipStream_t)stream>>>((uint4 *)dst, (const uint4 *)src, bytes / 16);
+    return hipGetLastError() == hipSuccess ? GS_OK : GS_E_HIP;
+}
+
+int gs_stream_read(const void *src, uint64_t bytes, uint32_t width, uint64_t *sink, void *stream) {
+    if (!src || !sink || (width != 8 && width != 16) || (bytes % width) || ((uintptr_t)src & 15u))
+        return GS_E_INVALID;
+    if (width == 8)
+        k_read<uint2><<<2048, 256, 0, (hipStream_t)stream>>>((const uint2 *)src, bytes / 8,
+                                                              (unsigned long long *)sink);
+    else
+        k_read<uint4><<<2048, 256, 0, (hipStream_t)stream>>>((const uint4 *)src, bytes / 16,
+                                                              (unsigned long long *)sink);
+    return hipGetLastError() == hipSuccess ? GS_OK : GS_E_HIP;
 }
 
 int gs_sync(gs_handle *h) {

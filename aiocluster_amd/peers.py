@@ -18,26 +18,29 @@ import ctypes as C
 
 import numpy as np
 
-from ._lib import GsError
+from ._lib import MAX_PHASES, GsError
 
 
 class PeerSelector:
     """Device buffers for one cluster's per-round peer selection and phase schedule."""
 
-    def __init__(self, sim, fanout: int = 3, seeds=(), seed: int = 0, iters: int = 4):
+    def __init__(self, sim, fanout: int = 3, seeds=(), seed: int = 0, iters: int = 4, max_phases: int = 62):
         if sim.shards > 1:
             raise GsError("peer selection needs the whole matrix (one slice)")
         if not 1 <= fanout <= 8:
             raise GsError("fanout must be in 1..8")
         torch = sim.torch
+        if not 1 <= max_phases <= MAX_PHASES:
+            raise GsError(f"max_phases must be in 1..{MAX_PHASES}")
         self.sim, self.fanout, self.seed, self.iters = sim, int(fanout), int(seed), int(iters)
+        self.max_phases = int(max_phases)
         n, F = sim.n, self.fanout
         dev = sim.device
         self.seeds = torch.tensor(sorted(set(int(x) for x in seeds)) or [0], dtype=torch.int32, device=dev)
         self.n_seeds = len(set(seeds))
         self.targets = torch.empty((n, F + 2), dtype=torch.int32, device=dev)
         self.sel_scratch = torch.empty(4 * n * (F + 6), dtype=torch.uint8, device=dev)
-        self.sched_scratch = torch.empty(4 * (n * (F + 6) + 64) + 16 * n, dtype=torch.uint8, device=dev)
+        self.sched_scratch = torch.empty(4 * n * (F + 2) + 24 * n + 1040, dtype=torch.uint8, device=dev)
         self.ini = torch.empty(n * (F + 2), dtype=torch.int32, device=dev)
         self.res = torch.empty(n * (F + 2), dtype=torch.int32, device=dev)
 
@@ -51,18 +54,22 @@ class PeerSelector:
         return self.targets
 
     def schedule(self, up_dev, r: int):
-        """gs_schedule_phases: [(initiators, responders, n)] per non-empty phase (device views), and
-        the number of exchanges that did not fit in 16 phases."""
+        """gs_schedule_phases: ``(phases, offsets, unscheduled)`` -- [(initiators, responders, n)] per
+        non-empty phase (device views), the phase offsets (``offsets[-1]`` = exchanges scheduled) and the
+        number of selected exchanges with an up responder that did not fit in ``max_phases`` phases
+        (``_gossip_multiple`` contacts every selected peer, server.py:476-493: callers assert 0)."""
         s = self.sim
-        off = (C.c_uint32 * 17)()
+        P = self.max_phases
+        off = (C.c_uint32 * (P + 1))()
+        left = C.c_uint32()
         s._chk(s.L.gs_schedule_phases(s.h, C.c_void_p(up_dev.data_ptr()), self.fanout,
-                                      C.c_void_p(self.targets.data_ptr()), self.seed, r, self.iters,
+                                      C.c_void_p(self.targets.data_ptr()), self.seed, r, self.iters, P,
                                       C.c_void_p(self.sched_scratch.data_ptr()), C.c_void_p(self.ini.data_ptr()),
-                                      C.c_void_p(self.res.data_ptr()), off), "gs_schedule_phases")
+                                      C.c_void_p(self.res.data_ptr()), off, C.byref(left)), "gs_schedule_phases")
         offs = list(off)
         phases = [(self.ini[offs[p]:offs[p + 1]], self.res[offs[p]:offs[p + 1]], offs[p + 1] - offs[p])
-                  for p in range(16) if offs[p + 1] > offs[p]]
-        return phases, offs
+                  for p in range(P) if offs[p + 1] > offs[p]]
+        return phases, offs, int(left.value)
 
     def scheduled_pairs(self, phases) -> list[set]:
         """Host copy of a schedule: one set of (initiator, responder) per phase."""
@@ -80,8 +87,10 @@ def run_selected_round(sim, sel: PeerSelector, r: int, up, writes=None, tick0: i
             sim.write(t, j, k, op, v)
     sim.begin_round(t, up_dev)
     sel.select(up_dev, r)  # live / dead sets of the previous round's liveness (server.py:448-469)
-    phases, offs = sel.schedule(up_dev, r)
+    phases, offs, left = sel.schedule(up_dev, r)
+    if left:
+        raise GsError(f"round {r}: {left} selected exchanges did not fit in {sel.max_phases} phases")
     for p, (a, b, n) in enumerate(phases):
         sim.run_phase_arrays(phase_tick(r, p), a, b)
     sim.update_node_liveness(liveness_tick(r, len(phases)), up_dev)
-    return {"phases": len(phases), "exchanges": offs[16]}
+    return {"phases": len(phases), "exchanges": offs[-1]}

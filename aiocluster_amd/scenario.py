@@ -76,6 +76,30 @@ def state_hash(state) -> str:
     return hashlib.sha256(json.dumps(state, separators=(",", ":")).encode()).hexdigest()
 
 
+# fields of an ``export()`` dict that the compact digest covers, with their canonical dtypes
+DIGEST_FIELDS = {
+    "pos": "<i4", "hb": "<u4", "mv": "<u4", "gc": "<u4", "kv_version": "<u4", "kv_status": "<i4",
+    "kv_ts": "<i8", "fd_last": "<i8", "fd_len": "<i4", "fd_sum": "<f8", "live": "<i4", "tod": "<i8",
+}
+
+
+def export_digest(ex: dict, fields=None) -> dict[str, str]:
+    """SHA-256 per field of an ``export()`` dict (every observer row, every owner column), for
+    fixtures too large to store as canonical JSON states (config 2: 1,024 x 1,024 views x 64 keys).
+    Every backend's export has the same layout: ``pos`` = dict position or -1, times in ticks,
+    ``kv_ts`` only where the status is not SET, ``fd_last`` -1 without a window; values are left
+    out (an owner's version identifies its write, so the versions pin the values)."""
+    import numpy as np
+
+    out = {}
+    for name, dt in (fields or DIGEST_FIELDS).items():
+        a = np.asarray(ex[name])
+        if name == "kv_ts":
+            a = np.where(np.asarray(ex["kv_status"]) != 0, a, 0)
+        out[name] = hashlib.sha256(np.ascontiguousarray(a.astype(dt)).tobytes()).hexdigest()
+    return out
+
+
 def replay(backend, scen: dict, on_round=None, rounds: int | None = None):
     """Drive ``backend`` through ``scen``'s rounds (backend already booted at tick 0).
 

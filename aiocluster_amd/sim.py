@@ -347,6 +347,11 @@ class GossipSim:
     def sync(self):
         self._chk(self.L.gs_sync(self.h), "gs_sync")
 
+    def check_heartbeat_lag(self):
+        """gs_check_heartbeat_lag: count views lagging their owner by >= 2^15 heartbeats in err_hb_lag
+        (gs_begin_round also runs it every 2^14 round starts + phases)."""
+        self._chk(self.L.gs_check_heartbeat_lag(self.h), "gs_check_heartbeat_lag")
+
     # --------------------------------------------------------------- hook events
     def enable_events(self, capacity: int = 1 << 20):
         """gs_set_events: record on_key_change / on_node_join / on_node_leave (see drain_events)."""
@@ -366,7 +371,11 @@ class GossipSim:
         self.sync()
         n = int(self._ev_count.item())
         if n > self._ev.shape[0]:
-            raise GsError(f"event buffer overflow: {n} events, capacity {self._ev.shape[0]}")
+            # reset first, so the next drain starts clean (the caller can resize with enable_events)
+            self._ev_count.zero_()
+            self.sync()
+            raise GsError(f"event buffer overflow: {n} events, capacity {self._ev.shape[0]} "
+                          f"(the records of this drain are lost; enable_events with a larger capacity)")
         ev = self._ev[:n].cpu().numpy().view(np.uint32)
         self._ev_count.zero_()
         order = np.lexsort(ev.T[::-1])
@@ -403,42 +412,56 @@ class GossipSim:
         return mv.to(self.torch.int32) & 0x7FFF
 
     # --------------------------------------------------------------- readback
-    def _host(self):
+    def _host(self, rows=None):
+        """Host copies of the state; ``rows`` = observer rows to read (default: all of them)."""
         n, NP, KP, K, Cc = self.n, self.np_, self.kp, self.k, self.hist_cap
         torch = self.torch
-        self.materialize_held()
+        if rows is None:
+            self.materialize_held()
+            sel = slice(None)
+        else:
+            rows = np.asarray(rows, dtype=np.int64)
+            for o in rows.tolist():
+                self.materialize_held(o, o + 1)
+            sel = torch.as_tensor(rows, device=self.device)
         self.sync()
-        g = {}
-        g["HB"] = self.decode_heartbeats(self.region("HB", torch.int16, (n, NP)).cpu().numpy())
-        for name in ("GC", "FD_STATE"):
+
+        def rd(name, dt, shape):
+            t = self.region(name, dt, shape)
+            return (t if rows is None else t.index_select(0, sel)).cpu().numpy()
+
+        g = {"rows": np.arange(n) if rows is None else rows}
+        g["HB"] = self.decode_heartbeats(rd("HB", torch.int16, (n, NP)))
+        for name in ("GC", "FD_STATE", "POS"):
             if name in self.regions:
-                g[name] = self.region(name, torch.int32, (n, NP)).cpu().numpy().view(np.uint32)
-        mv = self.region("MV", torch.int16, (n, NP)).cpu().numpy().view(np.uint16).astype(np.uint32)
+                g[name] = rd(name, torch.int32, (n, NP)).view(np.uint32)
+        mv = rd("MV", torch.int16, (n, NP)).view(np.uint16).astype(np.uint32)
         g["MV_INEXACT"] = (mv >> np.uint32(15)).astype(np.uint8)  # prefix-view flag (GS_MV_INEXACT)
         g["MV"] = mv & np.uint32(0x7FFF)
+        nr = g["MV"].shape[0]
         if "GC" not in g:  # no tombstone GC: last_gc_version is 0 everywhere
-            g["GC"] = np.zeros((n, NP), dtype=np.uint32)
-        g["FD_LAST"], g["FD_SUM"], g["FD_CNT"] = self.unpack_fd(self.region("FD", torch.int64, (n, NP)).cpu().numpy())
+            g["GC"] = np.zeros((nr, NP), dtype=np.uint32)
+        g["FD_LAST"], g["FD_SUM"], g["FD_CNT"] = self.unpack_fd(rd("FD", torch.int64, (n, NP)))
         nc = self.ncol
         hist = self.region("HIST", torch.int64, (nc, Cc, K)).cpu().numpy().view(np.uint64)
         g["HIST_VER"] = (hist & 0xFFFFFFFF).astype(np.uint32)
         if "HELD" in self.regions:
-            g["HELD"] = self.region("HELD", torch.uint8, (n, NP, KP)).cpu().numpy()
+            g["HELD"] = rd("HELD", torch.uint8, (n, NP, KP))
         else:  # GS_NO_HELD: every view is S_j(max_version); count each key's writes <= max_version
             last_w = self.region("LAST_W", torch.uint8, (nc, KP)).cpu().numpy()[:, :K].astype(np.int64)
             M = g["MV"][:, :nc].astype(np.int64)
-            held = np.zeros((n, NP, KP), dtype=np.uint8)
+            held = np.zeros((nr, NP, KP), dtype=np.uint8)
             for w in range(1, Cc):
                 ok = (w <= last_w) & (g["HIST_VER"][:, w, :] > 0)  # [nc, K]
                 held[:, :nc, :K] += (ok[None, :, :] & (g["HIST_VER"][None, :, w, :] <= M[:, :, None])).astype(np.uint8)
             g["HELD"] = held
         g["HIST_META"] = (hist >> 32).astype(np.uint32)
         g["HIST_VID"] = self.region("HIST_VID", torch.int32, (nc, Cc, K)).cpu().numpy().view(np.uint32)
-        g["ROW"] = self.region("ROW", torch.int32, (n, 4)).cpu().numpy().view(np.uint32)
+        g["ROW"] = rd("ROW", torch.int32, (n, 4)).view(np.uint32)
         if "TS" in self.regions:
-            g["TS"] = self.region("TS", torch.int32, (n, NP, KP)).cpu().numpy().view(np.uint32)
+            g["TS"] = rd("TS", torch.int32, (n, NP, KP)).view(np.uint32)
         if "ORD" in self.regions:
-            g["ORD"] = self.region("ORD", torch.int32, (n, NP)).cpu().numpy().view(np.uint32)
+            g["ORD"] = rd("ORD", torch.int32, (n, NP)).view(np.uint32)
         return g
 
     def export(self, g=None) -> dict:
@@ -446,7 +469,8 @@ class GossipSim:
 
         A column slice exports its own owner columns (``ShardGroup.export`` joins them)."""
         g = self._host() if g is None else g
-        nr, n, K = self.n, self.ncol, self.k
+        n, K = self.ncol, self.k
+        nr = g["MV"].shape[0]
         held = g["HELD"][:, :n, :K].astype(np.int64)
         jj = np.arange(n)[None, :, None]
         kk = np.arange(K)[None, None, :]
@@ -463,7 +487,7 @@ class GossipSim:
         if self.canonical:
             out["pos"] = np.broadcast_to(np.arange(self.col_lo, self.col_lo + n, dtype=np.int32), (nr, n)).copy()
         else:
-            pos = self.region("POS", self.torch.int32, (n, self.np_)).cpu().numpy()[:, :n]
+            pos = g["POS"][:, :n].view(np.int32)
             out["pos"] = np.where(pos == -1, -1, pos).astype(np.int32)
         ts = g["TS"][:, :n, :K].astype(np.int64) if "TS" in g else np.zeros((nr, n, K), np.int64)
         out["kv_ts"] = np.where(out["kv_status"] != 0, ts, 0)
@@ -477,6 +501,11 @@ class GossipSim:
         out["live"] = (st == 1).astype(np.int32)
         out["tod"] = np.where(st >= 2, st.astype(np.int64) - 2, -1)
         return out
+
+    def export_rows(self, rows) -> dict:
+        """``export()`` of the observer rows ``rows`` only (full-size parity checks: a few rows of a
+        65,536-node matrix)."""
+        return self.export(self._host(rows))
 
     def unpack_fd(self, packed: np.ndarray):
         """Split packed windows (GS_R_FD) into (last tick or GS_NONE, sum in ticks, appended count)."""
@@ -546,17 +575,44 @@ class GossipSim:
 
     # --------------------------------------------------------------- reference-shaped views
     def node_state(self, observer: int, owner: int) -> NodeState | None:
-        """``ClusterState.node_state`` of ``observer`` for ``owner`` (state.py:295-296)."""
+        """``ClusterState.node_state`` of ``observer`` for ``owner`` (state.py:295-296).  Reads only
+        that view (a few bytes of the observer's row) and the owner's history rows."""
         self._whole()
-        g = self._host()
-        if owner not in self._order(g, observer):
-            return None
-        kvs = {
-            key: VersionedValue(val, ver, VersionStatusEnum(st), ts)
-            for key, val, ver, st, ts in self._kvs(g, observer, owner)
-        }
-        return NodeState(self.node_ids[owner], int(g["HB"][observer, owner]), kvs, int(g["MV"][observer, owner]),
-                         int(g["GC"][observer, owner]))
+        torch, n, K, KP, Cc = self.torch, self.n, self.k, self.kp, self.hist_cap
+        o, j = int(observer), int(owner)
+        if not self.canonical:
+            pos = int(self.region("POS", torch.int32, (n, self.np_))[o, j].item())
+            if pos == -1:
+                return None
+        self.materialize_held(o, o + 1)
+        self.sync()
+        R = int(self.region("SELF_HB", torch.int32, (self.np_,))[j].item()) & 0xFFFFFFFF
+        s = int(self.region("HB", torch.int16, (n, self.np_))[o, j].item()) & 0xFFFF
+        hb = (R - ((R - s) & 0xFFFF)) & 0xFFFFFFFF
+        mv = int(self.region("MV", torch.int16, (n, self.np_))[o, j].item()) & 0x7FFF
+        gc = int(self.region("GC", torch.int32, (n, self.np_))[o, j].item()) & 0xFFFFFFFF \
+            if "GC" in self.regions else 0
+        hist = self.region("HIST", torch.int64, (n, Cc, K))[j].cpu().numpy().view(np.uint64)
+        hvid = self.region("HIST_VID", torch.int32, (n, Cc, K))[j].cpu().numpy().view(np.uint32)
+        if "HELD" in self.regions:
+            held = self.region("HELD", torch.uint8, (n, self.np_, KP))[o, j, :K].cpu().numpy()
+        else:  # GS_NO_HELD: the view is S_j(max_version): each key's latest write <= mv
+            ver = (hist & np.uint64(0xFFFFFFFF)).astype(np.int64)
+            last_w = self.region("LAST_W", torch.uint8, (n, KP))[j, :K].cpu().numpy().astype(np.int64)
+            w = np.arange(Cc)[:, None]
+            held = (((w >= 1) & (w <= last_w[None, :]) & (ver > 0) & (ver <= mv)).sum(0)).astype(np.uint8)
+        ts = self.region("TS", torch.int32, (n, self.np_, KP))[o, j, :K].cpu().numpy().view(np.uint32) \
+            if "TS" in self.regions else None
+        kvs = {}
+        for k in range(K):
+            w = int(held[k])
+            if not w:
+                continue
+            e = int(hist[w, k])
+            st = VersionStatusEnum((e >> 48) & 3)
+            kvs[self.keys[k]] = VersionedValue(self.values[int(hvid[w, k])], e & 0xFFFFFFFF, st,
+                                               int(ts[k]) if (st and ts is not None) else None)
+        return NodeState(self.node_ids[j], hb, kvs, mv, gc)
 
     def snapshot(self, observer: int, cluster_id: str = "default") -> ClusterSnapshot:
         """``Cluster.snapshot`` of node ``observer`` (server.py:168-175), read from its rows only: its
@@ -575,13 +631,18 @@ class GossipSim:
         mv = row("MV", torch.int16).view(np.uint16).astype(np.uint32) & np.uint32(0x7FFF)
         gc = row("GC").view(np.uint32) if "GC" in self.regions else np.zeros(n, np.uint32)
         st = row("FD_STATE").view(np.uint32)
+        hist = self.region("HIST", torch.int64, (n, Cc, K)).cpu().numpy().view(np.uint64)
         if "HELD" in self.regions:
             held = self.region("HELD", torch.uint8, (n, self.np_, KP))[o, :n, :K].cpu().numpy()
-        else:  # GS_NO_HELD: every view is S_j(max_version)
-            held = self._host()["HELD"][o, :n, :K]
+        else:  # GS_NO_HELD: every view is S_j(max_version): count each key's writes <= the row's mv
+            ver = (hist & np.uint64(0xFFFFFFFF)).astype(np.int64)  # [n, C, K]
+            last_w = self.region("LAST_W", torch.uint8, (n, KP))[:, :K].cpu().numpy().astype(np.int64)
+            held = np.zeros((n, K), dtype=np.uint8)
+            for w in range(1, Cc):
+                ok = (w <= last_w) & (ver[:, w, :] > 0) & (ver[:, w, :] <= mv.astype(np.int64)[:, None])
+                held += ok.astype(np.uint8)
         ts = self.region("TS", torch.int32, (n, self.np_, KP))[o, :n, :K].cpu().numpy().view(np.uint32) \
             if "TS" in self.regions else None
-        hist = self.region("HIST", torch.int64, (n, Cc, K)).cpu().numpy().view(np.uint64)
         hvid = self.region("HIST_VID", torch.int32, (n, Cc, K)).cpu().numpy().view(np.uint32)
         if self.canonical:
             order = range(n)

@@ -42,146 +42,55 @@ def log(*a):
         print(*a, file=sys.stderr, flush=True)
 
 
-def digits(x: np.ndarray) -> np.ndarray:
-    return np.floor(np.log10(np.maximum(x, 1))).astype(np.int64) + 1
+from aiocluster_amd.driver import digits, prepare, run_round  # noqa: E402,F401  (tools/ import them from here)
 
 
-def prepare(sim, spec, rounds, torch, dev):
-    """Precompute every round's device inputs (host schedule generation is not timed)."""
-    from aiocluster_amd.workload import Workload, liveness_tick, phase_tick, round_tick
+def cpu_baseline(sim, cfg, rd, sample: int, min_seconds: float = 10.0, threads: int = 1):
+    """The C oracle (``threads`` host cores) on ``sample`` exchanges of the first phase of round ``rd``,
+    on rows copied from the device after that round's ``gs_begin_round`` -- the same workload at full N.
 
-    wl = Workload(spec)
-    out = []
-    vid = 1 << 24
-    for _ in range(rounds):
-        p = wl.next_round(materialize_values=False)
-        w = p.writes
-        ops = np.zeros((len(w), 5), dtype=np.int64)
-        if len(w):
-            # value "v{j}.{k}.{r}" (workload.write_value): byte length without materialising strings
-            ops[:, 0], ops[:, 1], ops[:, 2] = w[:, 0], w[:, 1], w[:, 2]
-            ops[:, 3] = vid + np.arange(len(w))
-            vid += len(w)
-            ops[:, 4] = 3 + digits(w[:, 0]) + digits(w[:, 1]) + digits(np.full(len(w), p.r))
-        r = p.r
-        out.append({
-            "r": r,
-            "t": round_tick(r),
-            "ops": torch.from_numpy(ops.astype(np.int32)).to(dev),
-            "nops": len(w),
-            "up": torch.from_numpy(p.up.astype(np.uint8)).to(dev),
-            "phases": [(torch.from_numpy(a).to(dev), torch.from_numpy(b).to(dev), len(a), phase_tick(r, i))
-                       for i, (a, b) in enumerate(p.phases)],
-            "t_live": liveness_tick(r, len(p.phases)),
-            "exchanges": p.n_exchanges,
-        })
-    return out
-
-
-def run_round(sims, rd, events=None, group=None, sel=None):
-    """One gossip round on the slices this process drives (one GossipSim when unsliced).  With ``sel``
-    (a PeerSelector) the round's exchanges come from the device's select_nodes_for_gossip + phase
-    schedule instead of the workload's explicit schedule."""
-    from aiocluster_amd.shard import run_sliced_phase
-    from aiocluster_amd.workload import phase_tick
-
-    s0 = sims[0]
-    for sim in sims:
-        if rd["nops"]:
-            sim._chk(sim.L.gs_owner_writes(sim.h, C.c_void_p(rd["ops"].data_ptr()), rd["nops"], rd["t"]),
-                     "gs_owner_writes")
-        sim._chk(sim.L.gs_begin_round(sim.h, C.c_void_p(rd["up"].data_ptr()), rd["t"]), "gs_begin_round")
-    phases = rd["phases"]
-    if sel is not None:
-        sel.select(rd["up"], rd["r"])
-        ph, offs = sel.schedule(rd["up"], rd["r"])
-        phases = [(a, b, n, phase_tick(rd["r"], p)) for p, (a, b, n) in enumerate(ph)]
-        rd["exchanges"] = offs[16]
-        rd["t_live"] = rd["t"] + 1 + len(phases)
-    for a, b, n, t in phases:
-        if not n:
-            continue
-        if events is not None:
-            e0 = s0.torch.cuda.Event(enable_timing=True)
-            e1 = s0.torch.cuda.Event(enable_timing=True)
-            e0.record(s0.stream)
-        if group is None:
-            s0._chk(s0.L.gs_run_phase(s0.h, C.c_void_p(a.data_ptr()), C.c_void_p(b.data_ptr()), n, t),
-                    "gs_run_phase")
-        else:
-            run_sliced_phase(sims, group.comm, group.mtu, t, a, b)
-        if events is not None:
-            e1.record(s0.stream)
-            events.append((e0, e1))
-    for sim in sims:
-        sim._chk(sim.L.gs_liveness(sim.h, C.c_void_p(rd["up"].data_ptr()), rd["t_live"]), "gs_liveness")
-
-
-def cpu_baseline(sim, spec, cfg, next_plan, sample: int, min_seconds: float = 10.0, threads: int = 1):
-    """The C oracle (`threads` host cores) on `sample` exchanges whose two rows are copied from the device."""
+    Before timing, the copied rows double as a full-size parity check (oracle/rowcheck.py): the device
+    runs that phase (all of it) and closes the round, the oracle runs the sampled exchanges and the
+    liveness sweep of their rows, and the rows must be bit-identical (raises otherwise).  Then the
+    oracle's exchanges are timed alone, repeated on restored rows."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
-    import oracle as orc_mod  # test infrastructure: the checker, timed here as the CPU baseline
+    import rowcheck  # test infrastructure: the checker, timed here as the CPU baseline
 
-    torch = sim.torch
-    n, K, NP, KP, Cc = sim.n, sim.k, sim.np_, sim.kp, sim.hist_cap
-    L = orc_mod.lib()
-    from aiocluster_amd.workload import synthetic_node_ids
-    from aiocluster_amd.pbsize import nodeid_size
+    from aiocluster_amd import driver
 
-    ids = synthetic_node_ids(n)
-    ns = (C.c_int32 * n)(*[nodeid_size(x.name, x.generation_id, x.gossip_advertise_addr[0],
-                                       x.gossip_advertise_addr[1], x.tls_name) for x in ids])
-    kl = (C.c_int32 * K)(*[6] * K)
-    oc = orc_mod._Cfg(n, K, int(cfg["mtu"]), orc_mod.us(cfg["tombstone_grace_s"]), float(cfg["phi_threshold"]),
-                      int(cfg["window"]), orc_mod.us(cfg["max_interval_s"]), orc_mod.us(cfg["initial_interval_s"]),
-                      orc_mod.us(cfg["dead_grace_s"]))
-    # disjoint pairs from the first phase of the next round; `threads` host cores, one oracle handle
-    # each (the oracle keeps per-handle scratch), pairs dealt round-robin (SURVEY.md §8(d): one
-    # thread and threads over a phase, core count stated)
-    a_all, b_all, _, t = next_plan["phases"][0]
-    a_all, b_all = a_all.cpu().numpy(), b_all.cpu().numpy()
-    pairs = list(zip(a_all[:sample].tolist(), b_all[:sample].tolist()))
+    a_all, b_all, _, t = rd["phases"][0]
+    pairs = list(zip(a_all[:sample].cpu().numpy().tolist(), b_all[:sample].cpu().numpy().tolist()))
     T = max(1, min(threads, len(pairs)))
-    hs = [L.orc_create(C.byref(oc), ns, kl) for _ in range(T)]
+    ro = rowcheck.RowOracle(sim, cfg)
+    hs = [ro.new_handle() for _ in range(T)]
     mine = [pairs[i::T] for i in range(T)]
-    hist = sim.region("HIST", torch.int64, (n, Cc, K)).cpu().numpy().view(np.uint64)
-    hist_ver = np.ascontiguousarray((hist & 0xFFFFFFFF).astype(np.uint32))
-    hist_vid = sim.region("HIST_VID", torch.int32, (n, Cc, K)).cpu().numpy().view(np.uint32).copy()
-    meta = (hist >> 32).astype(np.uint32)
-    hist_vlen = (meta >> 18).astype(np.int32)
-    hist_st = ((meta >> 16) & 3).astype(np.uint8)
-    order = np.arange(n, dtype=np.int32)
-
-    def rows(name, dt, shape):
-        return sim.region(name, dt, shape)
-
-    for a, b in pairs:  # prefix views keep no HELD row on the device: write them out for these rows
-        sim.materialize_held(a, a + 1)
-        sim.materialize_held(b, b + 1)
-    hb16 = rows("HB", torch.int16, (n, NP))  # heartbeat mod 2^16 (decoded per row below)
-    fst = rows("FD_STATE", torch.int32, (n, NP))
-    mv16 = rows("MV", torch.int16, (n, NP))  # u16 max_version | GS_MV_INEXACT
-    gc = rows("GC", torch.int32, (n, NP)) if "GC" in sim.regions else torch.zeros((n, NP), dtype=torch.int32)
-    fdw = rows("FD", torch.int64, (n, NP))
-    held = rows("HELD", torch.uint8, (n, NP, KP))
-    P = C.c_void_p
-    for h, prs in zip(hs, mine):
+    rows, owner = [], []
+    for i, prs in enumerate(mine):
         for a, b in prs:
-            for o in (a, b):
-                def g(x):
-                    return np.ascontiguousarray(x[o, :n].cpu().numpy().view(np.uint32))
-                hb = np.ascontiguousarray(sim.decode_heartbeats(hb16[o].cpu().numpy())[:n])
-                mv = np.ascontiguousarray((mv16[o, :n].cpu().numpy().view(np.uint16) & 0x7FFF).astype(np.uint32))
-                fl, fs, fc = (np.ascontiguousarray(x) for x in sim.unpack_fd(fdw[o, :n].cpu().numpy()))
-                hw = np.ascontiguousarray(held[o, :n, :K].cpu().numpy())
-                L.orc_load_row(h, o, n, order.ctypes.data_as(P), hb.ctypes.data_as(P), mv.ctypes.data_as(P),
-                               g(gc).ctypes.data_as(P), hw.ctypes.data_as(P), Cc, hist_ver.ctypes.data_as(P),
-                               hist_vid.ctypes.data_as(P), hist_vlen.ctypes.data_as(P), hist_st.ctypes.data_as(P),
-                               fl.ctypes.data_as(P), fs.ctypes.data_as(P), fc.ctypes.data_as(P),
-                               g(fst).ctypes.data_as(P), 15625)
+            rows += [a, b]
+            owner += [hs[i], hs[i]]
+    ro.load(rows, hs, owner=owner)
+    L = ro.L
+    for h, prs in zip(hs, mine):
         for a, b in prs:
             L.orc_snapshot_row(h, a)
             L.orc_snapshot_row(h, b)
+    # -- full-size parity on the sample (untimed)
+    driver.run_phases([sim], rd, phases=[rd["phases"][0]])
+    driver.end([sim], rd, tick=t + 1)
+    for h, prs in zip(hs, mine):
+        for a, b in prs:
+            ro.exchange(h, a, b, t)
+        for a, b in prs:
+            ro.liveness(h, a, t + 1)
+            ro.liveness(h, b, t + 1)
+    got = sim.export_rows(rows)
+    parts = [ro.export_rows(h, [x for a, b in prs for x in (a, b)]) for h, prs in zip(hs, mine)]
+    want = {k: np.concatenate([p_[k] for p_ in parts]) for k in parts[0]}
+    diff = rowcheck.compare_exports(got, want)
+    if diff is not None:
+        raise SystemExit(f"full-size parity FAILED on the CPU-baseline sample: device vs oracle: {diff}")
+    nd_check = sum(ro.stats(h)["node_deltas"] for h in hs)
 
     def restore(i):
         for a, b in mine[i]:
@@ -190,14 +99,13 @@ def cpu_baseline(sim, spec, cfg, next_plan, sample: int, min_seconds: float = 10
 
     def run(i):
         for a, b in mine[i]:
-            L.orc_exchange(hs[i], a, b, t * 15625)
+            L.orc_exchange(hs[i], a, b, t * rowcheck.TICK_US)
 
     # one thread: every handle's pairs in turn, on restored rows, until ~min_seconds/3 are timed
     dt1, reps1 = 0.0, 0
     while dt1 < min_seconds / 3 or reps1 == 0:
-        if reps1:
-            for i in range(T):
-                restore(i)
+        for i in range(T):
+            restore(i)
         t0 = time.perf_counter()
         for i in range(T):
             run(i)
@@ -233,22 +141,20 @@ def cpu_baseline(sim, spec, cfg, next_plan, sample: int, min_seconds: float = 10
     bar.wait()
     for th in ths:
         th.join()
-    nd = 0
-    for h in hs:
-        st = orc_mod._Stats()
-        L.orc_get_stats(h, C.byref(st))
-        nd += st.node_deltas
-        L.orc_destroy(h)
+    ro.close()
+    n, K = sim.n, sim.k
     return {
         "value": len(pairs) * repsT / dtT,
         "unit": "exchanges/s",
         "cores": T,
         "kind": "port",
         "single_core_value": len(pairs) * reps1 / dt1,
-        "sample": f"{len(pairs)} exchanges (disjoint pairs of the next round's first phase) at N={n}, K={K} on "
-                  f"oracle rows copied from the device state after the timed rounds, dealt to {T} host threads "
-                  f"(one oracle handle each) and run {repsT}x on restored rows ({dtT:.1f} s wall); one thread: "
-                  f"{reps1}x ({dt1:.1f} s); {nd // (reps1 + repsT)} NodeDeltas per pass",
+        "sample": f"{len(pairs)} exchanges (disjoint pairs of the first phase of the round after the timed ones) "
+                  f"at N={n}, K={K}, on oracle rows copied from the device state after that round's "
+                  f"gs_begin_round, dealt to {T} host threads (one oracle handle each) and run {repsT}x on "
+                  f"restored rows ({dtT:.1f} s wall); one thread: {reps1}x ({dt1:.1f} s); {nd_check} NodeDeltas "
+                  f"per pass",
+        "parity_check": f"{len(rows)} device rows after that phase + liveness == oracle rows (bit-exact)",
     }
 
 
@@ -287,37 +193,119 @@ def aggregate(exchanges: float, elapsed: float, dist=None, dev=None) -> tuple[fl
     return float(ex.item()), float(tm.item())
 
 
-def copy_ceiling(torch, dev, nbytes: int = 1 << 30, reps: int = 20) -> float:
-    """Measured streaming-copy ceiling: read + write bytes of a 1 GiB
-    device-to-device copy over its HIP-event time, in GB/s."""
-    src = torch.empty(nbytes // 4, dtype=torch.int32, device=dev).fill_(1)
+def copy_ceiling(torch, dev, stream, nbytes: int = 2 << 30, reps: int = 10) -> float:
+    """Measured streaming-copy ceiling: read + write bytes of a 2 GiB copy by the
+    library's hand-written 16-B-per-lane kernel (gs_stream_copy) over its HIP-event time, in GB/s."""
+    from aiocluster_amd import _lib
+
+    L = _lib.load()
+    src = torch.empty(nbytes, dtype=torch.uint8, device=dev).fill_(1)
     dst = torch.empty_like(src)
-    dst.copy_(src)
+    P = C.c_void_p
+
+    def go():
+        rc = L.gs_stream_copy(P(dst.data_ptr()), P(src.data_ptr()), nbytes, P(stream.cuda_stream))
+        assert rc == 0, rc
+
+    go()
     torch.cuda.synchronize(dev)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
+    e0.record(stream)
     for _ in range(reps):
-        dst.copy_(src)
-    e1.record()
+        go()
+    e1.record(stream)
     torch.cuda.synchronize(dev)
     gbs = 2.0 * nbytes * reps / (e0.elapsed_time(e1) / 1e3) / 1e9
     del src, dst
     return gbs
 
 
+def kernel_source_hash() -> str:
+    """SHA-256 (16 hex) of the HIP source + header: ties a committed PMC summary to the kernels it measured."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for f in (os.path.join(REPO, "aiocluster_amd", "csrc", "gossip_sim.hip"), os.path.join(REPO, "include",
+                                                                                          "gossip_sim.h")):
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 def load_traffic(workload: str, exchanges_per_launch: float):
-    """HBM bytes per k_exchange launch from the committed rocprofv3 PMC summary of this workload
-    (tools/profile.sh + tools/pmc_summary.py): measured bytes per exchange x this run's exchanges per launch."""
+    """HBM bytes per k_exchange launch from the rocprofv3 PMC summary (tools/profile.sh +
+    tools/pmc_summary.py), only if it measured THESE kernels (same source hash): measured bytes per
+    exchange x this run's exchanges per launch.  Returns (bytes or None, provenance note)."""
     path = os.path.join(REPO, "profiles", "pmc_summary.json")
     if not os.path.exists(path):
-        return None
+        return None, "no PMC summary"
     try:
         e = json.load(open(path)).get(workload)
-        if e is None or e.get("k_exchange_bytes_per_exchange") is None:
-            return None
-        return e["k_exchange_bytes_per_exchange"] * exchanges_per_launch
-    except Exception:
-        return None
+    except Exception as x:  # noqa: BLE001
+        return None, f"unreadable PMC summary: {x}"
+    if e is None or e.get("k_exchange_bytes_per_exchange") is None:
+        return None, "no PMC summary for this workload"
+    src = kernel_source_hash()
+    if e.get("source_hash") != src:
+        return None, f"PMC summary is stale (kernels {e.get('source_hash')} != {src})"
+    return e["k_exchange_bytes_per_exchange"] * exchanges_per_launch, (
+        f"rocprofv3 PMC run {e.get('tag')} of these kernels ({src}): (FETCH_SIZE x {e.get('fetch_factor')} + "
+        f"WRITE_SIZE) per exchange x this run's exchanges per launch")
+
+
+def roofline(sims, local_c, exch, kern_ms, launches, elapsed, torch, dev, rank, group, workload) -> dict:
+    """Roofline of the dominant kernel (k_exchange): HBM-bound integer/byte work, no MFMA.
+
+    ``achieved`` = the layout's algorithmic bytes per launch (element bytes the kernel must load and
+    store, counted in-kernel: C_ALG) / the launch's average HIP-event time.  The SURVEY
+    §8(d) formula (u32 M/G/H rows) is kept as a secondary figure: this layout stores heartbeats and
+    max versions as u16 and has no last_gc region without tombstones, so that formula overstates the
+    bytes the kernel has to move."""
+    launches = max(1, launches)
+    avg_s = kern_ms / launches / 1e3
+    alg = sum(x["alg_bytes"] for x in local_c) / launches
+    ncols = sum(s_.ncol for s_ in sims)
+    survey = (exch * 32 * ncols + sum(x["pack_bytes"] for x in local_c)) / launches
+    achieved = alg / avg_s / 1e9 if kern_ms > 0 else 0.0
+    copy_gbs = copy_ceiling(torch, dev, sims[0].stream) if rank == 0 else None
+    traffic, tnote = load_traffic(workload, exch / launches) if group is None else (None, "sliced run")
+    return {
+        "bound": "hbm",
+        "kernel": "k_exchange" if group is None else "sliced phase (count + gather + pack), per rank",
+        "achieved": achieved,
+        "peak": HBM_PEAK_GBPS,
+        "unit": "GB/s",
+        "frac": achieved / HBM_PEAK_GBPS,
+        "traffic": traffic,
+        "traffic_source": tnote,
+        "alg_bytes_per_launch": alg,
+        "alg_bytes_basis": "in-kernel element bytes (C_ALG): both rows' u16 heartbeats + max versions, changed "
+                           "heartbeat groups written, report bit planes, packing + apply (pass 3)",
+        "avg_launch_ms": avg_s * 1e3,
+        "launches": launches,
+        "kernel_share_of_step": kern_ms / 1e3 / elapsed,
+        "measured_copy_ceiling": copy_gbs,
+        "achieved_frac_of_copy_ceiling": achieved / copy_gbs if copy_gbs else None,
+        "traffic_gbs": traffic / avg_s / 1e9 if traffic and kern_ms else None,
+        "survey_formula_bytes_per_launch": survey,
+        "survey_formula_gbs": survey / avg_s / 1e9 if kern_ms > 0 else None,
+    }
+
+
+def launch_ranks(n: int) -> int:
+    """``--gpus N`` without a torch.distributed launcher: start N ranks (one per GPU) with
+    torch.distributed.run as a child process -- before this process touches the GPU -- and return its
+    exit code."""
+    import socket
+    import subprocess
+
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    return subprocess.call(cmd, env=env)
 
 
 def main():
@@ -349,11 +337,18 @@ def main():
                     help="version-only layout (GS_NO_HELD, config 4): needs an mtu no delta reaches")
     args = ap.parse_args()
 
-    import torch
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world = int(os.environ.get("WORLD_SIZE", "0"))
+    if world == 0:
+        if args.gpus > 1:  # plain `python bench.py --gpus N`: become the launcher of N ranks
+            raise SystemExit(launch_ranks(args.gpus))
+        world = 1
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: one rank per GPU")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch
+
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -363,6 +358,7 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
+    from aiocluster_amd import driver
     from aiocluster_amd.scenario import DEFAULT_CFG
     from aiocluster_amd.shard import DistComm, LocalComm, ShardGroup
     from aiocluster_amd.sim import GossipSim
@@ -379,16 +375,8 @@ def main():
                    else ""))
     t_setup = time.perf_counter()
     ids = synthetic_node_ids(n)
-    boot = []  # Cluster(initial_key_values): key k of owner j = "v{j}.{k}.i", as K batches of distinct owners
-    for k in range(K):
-        ops = np.zeros((n, 5), dtype=np.uint32)
-        ops[:, 0] = np.arange(n)
-        ops[:, 1] = k
-        ops[:, 3] = 1 + k * n + np.arange(n)
-        ops[:, 4] = 3 + digits(np.arange(n)) + digits(np.full(n, k)) + 1
-        boot.append(ops)
-    kw = dict(init="warm", device=str(dev), tombstones=False, fd_ring=False, hist_cap=16, initial_ops=boot,
-              held=not args.no_held)
+    kw = dict(init="warm", device=str(dev), tombstones=False, fd_ring=False, hist_cap=16,
+              initial_ops=driver.boot_ops(n, K), held=not args.no_held)
     if world > 1 and args.slices > 1:
         raise SystemExit("--slices is a one-process rehearsal; with --gpus N each rank holds one slice")
     group = None
@@ -405,7 +393,7 @@ def main():
         sims = [GossipSim(ids, key_names(K), cfg, **kw)]
     sim = sims[0]
     R0 = args.settle + args.warmup  # first timed round
-    plans = prepare(sim, spec, R0 + args.steps + 1, torch, dev)
+    plans = driver.prepare(spec, R0 + args.steps + 1, torch, dev)
     sel = None
     if args.peer_select:
         from aiocluster_amd.peers import PeerSelector
@@ -418,11 +406,11 @@ def main():
 
     for r in range(args.settle):
         ts = time.perf_counter()
-        run_round(sims, plans[r], group=group, sel=sel)
+        driver.run_round(sims, plans[r], group=group, sel=sel)
         torch.cuda.synchronize(dev)
         log(f"settle round {r}: {(time.perf_counter() - ts) * 1e3:.1f} ms, {plans[r]['exchanges']} exchanges")
     for r in range(args.settle, R0):
-        run_round(sims, plans[r], group=group, sel=sel)
+        driver.run_round(sims, plans[r], group=group, sel=sel)
     torch.cuda.synchronize(dev)
     for s_ in sims:
         s_.check()
@@ -433,35 +421,27 @@ def main():
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for r in range(R0, R0 + args.steps):
-        run_round(sims, plans[r], events, group, sel)
+        driver.run_round(sims, plans[r], events, group, sel)
     torch.cuda.synchronize(dev)
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    local = [s_.check() for s_ in sims]
+    local_c = [s_.check() for s_ in sims]
     inexact = sum(s_.inexact_views() for s_ in sims)  # views with holes (HELD kept), GS_MV_INEXACT
-    c = group.comm.sum_counters(local) if group is not None else local[0]
+    c = group.comm.sum_counters(local_c) if group is not None else local_c[0]
     exch = sum(plans[r]["exchanges"] for r in range(R0, R0 + args.steps))
+    unscheduled = sum(plans[r].get("unscheduled", 0) for r in range(R0, R0 + args.steps))
     assert c["exchanges"] == exch, (c["exchanges"], exch)
     kern_ms = sum(e0.elapsed_time(e1) for e0, e1 in events)
     launches = len(events)
     # a sliced cluster: every rank runs the same exchanges on its columns -> count them once
     exch_total, elapsed_max = aggregate(exch if (group is None or rank == 0) else 0, elapsed, dist, dev)
-    # this process's algorithmic bytes (all its slices) over its phase time
-    alg_local = sum(x["alg_bytes"] for x in local)
-    # algorithmic bytes per exchange, SURVEY.md §8(d): N(24 + 8) (read M, G, H of both rows, write both
-    # H rows) + D (delta packing + apply bytes, counted in-kernel); the 32r failure-detector bytes are
-    # priced into k_liveness, where this design performs the window updates
-    ncols = sum(s_.ncol for s_ in sims)
-    alg_survey = exch * 32 * ncols + sum(x["pack_bytes"] for x in local)
-    achieved = alg_survey / (kern_ms / 1e3) / 1e9 if kern_ms > 0 else 0.0
-    achieved_in_kernel = alg_local / (kern_ms / 1e3) / 1e9 if kern_ms > 0 else 0.0
-    traffic = load_traffic(workload, exch / max(1, len(events))) if group is None else None
-    copy_gbs = copy_ceiling(torch, dev) if rank == 0 else None
+    roof = roofline(sims, local_c, exch, kern_ms, launches, elapsed, torch, dev, rank, group, workload)
     cpu = None
     if rank == 0 and group is None and not args.no_cpu_baseline:
-        cpu = cpu_baseline(sim, spec, cfg, plans[R0 + args.steps], args.cpu_sample, args.cpu_seconds,
-                           args.cpu_threads)
+        rd = plans[R0 + args.steps]
+        driver.begin(sims, rd)
+        cpu = cpu_baseline(sim, cfg, rd, args.cpu_sample, args.cpu_seconds, args.cpu_threads)
     if rank == 0:
         line = {
             "metric": ("REHEARSAL (one GPU's slice of a %d-GPU run, packing not the cluster's): exchanges/s"
@@ -476,7 +456,9 @@ def main():
             "higher_is_better": True,
             "scaling": "strong" if group is not None else "weak",
             "vs_baseline": None,
-            "dtype": "u32",
+            # the state is integer: heartbeats and max versions stored as u16 (exact decode),
+            # computed in u32; phi in binary64
+            "dtype": "u16/u32 int (phi f64)",
             "data": "synthetic (seeded workload generator; no dataset)",
             "config": {
                 "workload": workload,
@@ -488,29 +470,9 @@ def main():
                                 else f"slice 0 of {args.rehearse_slices} (rehearsal)" if args.rehearse_slices > 1
                                 else f"owner-column slices x{args.slices} in one process" if group is not None
                                 else "1 GPU"),
+                **({"unscheduled_exchanges": unscheduled} if sel is not None else {}),
             },
-            "roofline": {
-                "bound": "hbm",
-                "kernel": "k_exchange" if group is None else "sliced phase (count + gather + pack), per rank",
-                "achieved": achieved,
-                "peak": HBM_PEAK_GBPS,
-                "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBPS,
-                "traffic": traffic,
-                "measured_copy_ceiling": copy_gbs,
-                # the PMC-measured HBM bytes of one launch over its HIP-event time, against the copy
-                # ceiling ("achieved" prices the SURVEY formula's u32 rows; this layout moves fewer bytes)
-                "traffic_gbs": traffic / (kern_ms / max(1, launches) / 1e3) / 1e9 if traffic and kern_ms else None,
-                "traffic_frac_of_copy_ceiling": (traffic / (kern_ms / max(1, launches) / 1e3) / 1e9 / copy_gbs
-                                                 if traffic and kern_ms and copy_gbs else None),
-                "alg_bytes_per_launch": alg_survey / max(1, launches),
-                "alg_bytes_formula": "exchanges x 32 x N + pack_bytes (SURVEY 8(d) minus the FD term, see DESIGN.md)",
-                "in_kernel_bytes_per_launch": alg_local / max(1, launches),
-                "achieved_in_kernel": achieved_in_kernel,
-                "avg_launch_ms": kern_ms / max(1, launches),
-                "launches": launches,
-                "kernel_share_of_step": kern_ms / 1e3 / elapsed,
-            },
+            "roofline": roof,
             "cpu_baseline": cpu,
             **({"ABLATION_RESULTS_INVALID": os.environ["GS_ABLATE"]} if os.environ.get("GS_ABLATE") else {}),
             "counters": {**{k: v for k, v in c.items() if not k.startswith("err_")}, "inexact_views": inexact},

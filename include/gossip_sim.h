@@ -28,7 +28,8 @@
 extern "C" {
 #endif
 
-#define GS_API_VERSION 7
+#define GS_API_VERSION 8
+#define GS_MAX_PHASES 64  /* gs_schedule_phases: phases per round */
 #define GS_TICK_US 15625u
 #define GS_NONE 0xFFFFFFFFu
 
@@ -151,7 +152,10 @@ typedef struct gs_counters {
     uint64_t q9;               /* garbage_collect calls that raised KeyError */
     uint64_t pack_bytes;       /* the part of alg_bytes moved by delta packing + apply (pass 3) */
     uint64_t err_holes;        /* GS_NO_HELD: a view got holes (a truncated NodeDelta); result inexact */
-    uint64_t reserved[11];
+    uint64_t err_hb_lag;       /* a view lagged its owner's heartbeat by >= 2^15 at a gs_check_heartbeat_lag
+                                  sweep: the 16-bit heartbeat store is no longer known to be exact */
+    uint64_t plane_flushes;    /* host count: mid-round report replays (phases > 16 ticks after the round start) */
+    uint64_t reserved[9];
 } gs_counters;
 
 /* Failure-detector membership census (gs_fd_census): (observer, target) pairs with the observer up and
@@ -200,11 +204,12 @@ int gs_begin_round(gs_handle *h, const uint8_t *up, uint32_t tick);
 /* One conflict-free phase of exchanges initiators[e] -> responders[e] (DEVICE int32 arrays):
  * Syn/SynAck/Ack = server.py:327-376 + 524, i.e. compute_digest, _report_heartbeat,
  * compute_partial_delta_respecting_mtu and apply_delta on both sides.  At most n_nodes/2 exchanges;
- * `tick` must lie in (round tick, round tick + 16] of the last gs_begin_round, and the round must
- * still be open (no gs_liveness since that gs_begin_round).  The failure detector's
- * report_heartbeat calls are recorded per phase (GS_R_PEND bit planes) and applied to the
+ * the round must still be open (no gs_liveness since the last gs_begin_round) and `tick` must be
+ * later than the round start and than the round's previous phase.  The failure detector's
+ * report_heartbeat calls are recorded per phase (GS_R_PEND bit planes, 16 per row) and applied to the
  * sampling windows, in tick order, by the gs_liveness that closes the round (nothing reads a
- * window in between). */
+ * window in between); a phase more than 16 ticks after the planes' base replays the pending planes
+ * into the windows first (counted in plane_flushes). */
 int gs_run_phase(gs_handle *h, const int32_t *initiators, const int32_t *responders, uint32_t n, uint32_t tick);
 /* Owner-column sliced phase (n_shards > 1; gs_run_phase refuses sliced handles).  The slices of one
  * cluster run, per phase, on the same initiators/responders:
@@ -234,6 +239,13 @@ int gs_liveness(gs_handle *h, const uint8_t *up, uint32_t tick);
  * returns None). */
 int gs_phi_row(gs_handle *h, uint32_t observer, uint32_t tick, double *out);
 
+/* Heartbeat-lag sweep over every view of this handle (asynchronous): counts in err_hb_lag the views
+ * whose heartbeat lags the owner's own by >= 2^15 (GS_R_HB stores heartbeats mod 2^16).  An owner's
+ * heartbeat grows by at most one per round start or phase; gs_begin_round runs this sweep by itself
+ * whenever 2^14 round starts + phases have passed since the last one, which keeps every decode exact
+ * until a sweep reports otherwise. */
+int gs_check_heartbeat_lag(gs_handle *h);
+
 /* Batched hook events (Cluster.on_key_change / on_node_join / on_node_leave, server.py:217-257).
  * When enabled, every kernel that changes what a hook reports appends 6 x u32 records
  * {observer, owner, key | kind << 8, old version (0 = none), new version, tick} to the DEVICE array
@@ -255,16 +267,17 @@ int gs_set_events(gs_handle *h, uint32_t *records, uint32_t capacity, uint32_t *
  * 4 * N * (fanout + 6) bytes.  1 <= fanout <= 8; one slice only. */
 int gs_select_peers(gs_handle *h, const uint8_t *up, uint32_t fanout, const int32_t *seeds, uint32_t n_seeds,
                     uint64_t seed, uint32_t round, int32_t *targets, void *scratch);
-/* The round's exchanges (initiator o, responder targets[o][s], responder up) in <= 16 conflict-free
- * phases: per phase `iters` rounds of a deterministic Luby matching (an exchange whose endpoints are
- * free in that phase takes it if its priority key is the smallest at both).  Writes the exchanges of
- * phase p to DEVICE initiators/responders[phase_offsets[p] .. phase_offsets[p+1]) (order within a
- * phase unspecified: exchanges of one phase commute) and the host array phase_offsets[17]; exchanges
- * left after 16 phases are not scheduled (N * (fanout + 2) - phase_offsets[16] minus the empty and
- * down-responder slots).  DEVICE scratch of 4 * (N * (fanout + 6) + 64) + 16 * N bytes.  Blocking. */
+/* The round's exchanges (initiator o, responder targets[o][s], responder up) in <= max_phases
+ * (<= GS_MAX_PHASES) conflict-free phases: per phase `iters` rounds of a deterministic Luby matching
+ * (an exchange whose endpoints are free in that phase takes it if its priority key is the smallest at
+ * both).  Writes the exchanges of phase p to DEVICE initiators/responders[phase_offsets[p] ..
+ * phase_offsets[p+1]) (order within a phase unspecified: exchanges of one phase commute) and the host
+ * array phase_offsets[max_phases + 1]; *unscheduled (host) = valid exchanges (responder up) left
+ * after max_phases phases, which are not run (0 unless the round needs more phases).  DEVICE scratch
+ * of 4 * N * (fanout + 2) + 24 * N + 1040 bytes.  Blocking. */
 int gs_schedule_phases(gs_handle *h, const uint8_t *up, uint32_t fanout, const int32_t *targets, uint64_t seed,
-                       uint32_t round, uint32_t iters, void *scratch, int32_t *initiators, int32_t *responders,
-                       uint32_t *phase_offsets);
+                       uint32_t round, uint32_t iters, uint32_t max_phases, void *scratch, int32_t *initiators,
+                       int32_t *responders, uint32_t *phase_offsets, uint32_t *unscheduled);
 
 /* FailureDetector.live_nodes / dead_nodes of every up observer (failure_detector.py:63-67) counted
  * against the DEVICE up mask; blocking.  Sliced handles count their own target columns. */
@@ -296,6 +309,13 @@ int gs_emit_digest(gs_handle *h, const gs_wire *w, uint32_t observer, uint32_t t
                    uint64_t *len, void *scratch);
 int gs_emit_delta(gs_handle *h, const gs_wire *w, uint32_t sender, uint32_t receiver, uint32_t tick, uint8_t *out,
                   uint64_t cap, uint64_t *len, void *scratch);
+
+/* Measurement (no handle; asynchronous on `stream`): a 16-B-per-lane streaming copy of `bytes`
+ * (multiple of 16, 16-B aligned DEVICE buffers) -- the HBM ceiling bench.py reports -- and a
+ * read-only stream of `bytes` at `width` = 8 or 16 B per lane (DEVICE u64 *sink keeps the loads), the
+ * known byte count that calibrates rocprofv3's FETCH_SIZE for those access widths. */
+int gs_stream_copy(void *dst, const void *src, uint64_t bytes, void *stream);
+int gs_stream_read(const void *src, uint64_t bytes, uint32_t width, uint64_t *sink, void *stream);
 
 int gs_read_counters(gs_handle *h, gs_counters *out);
 int gs_reset_counters(gs_handle *h);

@@ -28,7 +28,14 @@ REPO = os.path.dirname(HERE)
 sys.path.insert(0, REPO)
 sys.path.insert(0, HERE)
 
-from aiocluster_amd.scenario import initial_by_owner, make_scenario, replay, scenario_node_ids, state_hash  # noqa: E402
+from aiocluster_amd.scenario import (  # noqa: E402
+    export_digest,
+    initial_by_owner,
+    make_scenario,
+    replay,
+    scenario_node_ids,
+    state_hash,
+)
 from aiocluster_amd.workload import WorkloadSpec  # noqa: E402
 from refharness import RefSim, import_reference  # noqa: E402
 
@@ -89,6 +96,24 @@ SCENARIOS = {
         {"mtu": 6000},
         False,
     ),
+    # SURVEY 8(c) tier "N=64/256": cold start at 256 nodes with deletes, TTL writes, tombstone GC,
+    # MTU truncation and churn (hashes per round, full final state)
+    "cold256": (
+        WorkloadSpec(n=256, k=8, fanout=3, seed=7, init="cold", write_frac=0.08, delete_frac=0.1, ttl_frac=0.05,
+                     down_frac=0.05, down_rounds=3),
+        18,
+        {"mtu": 3000, "tombstone_grace_s": 5},
+        False,
+    ),
+    # BASELINE config 2: 1,024 nodes x 64 keys, fanout 3, cold start to version convergence (the
+    # workload of tests/test_gpu_parity.py::test_config2_cold_1024x64_converges_bit_exact): per-round
+    # digests of the whole export (scenario.export_digest) and the final max_version matrix
+    "config2": (
+        WorkloadSpec(n=1024, k=64, fanout=3, seed=2, init="cold", write_frac=0.0),
+        24,
+        {},
+        "digest",
+    ),
 }
 
 
@@ -126,6 +151,25 @@ def gen_scenario(name: str) -> dict:
     scen = make_scenario(name, spec, rounds, cfg)
     sim = RefSim(scenario_node_ids(scen), scen["keys"], scen["config"], scen["init"], initial_by_owner(scen))
     states, hashes = [], []
+    t0 = time.time()
+    if full == "digest":
+        digests = []
+
+        def on_digest(r):
+            digests.append(export_digest(sim.export()))
+            print(f"{name}: round {r} done, {time.time() - t0:.0f}s", flush=True)
+
+        replay(sim, scen, on_round=on_digest)
+        ex = sim.export()
+        scen["expect"] = {
+            "digests": digests,
+            "final_mv": ex["mv"].tolist(),
+            "final_holes": int(((ex["kv_version"] == 0) & (ex["pos"] >= 0)[:, :, None]).sum()),
+            "q9": sim.q9_events,
+            "generator": "oracle/gen_golden.py via oracle/refharness.py (reference @ /root/reference)",
+        }
+        print(f"{name}: {rounds} rounds, {time.time() - t0:.1f}s")
+        return scen
 
     def on_round(r):
         st = sim.state()
@@ -133,7 +177,6 @@ def gen_scenario(name: str) -> dict:
         if full:
             states.append(st)
 
-    t0 = time.time()
     replay(sim, scen, on_round=on_round)
     scen["expect"] = {
         "hashes": hashes,

@@ -742,6 +742,19 @@ void orc_load_row(orc *o, int32_t obs, int32_t cnt, const int32_t *order,
     b->cnt = cnt;
 }
 
+void orc_set_row_ts(orc *o, int32_t obs, const uint32_t *ts_tick, int64_t tick_us) {
+    oobs *b = row(o, obs);
+    const int32_t N = o->N, K = o->K;
+    for (int32_t j = 0; j < N; j++) {
+        if (b->pos[j] < 0) continue;
+        okv *kv = kvp(o, b, j);
+        for (int32_t k = 0; k < K; k++) {
+            const uint32_t t = ts_tick[(size_t)j * K + k];
+            if (kv[k].present && kv[k].status != 0 && t != 0xFFFFFFFFu) kv[k].ts = (int64_t)t * tick_us;
+        }
+    }
+}
+
 /* ------------------------------------------- method-level hooks (KAT ports) */
 void orc_kat_set_view(orc *o, int32_t obs, int32_t owner, uint32_t hb, uint32_t mv, uint32_t gc) {
     oobs *b = row(o, obs);

@@ -109,6 +109,10 @@ void orc_load_row(orc *o, int32_t obs, int32_t cnt, const int32_t *order,
                   const uint32_t *fd_last_tick, const uint32_t *fd_sum_tick, const uint32_t *fd_len,
                   const uint32_t *fd_state, int64_t tick_us);
 
+/* status_change_ts (state.py:124-131, 222-227) of the tombstones of a row loaded by orc_load_row:
+ * ts_tick[N][K] in ticks, 0xFFFFFFFF = none. */
+void orc_set_row_ts(orc *o, int32_t obs, const uint32_t *ts_tick, int64_t tick_us);
+
 /* Keep a copy of observer obs's row / put it back (the CPU baseline re-runs the same
  * exchanges on restored rows to accumulate a bounded, repeatable sample). */
 void orc_snapshot_row(orc *o, int32_t obs);

@@ -102,15 +102,15 @@ def luby_key(seed, r, e, p, it):
     return (h << 32) | e
 
 
-def schedule_phases(targets, up, seed, r, iters):
-    """Phase of every exchange slot e = o * (F + 2) + s (-1 = not scheduled)."""
+def schedule_phases(targets, up, seed, r, iters, max_phases=16):
+    """Phase of every exchange slot e = o * (F + 2) + s (-1 = not scheduled after max_phases)."""
     n, W = targets.shape
     E = n * W
     flat = targets.reshape(-1)
     eph = np.full(E, -1, dtype=np.int64)
     busy = np.zeros(n, dtype=np.int64)
     cand = [e for e in range(E) if flat[e] >= 0 and up[flat[e]]]
-    for p in range(16):
+    for p in range(max_phases):
         for it in range(iters):
             best = {}
             act = []

@@ -217,3 +217,45 @@ class RefSim:
 
     def state(self) -> list[dict]:
         return [self.observer_state(o) for o in range(len(self.clusters))]
+
+    def export(self) -> dict:
+        """Every observer as numpy arrays in the ``GossipSim.export`` / ``OracleSim.export`` format
+        (times in ticks; kv_value_id is left out: an owner's version identifies its write, hence the
+        value).  Used for the compact per-round digests of large fixtures
+        (``aiocluster_amd.scenario.export_digest``)."""
+        import numpy as np
+
+        n, K = len(self.clusters), len(self.keys)
+        kidx = {k: i for i, k in enumerate(self.keys)}
+        SET = self.R.ent.VersionStatusEnum.SET
+        out = {
+            "pos": np.full((n, n), -1, np.int32), "hb": np.zeros((n, n), np.uint32),
+            "mv": np.zeros((n, n), np.uint32), "gc": np.zeros((n, n), np.uint32),
+            "kv_version": np.zeros((n, n, K), np.uint32), "kv_status": np.zeros((n, n, K), np.int32),
+            "kv_ts": np.zeros((n, n, K), np.int64), "fd_last": np.full((n, n), -1, np.int64),
+            "fd_len": np.zeros((n, n), np.int32), "fd_sum": np.zeros((n, n), np.float64),
+            "live": np.zeros((n, n), np.int32), "tod": np.full((n, n), -1, np.int64),
+        }
+        for o, c in enumerate(self.clusters):
+            for p, (nid, ns) in enumerate(c._cluster_state._node_states.items()):
+                j = self.idx[nid]
+                out["pos"][o, j] = p
+                out["hb"][o, j], out["mv"][o, j], out["gc"][o, j] = ns.heartbeat, ns.max_version, ns.last_gc_version
+                for key, vv in ns.key_values.items():
+                    k = kidx[key]
+                    out["kv_version"][o, j, k] = vv.version
+                    out["kv_status"][o, j, k] = int(vv.status)
+                    if vv.status != SET:
+                        out["kv_ts"][o, j, k] = dt_tick(vv.status_change_ts)
+            fd = c._failure_detector
+            for nid in fd._live_nodes:
+                out["live"][o, self.idx[nid]] = 1
+            for nid, t in fd._dead_nodes.items():
+                out["tod"][o, self.idx[nid]] = dt_tick(t)
+            for nid, sw in fd._node_samples.items():
+                j = self.idx[nid]
+                if sw._last_heartbeat is not None:
+                    out["fd_last"][o, j] = dt_tick(sw._last_heartbeat)
+                out["fd_len"][o, j] = len(sw._intervals)
+                out["fd_sum"][o, j] = sw._intervals.sum()
+        return out

@@ -4,10 +4,12 @@ import gzip
 import json
 import os
 
+from rowcheck import compare_exports  # noqa: F401  (re-exported for the tests)
+
 from aiocluster_amd.scenario import initial_by_owner, replay, scenario_node_ids, state_hash
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
-SCENARIOS = ["simple3", "trunc8", "sched16", "fdgc12", "q9x10", "cold64", "warm128"]
+SCENARIOS = ["simple3", "trunc8", "sched16", "fdgc12", "q9x10", "cold64", "warm128", "cold256"]
 
 
 def load_scenario(name):
@@ -59,22 +61,3 @@ def replay_and_compare(backend, scen, expect_states=None, expect_hashes=None, ro
 
 def make_backend(cls, scen, **kw):
     return cls(scenario_node_ids(scen), scen["keys"], scen["config"], scen["init"], initial_by_owner(scen), **kw)
-
-
-def compare_exports(got: dict, want: dict):
-    """First mismatching (field, observer, index) between two ``export()`` dicts, or None."""
-    import numpy as np
-
-    for key in ("pos", "hb", "mv", "gc", "kv_version", "kv_status", "kv_value_id", "kv_ts", "fd_last", "fd_len",
-                "fd_sum", "live", "tod"):
-        a, b = np.asarray(got[key]), np.asarray(want[key])
-        if a.shape != b.shape:
-            return f"{key}: shape {a.shape} != {b.shape}"
-        if key == "kv_ts":
-            mask = np.asarray(want["kv_status"]) != 0
-            a, b = np.where(mask, a, 0), np.where(mask, b, 0)
-        ne = np.argwhere(a != b)
-        if len(ne):
-            idx = tuple(ne[0])
-            return f"{key}{list(idx)}: got {a[idx]!r} want {b[idx]!r} ({len(ne)} mismatches)"
-    return None

@@ -1,0 +1,128 @@
+"""Full-size parity (GPU only): BASELINE configs 3 and 5 at their real sizes.
+
+The oracle cannot replay a 65,536-node run (N^2 views), but one conflict-free phase touches only
+its own rows: after ~20 settle rounds on the device, the rows of 64 exchanges of the next phase are
+copied into the C oracle (``oracle/rowcheck.py``), the whole phase runs on the device and in the
+oracle (the 64 exchanges), both close the round with the liveness sweep, and the 128 rows must be
+bit-identical: decoded heartbeats, max versions, last_gc versions, held keys (version, status,
+value, tombstone tick), failure-detector windows (last report, length, binary64 sum), live/dead.
+The reference semantics checked: ``aiocluster/state.py:190-233, 340-415``, ``server.py:327-376,
+599-620``, ``failure_detector.py:12-128``.
+"""
+
+import numpy as np
+import pytest
+from rowcheck import check_phase_rows
+
+from aiocluster_amd import driver
+from aiocluster_amd.scenario import DEFAULT_CFG
+from aiocluster_amd.sim import GossipSim
+from aiocluster_amd.workload import WorkloadSpec, key_names, synthetic_node_ids
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(sim, plans, rounds):
+    for r in range(rounds):
+        driver.run_round([sim], plans[r])
+    sim.check()
+
+
+def test_config3_65536_sampled_phase_matches_oracle():
+    """BASELINE config 3 (the bench workload): 65,536 nodes x 16 keys, fanout 3, warm, 5 % writes + 5 %
+    up/down churn, window 1000, mtu 65,507, prefix-view layout; 20 settle rounds, then phase 0 of
+    round 20 on 64 sampled exchanges."""
+    import torch
+
+    n, K = 65536, 16
+    cfg = dict(DEFAULT_CFG)
+    spec = WorkloadSpec(n=n, k=K, fanout=3, seed=0, init="warm", write_frac=0.05, down_frac=0.05, down_rounds=3)
+    sim = GossipSim(synthetic_node_ids(n), key_names(K), cfg, init="warm", tombstones=False, fd_ring=False,
+                    hist_cap=16, initial_ops=driver.boot_ops(n, K))
+    dev = sim.device
+    plans = driver.prepare(spec, 21, torch, dev)
+    _run(sim, plans, 20)
+    rd = plans[20]
+    driver.begin([sim], rd)
+    diff, info = check_phase_rows(sim, cfg, rd, sample=64)
+    assert diff is None, diff
+    c = sim.check()
+    # the sample did real work: deltas, heartbeat reports (the oracle's counts)
+    assert info["node_deltas"] > 0 and info["hb_reports"] > 0, info
+    assert c["exchanges"] > 0
+    sim.close()
+
+
+def test_config5_16384_partition_heal_sampled_phases_match_oracle():
+    """BASELINE config 5: 16,384 nodes, K = 16, 5 % writes (1 % deletes), tombstone grace 10 rounds,
+    mtu 65,507, partition into halves for rounds 10-29, heal from round 30.  Sampled phases: the last
+    partitioned round (dead-marked peers: false positives) and the first healed round (the heal burst:
+    MTU-truncated NodeDeltas, tombstones collected)."""
+    import torch
+
+    n, K = 16384, 16
+    cfg = dict(DEFAULT_CFG)
+    cfg["tombstone_grace_s"] = 10
+    spec = WorkloadSpec(n=n, k=K, fanout=3, seed=5, init="warm", write_frac=0.05, delete_frac=0.01,
+                        partition=(10, 30))
+    sim = GossipSim(synthetic_node_ids(n), key_names(K), cfg, init="warm", tombstones=True, fd_ring=False,
+                    hist_cap=32, initial_ops=driver.boot_ops(n, K))
+    plans = driver.prepare(spec, 31, torch, sim.device)
+    _run(sim, plans, 29)
+    rd = plans[29]
+    driver.begin([sim], rd)
+    diff, info = check_phase_rows(sim, cfg, rd, sample=64)
+    assert diff is None, f"partitioned round: {diff}"
+    cen = sim.fd_census(rd["up"])
+    assert cen["up_dead"] > 0  # the partition left peers dead-marked
+    rd = plans[30]
+    driver.begin([sim], rd)
+    before = sim.check()
+    diff, info = check_phase_rows(sim, cfg, rd, sample=64)
+    assert diff is None, f"healed round: {diff}"
+    c = sim.check()
+    assert c["truncated"] - before["truncated"] > 0 and info["truncated"] > 0, (info, c["truncated"])
+    assert c["tomb_gc"] > 0
+    sim.close()
+
+
+def test_fullsize_check_detects_a_corrupted_row():
+    """The check is not vacuous: after a matching phase, one changed device value in a sampled row (a
+    heartbeat, a live flag) is reported."""
+    import torch
+
+    import rowcheck
+
+    n, K = 4096, 8
+    cfg = dict(DEFAULT_CFG)
+    spec = WorkloadSpec(n=n, k=K, fanout=3, seed=1, init="warm", write_frac=0.05, down_frac=0.05, down_rounds=3)
+    sim = GossipSim(synthetic_node_ids(n), key_names(K), cfg, init="warm", tombstones=False, fd_ring=False,
+                    hist_cap=16, initial_ops=driver.boot_ops(n, K))
+    plans = driver.prepare(spec, 6, torch, sim.device)
+    _run(sim, plans, 5)
+    rd = plans[5]
+    driver.begin([sim], rd)
+    a, b, _, t = rd["phases"][0]
+    rows = a[:8].cpu().numpy().tolist() + b[:8].cpu().numpy().tolist()
+    ro = rowcheck.RowOracle(sim, cfg)
+    (h,) = ro.load(rows)
+    driver.run_phases([sim], rd, phases=[rd["phases"][0]])
+    driver.end([sim], rd, tick=t + 1)
+    for x, y in zip(rows[:8], rows[8:]):
+        ro.exchange(h, x, y, t)
+    for o in rows:
+        ro.liveness(h, o, t + 1)
+    want = ro.export_rows(h, rows)
+    assert rowcheck.compare_exports(sim.export_rows(rows), want) is None
+    hb = sim.region("HB", torch.int16, (n, sim.np_))
+    o, j = rows[3], (rows[3] + 11) % n
+    hb[o, j] -= 1
+    d = rowcheck.compare_exports(sim.export_rows(rows), want)
+    assert d is not None and d.startswith("hb[3, "), d
+    hb[o, j] += 1
+    st = sim.region("FD_STATE", torch.int32, (n, sim.np_))
+    st[rows[12], (rows[12] + 5) % n] = 2 + t  # dead since t
+    d = rowcheck.compare_exports(sim.export_rows(rows), want)
+    assert d is not None and d.startswith("live[12, "), d
+    ro.close()
+    sim.close()

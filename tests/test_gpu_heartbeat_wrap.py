@@ -50,5 +50,40 @@ def test_heartbeats_past_2_16_match_oracle():
             assert diff is None, f"round {r}: {diff}"
     hb = np.asarray(want["hb"])
     assert hb.min() > 65536, "every heartbeat must have crossed 2^16"
-    c = gpu.check()
-    assert c["exchanges"] == rounds * 8
+    c = gpu.check()  # raises on err_hb_lag: the automatic sweeps (every 2^14 rounds + phases) ran clean
+    assert c["exchanges"] == rounds * 8 and c["err_hb_lag"] == 0
+
+
+def test_heartbeat_lag_sweep_flags_views_near_the_16_bit_bound():
+    """A view that lags its owner by >= 2^15 heartbeats (injected into GS_R_HB; in a run: an observer
+    cut off from an owner for ~2^15 of the owner's increments) trips err_hb_lag, so check() raises before
+    a 16-bit decode can go wrong; a lag just below the bound does not."""
+    import torch
+
+    from aiocluster_amd._lib import GsError
+
+    n = 8
+    ids, keys = synthetic_node_ids(n), key_names(2)
+    init = {j: [(0, f"v{j}")] for j in range(n)}
+    gpu = GossipSim(ids, keys, dict(DEFAULT_CFG), "warm", init, tombstones=False, fd_ring=True, hist_cap=8)
+    up_dev = torch.ones(n, dtype=torch.uint8, device=gpu.device)
+    gpu.begin_round(round_tick(0), up_dev)
+    gpu.liveness(liveness_tick(0, 0), up_dev)
+    R = gpu.region("SELF_HB", torch.int32, (gpu.np_,))
+    hb = gpu.region("HB", torch.int16, (n, gpu.np_))
+    def s16(v):  # a heartbeat as GS_R_HB stores it (mod 2^16), viewed as int16
+        v &= 0xFFFF
+        return v - 65536 if v >= 32768 else v
+
+    R[3] = 50000
+    hb[3, 3] = s16(50000)  # the owner's own view (diagonal)
+    hb[5, 3] = s16(50000 - 32767)  # lag 2^15 - 1: exact, not flagged
+    hb[6, 3] = s16(50000 - 32000)
+    for o in (0, 1, 2, 4, 7):
+        hb[o, 3] = s16(50000 - 10)
+    gpu.check_heartbeat_lag()
+    assert gpu.check()["err_hb_lag"] == 0
+    hb[6, 3] = s16(50000 - 32768)  # lag 2^15
+    gpu.check_heartbeat_lag()
+    with pytest.raises(GsError, match="err_hb_lag"):
+        gpu.check()

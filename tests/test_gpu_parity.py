@@ -184,6 +184,14 @@ def test_version_only_layout_matches_reference_golden(name):
     assert res is None, f"{name}: first mismatch at round {res[0]}: {res[1]}"
     c = sim.check()
     assert c["err_holes"] == 0 and c["truncated"] == 0
+    last = exp["states"][-1]
+    for o in range(scen["n"]):  # single-view reads and snapshots derive held keys from max_version
+        for j, hb, mv, gc, kvs in last[o]["nodes"]:
+            ns = sim.node_state(o, j)
+            got = sorted([k, v.value, v.version, int(v.status), v.status_change_ts] for k, v in ns.key_values.items())
+            assert [ns.heartbeat, ns.max_version, ns.last_gc_version, got] == [hb, mv, gc, kvs], (o, j)
+        snap = sim.snapshot(o)
+        assert len(snap.node_states) == len(last[o]["nodes"])
 
 
 def test_version_only_layout_vs_oracle_and_refuses_holes():
@@ -218,5 +226,10 @@ def test_snapshot_matches_reference_golden(name):
                          for k, v in ns.key_values.items())
             nodes.append([idx[nid], ns.heartbeat, ns.max_version, ns.last_gc_version, kvs])
         assert nodes == last[o]["nodes"], (o, nodes[:3], last[o]["nodes"][:3])
+        # ClusterState.node_state (state.py:295-296) of single views, read without the whole matrix
+        for j, hb, mv, gc, kvs in last[o]["nodes"][:4]:
+            ns = sim.node_state(o, j)
+            got = sorted([k, v.value, v.version, int(v.status), v.status_change_ts] for k, v in ns.key_values.items())
+            assert [ns.heartbeat, ns.max_version, ns.last_gc_version, got] == [hb, mv, gc, kvs], (o, j)
         assert sorted(idx[x] for x in snap.live_nodes) == last[o]["live"]
         assert sorted(idx[x] for x in snap.dead_nodes) == [d[0] for d in last[o]["dead"]]

@@ -37,22 +37,25 @@ def _warm_cluster(n=160, rounds=8, seed=3, init="warm"):
     return scen, gpu, orc
 
 
-@pytest.mark.parametrize("init", ["warm", "cold"])
-def test_selection_and_schedule_match_restatement(init):
+@pytest.mark.parametrize("init,iters,max_phases", [("warm", 4, 62), ("cold", 4, 62), ("warm", 1, 62),
+                                                   ("warm", 3, 62), ("warm", 1, 8), ("cold", 2, 16)])
+def test_selection_and_schedule_match_restatement(init, iters, max_phases):
+    """Odd `iters` and phase caps included: the Luby minimum buffers alternate by the global iteration
+    index, so every iteration starts from fresh minima as the restatement does."""
     scen, gpu, orc = _warm_cluster(init=init)
     up = np.asarray(scen["rounds"][-1]["up"], dtype=np.uint8)
     seeds = [0, 5, 77]
-    sel = PeerSelector(gpu, fanout=3, seeds=seeds, seed=1234)
+    sel = PeerSelector(gpu, fanout=3, seeds=seeds, seed=1234, iters=iters, max_phases=max_phases)
     up_dev = gpu._dev(up, gpu.torch.uint8)
     got = sel.select(up_dev, 9).cpu().numpy()
     live, tod, known = _state(orc)
     want = peer_select.select_peers(live, tod, known, up, 3, seeds, 1234, 9)
     assert np.array_equal(got, want)
     assert (got[:, 3] >= 0).any() and (got[:, 4] >= 0).any()  # dead probes and seed probes happened
-    phases, offs = sel.schedule(up_dev, 9)
-    eph = peer_select.schedule_phases(want, up, 1234, 9, 4)
+    phases, offs, left = sel.schedule(up_dev, 9)
+    eph = peer_select.schedule_phases(want, up, 1234, 9, iters, max_phases)
     W = want.shape[1]
-    want_sets = [set() for _ in range(16)]
+    want_sets = [set() for _ in range(max_phases)]
     for e in np.flatnonzero(eph >= 0):
         want_sets[eph[e]].add((int(e // W), int(want.reshape(-1)[e])))
     got_sets = sel.scheduled_pairs(phases)
@@ -60,8 +63,14 @@ def test_selection_and_schedule_match_restatement(init):
     for ph in got_sets:  # conflict-free
         nodes = [x for pr in ph for x in pr]
         assert len(nodes) == len(set(nodes))
-    valid = sum(1 for e in range(want.size) if want.reshape(-1)[e] >= 0 and up[want.reshape(-1)[e]])
-    assert offs[16] == int((eph >= 0).sum()) and offs[16] >= valid - 2  # (almost) nothing dropped
+    flat = want.reshape(-1)
+    valid = sum(1 for e in range(want.size) if flat[e] >= 0 and up[flat[e]])
+    assert offs[-1] == int((eph >= 0).sum())
+    assert left == valid - offs[-1]  # reported, never silently dropped
+    if max_phases == 62:
+        assert left == 0  # _gossip_multiple contacts every selected peer (server.py:476-493)
+    else:
+        assert max_phases > 8 or left > 0  # 8 phases cannot hold every node's exchanges
 
 
 def test_rounds_with_device_peer_selection_match_oracle():
@@ -77,7 +86,8 @@ def test_rounds_with_device_peer_selection_match_oracle():
         gpu.begin_round(t, up_dev)
         orc.begin_round(t, up)
         sel.select(up_dev, r)
-        phases, _ = sel.schedule(up_dev, r)
+        phases, _, left = sel.schedule(up_dev, r)
+        assert left == 0
         sets = sel.scheduled_pairs(phases)
         for p, (a, b, n) in enumerate(phases):
             gpu.run_phase_arrays(phase_tick(r, p), a, b)
@@ -121,3 +131,20 @@ def test_run_selected_round_helper():
         info = run_selected_round(gpu, sel, r, np.ones(96, dtype=np.uint8))
         assert 1 <= info["phases"] <= 16 and info["exchanges"] > 0
     gpu.check()
+
+
+def test_rounds_with_more_than_16_phases_match_oracle():
+    """Fanout 8 = 24 phases per round: phases more than 16 ticks after the round start replay the
+    pending report planes into the windows mid-round (plane_flushes); every round vs the oracle."""
+    spec = WorkloadSpec(n=96, k=4, fanout=8, seed=31, init="warm", write_frac=0.1, down_frac=0.1, down_rounds=3)
+    scen = make_scenario("f8", spec, 6, {"initial_interval_s": 1.0, "phi_threshold": 3.0, "mtu": 800})
+    assert max(len(rd["phases"]) for rd in scen["rounds"]) > 16
+    gpu = make_backend(GossipSim, scen, fd_ring=False)
+    orc = make_backend(OracleSim, scen)
+    for r in range(len(scen["rounds"])):
+        replay_round(gpu, scen, r)
+        replay_round(orc, scen, r)
+        diff = compare_exports(gpu.export(), orc.export())
+        assert diff is None, f"round {r}: {diff}"
+    c = gpu.check()
+    assert c["plane_flushes"] == len(scen["rounds"])

@@ -42,10 +42,10 @@ def main():
 
     import torch
 
+    from aiocluster_amd.driver import boot_ops, prepare, run_round
     from aiocluster_amd.scenario import DEFAULT_CFG
     from aiocluster_amd.sim import GossipSim
     from aiocluster_amd.workload import WorkloadSpec, key_names, synthetic_node_ids
-    from bench import digits, prepare, run_round
 
     n, K = args.nodes, args.keys
     dev = torch.device("cuda", 0)
@@ -55,18 +55,11 @@ def main():
     cfg["tombstone_grace_s"] = 10
     spec = WorkloadSpec(n=n, k=K, fanout=args.fanout, seed=args.seed, init="warm", write_frac=0.05,
                         delete_frac=0.01, partition=(args.warm, args.warm + args.partition))
-    boot = []
-    for k in range(K):
-        ops = np.zeros((n, 5), dtype=np.uint32)
-        ops[:, 0] = np.arange(n)
-        ops[:, 1] = k
-        ops[:, 3] = 1 + k * n + np.arange(n)
-        ops[:, 4] = 3 + digits(np.arange(n)) + digits(np.full(n, k)) + 1
-        boot.append(ops)
+    boot = boot_ops(n, K)
     t0 = time.perf_counter()
     sim = GossipSim(synthetic_node_ids(n), key_names(K), cfg, init="warm", device=str(dev), tombstones=True,
                     fd_ring=False, hist_cap=32, initial_ops=boot)
-    plans = prepare(sim, spec, rounds, torch, dev)
+    plans = prepare(spec, rounds, torch, dev)
     torch.cuda.synchronize(dev)
     print(f"setup {time.perf_counter() - t0:.1f}s", file=sys.stderr, flush=True)
     per_round = []

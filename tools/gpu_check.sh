@@ -1,7 +1,8 @@
+# GPU check on the box (gpurun): GPU tests, smoke, one bench line.  Each step under its own limit.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 && \
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 && \
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 && \
-timeout -k 10 400 python -u bench.py > gpurun_out/bench.log 2>&1
+timeout -k 10 500 python -u bench.py ${BENCH_ARGS:-} > gpurun_out/bench.log 2>&1
 echo exit $?
