@@ -51,7 +51,7 @@ def fd_sum_bits(window: int) -> int:
 REGIONS = [
     "HB", "MV", "GC", "HELD", "FD", "FD_STATE", "TS", "RING", "POS", "ORD", "ROW",
     "LAST_W", "HIST", "HIST_VID", "NID_SIZE", "KEY_LEN", "STAMP", "COUNTERS", "SLICE_BITS", "PEND", "PEND_STAMP", "LATEST",
-    "SELF_HB",
+    "SELF_HB", "CAND", "CAND_N",
 ]
 REGION = {n: i for i, n in enumerate(REGIONS)}
 
@@ -72,7 +72,7 @@ EXPORTS = [
     "gs_check_heartbeat_lag", "gs_stream_copy", "gs_stream_read",
 ]
 
-API_VERSION = 8
+API_VERSION = 9
 MAX_PHASES = 64  # GS_MAX_PHASES
 
 

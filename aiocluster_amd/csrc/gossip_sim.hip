@@ -91,6 +91,8 @@ struct Dev {
     uint32_t *stamp;
     unsigned long long *ctr;
     uint32_t *sbits;  // sharded phases: stale-owner bitmaps of both directions per exchange [e][2][NP/32]
+    uint2 *cand;       // split phases: stale-owner records [e][dir][half][GS_CAND_CAP] (GS_R_CAND)
+    uint32_t *cand_n;  // [e][dir][half] stale owners found (GS_R_CAND_N)
     // heartbeat reports of the current round not yet applied to the windows: one bit plane per phase
     // p (tick t_round + 1 + p) and observer row, [N][16][PW] u64 in quad-interleaved column order
     // (plane_word/plane_bit); a plane row is valid only if pstamp[o][p] holds that phase's tick
@@ -241,9 +243,10 @@ __device__ __forceinline__ void derive_held(const Dev &d, uint32_t j, uint32_t M
 // NodeDelta candidate (state.py:347-390): from_version_excluded, the NodeDeltaPb body without
 // kvs, the DeltaPb bytes of the whole NodeDelta (all kvs with version > from, 392-398) and of
 // its smallest-version kv alone.
-template <int KW, bool GENM>
+// HAVE_MV: both views' max_version words come from pass 1's candidate record (mvw = sender | receiver << 16)
+template <int KW, bool GENM, bool HAVE_MV = false>
 __device__ __forceinline__ void eval_cand(const Dev &d, uint32_t s, uint32_t r, const DigestSide &ds, uint32_t j,
-                                          uint32_t t, Cand<KW> &c, uint32_t &alg) {
+                                          uint32_t t, Cand<KW> &c, uint32_t &alg, uint32_t mvw = 0) {
     const size_t ps = pix(d, s, j), pr = pix(d, r, j);
     const uint32_t kw = d.KP >> 2;
     // round trip 1
@@ -262,7 +265,7 @@ __device__ __forceinline__ void eval_cand(const Dev &d, uint32_t s, uint32_t r, 
             lat[2 * q + 1] = v.y;
         }
     }
-    const uint32_t msw = d.mv[ps], mrw = d.mv[pr];
+    const uint32_t msw = HAVE_MV ? (mvw & 0xFFFFu) : d.mv[ps], mrw = HAVE_MV ? (mvw >> 16) : d.mv[pr];
     const uint32_t ms = msw & MV_MASK, mr = mrw & MV_MASK;
     const uint32_t gs = gct ? d.gc[ps] : 0u, gr = gct ? d.gc[pr] : 0u;
     const uint32_t pos_r = GENM ? d.pos[pr] : 0u;
@@ -438,42 +441,161 @@ __device__ __forceinline__ void apply_cand(const Dev &d, uint32_t r, const Cand<
 }
 
 // compute_partial_delta_respecting_mtu (state.py:340-415) of sender s for receiver r, fused with
-// r's apply_delta, by one wave.  The sender's dict order is walked in windows of 1024 positions;
-// each window's stale owners are compacted (ballot + popcount scan) into a wave-private LDS list
-// and evaluated 64 at a time, one candidate per lane.  Fewer than 64 left at the end of a window
-// are carried to the next one in a register (lane i = the i-th), so sparse stale sets still
-// fill whole groups.  Exactness vs the sequential loop: DESIGN.md.
+// r's apply_delta, by one wave: the sender's stale owners are evaluated 64 at a time in dict order,
+// one candidate per lane (pack_group).  They come either from a list pass 1 wrote (pack_list: the
+// canonical one-slice path) or from a stale-owner bitmap walked in windows of 1024 positions whose
+// stale owners are compacted (ballot + popcount scan) into a wave-private LDS list (pack_dir); fewer
+// than 64 left at the end of a window are carried to the next one in a register (lane i = the i-th),
+// so sparse stale sets still fill whole groups.  Exactness vs the sequential loop: DESIGN.md.
 struct PackState {
     uint32_t S;  // DeltaPb bytes committed so far (wave-uniform)
     bool tail;   // the budget was exceeded once: first-fit continuation mode
     bool stop;   // the delta is complete (>= mtu, or less than the smallest NodeDelta left)
 };
 
+// One group: lane i holds the i-th candidate of the group in sender order (cand = false: none).
 // COUNT: only sum the DeltaPb bytes of every candidate (owner-sharded runs: the slice total).
-// REC: record the selected NodeDeltas {owner, vsel} in sender order into rec[] (*nrec of them)
+// REC: record the selected NodeDeltas {owner, vsel} in sender order into rec[] (nr so far)
 // instead of applying them (the wire-format emitter, gs_emit_delta).
+template <int KW, bool COUNT, bool REC>
+__device__ __forceinline__ void pack_group(const Dev &d, uint32_t r, uint32_t t, const Cand<KW> &c, bool cand,
+                                           uint32_t &S, bool &tail, bool &stop, WStats &st, bool &tomb, uint2 *rec,
+                                           uint32_t &nr) {
+    const int lane = lane_id();
+    const uint32_t mtu = d.mtu;
+    const uint32_t em = cand ? c.emsg : 0u;
+    if (COUNT) {
+        S += (uint32_t)wave_sum(em);
+        return;
+    }
+    // this lane's NodeDelta: 0 = not sent, NONE = all its kvs, else kvs up to that version
+    uint32_t vsel = 0, nsel = 0;
+    int cur = 0;
+    bool seq = tail;
+    if (!tail) {
+        const uint32_t inc = wave_incl_scan(em);
+        const uint32_t total = __shfl(inc, WAVE - 1, WAVE);
+        if (S + total <= mtu) {  // every candidate of this group fits whole
+            if (em) vsel = NONE;
+            S += total;
+            if (S >= mtu || mtu - S < d.lb_min) stop = true;
+        } else {
+            const bool fail = em && (S + inc > mtu);
+            const int f = __builtin_ctzll(__ballot(fail));
+            if (lane < f && em) vsel = NONE;
+            S += __shfl(inc - em, f, WAVE);
+            tail = true;
+            seq = true;
+            cur = f;
+        }
+    }
+    // First-fit continuation (state.py:392-413): each later candidate sends the longest
+    // prefix of its version-sorted kvs that still fits; stop once the delta is >= mtu.
+    while (seq) {
+        const uint32_t R = mtu - S;
+        const bool elig = em && lane >= cur && c.min1 <= R;
+        const unsigned long long mm = __ballot(elig);
+        if (!mm) break;
+        const int x = __builtin_ctzll(mm);
+        const uint32_t emx = __shfl(em, x, WAVE);
+        if (emx <= R) {
+            if (lane == x) vsel = NONE;
+            S += emx;
+        } else {
+            // truncated NodeDelta: lanes = keys, rank kvs by version, longest fitting prefix
+            const uint32_t fx = __shfl(c.from, x, WAVE);
+            const uint32_t bx = __shfl(c.base, x, WAVE);
+            uint32_t v = 0, kvm = 0;
+#pragma unroll
+            for (int q = 0; q < 4 * KW; q++) {
+                const uint32_t vq = __shfl(c.ver[q], x, WAVE);
+                const uint32_t kq = __shfl(c.km[q], x, WAVE);
+                if (lane == q) { v = vq; kvm = kq & 0xFFFFu; }
+            }
+            const bool inc = lane < (int)d.K && v > fx;
+            const unsigned long long im = __ballot(inc);
+            uint32_t rank = 0, P = 0;
+            for (int l = 0; l < (int)d.K; l++) {
+                const uint32_t vl = __shfl(v, l, WAVE);
+                if (((im >> l) & 1ull) && vl < v) rank++;
+            }
+            for (int l = 0; l < (int)d.K; l++) {
+                const uint32_t rl = __shfl(rank, l, WAVE);
+                const uint32_t kl = __shfl(kvm, l, WAVE);
+                if (((im >> l) & 1ull) && (int)rl < lane) P += kl;
+            }
+            const uint32_t nkv = (uint32_t)__popcll(im);
+            const bool fit = lane >= 1 && (uint32_t)lane <= nkv && S + msgf(bx + P) <= mtu;
+            const uint32_t n = (uint32_t)__popcll(__ballot(fit));
+            if (n >= 1) {
+                const unsigned long long ym = __ballot(inc && rank == n - 1);
+                const uint32_t vmax = __shfl(v, __builtin_ctzll(ym), WAVE);
+                if (lane == x) { vsel = vmax; nsel = n; }
+                S += msgf(bx + __shfl(P, (int)n, WAVE));
+            }
+        }
+        if (S >= mtu) { stop = true; break; }
+        cur = x + 1;
+    }
+    if (tail && mtu - S < d.lb_min) stop = true;
+    if (REC) {  // lanes hold candidates in sender order: rank by lane
+        const unsigned long long sm = __ballot(vsel != 0u);
+        if (vsel) rec[nr + (uint32_t)__popcll(sm & ((1ull << lane) - 1ull))] = make_uint2(c.j, vsel);
+        nr += (uint32_t)__popcll(sm);
+        return;
+    }
+    // apply_delta at the receiver: one lane per NodeDelta, distinct owners, any order
+    if (vsel) {
+        apply_cand<KW>(d, r, c, vsel, t, tomb, st.alg);
+        st.nd++;
+        if (vsel == NONE) {
+            st.kvs += c.nkv;
+        } else {
+            st.kvs += nsel;
+            st.trunc++;
+        }
+    }
+}
+
+__device__ __forceinline__ void pack_begin(const Dev &d, bool count, const PackState &pst, uint32_t &S, bool &tail,
+                                           bool &stop) {
+    S = pst.S;
+    tail = pst.tail;
+    stop = pst.stop;
+    if (!count && !stop && (S >= d.mtu || d.mtu - S < d.lb_min)) stop = true;
+}
+
+// Bitmap source: positions [p0, cnt) of the sender's dict order (p0 = 0 in the general layout; a
+// multiple of 256 otherwise).
 template <int KW, bool GENM, bool COUNT, bool REC = false>
 __device__ __forceinline__ void pack_dir(const Dev &d, uint32_t s, uint32_t r, const DigestSide ds,
                                          const uint32_t *order, uint32_t cnt, const uint32_t *bits, uint16_t *wbuf,
                                          uint32_t t, WStats &st, bool &tomb, PackState &pst, uint2 *rec = nullptr,
-                                         uint32_t *nrec = nullptr) {
+                                         uint32_t *nrec = nullptr, uint32_t p0 = 0) {
     const int lane = lane_id();
-    const uint32_t mtu = d.mtu;
     const uint32_t S0 = pst.S;
-    uint32_t S = pst.S;
-    bool tail = pst.tail, stop = pst.stop;
-    if (!COUNT && !stop && (S >= mtu || mtu - S < d.lb_min)) stop = true;
+    uint32_t S;
+    bool tail, stop;
+    pack_begin(d, COUNT, pst, S, tail, stop);
     uint32_t nr = 0;    // REC: NodeDeltas recorded so far (wave-uniform)
     uint32_t pend = 0;  // wave-uniform: candidates carried from earlier windows (< 64), in rv
     uint32_t rv = 0;    // lane i < pend: the i-th carried candidate's position
-    for (uint32_t win = 0; win < cnt && !stop; win += WIN) {
+    // canonical: the next window's bitmap word is loaded one window ahead (the bitmap is in HBM on the
+    // split path, so the walk would otherwise pay one dependent round trip per window)
+    uint32_t wnext = 0;
+    if (!GENM && p0 + 16u * lane < cnt) wnext = bits[(p0 + 16u * lane) >> 5];
+    for (uint32_t win = p0; win < cnt && !stop; win += WIN) {
         // -- compact this window's stale owners (sender order) into wbuf, 16 positions per lane
         uint32_t m = 0;
         const uint32_t pb = win + 16u * lane;
+        if (!GENM) {
+            const uint32_t wcur = wnext;
+            const uint32_t pn = pb + WIN;
+            if (pn < cnt) wnext = bits[pn >> 5];
+            if (pb < cnt) m = (wcur >> (pb & 16u)) & 0xFFFFu;
+        }
         if (pb < cnt) {
-            if (!GENM) {
-                m = (bits[pb >> 5] >> (pb & 16u)) & 0xFFFFu;
-            } else {
+            if (GENM) {
                 for (uint32_t q = 0; q < 16; q++) {
                     const uint32_t p = pb + q;
                     if (p < cnt && bit(bits, order[p])) m |= 1u << q;
@@ -513,98 +635,7 @@ __device__ __forceinline__ void pack_dir(const Dev &d, uint32_t s, uint32_t r, c
                 eval_cand<KW, GENM>(d, s, r, ds, j, t, c, st.alg);
                 st.cand++;
             }
-            const uint32_t em = cand ? c.emsg : 0u;
-            if (COUNT) {
-                S += (uint32_t)wave_sum(em);
-                continue;
-            }
-            // this lane's NodeDelta: 0 = not sent, NONE = all its kvs, else kvs up to that version
-            uint32_t vsel = 0, nsel = 0;
-            int cur = 0;
-            bool seq = tail;
-            if (!tail) {
-                const uint32_t inc = wave_incl_scan(em);
-                const uint32_t total = __shfl(inc, WAVE - 1, WAVE);
-                if (S + total <= mtu) {  // every candidate of this group fits whole
-                    if (em) vsel = NONE;
-                    S += total;
-                    if (S >= mtu || mtu - S < d.lb_min) stop = true;
-                } else {
-                    const bool fail = em && (S + inc > mtu);
-                    const int f = __builtin_ctzll(__ballot(fail));
-                    if (lane < f && em) vsel = NONE;
-                    S += __shfl(inc - em, f, WAVE);
-                    tail = true;
-                    seq = true;
-                    cur = f;
-                }
-            }
-            // First-fit continuation (state.py:392-413): each later candidate sends the longest
-            // prefix of its version-sorted kvs that still fits; stop once the delta is >= mtu.
-            while (seq) {
-                const uint32_t R = mtu - S;
-                const bool elig = em && lane >= cur && c.min1 <= R;
-                const unsigned long long mm = __ballot(elig);
-                if (!mm) break;
-                const int x = __builtin_ctzll(mm);
-                const uint32_t emx = __shfl(em, x, WAVE);
-                if (emx <= R) {
-                    if (lane == x) vsel = NONE;
-                    S += emx;
-                } else {
-                    // truncated NodeDelta: lanes = keys, rank kvs by version, longest fitting prefix
-                    const uint32_t fx = __shfl(c.from, x, WAVE);
-                    const uint32_t bx = __shfl(c.base, x, WAVE);
-                    uint32_t v = 0, kvm = 0;
-#pragma unroll
-                    for (int q = 0; q < 4 * KW; q++) {
-                        const uint32_t vq = __shfl(c.ver[q], x, WAVE);
-                        const uint32_t kq = __shfl(c.km[q], x, WAVE);
-                        if (lane == q) { v = vq; kvm = kq & 0xFFFFu; }
-                    }
-                    const bool inc = lane < (int)d.K && v > fx;
-                    const unsigned long long im = __ballot(inc);
-                    uint32_t rank = 0, P = 0;
-                    for (int l = 0; l < (int)d.K; l++) {
-                        const uint32_t vl = __shfl(v, l, WAVE);
-                        if (((im >> l) & 1ull) && vl < v) rank++;
-                    }
-                    for (int l = 0; l < (int)d.K; l++) {
-                        const uint32_t rl = __shfl(rank, l, WAVE);
-                        const uint32_t kl = __shfl(kvm, l, WAVE);
-                        if (((im >> l) & 1ull) && (int)rl < lane) P += kl;
-                    }
-                    const uint32_t nkv = (uint32_t)__popcll(im);
-                    const bool fit = lane >= 1 && (uint32_t)lane <= nkv && S + msgf(bx + P) <= mtu;
-                    const uint32_t n = (uint32_t)__popcll(__ballot(fit));
-                    if (n >= 1) {
-                        const unsigned long long ym = __ballot(inc && rank == n - 1);
-                        const uint32_t vmax = __shfl(v, __builtin_ctzll(ym), WAVE);
-                        if (lane == x) { vsel = vmax; nsel = n; }
-                        S += msgf(bx + __shfl(P, (int)n, WAVE));
-                    }
-                }
-                if (S >= mtu) { stop = true; break; }
-                cur = x + 1;
-            }
-            if (tail && mtu - S < d.lb_min) stop = true;
-            if (REC) {  // lanes hold candidates in sender order: rank by lane
-                const unsigned long long sm = __ballot(vsel != 0u);
-                if (vsel) rec[nr + (uint32_t)__popcll(sm & ((1ull << lane) - 1ull))] = make_uint2(c.j, vsel);
-                nr += (uint32_t)__popcll(sm);
-                continue;
-            }
-            // apply_delta at the receiver: one lane per NodeDelta, distinct owners, any order
-            if (vsel) {
-                apply_cand<KW>(d, r, c, vsel, t, tomb, st.alg);
-                st.nd++;
-                if (vsel == NONE) {
-                    st.kvs += c.nkv;
-                } else {
-                    st.kvs += nsel;
-                    st.trunc++;
-                }
-            }
+            pack_group<KW, COUNT, REC>(d, r, t, c, cand, S, tail, stop, st, tomb, rec, nr);
         }
         if (!last) {  // carry the rest (< 64): entry lim + i to lane i
             const uint32_t rem = total - lim, idx = lim + lane;
@@ -623,6 +654,40 @@ __device__ __forceinline__ void pack_dir(const Dev &d, uint32_t s, uint32_t r, c
         return;
     }
     if (!COUNT && lane == 0) shard_add(d, C_DBYTES, S - S0);  // DeltaPb bytes this call added
+}
+
+// List source (canonical, one slice): the n stale owners pass 1 recorded for one row half, in column
+// order, each with both views' max_version words (GS_R_CAND), so no row is read again.  The next
+// group's records are loaded one group ahead.
+template <int KW>
+__device__ __forceinline__ void pack_list(const Dev &d, uint32_t s, uint32_t r, const DigestSide ds, const uint2 *L,
+                                          uint32_t n, uint32_t t, WStats &st, bool &tomb, PackState &pst) {
+    const int lane = lane_id();
+    const uint32_t S0 = pst.S;
+    uint32_t S;
+    bool tail, stop;
+    pack_begin(d, false, pst, S, tail, stop);
+    uint32_t nr = 0;
+    uint2 nxt = make_uint2(0u, 0u);
+    if ((uint32_t)lane < n) nxt = L[lane];
+    for (uint32_t c0 = 0; c0 < n && !stop; c0 += WAVE) {
+        const uint32_t ci = c0 + lane;
+        const bool cand = ci < n;
+        const uint2 cr = nxt;
+        if (ci + WAVE < n) nxt = L[ci + WAVE];
+        Cand<KW> c;
+        c.emsg = 0;
+        c.min1 = 0;
+        if (cand) {
+            eval_cand<KW, false, true>(d, s, r, ds, cr.x, t, c, st.alg, cr.y);
+            st.cand++;
+        }
+        pack_group<KW, false, false>(d, r, t, c, cand, S, tail, stop, st, tomb, nullptr, nr);
+    }
+    pst.S = S;
+    pst.tail = tail;
+    pst.stop = stop;
+    if (lane == 0) shard_add(d, C_DBYTES, S - S0);
 }
 
 // ------------------------------------------------------------------ exchange kernel
@@ -674,8 +739,8 @@ __device__ __forceinline__ void load_grp(const Dev &d, size_t ra, size_t rb, uin
     for (int i = 0; i < 4; i++) { g.hA[i] = hb_dec(g.hA[i], R[i]); g.hB[i] = hb_dec(g.hB[i], R[i]); }
     ld4h(d.mv + ra + c0, g.mA);
     ld4h(d.mv + rb + c0, g.mB);
-#pragma unroll
-    for (int i = 0; i < 4; i++) { g.mA[i] &= MV_MASK; g.mB[i] &= MV_MASK; }  // drop the prefix-view flag
+    // raw max_version words (prefix-view flag included): pass 1 masks them where it compares, and the
+    // split path hands them to the packer in its candidate records
 #pragma unroll
     for (int i = 0; i < 4; i++) { g.pA[i] = g.pB[i] = g.fA[i] = g.fB[i] = 0u; }
     if (GENM) { ld4(d.pos + ra + c0, g.pA); ld4(d.pos + rb + c0, g.pB); }
@@ -719,11 +784,12 @@ __device__ __forceinline__ Fd fd_report_val(const Dev &d, size_t p, uint32_t t, 
 // (same appends, same order).
 template <bool GENM>
 __device__ __forceinline__ void pass1_grp(const Dev &d, size_t ra, size_t rb, uint32_t c0, uint32_t a, uint32_t b,
-                                          uint32_t t, bool schA, bool schB, Grp &g, uint32_t *bBA, uint32_t *bAB,
-                                          uint32_t *bNB, uint32_t *bNA, uint32_t &alg, uint32_t &reports,
-                                          uint32_t &hbw, bool &anynew, uint32_t &rmA, uint32_t &rmB) {
+                                          uint32_t t, bool schA, bool schB, Grp &g, uint32_t &nBA, uint32_t &nAB,
+                                          uint32_t &nNB, uint32_t &nNA, uint32_t &alg, uint32_t &reports,
+                                          uint32_t &hbw, uint32_t &rmA, uint32_t &rmB) {
     bool dA = false, dB = false;
     rmA = rmB = 0u;
+    nBA = nAB = nNB = nNA = 0u;
     alg += 48 + (GENM ? 32 : 0) + (schA ? 16 : 0) + (schB ? 16 : 0);
 #pragma unroll
     for (int i = 0; i < 4; i++) {
@@ -755,12 +821,13 @@ __device__ __forceinline__ void pass1_grp(const Dev &d, size_t ra, size_t rb, ui
             if (repB) { rmB |= 1u << i; reports++; }
             if (repA) { rmA |= 1u << i; reports++; }
             // stale owners (state.py:347-357): sender's max_version above the digest's
-            const uint32_t dmA = inA ? g.mA[i] : 0u;
-            if (pb2 && !sb && g.mB[i] > dmA) atomicOr(&bBA[j >> 5], 1u << (j & 31u));
-            const uint32_t dmB = inB ? g.mB[i] : 0u;
-            if (pa && !sa && g.mA[i] > dmB) atomicOr(&bAB[j >> 5], 1u << (j & 31u));
-            if (newB) { atomicOr(&bNB[j >> 5], 1u << (j & 31u)); anynew = true; }
-            if (newA) { atomicOr(&bNA[j >> 5], 1u << (j & 31u)); anynew = true; }
+            const uint32_t mA = g.mA[i] & MV_MASK, mB = g.mB[i] & MV_MASK;
+            const uint32_t dmA = inA ? mA : 0u;
+            if (pb2 && !sb && mB > dmA) nBA |= 1u << i;
+            const uint32_t dmB = inB ? mB : 0u;
+            if (pa && !sa && mA > dmB) nAB |= 1u << i;
+            if (newB) nNB |= 1u << i;
+            if (newA) nNA |= 1u << i;
         }
     }
     // only changed 16/32-byte groups are written back (writing whole lines measured slower: r1c vs r1b)
@@ -782,6 +849,46 @@ __device__ __forceinline__ void store_plane(uint64_t *plane, uint32_t c0, uint32
     }
 }
 
+// bit m of an 8-bit value -> bit 4m
+__device__ __forceinline__ uint32_t spread8(uint32_t x) {
+    x &= 0xFFu;
+    x = (x | (x << 12)) & 0x000F000Fu;
+    x = (x | (x << 6)) & 0x03030303u;
+    x = (x | (x << 3)) & 0x11111111u;
+    return x;
+}
+
+// Split path (k_pass1): one wave step's stale owners of one direction (a nibble of 4 consecutive
+// columns per lane) go out twice, from the same four ballots (inactive lanes contribute zeros):
+//  * as natural-order bitmap words (bit c % 32 of word c / 32), zeros included, so the buffer never
+//    needs clearing; the first lane of each 8 stores its word: 32 contiguous bytes per wave;
+//  * as records {column, sender max_version word | receiver max_version word << 16} appended in
+//    column order to the wave's list L (the first GS_CAND_CAP of them; cnt counts all, wave-uniform).
+__device__ __forceinline__ void emit_dir(uint32_t *gw, uint2 *L, uint32_t &cnt, uint32_t c0, uint32_t nib,
+                                         const uint32_t (&ms)[4], const uint32_t (&mr)[4], uint32_t &alg) {
+    const uint64_t b0 = __ballot(nib & 1u), b1 = __ballot(nib & 2u), b2 = __ballot(nib & 4u), b3 = __ballot(nib & 8u);
+    const int l = lane_id();
+    const bool any = (b0 | b1 | b2 | b3) != 0ull;
+    if ((l & 7) == 0) {
+        const uint32_t w = !any ? 0u
+                                : spread8((uint32_t)(b0 >> l)) | (spread8((uint32_t)(b1 >> l)) << 1) |
+                                      (spread8((uint32_t)(b2 >> l)) << 2) | (spread8((uint32_t)(b3 >> l)) << 3);
+        gw[c0 >> 5] = w;
+        alg += 4;
+    }
+    if (!any) return;
+    const uint64_t lt = (1ull << l) - 1ull;
+    uint32_t off = cnt + (uint32_t)(__popcll(b0 & lt) + __popcll(b1 & lt) + __popcll(b2 & lt) + __popcll(b3 & lt));
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        if ((nib >> i) & 1u) {
+            if (off < GS_CAND_CAP) { L[off] = make_uint2(c0 + i, (ms[i] & 0xFFFFu) | (mr[i] << 16)); alg += 8; }
+            off++;
+        }
+    }
+    cnt += (uint32_t)(__popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3));
+}
+
 // Owner-column sharded phases ("multi-GPU"): the count pass leaves each exchange's
 // stale-owner bitmaps in GS_R_SLICE_BITS and the DeltaPb bytes of all this slice's candidates per
 // direction in tot[e][dir]; the pack passes resume the sender-order packing where the previous
@@ -799,6 +906,83 @@ __device__ inline uint64_t chain_pack(const PackState &p) {
 }
 __device__ inline PackState chain_unpack(uint64_t v) {
     return PackState{(uint32_t)v, ((v >> 32) & 1ull) != 0, ((v >> 33) & 1ull) != 0};
+}
+
+// Split canonical phase, kernel 1 of 2 (k_pass1 -> k_pack_slice): pass 1 alone, streaming both rows with
+// no LDS at all; the stale-owner bitmaps of both directions go to GS_R_SLICE_BITS ([e][2][NP/32],
+// natural bit order) for the packer.  Without LDS the occupancy is set by registers only, and the
+// latency-bound packing no longer holds a streaming workgroup's slot.
+#ifndef P1_WAVES
+#define P1_WAVES 4
+#endif
+__global__ __launch_bounds__(XB, P1_WAVES) void k_pass1(Dev d, const int32_t *ini, const int32_t *res, uint32_t n,
+                                                        uint32_t t, uint32_t seq) {
+    const uint32_t e = blockIdx.x;
+    if (e >= n) return;
+    const int tid = threadIdx.x, lane = tid & (WAVE - 1), wid = tid >> 6;
+    const int32_t ai = ini[e], bi = res[e];
+    if (ai < 0 || bi < 0 || (uint32_t)ai >= d.N || (uint32_t)bi >= d.N || ai == bi) {
+        if (tid == 0) shard_add(d, C_E_IDX, 1);
+        return;
+    }
+    const uint32_t a = (uint32_t)ai, b = (uint32_t)bi;
+    if (tid == 0) {
+        const uint32_t oa = atomicMax(&d.stamp[a], seq), ob = atomicMax(&d.stamp[b], seq);
+        if (oa == seq || ob == seq) shard_add(d, C_E_CONFLICT, 1);
+    }
+    const bool schA = t >= d.row[a * 4 + 2];
+    const bool schB = t >= d.row[b * 4 + 2];
+    const size_t ra = (size_t)a * d.NP, rb = (size_t)b * d.NP;
+    const uint32_t words = d.NP / 32;
+    uint32_t *gBA = d.sbits + (size_t)e * 2 * words, *gAB = gBA + words;
+    // wave w streams row half w (columns [w*H, min((w+1)*H, ncol)), H a multiple of 256), so its candidate
+    // lists hold that half in column order and the packer reads half 0's list, then half 1's
+    const uint32_t H = ((d.ncol + 1u) / 2u + 255u) & ~255u;
+    const uint32_t lo = (uint32_t)wid * H, hi = min(lo + H, d.ncol);
+    uint2 *LBA = d.cand + ((size_t)e * 4 + 0 * 2 + wid) * GS_CAND_CAP;
+    uint2 *LAB = d.cand + ((size_t)e * 4 + 1 * 2 + wid) * GS_CAND_CAP;
+    uint32_t nBAc = 0, nABc = 0;
+    uint32_t alg = 0, reports = 0, hbw = 0;
+    bool anynew = false;
+    const uint32_t ph = t - d.t_round - 1u;
+    uint64_t *planeA = d.pend + ((size_t)a * 16u + ph) * d.PW;
+    uint64_t *planeB = d.pend + ((size_t)b * 16u + ph) * d.PW;
+    if (tid == 0) {
+        d.pstamp[a * 16u + ph] = t;
+        d.pstamp[b * 16u + ph] = t;
+    }
+    uint32_t c0 = lo + (uint32_t)lane * 4u;
+    Grp g0, g1;
+    if (c0 < hi) load_grp<false>(d, ra, rb, c0, schA, schB, g0);
+    while (c0 < hi) {
+        const uint32_t c1 = c0 + WAVE * 4u;
+        if (c1 < hi) load_grp<false>(d, ra, rb, c1, schA, schB, g1);
+        uint32_t rmA, rmB, nBA, nAB, nNB, nNA;
+        const uint32_t mA[4] = {g0.mA[0], g0.mA[1], g0.mA[2], g0.mA[3]};
+        const uint32_t mB[4] = {g0.mB[0], g0.mB[1], g0.mB[2], g0.mB[3]};
+        pass1_grp<false>(d, ra, rb, c0, a, b, t, schA, schB, g0, nBA, nAB, nNB, nNA, alg, reports, hbw, rmA, rmB);
+        anynew = anynew || (nNB | nNA) != 0u;
+        store_plane(planeA, c0, rmA, alg);
+        store_plane(planeB, c0, rmB, alg);
+        emit_dir(gBA, LBA, nBAc, c0, nBA, mB, mA, alg);  // b -> a: sender b, receiver a
+        emit_dir(gAB, LAB, nABc, c0, nAB, mA, mB, alg);
+        g0 = g1;
+        c0 = c1;
+    }
+    if (lane == 0) {
+        d.cand_n[(size_t)e * 4 + 0 * 2 + wid] = nBAc;
+        d.cand_n[(size_t)e * 4 + 1 * 2 + wid] = nABc;
+    }
+    // canonical: every observer knows every owner, so no owner can be new to a side
+    const unsigned long long s_alg = wave_sum(alg), s_rep = wave_sum(reports), s_hbw = wave_sum(hbw);
+    const bool wnew = __ballot(anynew) != 0ull;
+    if (lane == 0) {
+        shard_add(d, C_ALG, s_alg);
+        shard_add(d, C_REPORTS, s_rep);
+        shard_add(d, C_HBW, s_hbw);
+        if (wnew) shard_add(d, C_E_INSERT, 1);
+        if (wid == 0) shard_add(d, C_EXCH, 1);
+    }
 }
 
 // MODE 0: the whole exchange (one slice).  MODE 1: sharded count pass (pass 1, then the slice totals).
@@ -855,9 +1039,14 @@ __global__ __launch_bounds__(XB, (KW == 4 ? XB_WAVES : 1)) void k_exchange(Dev d
     while (c0 < d.ncol) {
         const uint32_t c1 = c0 + XB * 4u;
         if (c1 < d.ncol) load_grp<GENM>(d, ra, rb, c1, schA, schB, g1);
-        uint32_t rmA, rmB;
-        pass1_grp<GENM>(d, ra, rb, c0, a, b, t, schA, schB, g0, bBA, bAB, bNB, bNA, alg, reports, hbw, anynew, rmA,
-                        rmB);
+        uint32_t rmA, rmB, nBA, nAB, nNB, nNA;
+        pass1_grp<GENM>(d, ra, rb, c0, a, b, t, schA, schB, g0, nBA, nAB, nNB, nNA, alg, reports, hbw, rmA, rmB);
+        // one LDS atomic per lane and bitmap (4 consecutive columns sit in one word); stale owners are sparse
+        const uint32_t sh = c0 & 31u;
+        if (nBA) atomicOr(&bBA[c0 >> 5], nBA << sh);
+        if (nAB) atomicOr(&bAB[c0 >> 5], nAB << sh);
+        if (nNB) { atomicOr(&bNB[c0 >> 5], nNB << sh); anynew = true; }
+        if (nNA) { atomicOr(&bNA[c0 >> 5], nNA << sh); anynew = true; }
         if (!(d.ablate & 2u)) {
             store_plane(planeA, c0, rmA, alg);
             store_plane(planeB, c0, rmB, alg);
@@ -968,7 +1157,10 @@ __global__ __launch_bounds__(XB, (KW == 4 ? XB_WAVES : 1)) void k_exchange(Dev d
 // finished continues from the predecessor's state.  Sequential semantics over the slices in
 // column (= canonical dict) order, so the result is the single-slice result bit for bit.
 template <int KW>
-__global__ __launch_bounds__(XB) void k_pack_slice(Dev d, const int32_t *ini, const int32_t *res, uint32_t n,
+#ifndef PK_WAVES
+#define PK_WAVES 4
+#endif
+__global__ __launch_bounds__(XB, (KW == 4 ? PK_WAVES : 1)) void k_pack_slice(Dev d, const int32_t *ini, const int32_t *res, uint32_t n,
                                                    uint32_t t, SliceIO io) {
     __shared__ __attribute__((aligned(16))) uint16_t s_wbuf[2 * WIN];
     const uint32_t e = blockIdx.x;
@@ -999,8 +1191,23 @@ __global__ __launch_bounds__(XB) void k_pack_slice(Dev d, const int32_t *ini, co
     const uint32_t words = d.NP / 32;
     WStats st{0, 0, 0, 0, 0};
     bool tomb = false;
-    pack_dir<KW, false, false>(d, snd, rcv, ds, nullptr, d.ncol, d.sbits + (slot * words), s_wbuf + wid * WIN, t,
-                               st, tomb, pst);
+    if (d.cand && d.shards == 1) {
+        // one-slice split phase: pass 1's candidate lists, half 0 then half 1; a half with more stale
+        // owners than the list holds is walked in the bitmap instead
+        const uint32_t H = ((d.ncol + 1u) / 2u + 255u) & ~255u;
+        for (uint32_t hf = 0; hf < 2 && !pst.stop; hf++) {
+            const uint32_t nh = d.cand_n[slot * 2 + hf];
+            if (nh <= GS_CAND_CAP)
+                pack_list<KW>(d, snd, rcv, ds, d.cand + (slot * 2 + hf) * GS_CAND_CAP, nh, t, st, tomb, pst);
+            else
+                pack_dir<KW, false, false>(d, snd, rcv, ds, nullptr, min(H * (hf + 1), d.ncol),
+                                           d.sbits + (slot * words), s_wbuf + wid * WIN, t, st, tomb, pst, nullptr,
+                                           nullptr, H * hf);
+        }
+    } else {
+        pack_dir<KW, false, false>(d, snd, rcv, ds, nullptr, d.ncol, d.sbits + (slot * words), s_wbuf + wid * WIN, t,
+                                   st, tomb, pst);
+    }
     if (tomb) d.row[rcv * 4 + 1] = 1u;
     if (lane == 0 && io.chain) io.chain[slot] = chain_pack(pst);
     const unsigned long long s_alg = wave_sum(st.alg), s_nd = wave_sum(st.nd), s_kv = wave_sum(st.kvs);
@@ -1960,6 +2167,9 @@ struct gs_handle {
     hipStream_t stream;
     uint32_t seq;
     bool booted;
+    // canonical unsliced handles run a phase as two kernels (k_pass1, k_pack_slice); env GS_FUSED=1
+    // selects the single fused k_exchange instead (A/B measurements)
+    bool split;
     std::string err;
 };
 
@@ -2008,6 +2218,8 @@ int check_bound(gs_handle *h) {
     d.stamp = (uint32_t *)h->reg[GS_R_STAMP];
     d.ctr = (unsigned long long *)h->reg[GS_R_COUNTERS];
     d.sbits = (uint32_t *)h->reg[GS_R_SLICE_BITS];
+    d.cand = (uint2 *)h->reg[GS_R_CAND];
+    d.cand_n = (uint32_t *)h->reg[GS_R_CAND_N];
     d.pend = (uint64_t *)h->reg[GS_R_PEND];
     d.pstamp = (uint32_t *)h->reg[GS_R_PEND_STAMP];
     return GS_OK;
@@ -2140,7 +2352,10 @@ int gs_create(const gs_config *cfg, gs_handle **out) {
     b[GS_R_KEY_LEN] = KP;
     b[GS_R_STAMP] = NR * 4;
     b[GS_R_COUNTERS] = (uint64_t)NSHARD * 32 * 8;
-    b[GS_R_SLICE_BITS] = G > 1 ? (N / 2) * 2 * (NP / 32) * 4 : 0;
+    h->split = G == 1 && (c.flags & GS_CANONICAL) && !(getenv("GS_FUSED") && atoi(getenv("GS_FUSED")));
+    b[GS_R_SLICE_BITS] = (G > 1 || h->split) ? (N / 2) * 2 * (NP / 32) * 4 : 0;
+    b[GS_R_CAND] = h->split ? (N / 2) * 4 * GS_CAND_CAP * 8 : 0;
+    b[GS_R_CAND_N] = h->split ? (N / 2) * 4 * 4 : 0;
     const uint64_t PW = round_up(h->NP, 256) / 64;
     b[GS_R_PEND] = N * 16 * PW * 8;  // 16 phase bit planes per observer row
     b[GS_R_PEND_STAMP] = N * 16 * 4;
@@ -2299,6 +2514,14 @@ int gs_run_phase(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t 
     h->reports_pending = true;
     h->last_phase_tick = tick;
     h->hb_incs++;
+    if (h->split) {
+        k_pass1<<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, h->seq);
+        HIPCHK(h, hipGetLastError());
+        if (h->KP <= 16) k_pack_slice<4><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, io);
+        else k_pack_slice<16><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, io);
+        HIPCHK(h, hipGetLastError());
+        return GS_OK;
+    }
     if (h->KP <= 16) return genm ? launch_exchange<4, true, 0>(h, ini, res, n, tick, lds, io)
                                  : launch_exchange<4, false, 0>(h, ini, res, n, tick, lds, io);
     return genm ? launch_exchange<16, true, 0>(h, ini, res, n, tick, lds, io)

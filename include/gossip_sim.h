@@ -28,10 +28,11 @@
 extern "C" {
 #endif
 
-#define GS_API_VERSION 8
+#define GS_API_VERSION 9
 #define GS_MAX_PHASES 64  /* gs_schedule_phases: phases per round */
 #define GS_TICK_US 15625u
 #define GS_NONE 0xFFFFFFFFu
+#define GS_CAND_CAP 1024u /* GS_R_CAND records per exchange, direction and row half */
 
 /* error codes */
 #define GS_OK 0
@@ -109,8 +110,9 @@ enum gs_region {
     GS_R_KEY_LEN,     /* u8  [KP]      UTF-8 key length per key index */
     GS_R_STAMP,       /* u32 [N rounded to 64] per-node phase stamp (conflict check) */
     GS_R_COUNTERS,    /* u64 [64][32]  sharded gs_counters (summed by gs_read_counters) */
-    GS_R_SLICE_BITS,  /* u32 [N/2][2][NP/32] stale-owner bitmaps between gs_phase_count and
-                                        gs_phase_pack (n_shards > 1 only) */
+    GS_R_SLICE_BITS,  /* u32 [N/2][2][NP/32] stale-owner bitmaps per exchange and direction: between
+                                        gs_phase_count and gs_phase_pack (n_shards > 1), and between the two
+                                        kernels of a canonical one-slice gs_run_phase */
     GS_R_PEND,        /* u64 [N][16][PW] heartbeat reports of the current round: one bit plane per phase
                                         p (tick = round tick + 1 + p) and observer row, PW = NP rounded up
                                         to 256, / 64; column c at word (c/256)*4 + c%4, bit (c/4)%64;
@@ -119,6 +121,12 @@ enum gs_region {
                                         valid for the current round only if it equals round tick + 1 + p */
     GS_R_LATEST,      /* u64 [NC][KP]  the HIST entry of each key's latest write (no GS_TOMBSTONES only) */
     GS_R_SELF_HB,     /* u32 [NP]      each owner column's own heartbeat (the diagonal of GS_R_HB, full width) */
+    GS_R_CAND,        /* u64 [N/2][2][2][GS_CAND_CAP] canonical one-slice phases: each exchange's stale owners
+                                        per direction and row half, in column order, as {local column,
+                                        sender max_version word | receiver max_version word << 16}, written
+                                        by pass 1 for the packer (the first GS_CAND_CAP of each half) */
+    GS_R_CAND_N,      /* u32 [N/2][2][2] stale owners found per exchange, direction and row half (may exceed
+                                        GS_CAND_CAP: the packer then walks GS_R_SLICE_BITS for that half) */
     GS_NUM_REGIONS
 };
 
