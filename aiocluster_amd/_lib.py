@@ -69,7 +69,7 @@ EXPORTS = [
     "gs_boot", "gs_warm", "gs_owner_writes", "gs_begin_round", "gs_run_phase", "gs_liveness", "gs_phi_row",
     "gs_read_counters", "gs_reset_counters", "gs_sync", "gs_shard_columns", "gs_phase_count", "gs_phase_pack", "gs_materialize_held", "gs_fd_census",
     "gs_select_peers", "gs_schedule_phases", "gs_set_events", "gs_emit_scratch_bytes", "gs_emit_digest", "gs_emit_delta",
-    "gs_check_heartbeat_lag", "gs_stream_copy", "gs_stream_read",
+    "gs_check_heartbeat_lag", "gs_stream_copy", "gs_stream_read", "gs_stream_write", "gs_set_timing", "gs_kernel_times",
 ]
 
 API_VERSION = 9
@@ -100,6 +100,13 @@ class GsCounters(C.Structure):
 
 
 CENSUS_FIELDS = ["up_pairs", "up_dead", "up_live", "down_pairs", "down_live"]
+
+
+KT_KINDS = ["pass1", "pack", "liveness"]  # GS_KT_PASS1, GS_KT_PACK, GS_KT_LIVENESS
+
+
+class GsKtimes(C.Structure):
+    _fields_ = [("ms", C.c_double * 4), ("launches", C.c_uint64 * 4)]
 
 
 class GsCensus(C.Structure):
@@ -157,6 +164,8 @@ def load():
         "gs_phi_row": (C.c_int, [P, u32, u32, P]),
         "gs_read_counters": (C.c_int, [P, C.POINTER(GsCounters)]),
         "gs_reset_counters": (C.c_int, [P]),
+        "gs_set_timing": (C.c_int, [P, C.c_int]),
+        "gs_kernel_times": (C.c_int, [P, C.POINTER(GsKtimes)]),
         "gs_sync": (C.c_int, [P]),
         "gs_shard_columns": (C.c_int, [P, C.POINTER(u32), C.POINTER(u32)]),
         "gs_phase_count": (C.c_int, [P, P, P, u32, u32, P]),
@@ -170,6 +179,7 @@ def load():
         "gs_check_heartbeat_lag": (C.c_int, [P]),
         "gs_stream_copy": (C.c_int, [P, P, u64, P]),
         "gs_stream_read": (C.c_int, [P, u64, u32, P, P]),
+        "gs_stream_write": (C.c_int, [P, u64, u32, P]),
         "gs_emit_scratch_bytes": (C.c_int, [P, C.POINTER(u64)]),
         "gs_emit_digest": (C.c_int, [P, C.POINTER(GsWire), u32, u32, P, u64, C.POINTER(u64), P]),
         "gs_emit_delta": (C.c_int, [P, C.POINTER(GsWire), u32, u32, u32, P, u64, C.POINTER(u64), P]),

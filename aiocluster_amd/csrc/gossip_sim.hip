@@ -36,6 +36,7 @@
 #include <cstring>
 #include <string>
 #include <vector>
+#include <type_traits>
 
 #include "../../include/gossip_sim.h"
 
@@ -782,7 +783,9 @@ __device__ __forceinline__ Fd fd_report_val(const Dev &d, size_t p, uint32_t t, 
 // sweep at the end of the round, so pass 1 records each report as one bit in the phase's bit plane
 // (rmA/rmB: bit i = column c0 + i) and k_liveness replays them in tick order before computing phi
 // (same appends, same order).
-template <bool GENM>
+// SCH = false: neither row can have a target scheduled for deletion at t (schA = schB = false; the
+// per-column predicates drop out).  SELF = false: the caller stores the responder's own new heartbeat.
+template <bool GENM, bool SCH = true, bool SELF = true>
 __device__ __forceinline__ void pass1_grp(const Dev &d, size_t ra, size_t rb, uint32_t c0, uint32_t a, uint32_t b,
                                           uint32_t t, bool schA, bool schB, Grp &g, uint32_t &nBA, uint32_t &nAB,
                                           uint32_t &nNB, uint32_t &nNA, uint32_t &alg, uint32_t &reports,
@@ -790,45 +793,56 @@ __device__ __forceinline__ void pass1_grp(const Dev &d, size_t ra, size_t rb, ui
     bool dA = false, dB = false;
     rmA = rmB = 0u;
     nBA = nAB = nNB = nNA = 0u;
-    alg += 48 + (GENM ? 32 : 0) + (schA ? 16 : 0) + (schB ? 16 : 0);
+    // HBM-resident elements only: the SELF_HB row (16 B per group, 256 KiB per row, L2-resident) is not counted
+    alg += 32 + (GENM ? 32 : 0) + (schA ? 16 : 0) + (schB ? 16 : 0);
+    // Branch-free (selects, no exec-mask juggling per column): the per-column rules of the reference,
+    // restated as predicates.  _report_heartbeat (server.py:599-604, state.py:280-287) of a known view
+    // stores the larger heartbeat and reports only if the old one was non-zero; an unknown owner is
+    // inserted with the sender's heartbeat (node_state_or_default).
 #pragma unroll
     for (int i = 0; i < 4; i++) {
         const uint32_t j = c0 + i, jg = d.col_lo + j;  // local column, node id
-        if (j < d.ncol) {
-            const bool pa = GENM ? g.pA[i] != NONE : true;
-            const bool pb = GENM ? g.pB[i] != NONE : true;
-            const bool sa = schA && pa && is_sched(g.fA[i], t, d.sched_delay);
-            const bool sb = schB && pb && is_sched(g.fB[i], t, d.sched_delay);
-            const bool inA = pa && !sa;  // j is in a's digest (compute_digest, state.py:324-331)
-            uint32_t hA = g.hA[i], hB = g.hB[i];
-            if (jg == b) { hB += 1u; dB = true; hbw++; d.self_hb[j] = hB; }  // responder inc_heartbeat (server.py:524)
-            bool newB = false, repB = false;
-            if (inA && jg != b) {  // b: _report_heartbeat over a's digest (server.py:336-337, 599-604)
-                if (!pb) { newB = true; hB = hA; dB = true; hbw++; }
-                else if (hB == 0u) { if (hA) { hB = hA; dB = true; hbw++; } }
-                else if (hA > hB) { hB = hA; dB = true; hbw++; repB = true; }
-            }
-            const bool pb2 = pb || newB;
-            const bool inB = pb2 && !sb;  // j is in b's digest, computed after the merge (server.py:340)
-            bool newA = false, repA = false;
-            if (inB && jg != a) {  // a: _report_heartbeat over b's digest (server.py:356-357)
-                if (!pa) { newA = true; hA = hB; dA = true; hbw++; }
-                else if (hA == 0u) { if (hB) { hA = hB; dA = true; hbw++; } }
-                else if (hB > hA) { hA = hB; dA = true; hbw++; repA = true; }
-            }
-            g.hA[i] = hA;
-            g.hB[i] = hB;
-            if (repB) { rmB |= 1u << i; reports++; }
-            if (repA) { rmA |= 1u << i; reports++; }
-            // stale owners (state.py:347-357): sender's max_version above the digest's
-            const uint32_t mA = g.mA[i] & MV_MASK, mB = g.mB[i] & MV_MASK;
-            const uint32_t dmA = inA ? mA : 0u;
-            if (pb2 && !sb && mB > dmA) nBA |= 1u << i;
-            const uint32_t dmB = inB ? mB : 0u;
-            if (pa && !sa && mA > dmB) nAB |= 1u << i;
-            if (newB) nNB |= 1u << i;
-            if (newA) nNA |= 1u << i;
-        }
+        const bool valid = j < d.ncol;
+        const bool pa = GENM ? g.pA[i] != NONE : true;
+        const bool pb = GENM ? g.pB[i] != NONE : true;
+        const bool sa = SCH && schA && pa && is_sched(g.fA[i], t, d.sched_delay);
+        const bool sb = SCH && schB && pb && is_sched(g.fB[i], t, d.sched_delay);
+        const bool inA = pa && !sa;  // j is in a's digest (compute_digest, state.py:324-331)
+        uint32_t hA = g.hA[i], hB = g.hB[i];
+        // responder inc_heartbeat (server.py:524): b's view of itself
+        const bool isb = valid && jg == b;
+        hB += isb ? 1u : 0u;
+        if (SELF && isb) d.self_hb[j] = hB;
+        // b: _report_heartbeat over a's digest (server.py:336-337, 599-604)
+        const bool mrgB = valid && inA && jg != b;
+        const bool newB = mrgB && !pb;
+        const bool upB = mrgB && (newB || hA > hB);
+        const bool repB = upB && pb && hB != 0u;
+        hB = upB ? hA : hB;
+        // a: _report_heartbeat over b's digest, computed after b's merge (server.py:340, 356-357)
+        const bool pb2 = pb || newB;
+        const bool inB = pb2 && !sb;  // j is in b's digest
+        const bool mrgA = valid && inB && jg != a;
+        const bool newA = mrgA && !pa;
+        const bool upA = mrgA && (newA || hB > hA);
+        const bool repA = upA && pa && hA != 0u;
+        hA = upA ? hB : hA;
+        g.hA[i] = hA;
+        g.hB[i] = hB;
+        dA = dA || upA;
+        dB = dB || upB || isb;
+        hbw += (uint32_t)upA + (uint32_t)upB + (uint32_t)isb;
+        rmB |= (uint32_t)repB << i;
+        rmA |= (uint32_t)repA << i;
+        reports += (uint32_t)repA + (uint32_t)repB;
+        // stale owners (state.py:347-357): sender's max_version above the digest's
+        const uint32_t mA = g.mA[i] & MV_MASK, mB = g.mB[i] & MV_MASK;
+        const uint32_t dmA = inA ? mA : 0u;
+        const uint32_t dmB = inB ? mB : 0u;
+        nBA |= (uint32_t)(valid && pb2 && !sb && mB > dmA) << i;
+        nAB |= (uint32_t)(valid && pa && !sa && mA > dmB) << i;
+        nNB |= (uint32_t)newB << i;
+        nNA |= (uint32_t)newA << i;
     }
     // only changed 16/32-byte groups are written back (writing whole lines measured slower: r1c vs r1b)
     if (d.ablate & 2u) return;
@@ -916,8 +930,8 @@ __device__ inline PackState chain_unpack(uint64_t v) {
 #define P1_WAVES 4
 #endif
 __global__ __launch_bounds__(XB, P1_WAVES) void k_pass1(Dev d, const int32_t *ini, const int32_t *res, uint32_t n,
-                                                        uint32_t t, uint32_t seq) {
-    const uint32_t e = blockIdx.x;
+                                                        uint32_t t, uint32_t seq, uint32_t e0) {
+    const uint32_t e = e0 + blockIdx.x;  // exchanges [e0, e0 + grid) of the phase (one chunk)
     if (e >= n) return;
     const int tid = threadIdx.x, lane = tid & (WAVE - 1), wid = tid >> 6;
     const int32_t ai = ini[e], bi = res[e];
@@ -951,24 +965,35 @@ __global__ __launch_bounds__(XB, P1_WAVES) void k_pass1(Dev d, const int32_t *in
         d.pstamp[a * 16u + ph] = t;
         d.pstamp[b * 16u + ph] = t;
     }
-    uint32_t c0 = lo + (uint32_t)lane * 4u;
-    Grp g0, g1;
-    if (c0 < hi) load_grp<false>(d, ra, rb, c0, schA, schB, g0);
-    while (c0 < hi) {
-        const uint32_t c1 = c0 + WAVE * 4u;
-        if (c1 < hi) load_grp<false>(d, ra, rb, c1, schA, schB, g1);
-        uint32_t rmA, rmB, nBA, nAB, nNB, nNA;
-        const uint32_t mA[4] = {g0.mA[0], g0.mA[1], g0.mA[2], g0.mA[3]};
-        const uint32_t mB[4] = {g0.mB[0], g0.mB[1], g0.mB[2], g0.mB[3]};
-        pass1_grp<false>(d, ra, rb, c0, a, b, t, schA, schB, g0, nBA, nAB, nNB, nNA, alg, reports, hbw, rmA, rmB);
-        anynew = anynew || (nNB | nNA) != 0u;
-        store_plane(planeA, c0, rmA, alg);
-        store_plane(planeB, c0, rmB, alg);
-        emit_dir(gBA, LBA, nBAc, c0, nBA, mB, mA, alg);  // b -> a: sender b, receiver a
-        emit_dir(gAB, LAB, nABc, c0, nAB, mA, mB, alg);
-        g0 = g1;
-        c0 = c1;
-    }
+    // responder inc_heartbeat (server.py:524): the owner's own heartbeat R is raised once, here; the
+    // view hb[b][b] is raised in the loop.  Other exchanges of the phase decode column b against R or
+    // R + 1, and both bound every view of b in the rows they touch
+    if (tid == 0 && b - d.col_lo < d.ncol) d.self_hb[b - d.col_lo] += 1u;
+    const uint32_t c0s = lo + (uint32_t)lane * 4u;
+    auto loop = [&](auto sch) {
+        constexpr bool SCH = decltype(sch)::value;
+        uint32_t c0 = c0s;
+        Grp g0, g1;
+        if (c0 < hi) load_grp<false>(d, ra, rb, c0, SCH && schA, SCH && schB, g0);
+        while (c0 < hi) {
+            const uint32_t c1 = c0 + WAVE * 4u;
+            if (c1 < hi) load_grp<false>(d, ra, rb, c1, SCH && schA, SCH && schB, g1);
+            uint32_t rmA, rmB, nBA, nAB, nNB, nNA;
+            const uint32_t mA[4] = {g0.mA[0], g0.mA[1], g0.mA[2], g0.mA[3]};
+            const uint32_t mB[4] = {g0.mB[0], g0.mB[1], g0.mB[2], g0.mB[3]};
+            pass1_grp<false, SCH, false>(d, ra, rb, c0, a, b, t, schA, schB, g0, nBA, nAB, nNB, nNA, alg, reports, hbw,
+                                         rmA, rmB);
+            anynew = anynew || (nNB | nNA) != 0u;
+            store_plane(planeA, c0, rmA, alg);
+            store_plane(planeB, c0, rmB, alg);
+            emit_dir(gBA, LBA, nBAc, c0, nBA, mB, mA, alg);  // b -> a: sender b, receiver a
+            emit_dir(gAB, LAB, nABc, c0, nAB, mA, mB, alg);
+            g0 = g1;
+            c0 = c1;
+        }
+    };
+    if (schA || schB) loop(std::true_type{});
+    else loop(std::false_type{});
     if (lane == 0) {
         d.cand_n[(size_t)e * 4 + 0 * 2 + wid] = nBAc;
         d.cand_n[(size_t)e * 4 + 1 * 2 + wid] = nABc;
@@ -1161,9 +1186,9 @@ template <int KW>
 #define PK_WAVES 4
 #endif
 __global__ __launch_bounds__(XB, (KW == 4 ? PK_WAVES : 1)) void k_pack_slice(Dev d, const int32_t *ini, const int32_t *res, uint32_t n,
-                                                   uint32_t t, SliceIO io) {
+                                                   uint32_t t, SliceIO io, uint32_t e0) {
     __shared__ __attribute__((aligned(16))) uint16_t s_wbuf[2 * WIN];
-    const uint32_t e = blockIdx.x;
+    const uint32_t e = e0 + blockIdx.x;
     if (e >= n) return;
     const int tid = threadIdx.x, lane = tid & (WAVE - 1), wid = tid >> 6;
     const int32_t ai = ini[e], bi = res[e];
@@ -2124,17 +2149,26 @@ __global__ __launch_bounds__(LB) void k_luby_scatter(const int32_t *out, const u
 // Streaming copy at 16 B per lane (4 loads in flight per lane, then 4 stores): the measured HBM
 // ceiling bench.py prices k_exchange against.  And a read-only stream at 8 or 16 B per lane whose
 // known byte count calibrates rocprofv3's FETCH_SIZE for the widths the exchange kernel uses.
+// measurement kernels (gs_stream_copy / _read / _write): grid-stride, 8 loads in flight per lane,
+// launched with 32,768 blocks -- the fastest of the copy shapes tools/membench.hip compares
 __global__ __launch_bounds__(256) void k_copy16(uint4 *__restrict__ dst, const uint4 *__restrict__ src, uint64_t n16) {
     const uint64_t stride = (uint64_t)gridDim.x * 256u;
     uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
-    for (; i + 3 * stride < n16; i += 4 * stride) {
-        const uint4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], e = src[i + 3 * stride];
-        dst[i] = a;
-        dst[i + stride] = b;
-        dst[i + 2 * stride] = c;
-        dst[i + 3 * stride] = e;
+    for (; i + 7 * stride < n16; i += 8 * stride) {
+        uint4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) v[u] = src[i + u * stride];
+#pragma unroll
+        for (int u = 0; u < 8; u++) dst[i + u * stride] = v[u];
     }
     for (; i < n16; i += stride) dst[i] = src[i];
+}
+template <typename V>
+__global__ __launch_bounds__(256) void k_write(V *__restrict__ dst, uint64_t n) {
+    const uint64_t stride = (uint64_t)gridDim.x * 256u;
+    V v;
+    memset(&v, 0x5A, sizeof v);
+    for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < n; i += stride) dst[i] = v;
 }
 template <typename V>
 __global__ __launch_bounds__(256) void k_read(const V *__restrict__ src, uint64_t n, unsigned long long *sink) {
@@ -2170,6 +2204,10 @@ struct gs_handle {
     // canonical unsliced handles run a phase as two kernels (k_pass1, k_pack_slice); env GS_FUSED=1
     // selects the single fused k_exchange instead (A/B measurements)
     bool split;
+    // gs_set_timing: HIP events around each kernel launch of a kind (gs_ktimes), on the library's stream
+    bool timing;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> tev[4];
+    std::vector<hipEvent_t> evpool;
     std::string err;
 };
 
@@ -2192,6 +2230,27 @@ int fail(gs_handle *h, int code, const char *fmt, ...) {
     } while (0)
 
 uint32_t round_up(uint32_t x, uint32_t m) { return (x + m - 1) / m * m; }
+
+// gs_set_timing: an event pair around each timed launch, recorded on the library's stream
+int time_begin(gs_handle *h, hipEvent_t &e0) {
+    if (!h->timing) return GS_OK;
+    if (h->evpool.empty()) {
+        HIPCHK(h, hipEventCreate(&e0));
+    } else {
+        e0 = h->evpool.back();
+        h->evpool.pop_back();
+    }
+    HIPCHK(h, hipEventRecord(e0, h->stream));
+    return GS_OK;
+}
+int time_end(gs_handle *h, int kind, hipEvent_t e0) {
+    if (!h->timing) return GS_OK;
+    hipEvent_t e1;
+    int rc = time_begin(h, e1);
+    if (rc) return rc;
+    h->tev[kind].push_back({e0, e1});
+    return GS_OK;
+}
 
 int check_bound(gs_handle *h) {
     for (int r = 0; r < GS_NUM_REGIONS; r++)
@@ -2245,12 +2304,15 @@ size_t exchange_lds(const gs_handle *h) {
 int launch_liveness(gs_handle *h, const uint8_t *up, uint32_t tick, bool replay, bool decide) {
     const uint32_t chunks = (h->ncol + 4 * LB - 1) / (4 * LB);
     const uint32_t per = LIVE_PER, groups = (chunks + per - 1) / per;
+    hipEvent_t e0 = nullptr;
+    int rc = time_begin(h, e0);
+    if (rc) return rc;
     if (h->cfg.flags & GS_FD_RING)
         k_liveness<true><<<groups * h->N, LB, 0, h->stream>>>(h->d, up, tick, chunks, per, replay, decide);
     else
         k_liveness<false><<<groups * h->N, LB, 0, h->stream>>>(h->d, up, tick, chunks, per, replay, decide);
     HIPCHK(h, hipGetLastError());
-    return GS_OK;
+    return time_end(h, GS_KT_LIVENESS, e0);
 }
 
 // A phase more than 16 ticks after the plane base: replay the pending report planes into the sampling
@@ -2281,6 +2343,23 @@ int check_phase(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t n
     if (exchange_lds(h) > 160 * 1024)
         return fail(h, GS_E_UNSUPPORTED, "slice too wide for the LDS bitmaps (%zu B)", exchange_lds(h));
     return GS_OK;
+}
+
+// One canonical one-slice phase: k_pass1, then k_pack_slice, on the caller's stream.  (Overlapping
+// the packing of one chunk of the exchanges with pass 1 of the next, on a second stream, measured
+// slower: 1.92 M vs 2.34 M exchanges/s with 4 chunks, profiles/r2c.)
+int run_split_phase(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t n, uint32_t tick) {
+    const SliceIO io{};
+    hipEvent_t e0 = nullptr;
+    int rc = time_begin(h, e0);
+    if (rc) return rc;
+    k_pass1<<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, h->seq, 0u);
+    HIPCHK(h, hipGetLastError());
+    if ((rc = time_end(h, GS_KT_PASS1, e0)) || (rc = time_begin(h, e0))) return rc;
+    if (h->KP <= 16) k_pack_slice<4><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, io, 0u);
+    else k_pack_slice<16><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, io, 0u);
+    HIPCHK(h, hipGetLastError());
+    return time_end(h, GS_KT_PACK, e0);
 }
 
 }  // namespace
@@ -2386,7 +2465,13 @@ int gs_create(const gs_config *cfg, gs_handle **out) {
     return GS_OK;
 }
 
-void gs_destroy(gs_handle *h) { delete h; }
+void gs_destroy(gs_handle *h) {
+    if (!h) return;
+    for (auto &v : h->tev)
+        for (auto &pr : v) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
+    for (hipEvent_t e : h->evpool) (void)hipEventDestroy(e);
+    delete h;
+}
 
 int gs_region_bytes(const gs_handle *h, int region, uint64_t *bytes) {
     if (!h || !bytes || region < 0 || region >= GS_NUM_REGIONS) return GS_E_INVALID;
@@ -2514,18 +2599,14 @@ int gs_run_phase(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t 
     h->reports_pending = true;
     h->last_phase_tick = tick;
     h->hb_incs++;
-    if (h->split) {
-        k_pass1<<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, h->seq);
-        HIPCHK(h, hipGetLastError());
-        if (h->KP <= 16) k_pack_slice<4><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, io);
-        else k_pack_slice<16><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, io);
-        HIPCHK(h, hipGetLastError());
-        return GS_OK;
-    }
-    if (h->KP <= 16) return genm ? launch_exchange<4, true, 0>(h, ini, res, n, tick, lds, io)
-                                 : launch_exchange<4, false, 0>(h, ini, res, n, tick, lds, io);
-    return genm ? launch_exchange<16, true, 0>(h, ini, res, n, tick, lds, io)
-                : launch_exchange<16, false, 0>(h, ini, res, n, tick, lds, io);
+    if (h->split) return run_split_phase(h, ini, res, n, tick);
+    hipEvent_t e0 = nullptr;
+    if ((rc = time_begin(h, e0))) return rc;
+    if (h->KP <= 16) rc = genm ? launch_exchange<4, true, 0>(h, ini, res, n, tick, lds, io)
+                               : launch_exchange<4, false, 0>(h, ini, res, n, tick, lds, io);
+    else rc = genm ? launch_exchange<16, true, 0>(h, ini, res, n, tick, lds, io)
+                   : launch_exchange<16, false, 0>(h, ini, res, n, tick, lds, io);
+    return rc ? rc : time_end(h, GS_KT_PASS1, e0);
 }
 
 int gs_shard_columns(const gs_handle *h, uint32_t *col_lo, uint32_t *n_cols) {
@@ -2550,8 +2631,11 @@ int gs_phase_count(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_
     h->reports_pending = true;
     h->last_phase_tick = tick;
     h->hb_incs++;
-    if (h->KP <= 16) return launch_exchange<4, false, 1>(h, ini, res, n, tick, lds, io);
-    return launch_exchange<16, false, 1>(h, ini, res, n, tick, lds, io);
+    hipEvent_t e0 = nullptr;
+    if ((rc = time_begin(h, e0))) return rc;
+    rc = h->KP <= 16 ? launch_exchange<4, false, 1>(h, ini, res, n, tick, lds, io)
+                     : launch_exchange<16, false, 1>(h, ini, res, n, tick, lds, io);
+    return rc ? rc : time_end(h, GS_KT_PASS1, e0);
 }
 
 int gs_phase_pack(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t n, uint32_t tick, uint32_t step,
@@ -2568,10 +2652,12 @@ int gs_phase_pack(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t
     io.chain = chain;
     io.step = step;
     if (step && h->shard == 0) return GS_OK;  // slice 0 always finishes at step 0
-    if (h->KP <= 16) k_pack_slice<4><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, io);
-    else k_pack_slice<16><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, io);
+    hipEvent_t e0 = nullptr;
+    if ((rc = time_begin(h, e0))) return rc;
+    if (h->KP <= 16) k_pack_slice<4><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, io, 0u);
+    else k_pack_slice<16><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, io, 0u);
     HIPCHK(h, hipGetLastError());
-    return GS_OK;
+    return time_end(h, GS_KT_PACK, e0);
 }
 
 int gs_liveness(gs_handle *h, const uint8_t *up, uint32_t tick) {
@@ -2727,6 +2813,30 @@ int gs_read_counters(gs_handle *h, gs_counters *out) {
     return GS_OK;
 }
 
+int gs_set_timing(gs_handle *h, int on) {
+    if (!h) return GS_E_INVALID;
+    h->timing = on != 0;
+    return GS_OK;
+}
+
+int gs_kernel_times(gs_handle *h, gs_ktimes *out) {
+    if (!h || !out) return GS_E_INVALID;
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    memset(out, 0, sizeof *out);
+    for (int k = 0; k < 4; k++) {
+        for (auto &pr : h->tev[k]) {
+            float ms = 0.f;
+            HIPCHK(h, hipEventElapsedTime(&ms, pr.first, pr.second));
+            out->ms[k] += ms;
+            out->launches[k]++;
+            h->evpool.push_back(pr.first);
+            h->evpool.push_back(pr.second);
+        }
+        h->tev[k].clear();
+    }
+    return GS_OK;
+}
+
 int gs_reset_counters(gs_handle *h) {
     if (!h || !h->reg[GS_R_COUNTERS]) return GS_E_INVALID;
     HIPCHK(h, hipMemsetAsync(h->reg[GS_R_COUNTERS], 0, h->bytes[GS_R_COUNTERS], h->stream));
@@ -2838,7 +2948,16 @@ int gs_fd_census(gs_handle *h, const uint8_t *up, gs_census *out) {
 
 int gs_stream_copy(void *dst, const void *src, uint64_t bytes, void *stream) {
     if (!dst || !src || (bytes & 15u) || ((uintptr_t)dst & 15u) || ((uintptr_t)src & 15u)) return GS_E_INVALID;
-    k_copy16<<<2048, 256, 0, (hipStream_t)stream>>>((uint4 *)dst, (const uint4 *)src, bytes / 16);
+    k_copy16<<<32768, 256, 0, (hipStream_t)stream>>>((uint4 *)dst, (const uint4 *)src, bytes / 16);
+    return hipGetLastError() == hipSuccess ? GS_OK : GS_E_HIP;
+}
+
+int gs_stream_write(void *dst, uint64_t bytes, uint32_t width, void *stream) {
+    if (!dst || (width != 8 && width != 16) || (bytes % width) || ((uintptr_t)dst & 15u)) return GS_E_INVALID;
+    if (width == 8)
+        k_write<uint2><<<32768, 256, 0, (hipStream_t)stream>>>((uint2 *)dst, bytes / 8);
+    else
+        k_write<uint4><<<32768, 256, 0, (hipStream_t)stream>>>((uint4 *)dst, bytes / 16);
     return hipGetLastError() == hipSuccess ? GS_OK : GS_E_HIP;
 }
 
@@ -2846,10 +2965,10 @@ int gs_stream_read(const void *src, uint64_t bytes, uint32_t width, uint64_t *si
     if (!src || !sink || (width != 8 && width != 16) || (bytes % width) || ((uintptr_t)src & 15u))
         return GS_E_INVALID;
     if (width == 8)
-        k_read<uint2><<<2048, 256, 0, (hipStream_t)stream>>>((const uint2 *)src, bytes / 8,
+        k_read<uint2><<<32768, 256, 0, (hipStream_t)stream>>>((const uint2 *)src, bytes / 8,
                                                               (unsigned long long *)sink);
     else
-        k_read<uint4><<<2048, 256, 0, (hipStream_t)stream>>>((const uint4 *)src, bytes / 16,
+        k_read<uint4><<<32768, 256, 0, (hipStream_t)stream>>>((const uint4 *)src, bytes / 16,
                                                               (unsigned long long *)sink);
     return hipGetLastError() == hipSuccess ? GS_OK : GS_E_HIP;
 }

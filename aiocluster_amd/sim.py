@@ -333,6 +333,16 @@ class GossipSim:
     def reset_counters(self):
         self._chk(self.L.gs_reset_counters(self.h), "gs_reset_counters")
 
+    def set_timing(self, on: bool = True):
+        """gs_set_timing: HIP events around every pass-1 / packing / liveness launch (measurement)."""
+        self._chk(self.L.gs_set_timing(self.h, 1 if on else 0), "gs_set_timing")
+
+    def kernel_times(self) -> dict:
+        """gs_kernel_times (blocking): {kind: (ms summed, launches)} since the previous call."""
+        kt = _lib.GsKtimes()
+        self._chk(self.L.gs_kernel_times(self.h, C.byref(kt)), "gs_kernel_times")
+        return {k: (kt.ms[i], int(kt.launches[i])) for i, k in enumerate(_lib.KT_KINDS)}
+
     def check(self) -> dict:
         """Raise if any device-side check failed; return the counters."""
         c = self.counters()

@@ -14,10 +14,11 @@ runs every exchange on its columns, and the ranks exchange only 16 bytes per exc
 overflows the MTU).  ``value`` is the cluster's exchanges / the slowest rank's time.
 ``--slices G`` rehearses the same sliced path with G slices in one process on one GPU.
 
-Prints ONE JSON line (rank 0) with the roofline of the dominant kernel (k_exchange,
-HIP-event timed on the library's stream) and the CPU baseline (the C oracle on one
-host core, timed on a bounded sample of exchanges whose rows are copied from the
-device state).
+Prints ONE JSON line (rank 0) with the roofline of the dominant kernel (k_pass1: each phase runs
+k_pass1 then k_pack_slice; every kernel HIP-event timed on the library's stream, gs_kernel_times) and
+the CPU baseline (the C oracle on 16 host threads and on one, timed on a bounded sample of exchanges
+whose rows are copied from the device state after the timed rounds, checked bit-exact against the
+device first).
 """
 
 from __future__ import annotations
@@ -232,10 +233,11 @@ def kernel_source_hash() -> str:
     return h.hexdigest()[:16]
 
 
-def load_traffic(workload: str, exchanges_per_launch: float):
-    """HBM bytes per k_exchange launch from the rocprofv3 PMC summary (tools/profile.sh +
-    tools/pmc_summary.py), only if it measured THESE kernels (same source hash): measured bytes per
-    exchange x this run's exchanges per launch.  Returns (bytes or None, provenance note)."""
+def load_traffic(workload: str, kernel: str, units_per_launch: float):
+    """HBM bytes per launch of ``kernel`` from the rocprofv3 PMC summary (tools/profile.sh +
+    tools/pmc_summary.py), only if it measured THESE kernels (same source hash): measured bytes per unit
+    (exchange for the phase kernels, launch for k_liveness) x this run's units per launch.
+    Returns (bytes or None, provenance note)."""
     path = os.path.join(REPO, "profiles", "pmc_summary.json")
     if not os.path.exists(path):
         return None, "no PMC summary"
@@ -243,52 +245,81 @@ def load_traffic(workload: str, exchanges_per_launch: float):
         e = json.load(open(path)).get(workload)
     except Exception as x:  # noqa: BLE001
         return None, f"unreadable PMC summary: {x}"
-    if e is None or e.get("k_exchange_bytes_per_exchange") is None:
-        return None, "no PMC summary for this workload"
+    if e is None or kernel not in e.get("kernels", {}):
+        return None, f"no PMC summary of {kernel} for this workload"
     src = kernel_source_hash()
     if e.get("source_hash") != src:
         return None, f"PMC summary is stale (kernels {e.get('source_hash')} != {src})"
-    return e["k_exchange_bytes_per_exchange"] * exchanges_per_launch, (
-        f"rocprofv3 PMC run {e.get('tag')} of these kernels ({src}): (FETCH_SIZE x {e.get('fetch_factor')} + "
-        f"WRITE_SIZE) per exchange x this run's exchanges per launch")
+    k = e["kernels"][kernel]
+    return k["hbm_bytes_per_unit"] * units_per_launch, (
+        f"rocprofv3 PMC run {e.get('tag')} of these kernels ({src}): (FETCH_SIZE x {k.get('fetch_factor')} + "
+        f"WRITE_SIZE x {k.get('write_factor')}) per {k.get('unit')}, factors calibrated on known-byte streams "
+        f"({e.get('calibration')}), x this run's units per launch")
 
 
-def roofline(sims, local_c, exch, kern_ms, launches, elapsed, torch, dev, rank, group, workload) -> dict:
-    """Roofline of the dominant kernel (k_exchange): HBM-bound integer/byte work, no MFMA.
+KERNEL_OF = {"pass1": "k_pass1", "pack": "k_pack_slice", "liveness": "k_liveness"}
 
-    ``achieved`` = the layout's algorithmic bytes per launch (element bytes the kernel must load and
-    store, counted in-kernel: C_ALG) / the launch's average HIP-event time.  The SURVEY
-    §8(d) formula (u32 M/G/H rows) is kept as a secondary figure: this layout stores heartbeats and
-    max versions as u16 and has no last_gc region without tombstones, so that formula overstates the
-    bytes the kernel has to move."""
-    launches = max(1, launches)
-    avg_s = kern_ms / launches / 1e3
-    alg = sum(x["alg_bytes"] for x in local_c) / launches
+
+def roofline(sims, local_c, exch, kt, elapsed, torch, dev, rank, group, workload) -> dict:
+    """Roofline of the dominant kernel (by summed time; HBM-bound integer/byte work, no MFMA) plus the
+    same figures for the other kernels of the round.
+
+    Times: the library's HIP events around every launch of each kind, on the stream the kernels run on
+    (gs_set_timing / gs_kernel_times).  Bytes (``achieved``): the layout's algorithmic HBM bytes per
+    launch, counted in-kernel (C_ALG: element bytes of HBM-resident regions the kernel must load and
+    store; pass-3 part C_PACKB), DESIGN.md §4/§7.  The SURVEY §8(d) formula (u32 M/G/H rows) is kept as
+    a secondary figure: this layout stores heartbeats and max versions as u16 and has no last_gc
+    region without tombstones, so that formula overstates the bytes."""
+    alg = sum(x["alg_bytes"] for x in local_c)
+    packb = sum(x["pack_bytes"] for x in local_c)
     ncols = sum(s_.ncol for s_ in sims)
-    survey = (exch * 32 * ncols + sum(x["pack_bytes"] for x in local_c)) / launches
-    achieved = alg / avg_s / 1e9 if kern_ms > 0 else 0.0
+    fused = kt["pack"][1] == 0
+    per = {}
+    for kind, (ms, launches) in kt.items():
+        if not launches:
+            continue
+        avg_s = ms / launches / 1e3
+        b = None
+        if kind == "pass1":
+            b = (alg if fused else alg - packb) / launches
+        elif kind == "pack":
+            b = packb / launches
+        ent = {"kernel": "k_exchange (fused)" if (fused and kind == "pass1") else KERNEL_OF[kind],
+               "avg_launch_ms": avg_s * 1e3, "launches": launches, "share_of_step": ms / 1e3 / elapsed}
+        if b is not None:
+            ent.update(alg_bytes_per_launch=b, achieved=b / avg_s / 1e9, frac=b / avg_s / 1e9 / HBM_PEAK_GBPS)
+        units = exch / launches if kind != "liveness" else 1.0
+        if group is None and not fused:
+            tr, note = load_traffic(workload, KERNEL_OF[kind], units)
+            ent.update(traffic=tr, traffic_source=note, traffic_gbs=tr / avg_s / 1e9 if tr else None)
+        per[kind] = ent
+    dom = max(per, key=lambda k: kt[k][0])
+    d = per[dom]
     copy_gbs = copy_ceiling(torch, dev, sims[0].stream) if rank == 0 else None
-    traffic, tnote = load_traffic(workload, exch / launches) if group is None else (None, "sliced run")
+    launches = kt["pass1"][1] or 1
+    survey = (exch * 32 * ncols + packb) / launches
     return {
         "bound": "hbm",
-        "kernel": "k_exchange" if group is None else "sliced phase (count + gather + pack), per rank",
-        "achieved": achieved,
+        "kernel": d["kernel"] if group is None else d["kernel"] + " (one owner-column slice, per rank)",
+        "achieved": d.get("achieved"),
         "peak": HBM_PEAK_GBPS,
         "unit": "GB/s",
-        "frac": achieved / HBM_PEAK_GBPS,
-        "traffic": traffic,
-        "traffic_source": tnote,
-        "alg_bytes_per_launch": alg,
-        "alg_bytes_basis": "in-kernel element bytes (C_ALG): both rows' u16 heartbeats + max versions, changed "
-                           "heartbeat groups written, report bit planes, packing + apply (pass 3)",
-        "avg_launch_ms": avg_s * 1e3,
-        "launches": launches,
-        "kernel_share_of_step": kern_ms / 1e3 / elapsed,
+        "frac": d.get("frac"),
+        "traffic": d.get("traffic"),
+        "traffic_source": d.get("traffic_source", "sliced run: not profiled"),
+        "alg_bytes_per_launch": d.get("alg_bytes_per_launch"),
+        "alg_bytes_basis": "in-kernel element bytes of HBM-resident regions (C_ALG): both rows' u16 heartbeats + "
+                           "max versions read, changed heartbeat groups written, report bit planes, stale-owner "
+                           "bitmaps and candidate records written (pass 1); packing + apply (C_PACKB)",
+        "avg_launch_ms": d["avg_launch_ms"],
+        "launches": d["launches"],
+        "kernel_share_of_step": d["share_of_step"],
         "measured_copy_ceiling": copy_gbs,
-        "achieved_frac_of_copy_ceiling": achieved / copy_gbs if copy_gbs else None,
-        "traffic_gbs": traffic / avg_s / 1e9 if traffic and kern_ms else None,
-        "survey_formula_bytes_per_launch": survey,
-        "survey_formula_gbs": survey / avg_s / 1e9 if kern_ms > 0 else None,
+        "achieved_frac_of_copy_ceiling": d["achieved"] / copy_gbs if copy_gbs and d.get("achieved") else None,
+        "traffic_gbs": d.get("traffic_gbs"),
+        "kernels": per,
+        "survey_formula_bytes_per_phase": survey,
+        "survey_formula_gbs_over_pass1": survey / (kt["pass1"][0] / launches / 1e3) / 1e9 if kt["pass1"][0] else None,
     }
 
 
@@ -415,13 +446,14 @@ def main():
     for s_ in sims:
         s_.check()
         s_.reset_counters()
-    events = []
+        s_.set_timing(True)
+        s_.kernel_times()  # clear
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for r in range(R0, R0 + args.steps):
-        driver.run_round(sims, plans[r], events, group, sel)
+        driver.run_round(sims, plans[r], None, group, sel)
     torch.cuda.synchronize(dev)
     if dist is not None:
         dist.barrier()
@@ -432,11 +464,12 @@ def main():
     exch = sum(plans[r]["exchanges"] for r in range(R0, R0 + args.steps))
     unscheduled = sum(plans[r].get("unscheduled", 0) for r in range(R0, R0 + args.steps))
     assert c["exchanges"] == exch, (c["exchanges"], exch)
-    kern_ms = sum(e0.elapsed_time(e1) for e0, e1 in events)
-    launches = len(events)
+    kt = sims[0].kernel_times()  # slice 0's kernels (each rank: its own slice)
+    for s_ in sims:
+        s_.set_timing(False)
     # a sliced cluster: every rank runs the same exchanges on its columns -> count them once
     exch_total, elapsed_max = aggregate(exch if (group is None or rank == 0) else 0, elapsed, dist, dev)
-    roof = roofline(sims, local_c, exch, kern_ms, launches, elapsed, torch, dev, rank, group, workload)
+    roof = roofline(sims[:1], local_c[:1], exch, kt, elapsed, torch, dev, rank, group, workload)
     cpu = None
     if rank == 0 and group is None and not args.no_cpu_baseline:
         rd = plans[R0 + args.steps]

@@ -145,7 +145,8 @@ typedef struct gs_counters {
     uint64_t kvs_sent;      /* KeyValueUpdates sent */
     uint64_t truncated;     /* NodeDeltas cut by the MTU (sent with a prefix of their kvs) */
     uint64_t delta_bytes;   /* sum of DeltaPb sizes */
-    uint64_t alg_bytes;     /* element-granular bytes loaded + stored by the exchange kernel */
+    uint64_t alg_bytes;     /* element-granular bytes of HBM-resident regions loaded + stored by the exchange
+                               kernels (the L2-resident SELF_HB row they also read is not counted) */
     uint64_t hb_writes;     /* heartbeat entries changed */
     uint64_t candidates;    /* stale owners evaluated by the packers */
     uint64_t live_pairs;    /* (observer, target) pairs swept by the liveness kernel */
@@ -324,6 +325,21 @@ int gs_emit_delta(gs_handle *h, const gs_wire *w, uint32_t sender, uint32_t rece
  * known byte count that calibrates rocprofv3's FETCH_SIZE for those access widths. */
 int gs_stream_copy(void *dst, const void *src, uint64_t bytes, void *stream);
 int gs_stream_read(const void *src, uint64_t bytes, uint32_t width, uint64_t *sink, void *stream);
+/* a write-only stream of `bytes` at `width` = 8 or 16 B per lane: the known byte count for WRITE_SIZE */
+int gs_stream_write(void *dst, uint64_t bytes, uint32_t width, void *stream);
+
+/* Per-kernel timing (measurement): with timing on, every launch of the kinds below is bracketed by HIP
+ * events on the library's stream; gs_kernel_times (blocking) returns the summed milliseconds and launch
+ * counts since the previous call and clears them. */
+#define GS_KT_PASS1 0     /* pass 1: k_pass1 (canonical one slice), the fused k_exchange, gs_phase_count */
+#define GS_KT_PACK 1      /* delta packing + apply_delta: k_pack_slice (canonical one slice, gs_phase_pack) */
+#define GS_KT_LIVENESS 2  /* k_liveness (report replay + liveness sweep) */
+typedef struct gs_ktimes {
+    double ms[4];
+    uint64_t launches[4];
+} gs_ktimes;
+int gs_set_timing(gs_handle *h, int on);
+int gs_kernel_times(gs_handle *h, gs_ktimes *out);
 
 int gs_read_counters(gs_handle *h, gs_counters *out);
 int gs_reset_counters(gs_handle *h);

@@ -1,13 +1,21 @@
-"""Summarise a tools/profile.sh run into profiles/ (kernel stats + HBM traffic per launch).
+"""Summarise a tools/profile.sh run into profiles/ (kernel stats + HBM traffic per launch and per unit).
 
-HBM bytes follow MI355X_MICROARCH.md (HBM section): FETCH_SIZE and WRITE_SIZE are
-collected in separate passes, are in KiB, and on gfx950 FETCH_SIZE reports half
-the bytes of wide (16 B/lane) coalesced streaming reads, so reads are doubled:
-    hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024.
-k_exchange's reads are dominated by 16 B/lane streaming loads (pass 1); its
-gathers (pass 3) are a few percent of the bytes, so the x2 may overstate them.
+HBM bytes follow MI355X_MICROARCH.md (HBM section): FETCH_SIZE and WRITE_SIZE are collected in
+separate passes and are in KiB.  The guide calibrates FETCH_SIZE only for 16-B-per-lane streaming
+reads (it reports half their bytes); other widths are "uncalibrated: calibrate on a known byte count".
+So tools/fetch_calib.py streams a known 1 GiB at 8 and at 16 B per lane, read-only and write-only,
+under the same counters, and this script derives a factor per access width:
+    factor = known bytes / (counter KiB x 1024)
+Each kernel's bytes are then (FETCH_SIZE x f_read(width) + WRITE_SIZE x f_write(width)) x 1024 with the
+width of the kernel's dominant streams:
+    k_pass1       8 B per lane (u16 heartbeat / max_version rows, 4 columns per lane; stores likewise)
+    k_pack_slice  8 B (candidate records; the rest are gathers, which no stream calibrates)
+    k_liveness    16 B per lane (two 16-B window loads + one 16-B state load per 4 columns)
+Only the launches inside bench.py's timed region are averaged (the last N of each kernel, N from the
+bench's JSON line).  The entry written to profiles/pmc_summary.json carries the source hash of the
+kernels it measured, so bench.py ignores it once the kernels change.
 
-Usage: python tools/pmc_summary.py gpurun_out/prof_<tag> <tag> "<workload string>"
+Usage: python tools/pmc_summary.py gpurun_out/prof_<tag> <tag>
 """
 
 from __future__ import annotations
@@ -20,11 +28,20 @@ import sys
 from collections import defaultdict
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+KERNELS = ("k_pass1", "k_pack_slice", "k_liveness", "k_exchange", "k_begin_round", "k_owner_writes",
+           "k_reset_sched", "k_warm", "k_boot_self", "k_phi_row")
+WIDTH = {"k_pass1": 8, "k_pack_slice": 8, "k_liveness": 16, "k_exchange": 8}
+KIND = {"k_pass1": "pass1", "k_pack_slice": "pack", "k_liveness": "liveness", "k_exchange": "pass1"}
+CAL_BYTES = 1 << 30
 
 
 def short(name: str) -> str:
-    for k in ("k_exchange", "k_liveness", "k_begin_round", "k_owner_writes", "k_reset_sched", "k_warm",
-              "k_boot_self", "k_phi_row"):
+    if "k_read<" in name or "k_write<" in name:
+        w = 8 if "2u>" in name else 16
+        return ("read" if "k_read<" in name else "write") + str(w)
+    for k in KERNELS:
         if k in name:
             return k
     return name[:60]
@@ -43,33 +60,42 @@ def kernel_stats(root: str) -> dict:
     return out
 
 
-def timed_launches(root: str, sub: str = "kt") -> int | None:
-    """k_exchange launches inside bench.py's timed region (its JSON line's roofline.launches): the
-    trace's LAST that many k_exchange launches, so settle/warmup rounds are not averaged in."""
+def bench_line(root: str, sub: str) -> dict | None:
     path = os.path.join(root, f"bench_{sub}.log")
     if not os.path.exists(path):
         return None
     for line in open(path):
         if line.startswith("{"):
-            return json.loads(line)["roofline"]["launches"]
+            return json.loads(line)
     return None
 
 
-def trace_avg(root: str, last: int | None) -> dict:
-    """Average k_exchange duration (ms) over the last `last` launches of the kernel trace."""
-    d = []
+def timed_launches(line: dict | None) -> dict:
+    """Launches of each kernel inside bench.py's timed region (its roofline.kernels[kind].launches)."""
+    if not line:
+        return {}
+    per = line.get("roofline", {}).get("kernels", {})
+    return {k: per[kind]["launches"] for k, kind in KIND.items() if kind in per}
+
+
+def trace_avg(root: str, last: dict) -> dict:
+    """Average duration (ms) of each kernel over its last `last[k]` launches of the kernel trace."""
+    d = defaultdict(list)
     for path in glob.glob(os.path.join(root, "kt", "**", "*kernel_trace.csv"), recursive=True):
         for row in csv.DictReader(open(path)):
-            if "k_exchange" in row["Kernel_Name"]:
-                d.append((int(row["Start_Timestamp"]), (int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) / 1e6))
-    d.sort()
-    tail = d[-last:] if last else d
-    return {"launches": len(tail), "avg_ms": sum(x for _, x in tail) / max(1, len(tail))} if tail else {}
+            k = short(row["Kernel_Name"])
+            if k in last:
+                d[k].append((int(row["Start_Timestamp"]), (int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) / 1e6))
+    out = {}
+    for k, v in d.items():
+        v.sort()
+        tail = v[-last[k]:]
+        out[k] = {"launches": len(tail), "avg_ms": sum(x for _, x in tail) / len(tail)}
+    return out
 
 
-def counters(root: str, sub: str, name: str, last: int | None = None) -> tuple[dict, dict]:
-    """Average counter value per launch, and per work-item-group unit (k_exchange: per exchange); with
-    `last`, over each kernel's last `last` dispatches only (the timed region)."""
+def counters(root: str, sub: str, name: str, last: dict | None = None) -> tuple[dict, dict]:
+    """Average counter value per launch and per workgroup, over each kernel's last `last[k]` dispatches."""
     rows = defaultdict(list)
     for path in glob.glob(os.path.join(root, sub, "**", "*counter_collection.csv"), recursive=True):
         for row in csv.DictReader(open(path)):
@@ -77,54 +103,84 @@ def counters(root: str, sub: str, name: str, last: int | None = None) -> tuple[d
                 k = short(row["Kernel_Name"])
                 wg = float(row.get("Grid_Size", 0) or 0) / max(1.0, float(row.get("Workgroup_Size", 1) or 1))
                 rows[k].append((int(row.get("Dispatch_Id", 0) or 0), float(row["Counter_Value"]), wg))
-    avg, per_unit = {}, {}
+    avg, per_wg = {}, {}
     for k, v in rows.items():
         v.sort()
-        if last and k == "k_exchange":
-            v = v[-last:]
+        if last and k in last:
+            v = v[-last[k]:]
         avg[k] = sum(x[1] for x in v) / len(v)
         u = sum(x[2] for x in v)
         if u > 0:
-            per_unit[k] = sum(x[1] for x in v) / u
-    return avg, per_unit
+            per_wg[k] = sum(x[1] for x in v) / u
+    return avg, per_wg
 
 
-def main(root: str, tag: str, workload: str):
+def calibration(root: str) -> dict:
+    f, _ = counters(root, "cal_fetch", "FETCH_SIZE")
+    w, _ = counters(root, "cal_write", "WRITE_SIZE")
+    cal = {}
+    for width in (8, 16):
+        r, wr = f.get(f"read{width}"), w.get(f"write{width}")
+        cal[f"read{width}"] = CAL_BYTES / (r * 1024) if r else None
+        cal[f"write{width}"] = CAL_BYTES / (wr * 1024) if wr else None
+    return cal
+
+
+def main(root: str, tag: str):
+    from bench import kernel_source_hash
+
+    line = bench_line(root, "kt")
+    last = timed_launches(line)
     ks = kernel_stats(root)
-    lastn = timed_launches(root)
-    timed = trace_avg(root, lastn)
-    fetch, fetch_u = counters(root, "fetch", "FETCH_SIZE", timed_launches(root, "fetch"))
-    write, write_u = counters(root, "write", "WRITE_SIZE", timed_launches(root, "write"))
-    traffic = {}
-    for k in set(fetch) | set(write):
-        f, w = fetch.get(k), write.get(k)
-        if f is not None and w is not None:
-            traffic[k] = {"fetch_kib": f, "write_kib": w, "hbm_bytes_per_launch": (2 * f + w) * 1024,
-                          "hbm_bytes_per_workgroup": (2 * fetch_u[k] + write_u[k]) * 1024}
-    summary = {"tag": tag, "workload": workload, "kernel_stats": ks, "k_exchange_timed_region": timed,
-               "traffic": traffic}
+    timed = trace_avg(root, last)
+    cal = calibration(root)
+    fetch, fetch_wg = counters(root, "fetch", "FETCH_SIZE", timed_launches(bench_line(root, "fetch")))
+    write, write_wg = counters(root, "write", "WRITE_SIZE", timed_launches(bench_line(root, "write")))
+    kern = {}
+    for k in WIDTH:
+        if k not in fetch or k not in write:
+            continue
+        ff = cal.get(f"read{WIDTH[k]}") or (2.0 if WIDTH[k] == 16 else None)
+        wf = cal.get(f"write{WIDTH[k]}") or 1.0
+        if ff is None:
+            continue
+        per_launch = (fetch[k] * ff + write[k] * wf) * 1024
+        phase = k != "k_liveness"
+        kern[k] = {
+            "fetch_kib": fetch[k], "write_kib": write[k], "fetch_factor": round(ff, 4), "write_factor": round(wf, 4),
+            "hbm_bytes_per_launch": per_launch,
+            "unit": "exchange" if phase else "launch",
+            "hbm_bytes_per_unit": (fetch_wg[k] * ff + write_wg[k] * wf) * 1024 if phase else per_launch,
+            "avg_ms_timed": timed.get(k, {}).get("avg_ms"),
+            "hbm_gbs": per_launch / (timed[k]["avg_ms"] * 1e6) if k in timed else None,
+        }
+    workload = (line or {}).get("config", {}).get("workload")
+    src = kernel_source_hash()
+    summary = {"tag": tag, "workload": workload, "source_hash": src, "calibration": cal, "kernel_stats": ks,
+               "timed_region": timed, "kernels": kern, "bench": line}
     sq = {}
     for name in ("SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU",
                  "SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_WAVES"):
-        avg, _ = counters(root, "sq", name)
+        avg, _ = counters(root, "sq", name, timed_launches(bench_line(root, "sq")))
         for k, v in avg.items():
             sq.setdefault(k, {})[name] = v
     if sq:
         summary["sq_per_launch"] = sq
-    os.makedirs(os.path.join(REPO, "profiles"), exist_ok=True)
     with open(os.path.join(REPO, "profiles", f"{tag}_summary.json"), "w") as f:
         json.dump(summary, f, indent=1)
     # the file bench.py reads for roofline.traffic
     agg_path = os.path.join(REPO, "profiles", "pmc_summary.json")
     agg = json.load(open(agg_path)) if os.path.exists(agg_path) else {}
-    if "k_exchange" in traffic:
-        agg[workload] = {"tag": tag, "k_exchange_bytes_per_launch": traffic["k_exchange"]["hbm_bytes_per_launch"],
-                         "k_exchange_bytes_per_exchange": traffic["k_exchange"]["hbm_bytes_per_workgroup"],
-                         "k_exchange_avg_ms": timed.get("avg_ms", ks.get("k_exchange", {}).get("avg_ms"))}
+    if workload and kern:
+        agg = {w: e for w, e in agg.items() if isinstance(e, dict) and "kernels" in e}  # drop the old format
+        agg[workload] = {"tag": tag, "source_hash": src, "calibration": cal,
+                         "kernels": {k: {x: v[x] for x in ("hbm_bytes_per_unit", "unit", "fetch_factor",
+                                                           "write_factor", "avg_ms_timed")}
+                                     for k, v in kern.items()}}
         with open(agg_path, "w") as f:
             json.dump(agg, f, indent=1)
-    print(json.dumps(summary, indent=1))
+    print(json.dumps({k: v for k, v in summary.items() if k != "bench"}, indent=1))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2], sys.argv[3])
+    main(sys.argv[1], sys.argv[2])
