@@ -70,6 +70,7 @@ EXPORTS = [
     "gs_read_counters", "gs_reset_counters", "gs_sync", "gs_shard_columns", "gs_phase_count", "gs_phase_pack", "gs_materialize_held", "gs_fd_census",
     "gs_select_peers", "gs_schedule_phases", "gs_set_events", "gs_emit_scratch_bytes", "gs_emit_digest", "gs_emit_delta",
     "gs_check_heartbeat_lag", "gs_stream_copy", "gs_stream_read", "gs_stream_write", "gs_set_timing", "gs_kernel_times",
+    "gs_phase_overflow", "gs_phase_chain",
 ]
 
 API_VERSION = 9
@@ -102,7 +103,7 @@ class GsCounters(C.Structure):
 CENSUS_FIELDS = ["up_pairs", "up_dead", "up_live", "down_pairs", "down_live"]
 
 
-KT_KINDS = ["pass1", "pack", "liveness"]  # GS_KT_PASS1, GS_KT_PACK, GS_KT_LIVENESS
+KT_KINDS = ["pass1", "pack", "liveness", "count"]  # GS_KT_PASS1, GS_KT_PACK, GS_KT_LIVENESS, GS_KT_COUNT
 
 
 class GsKtimes(C.Structure):
@@ -165,6 +166,8 @@ def load():
         "gs_read_counters": (C.c_int, [P, C.POINTER(GsCounters)]),
         "gs_reset_counters": (C.c_int, [P]),
         "gs_set_timing": (C.c_int, [P, C.c_int]),
+        "gs_phase_overflow": (C.c_int, [P, u32, P, P, P, P, C.POINTER(u32)]),
+        "gs_phase_chain": (C.c_int, [P, P, P, u32, u32, u32, P, u32, P, P, P]),
         "gs_kernel_times": (C.c_int, [P, C.POINTER(GsKtimes)]),
         "gs_sync": (C.c_int, [P]),
         "gs_shard_columns": (C.c_int, [P, C.POINTER(u32), C.POINTER(u32)]),

@@ -660,14 +660,14 @@ __device__ __forceinline__ void pack_dir(const Dev &d, uint32_t s, uint32_t r, c
 // List source (canonical, one slice): the n stale owners pass 1 recorded for one row half, in column
 // order, each with both views' max_version words (GS_R_CAND), so no row is read again.  The next
 // group's records are loaded one group ahead.
-template <int KW>
+template <int KW, bool COUNT = false>
 __device__ __forceinline__ void pack_list(const Dev &d, uint32_t s, uint32_t r, const DigestSide ds, const uint2 *L,
                                           uint32_t n, uint32_t t, WStats &st, bool &tomb, PackState &pst) {
     const int lane = lane_id();
     const uint32_t S0 = pst.S;
     uint32_t S;
     bool tail, stop;
-    pack_begin(d, false, pst, S, tail, stop);
+    pack_begin(d, COUNT, pst, S, tail, stop);
     uint32_t nr = 0;
     uint2 nxt = make_uint2(0u, 0u);
     if ((uint32_t)lane < n) nxt = L[lane];
@@ -683,12 +683,30 @@ __device__ __forceinline__ void pack_list(const Dev &d, uint32_t s, uint32_t r, 
             eval_cand<KW, false, true>(d, s, r, ds, cr.x, t, c, st.alg, cr.y);
             st.cand++;
         }
-        pack_group<KW, false, false>(d, r, t, c, cand, S, tail, stop, st, tomb, nullptr, nr);
+        pack_group<KW, COUNT, false>(d, r, t, c, cand, S, tail, stop, st, tomb, nullptr, nr);
     }
     pst.S = S;
     pst.tail = tail;
     pst.stop = stop;
-    if (lane == 0) shard_add(d, C_DBYTES, S - S0);
+    if (!COUNT && lane == 0) shard_add(d, C_DBYTES, S - S0);
+}
+
+// Candidates of one direction of exchange slot from pass 1's records (row half 0, then half 1), or
+// the bitmap walk for a half whose records overflowed GS_CAND_CAP.
+template <int KW, bool COUNT>
+__device__ __forceinline__ void pack_records(const Dev &d, uint32_t snd, uint32_t rcv, const DigestSide &ds,
+                                             size_t slot, uint16_t *wbuf, uint32_t t, WStats &st, bool &tomb,
+                                             PackState &pst) {
+    const uint32_t H = ((d.ncol + 1u) / 2u + 255u) & ~255u;
+    const uint32_t words = d.NP / 32;
+    for (uint32_t hf = 0; hf < 2 && (COUNT || !pst.stop); hf++) {
+        const uint32_t nh = d.cand_n[slot * 2 + hf];
+        if (nh <= GS_CAND_CAP)
+            pack_list<KW, COUNT>(d, snd, rcv, ds, d.cand + (slot * 2 + hf) * GS_CAND_CAP, nh, t, st, tomb, pst);
+        else
+            pack_dir<KW, false, COUNT>(d, snd, rcv, ds, nullptr, min(H * (hf + 1), d.ncol), d.sbits + (slot * words),
+                                       wbuf, t, st, tomb, pst, nullptr, nullptr, H * hf);
+    }
 }
 
 // ------------------------------------------------------------------ exchange kernel
@@ -929,8 +947,14 @@ __device__ inline PackState chain_unpack(uint64_t v) {
 #ifndef P1_WAVES
 #define P1_WAVES 4
 #endif
-__global__ __launch_bounds__(XB, P1_WAVES) void k_pass1(Dev d, const int32_t *ini, const int32_t *res, uint32_t n,
-                                                        uint32_t t, uint32_t seq, uint32_t e0) {
+// FUSE: the same workgroup then packs and applies both directions from the records (wave 0: b -> a,
+// wave 1: a -> b) right after streaming the rows, while the receivers' max_version lines are still in L2
+// (the applies are one scattered 2-byte store per NodeDelta; tools/membench.hip prices those at 25 G/s
+// from HBM).
+template <int KW, bool FUSE>
+__global__ __launch_bounds__(XB, (KW == 4 ? P1_WAVES : 1)) void k_pass1(Dev d, const int32_t *ini, const int32_t *res,
+                                                                       uint32_t n, uint32_t t, uint32_t seq,
+                                                                       uint32_t e0) {
     const uint32_t e = e0 + blockIdx.x;  // exchanges [e0, e0 + grid) of the phase (one chunk)
     if (e >= n) return;
     const int tid = threadIdx.x, lane = tid & (WAVE - 1), wid = tid >> 6;
@@ -1006,7 +1030,30 @@ __global__ __launch_bounds__(XB, P1_WAVES) void k_pass1(Dev d, const int32_t *in
         shard_add(d, C_REPORTS, s_rep);
         shard_add(d, C_HBW, s_hbw);
         if (wnew) shard_add(d, C_E_INSERT, 1);
-        if (wid == 0) shard_add(d, C_EXCH, 1);
+        if (wid == 0 && d.shard == 0) shard_add(d, C_EXCH, 1);  // slices: every slice runs every exchange
+    }
+    if constexpr (FUSE) {
+        __shared__ __attribute__((aligned(16))) uint16_t s_wbuf[2 * WIN];
+        __syncthreads();  // both halves' records and counts are written (workgroup scope)
+        const size_t slot = (size_t)e * 2 + wid;
+        const bool w0 = wid == 0;
+        const uint32_t snd = w0 ? b : a, rcv = w0 ? a : b;
+        const DigestSide ds{rcv, d.ncol, w0 ? schA : schB};
+        WStats st{0, 0, 0, 0, 0};
+        bool tomb = false;
+        PackState pst{0u, false, false};
+        pack_records<KW, false>(d, snd, rcv, ds, slot, s_wbuf + wid * WIN, t, st, tomb, pst);
+        if (tomb) d.row[rcv * 4 + 1] = 1u;
+        const unsigned long long p_alg = wave_sum(st.alg), p_nd = wave_sum(st.nd), p_kv = wave_sum(st.kvs);
+        const unsigned long long p_tr = wave_sum(st.trunc), p_cd = wave_sum(st.cand);
+        if (lane == 0) {
+            shard_add(d, C_ALG, p_alg);
+            shard_add(d, C_PACKB, p_alg);
+            shard_add(d, C_ND, p_nd);
+            shard_add(d, C_KVS, p_kv);
+            shard_add(d, C_TRUNC, p_tr);
+            shard_add(d, C_CAND, p_cd);
+        }
     }
 }
 
@@ -1216,19 +1263,10 @@ __global__ __launch_bounds__(XB, (KW == 4 ? PK_WAVES : 1)) void k_pack_slice(Dev
     const uint32_t words = d.NP / 32;
     WStats st{0, 0, 0, 0, 0};
     bool tomb = false;
-    if (d.cand && d.shards == 1) {
-        // one-slice split phase: pass 1's candidate lists, half 0 then half 1; a half with more stale
-        // owners than the list holds is walked in the bitmap instead
-        const uint32_t H = ((d.ncol + 1u) / 2u + 255u) & ~255u;
-        for (uint32_t hf = 0; hf < 2 && !pst.stop; hf++) {
-            const uint32_t nh = d.cand_n[slot * 2 + hf];
-            if (nh <= GS_CAND_CAP)
-                pack_list<KW>(d, snd, rcv, ds, d.cand + (slot * 2 + hf) * GS_CAND_CAP, nh, t, st, tomb, pst);
-            else
-                pack_dir<KW, false, false>(d, snd, rcv, ds, nullptr, min(H * (hf + 1), d.ncol),
-                                           d.sbits + (slot * words), s_wbuf + wid * WIN, t, st, tomb, pst, nullptr,
-                                           nullptr, H * hf);
-        }
+    if (d.cand) {
+        // pass 1's candidate lists (k_pass1), half 0 then half 1; a half with more stale owners than the
+        // list holds is walked in the bitmap instead
+        pack_records<KW, false>(d, snd, rcv, ds, slot, s_wbuf + wid * WIN, t, st, tomb, pst);
     } else {
         pack_dir<KW, false, false>(d, snd, rcv, ds, nullptr, d.ncol, d.sbits + (slot * words), s_wbuf + wid * WIN, t,
                                    st, tomb, pst);
@@ -1246,6 +1284,123 @@ __global__ __launch_bounds__(XB, (KW == 4 ? PK_WAVES : 1)) void k_pack_slice(Dev
         shard_add(d, C_CAND, s_cd);
     }
 }
+
+// Overflowing slots of a sliced phase (gs_phase_overflow): every (exchange, direction) slot whose slice
+// totals sum past the mtu, in slot order -- the same list on every slice, since all hold the same
+// gathered totals -- plus this slice's chain state of each listed slot (chainc[i] = chain[list[i]]).
+// Two launches of 1024-thread blocks: per-block counts, then per-block offsets (a sum over at most a
+// few dozen block counts) and a ballot scan inside the block.  scratch = list + 2n: [blocks] counts,
+// then the total.
+constexpr uint32_t OVB = 1024;
+__global__ __launch_bounds__(OVB) void k_ov_count(const uint64_t *tot_all, uint32_t slots, uint32_t G, uint32_t mtu,
+                                                  uint32_t *blkcnt) {
+    const uint32_t sl = blockIdx.x * OVB + threadIdx.x;
+    uint64_t sum = 0;
+    if (sl < slots)
+        for (uint32_t g = 0; g < G; g++) sum += tot_all[(size_t)g * slots + sl];
+    const int c = __syncthreads_count(sl < slots && sum > mtu);
+    if (threadIdx.x == 0) blkcnt[blockIdx.x] = (uint32_t)c;
+}
+__global__ __launch_bounds__(OVB) void k_ov_write(const uint64_t *tot_all, uint32_t slots, uint32_t G, uint32_t mtu,
+                                                  const uint64_t *chain, uint32_t *list, uint64_t *chainc) {
+    __shared__ uint32_t s_w[OVB / WAVE];
+    __shared__ uint32_t s_off;
+    const uint32_t nb = gridDim.x;
+    const uint32_t *blkcnt = list + slots;
+    if (threadIdx.x == 0) {
+        uint32_t off = 0, all = 0;
+        for (uint32_t b = 0; b < nb; b++) {
+            if (b < blockIdx.x) off += blkcnt[b];
+            all += blkcnt[b];
+        }
+        s_off = off;
+        if (blockIdx.x == nb - 1) list[slots + nb] = all;  // the count (read by the host)
+    }
+    const uint32_t sl = blockIdx.x * OVB + threadIdx.x;
+    uint64_t sum = 0;
+    if (sl < slots)
+        for (uint32_t g = 0; g < G; g++) sum += tot_all[(size_t)g * slots + sl];
+    const bool f = sl < slots && sum > mtu;
+    const unsigned long long m = __ballot(f);
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    if (l == 0) s_w[w] = (uint32_t)__popcll(m);
+    __syncthreads();
+    uint32_t pre = s_off;
+    for (int x = 0; x < w; x++) pre += s_w[x];
+    if (f) {
+        const uint32_t i = pre + (uint32_t)__popcll(m & ((1ull << l) - 1ull));
+        list[i] = sl;
+        chainc[i] = chain[sl];
+    }
+}
+
+// Chain step `step` >= 1 over the overflowing slots only (gs_phase_chain): one wave per listed slot; a
+// slot still pending on this slice continues from its predecessor's gathered state (chain_all =
+// [G][count] of every slice's chainc).  State goes to both chain (by slot) and chainc (by list index).
+template <int KW>
+__global__ __launch_bounds__(WAVE) void k_chain_step(Dev d, const int32_t *ini, const int32_t *res, uint32_t t,
+                                                     const uint32_t *list, uint32_t count, const uint64_t *chain_all,
+                                                     uint64_t *chain, uint64_t *chainc) {
+    __shared__ __attribute__((aligned(16))) uint16_t s_wbuf[WIN];
+    const int lane = lane_id();
+    for (uint32_t i = blockIdx.x; i < count; i += gridDim.x) {
+        const uint32_t slot = list[i];
+        if (chain[slot] != CHAIN_PENDING) continue;
+        const uint64_t prev = chain_all[(size_t)(d.shard - 1) * count + i];
+        if (prev == CHAIN_PENDING) continue;
+        PackState pst = chain_unpack(prev);
+        const uint32_t e = slot >> 1, wid = slot & 1u;
+        const uint32_t a = (uint32_t)ini[e], b = (uint32_t)res[e];
+        const bool w0 = wid == 0;
+        const uint32_t snd = w0 ? b : a, rcv = w0 ? a : b;
+        const DigestSide ds{rcv, d.ncol, t >= d.row[rcv * 4 + 2]};
+        WStats st{0, 0, 0, 0, 0};
+        bool tomb = false;
+        pack_records<KW, false>(d, snd, rcv, ds, slot, s_wbuf, t, st, tomb, pst);
+        if (tomb) d.row[rcv * 4 + 1] = 1u;
+        if (lane == 0) {
+            chain[slot] = chain_pack(pst);
+            chainc[i] = chain_pack(pst);
+        }
+        const unsigned long long s_alg = wave_sum(st.alg), s_nd = wave_sum(st.nd), s_kv = wave_sum(st.kvs);
+        const unsigned long long s_tr = wave_sum(st.trunc), s_cd = wave_sum(st.cand);
+        if (lane == 0) {
+            shard_add(d, C_ALG, s_alg);
+            shard_add(d, C_PACKB, s_alg);
+            shard_add(d, C_ND, s_nd);
+            shard_add(d, C_KVS, s_kv);
+            shard_add(d, C_TRUNC, s_tr);
+            shard_add(d, C_CAND, s_cd);
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// Sharded count pass, after k_pass1 on a sliced handle (gs_phase_count): the DeltaPb bytes of every
+// stale owner of this slice per exchange and direction (wave 0: b -> a, wave 1: a -> b), from pass 1's
+// candidate records, into tot[e][dir].  (Sizing every record with 4 waves per slot and handing the sizes
+// to the packer measured slower at 8 slices: 0.53 vs 0.45 ms per slice and phase, profiles/r2h.)
+template <int KW>
+__global__ __launch_bounds__(XB, (KW == 4 ? PK_WAVES : 1)) void k_count(Dev d, const int32_t *ini, const int32_t *res,
+                                                                       uint32_t n, uint32_t t, uint64_t *tot) {
+    __shared__ __attribute__((aligned(16))) uint16_t s_wbuf[2 * WIN];
+    const uint32_t e = blockIdx.x;
+    if (e >= n) return;
+    const int tid = threadIdx.x, lane = tid & (WAVE - 1), wid = tid >> 6;
+    const int32_t ai = ini[e], bi = res[e];
+    if (ai < 0 || bi < 0 || (uint32_t)ai >= d.N || (uint32_t)bi >= d.N || ai == bi) return;  // counted already
+    const uint32_t a = (uint32_t)ai, b = (uint32_t)bi;
+    const size_t slot = (size_t)e * 2 + wid;
+    const bool w0 = wid == 0;
+    const uint32_t snd = w0 ? b : a, rcv = w0 ? a : b;
+    const DigestSide ds{rcv, d.ncol, t >= d.row[rcv * 4 + 2]};
+    WStats st{0, 0, 0, 0, 0};
+    bool tomb = false;
+    PackState pst{0u, false, false};
+    pack_records<KW, true>(d, snd, rcv, ds, slot, s_wbuf + wid * WIN, t, st, tomb, pst);
+    if (lane == 0) tot[slot] = pst.S;
+}
+
 
 // ------------------------------------------------------------------ round start
 // inc_heartbeat + ClusterState.gc_marked_for_deletion (server.py:471-474; state.py:253-274, 333-338)
@@ -2202,7 +2357,7 @@ struct gs_handle {
     uint32_t seq;
     bool booted;
     // canonical unsliced handles run a phase as two kernels (k_pass1, k_pack_slice); env GS_FUSED=1
-    // selects the single fused k_exchange instead (A/B measurements)
+    // selects the single fused k_exchange (and, on sliced handles, the fused count pass) for A/B runs
     bool split;
     // gs_set_timing: HIP events around each kernel launch of a kind (gs_ktimes), on the library's stream
     bool timing;
@@ -2345,15 +2500,24 @@ int check_phase(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t n
     return GS_OK;
 }
 
-// One canonical one-slice phase: k_pass1, then k_pack_slice, on the caller's stream.  (Overlapping
-// the packing of one chunk of the exchanges with pass 1 of the next, on a second stream, measured
-// slower: 1.92 M vs 2.34 M exchanges/s with 4 chunks, profiles/r2c.)
+// One canonical one-slice phase on the caller's stream: k_pass1<FUSE = true> (pass 1, then packing and
+// apply in the same workgroup), or with env GS_PACK=split, k_pass1 then k_pack_slice.
 int run_split_phase(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t n, uint32_t tick) {
-    const SliceIO io{};
+    static const bool split = [] {
+        const char *m = getenv("GS_PACK");
+        return m && !strcmp(m, "split");
+    }();
     hipEvent_t e0 = nullptr;
     int rc = time_begin(h, e0);
     if (rc) return rc;
-    k_pass1<<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, h->seq, 0u);
+    if (!split) {
+        if (h->KP <= 16) k_pass1<4, true><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, h->seq, 0u);
+        else k_pass1<16, true><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, h->seq, 0u);
+        HIPCHK(h, hipGetLastError());
+        return time_end(h, GS_KT_PASS1, e0);
+    }
+    const SliceIO io{};
+    k_pass1<4, false><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, h->seq, 0u);
     HIPCHK(h, hipGetLastError());
     if ((rc = time_end(h, GS_KT_PASS1, e0)) || (rc = time_begin(h, e0))) return rc;
     if (h->KP <= 16) k_pack_slice<4><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, io, 0u);
@@ -2431,10 +2595,14 @@ int gs_create(const gs_config *cfg, gs_handle **out) {
     b[GS_R_KEY_LEN] = KP;
     b[GS_R_STAMP] = NR * 4;
     b[GS_R_COUNTERS] = (uint64_t)NSHARD * 32 * 8;
-    h->split = G == 1 && (c.flags & GS_CANONICAL) && !(getenv("GS_FUSED") && atoi(getenv("GS_FUSED")));
+    const bool fused = getenv("GS_FUSED") && atoi(getenv("GS_FUSED"));
+    h->split = G == 1 && (c.flags & GS_CANONICAL) && !fused;
     b[GS_R_SLICE_BITS] = (G > 1 || h->split) ? (N / 2) * 2 * (NP / 32) * 4 : 0;
-    b[GS_R_CAND] = h->split ? (N / 2) * 4 * GS_CAND_CAP * 8 : 0;
-    b[GS_R_CAND_N] = h->split ? (N / 2) * 4 * 4 : 0;
+    // candidate records: canonical handles (one slice: k_pass1 fused with packing; sliced: k_pass1 + k_count,
+    // gather, k_pack_slice)
+    const bool recs = (c.flags & GS_CANONICAL) && !fused;
+    b[GS_R_CAND] = recs ? (N / 2) * 4 * GS_CAND_CAP * 8 : 0;
+    b[GS_R_CAND_N] = recs ? (N / 2) * 4 * 4 : 0;
     const uint64_t PW = round_up(h->NP, 256) / 64;
     b[GS_R_PEND] = N * 16 * PW * 8;  // 16 phase bit planes per observer row
     b[GS_R_PEND_STAMP] = N * 16 * 4;
@@ -2633,9 +2801,18 @@ int gs_phase_count(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_
     h->hb_incs++;
     hipEvent_t e0 = nullptr;
     if ((rc = time_begin(h, e0))) return rc;
-    rc = h->KP <= 16 ? launch_exchange<4, false, 1>(h, ini, res, n, tick, lds, io)
-                     : launch_exchange<16, false, 1>(h, ini, res, n, tick, lds, io);
-    return rc ? rc : time_end(h, GS_KT_PASS1, e0);
+    if (!h->d.cand) {  // GS_FUSED: the fused count pass (LDS bitmaps)
+        rc = h->KP <= 16 ? launch_exchange<4, false, 1>(h, ini, res, n, tick, lds, io)
+                         : launch_exchange<16, false, 1>(h, ini, res, n, tick, lds, io);
+        return rc ? rc : time_end(h, GS_KT_PASS1, e0);
+    }
+    k_pass1<4, false><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, h->seq, 0u);
+    HIPCHK(h, hipGetLastError());
+    if ((rc = time_end(h, GS_KT_PASS1, e0)) || (rc = time_begin(h, e0))) return rc;
+    if (h->KP <= 16) k_count<4><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, slice_bytes);
+    else k_count<16><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, slice_bytes);
+    HIPCHK(h, hipGetLastError());
+    return time_end(h, GS_KT_COUNT, e0);
 }
 
 int gs_phase_pack(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t n, uint32_t tick, uint32_t step,
@@ -2656,6 +2833,42 @@ int gs_phase_pack(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t
     if ((rc = time_begin(h, e0))) return rc;
     if (h->KP <= 16) k_pack_slice<4><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, io, 0u);
     else k_pack_slice<16><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, io, 0u);
+    HIPCHK(h, hipGetLastError());
+    return time_end(h, GS_KT_PACK, e0);
+}
+
+int gs_phase_overflow(gs_handle *h, uint32_t n, const uint64_t *slice_bytes_all, const uint64_t *chain,
+                      uint32_t *list, uint64_t *chainc, uint32_t *count) {
+    if (!h || !h->booted) return GS_E_INVALID;
+    if (count) *count = 0;
+    if (!n) return GS_OK;
+    if (h->G < 2 || !h->d.cand) return fail(h, GS_E_UNSUPPORTED, "gs_phase_overflow needs a sliced canonical handle");
+    if (!slice_bytes_all || !chain || !list || !chainc) return GS_E_INVALID;
+    const uint32_t slots = 2 * n, nb = (slots + OVB - 1) / OVB;
+    k_ov_count<<<nb, OVB, 0, h->stream>>>(slice_bytes_all, slots, h->G, h->cfg.mtu, list + slots);
+    HIPCHK(h, hipGetLastError());
+    k_ov_write<<<nb, OVB, 0, h->stream>>>(slice_bytes_all, slots, h->G, h->cfg.mtu, chain, list, chainc);
+    HIPCHK(h, hipGetLastError());
+    if (count) {  // count = NULL: no read back (another slice in this process reads the same count)
+        HIPCHK(h, hipMemcpyAsync(count, list + slots + nb, 4, hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+    }
+    return GS_OK;
+}
+
+int gs_phase_chain(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t n, uint32_t tick, uint32_t step,
+                   const uint32_t *list, uint32_t count, const uint64_t *chain_all, uint64_t *chain, uint64_t *chainc) {
+    if (h && (!n || !count)) return GS_OK;
+    int rc = check_phase(h, ini, res, n, tick, true);
+    if (rc) return rc;
+    if (h->G < 2 || !h->d.cand) return fail(h, GS_E_UNSUPPORTED, "gs_phase_chain needs a sliced canonical handle");
+    if (!list || !chain_all || !chain || !chainc || step < 1 || step >= h->G || count > 2 * n) return GS_E_INVALID;
+    if (h->shard == 0) return GS_OK;  // slice 0 always finishes at step 0
+    hipEvent_t e0 = nullptr;
+    if ((rc = time_begin(h, e0))) return rc;
+    const uint32_t grid = std::min<uint32_t>(count, 2048u);
+    if (h->KP <= 16) k_chain_step<4><<<grid, WAVE, 0, h->stream>>>(h->d, ini, res, tick, list, count, chain_all, chain, chainc);
+    else k_chain_step<16><<<grid, WAVE, 0, h->stream>>>(h->d, ini, res, tick, list, count, chain_all, chain, chainc);
     HIPCHK(h, hipGetLastError());
     return time_end(h, GS_KT_PACK, e0);
 }

@@ -13,9 +13,12 @@ order — and stops adding once the DeltaPb is full.  Per phase:
 2. all-gather of those totals (16 B per exchange per slice; RCCL over xGMI);
 3. ``gs_phase_pack(step 0)``: each slice packs and applies its owners starting
    at the byte count its predecessors reach when they all fit whole;
-4. only when some exchange's totals sum past the MTU: G-1 further steps, each an
-   all-gather of the ``u64 [n][2]`` chain states and a ``gs_phase_pack`` that
-   lets the next slice continue where its predecessor's packing stopped.
+4. only for the (exchange, direction) slots whose totals sum past the MTU: G-1
+   further steps, each an all-gather of those slots' chain states (8 bytes per
+   overflowing slot and slice) and a ``gs_phase_chain`` that lets the next slice
+   continue where its predecessor's packing stopped.  ``gs_phase_overflow`` lists
+   the slots on the device -- the same list on every slice -- and returns their
+   number, the one host read per phase.
 
 The result equals ``gs_run_phase`` on a single handle bit for bit (tested on one
 GPU with G in-process slices).  ``comm`` abstracts the gather: ``LocalComm``
@@ -91,8 +94,8 @@ class DistComm:
 def run_sliced_phase(slices, comm, mtu: int, t: int, ini, res) -> int:
     """One phase on the slices this process drives; returns the pack steps taken (1 = no chain).
 
-    ``slices`` expose ``phase_count(t, ini, res) -> [n, 2]`` and
-    ``phase_pack(t, ini, res, step, tot_all, chain_all, chain) -> chain`` (``GossipSim`` does).
+    ``slices`` expose ``phase_count``, ``phase_pack``, ``phase_overflow`` and ``phase_chain``
+    (``GossipSim`` does).
     """
     import torch
 
@@ -104,13 +107,27 @@ def run_sliced_phase(slices, comm, mtu: int, t: int, ini, res) -> int:
     chains = [torch.empty_like(x) for x in tots]
     for s, ch in zip(slices, chains):
         s.phase_pack(t, ini, res, 0, tot_all, None, ch)
-    # every rank holds the same tot_all, so they agree on whether the chain steps run
-    if not bool((tot_all.sum(0) > mtu).any()):
+    if not all(s.has_records for s in slices):
+        # fused count pass (GS_FUSED=1): every slot's chain state travels; one host read decides
+        if not bool((tot_all.sum(0) > mtu).any()):
+            return 1
+        for step in range(1, comm.world):
+            chain_all = comm.gather(chains)
+            for s, ch in zip(slices, chains):
+                s.phase_pack(t, ini, res, step, tot_all, chain_all, ch)
+        return comm.world
+    dev = tots[0].device
+    lists = [torch.empty(2 * n + 256, dtype=torch.int32, device=dev) for _ in slices]
+    chaincs = [torch.empty(2 * n, dtype=torch.int64, device=dev) for _ in slices]
+    # the same gathered totals give every slice the same list: one host read per process
+    for i in range(len(slices) - 1, -1, -1):
+        count = slices[i].phase_overflow(tot_all, chains[i], lists[i], chaincs[i], read=i == 0)
+    if count == 0:
         return 1
     for step in range(1, comm.world):
-        chain_all = comm.gather(chains)
-        for s, ch in zip(slices, chains):
-            s.phase_pack(t, ini, res, step, tot_all, chain_all, ch)
+        chain_all = comm.gather([cc[:count] for cc in chaincs])
+        for s, ch, lb, cc in zip(slices, chains, lists, chaincs):
+            s.phase_chain(t, ini, res, step, lb, count, chain_all, ch, cc)
     return comm.world
 
 

@@ -315,6 +315,29 @@ class GossipSim:
                   "gs_phase_pack")
         return chain
 
+    @property
+    def has_records(self) -> bool:
+        """Candidate records are allocated (canonical layout): the compacted chain is available."""
+        return "CAND" in self.regions
+
+    def phase_overflow(self, tot_all, chain, list_buf, chainc, read: bool = True):
+        """gs_phase_overflow: the overflowing slots into list_buf, this slice's states into chainc; with
+        ``read`` (blocking) returns their number."""
+        n = int(chain.shape[0])
+        cnt = C.c_uint32()
+        self._chk(self.L.gs_phase_overflow(self.h, n, C.c_void_p(tot_all.data_ptr()), C.c_void_p(chain.data_ptr()),
+                                           C.c_void_p(list_buf.data_ptr()), C.c_void_p(chainc.data_ptr()),
+                                           C.byref(cnt) if read else None), "gs_phase_overflow")
+        return int(cnt.value) if read else None
+
+    def phase_chain(self, t: int, ini, res, step: int, list_buf, count: int, chain_all, chain, chainc):
+        """gs_phase_chain step ``step`` over the ``count`` listed slots (chain_all = gathered [G, count])."""
+        n = int(ini.numel())
+        self._chk(self.L.gs_phase_chain(self.h, C.c_void_p(ini.data_ptr()), C.c_void_p(res.data_ptr()), n, t, step,
+                                        C.c_void_p(list_buf.data_ptr()), count, C.c_void_p(chain_all.data_ptr()),
+                                        C.c_void_p(chain.data_ptr()), C.c_void_p(chainc.data_ptr())),
+                  "gs_phase_chain")
+
     def update_node_liveness(self, t: int, up):
         self._flush()
         u = up if hasattr(up, "data_ptr") else self._dev(np.asarray(up, dtype=np.uint8), self.torch.uint8)

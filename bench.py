@@ -257,7 +257,7 @@ def load_traffic(workload: str, kernel: str, units_per_launch: float):
         f"({e.get('calibration')}), x this run's units per launch")
 
 
-KERNEL_OF = {"pass1": "k_pass1", "pack": "k_pack_slice", "liveness": "k_liveness"}
+KERNEL_OF = {"pass1": "k_pass1", "pack": "k_pack_slice", "liveness": "k_liveness", "count": "k_count"}
 
 
 def roofline(sims, local_c, exch, kt, elapsed, torch, dev, rank, group, workload) -> dict:
@@ -284,12 +284,13 @@ def roofline(sims, local_c, exch, kt, elapsed, torch, dev, rank, group, workload
             b = (alg if fused else alg - packb) / launches
         elif kind == "pack":
             b = packb / launches
-        ent = {"kernel": "k_exchange (fused)" if (fused and kind == "pass1") else KERNEL_OF[kind],
+        ent = {"kernel": ("k_pass1<fused>: pass 1, then packing + apply_delta in the same workgroup"
+                          if (fused and kind == "pass1") else KERNEL_OF[kind]),
                "avg_launch_ms": avg_s * 1e3, "launches": launches, "share_of_step": ms / 1e3 / elapsed}
         if b is not None:
             ent.update(alg_bytes_per_launch=b, achieved=b / avg_s / 1e9, frac=b / avg_s / 1e9 / HBM_PEAK_GBPS)
         units = exch / launches if kind != "liveness" else 1.0
-        if group is None and not fused:
+        if group is None:
             tr, note = load_traffic(workload, KERNEL_OF[kind], units)
             ent.update(traffic=tr, traffic_source=note, traffic_gbs=tr / avg_s / 1e9 if tr else None)
         per[kind] = ent
@@ -320,6 +321,40 @@ def roofline(sims, local_c, exch, kt, elapsed, torch, dev, rank, group, workload
         "kernels": per,
         "survey_formula_bytes_per_phase": survey,
         "survey_formula_gbs_over_pass1": survey / (kt["pass1"][0] / launches / 1e3) / 1e9 if kt["pass1"][0] else None,
+    }
+
+
+def peer_select_rounds(sims, plans, r0: int, steps: int, args, n: int, dev) -> dict:
+    """Rounds r0 .. r0 + steps (the first untimed) on the headline's state, each scheduled on the device:
+    gs_select_peers (select_nodes_for_gossip for every up node from its failure detector's live / dead
+    sets, server.py:441-495, 656-717; 8 seeds) and gs_schedule_phases (Luby matchings into conflict-free
+    phases; the exchanges that do not fit in its phase budget are counted, not dropped silently)."""
+    import torch
+
+    from aiocluster_amd import driver
+    from aiocluster_amd.peers import PeerSelector
+
+    sel = PeerSelector(sims[0], fanout=args.fanout, seeds=list(range(0, n, max(1, n // 8))), seed=args.seed)
+    driver.run_round(sims, plans[r0], sel=sel)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for r in range(r0 + 1, r0 + 1 + steps):
+        driver.run_round(sims, plans[r], sel=sel)
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    rds = [plans[r] for r in range(r0 + 1, r0 + 1 + steps)]
+    exch = sum(rd["exchanges"] for rd in rds)
+    return {
+        "value": exch / dt,
+        "unit": "exchanges/s",
+        "steps": steps,
+        "ms_per_step": dt / steps * 1e3,
+        "exchanges_per_step": exch / steps,
+        "phases_per_round": [rd["t_live"] - rd["t"] - 1 for rd in rds],
+        "unscheduled_exchanges": sum(rd["unscheduled"] for rd in rds),
+        "note": "same cluster state and workload as the headline; the schedule comes from the device's "
+                "select_nodes_for_gossip + Luby phases instead of the workload generator's permutations "
+                "(selection, scheduling and the phase-offset read back are inside the timed region)",
     }
 
 
@@ -362,6 +397,10 @@ def main():
     ap.add_argument("--peer-select", action="store_true",
                     help="schedule each round with the device's select_nodes_for_gossip (gs_select_peers) and "
                          "Luby phases (gs_schedule_phases) instead of the workload's permutation schedule")
+    ap.add_argument("--peer-select-steps", type=int, default=3,
+                    help="after the headline: time this many more rounds scheduled by the device's "
+                         "select_nodes_for_gossip (gs_select_peers) + Luby phases (gs_schedule_phases), reported "
+                         "as the line's peer_select object (0 = skip)")
     ap.add_argument("--rehearse-slices", type=int, default=0,
                     help="hold only slice 0 of G owner-column slices (one GPU's share of a G-GPU run; timing only)")
     ap.add_argument("--no-held", action="store_true",
@@ -424,7 +463,8 @@ def main():
         sims = [GossipSim(ids, key_names(K), cfg, **kw)]
     sim = sims[0]
     R0 = args.settle + args.warmup  # first timed round
-    plans = driver.prepare(spec, R0 + args.steps + 1, torch, dev)
+    ps_steps = args.peer_select_steps if (group is None and not args.peer_select) else 0
+    plans = driver.prepare(spec, R0 + args.steps + 1 + (1 + ps_steps if ps_steps else 0), torch, dev)
     sel = None
     if args.peer_select:
         from aiocluster_amd.peers import PeerSelector
@@ -475,6 +515,9 @@ def main():
         rd = plans[R0 + args.steps]
         driver.begin(sims, rd)
         cpu = cpu_baseline(sim, cfg, rd, args.cpu_sample, args.cpu_seconds, args.cpu_threads)
+    ps = None
+    if ps_steps:
+        ps = peer_select_rounds(sims, plans, R0 + args.steps + 1, ps_steps, args, n, dev)
     if rank == 0:
         line = {
             "metric": ("REHEARSAL (one GPU's slice of a %d-GPU run, packing not the cluster's): exchanges/s"
@@ -507,6 +550,7 @@ def main():
             },
             "roofline": roof,
             "cpu_baseline": cpu,
+            "peer_select": ps,
             **({"ABLATION_RESULTS_INVALID": os.environ["GS_ABLATE"]} if os.environ.get("GS_ABLATE") else {}),
             "counters": {**{k: v for k, v in c.items() if not k.startswith("err_")}, "inexact_views": inexact},
         }

@@ -238,6 +238,19 @@ int gs_phase_count(gs_handle *h, const int32_t *initiators, const int32_t *respo
                    uint64_t *slice_bytes);
 int gs_phase_pack(gs_handle *h, const int32_t *initiators, const int32_t *responders, uint32_t n, uint32_t tick,
                   uint32_t step, const uint64_t *slice_bytes_all, const uint64_t *chain_all, uint64_t *chain);
+/* Compacted chain (replaces step 4 above on canonical handles built with candidate records):
+ *   gs_phase_overflow (blocking: one 4-byte read): the slots (2e + dir) whose gathered slice totals sum
+ *     past the mtu, in slot order, into DEVICE list[2n + 256] (the tail is scratch), this slice's chain
+ *     state of each into DEVICE chainc[2n], and their number into *count (host; NULL: not read back);
+ *   for step = 1 .. G-1: gather every slice's chainc[count] into chain_all[G][count], then
+ *     gs_phase_chain(step) (one wave per listed slot; chain and chainc updated).
+ * Every slice computes the same list from the same gathered totals, so only count x 8 bytes per slice
+ * travel per step. */
+int gs_phase_overflow(gs_handle *h, uint32_t n, const uint64_t *slice_bytes_all, const uint64_t *chain,
+                      uint32_t *list, uint64_t *chainc, uint32_t *count);
+int gs_phase_chain(gs_handle *h, const int32_t *initiators, const int32_t *responders, uint32_t n, uint32_t tick,
+                   uint32_t step, const uint32_t *list, uint32_t count, const uint64_t *chain_all, uint64_t *chain,
+                   uint64_t *chainc);
 
 /* _update_node_liveness for every up node (server.py:606-620; failure_detector.py:89-128),
  * including garbage_collect + remove_node (general layout only). */
@@ -331,9 +344,12 @@ int gs_stream_write(void *dst, uint64_t bytes, uint32_t width, void *stream);
 /* Per-kernel timing (measurement): with timing on, every launch of the kinds below is bracketed by HIP
  * events on the library's stream; gs_kernel_times (blocking) returns the summed milliseconds and launch
  * counts since the previous call and clears them. */
-#define GS_KT_PASS1 0     /* pass 1: k_pass1 (canonical one slice), the fused k_exchange, gs_phase_count */
-#define GS_KT_PACK 1      /* delta packing + apply_delta: k_pack_slice (canonical one slice, gs_phase_pack) */
+#define GS_KT_PASS1 0     /* a canonical one-slice phase (k_pass1 fused with packing; with env GS_PACK=split,
+                             pass 1 alone), the general-layout k_exchange, pass 1 of gs_phase_count */
+#define GS_KT_PACK 1      /* delta packing + apply_delta when it runs as its own kernel: k_pack_slice
+                             (GS_PACK=split, gs_phase_pack) and k_chain_step (gs_phase_chain) */
 #define GS_KT_LIVENESS 2  /* k_liveness (report replay + liveness sweep) */
+#define GS_KT_COUNT 3     /* the slice byte totals of gs_phase_count (k_count) */
 typedef struct gs_ktimes {
     double ms[4];
     uint64_t launches[4];

@@ -47,10 +47,35 @@ def dec(v):
 
 
 class ToySlice:
-    def __init__(self, g, cands):
+    """has_records = True: the compacted chain (gs_phase_overflow + gs_phase_chain); False: the fused
+    protocol (every slot's chain state gathered per step)."""
+
+    def __init__(self, g, cands, has_records=True):
         self.g = g
         self.cands = cands  # cands[e][dir] = [(id, size), ...] of this slice
         self.sent = {}
+        self.has_records = has_records
+
+    def phase_overflow(self, tot_all, chain, list_buf, chainc, read=True):
+        tot = tot_all.sum(0).reshape(-1)
+        idx = (tot > MTU).nonzero().flatten()
+        list_buf[: len(idx)] = idx.to(list_buf.dtype)
+        chainc[: len(idx)] = chain.reshape(-1)[idx]
+        return len(idx)
+
+    def phase_chain(self, t, ini, res, step, list_buf, count, chain_all, chain, chainc):
+        flat = chain.view(-1)
+        for i in range(count):
+            slot = int(list_buf[i])
+            e, d = slot // 2, slot % 2
+            if self.g == 0 or int(flat[slot]) != CHAIN_PENDING:
+                continue
+            prev = int(chain_all[self.g - 1, i])
+            if prev == CHAIN_PENDING:
+                continue
+            sent, S, tail, stop = seq_pack(self.cands[e][d], *dec(prev))
+            self.sent[(e, d)] = sent
+            flat[slot] = chainc[i] = enc(S, tail, stop)
 
     def phase_count(self, t, ini, res):
         n = int(ini.numel())
@@ -102,12 +127,12 @@ def check(slices, cands, G, n):
             assert got == want, (e, d, got, want)
 
 
-@pytest.mark.parametrize("G", [2, 3, 5])
-def test_chain_protocol_in_process(G):
+@pytest.mark.parametrize("G,records", [(2, True), (3, True), (5, True), (3, False)])
+def test_chain_protocol_in_process(G, records):
     rng = np.random.default_rng(G)
     n = 40
     cands = make_cands(rng, G, n)
-    slices = [ToySlice(g, cands[g]) for g in range(G)]
+    slices = [ToySlice(g, cands[g], records) for g in range(G)]
     ini = torch.zeros(n, dtype=torch.int32)
     steps = run_sliced_phase(slices, LocalComm(G), MTU, 0, ini, ini)
     assert steps == G  # these inputs overflow the MTU somewhere

@@ -13,6 +13,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
+#include <algorithm>
 
 #define CK(x)                                                                       \
     do {                                                                            \
@@ -95,6 +96,17 @@ __global__ __launch_bounds__(128) void rowpair(uint16_t *hb, const uint16_t *mv,
     }
 }
 
+// scatter: one 2-byte store per lane to arbitrary positions of a large u16 array (the packer's
+// max_version applies: ~570 sparse columns of one receiver row per exchange direction)
+__global__ __launch_bounds__(256) void scatter16(uint16_t *a, const uint64_t *pos, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    if (i < n) a[pos[i]] = (uint16_t)i;
+}
+__global__ __launch_bounds__(256) void gather16(const uint16_t *a, const uint64_t *pos, uint64_t n, unsigned *sink) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    if (i < n && a[pos[i]] == 0x1234u) atomicAdd(sink, 1u);
+}
+
 template <typename F>
 float timeit(F f, int reps) {
     hipEvent_t e0, e1;
@@ -158,5 +170,37 @@ int main() {
     printf("rowpair 8 B/lane: %.3f ms, %.0f GB/s\n", ms, moved / (ms * 1e6));
     ms = timeit([&] { rowpair<16><<<P, 128>>>(hb, mv, pa, pb, NC); }, reps);
     printf("rowpair 16 B/lane: %.3f ms, %.0f GB/s\n", ms, moved / (ms * 1e6));
+
+    // packer applies: 19,800 exchanges x 2 directions x ~570 sparse columns of the receiver row, sorted
+    // within a row (as the packer issues them), into the [R][NC] u16 max_version matrix
+    {
+        const uint32_t per = 570;
+        const uint64_t S = (uint64_t)P * 2 * per;
+        std::vector<uint64_t> pos(S);
+        uint64_t k = 0;
+        for (uint32_t e = 0; e < P; e++)
+            for (int dir = 0; dir < 2; dir++) {
+                const uint64_t row = dir ? hbv[e] : ha[e];
+                std::vector<uint32_t> cols(per);
+                for (auto &c : cols) c = (uint32_t)(rand() % NC);
+                std::sort(cols.begin(), cols.end());
+                for (auto c : cols) pos[k++] = row * NC + c;
+            }
+        uint64_t *dpos;
+        CK(hipMalloc(&dpos, S * 8));
+        CK(hipMemcpy(dpos, pos.data(), S * 8, hipMemcpyHostToDevice));
+        const uint32_t blocks = (uint32_t)((S + 255) / 256);
+        ms = timeit([&] { scatter16<<<blocks, 256>>>(mv, dpos, S); }, reps);
+        printf("scatter 2-B stores (%llu, row-sorted): %.3f ms, %.1f G stores/s\n", (unsigned long long)S, ms,
+               S / (ms * 1e6));
+        ms = timeit([&] { gather16<<<blocks, 256>>>(mv, dpos, S, sink); }, reps);
+        printf("gather 2-B loads (%llu, row-sorted): %.3f ms, %.1f G loads/s\n", (unsigned long long)S, ms,
+               S / (ms * 1e6));
+        // fully random order (no locality between neighbouring lanes)
+        for (uint64_t i = S - 1; i > 0; i--) std::swap(pos[i], pos[rand() % (i + 1)]);
+        CK(hipMemcpy(dpos, pos.data(), S * 8, hipMemcpyHostToDevice));
+        ms = timeit([&] { scatter16<<<blocks, 256>>>(mv, dpos, S); }, reps);
+        printf("scatter 2-B stores (random order): %.3f ms, %.1f G stores/s\n", ms, S / (ms * 1e6));
+    }
     return 0;
 }

@@ -30,10 +30,10 @@ from collections import defaultdict
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
-KERNELS = ("k_pass1", "k_pack_slice", "k_liveness", "k_exchange", "k_begin_round", "k_owner_writes",
+KERNELS = ("k_pass1", "k_pack_slice", "k_liveness", "k_exchange", "k_count", "k_begin_round", "k_owner_writes",
            "k_reset_sched", "k_warm", "k_boot_self", "k_phi_row")
-WIDTH = {"k_pass1": 8, "k_pack_slice": 8, "k_liveness": 16, "k_exchange": 8}
-KIND = {"k_pass1": "pass1", "k_pack_slice": "pack", "k_liveness": "liveness", "k_exchange": "pass1"}
+WIDTH = {"k_pass1": 8, "k_pack_slice": 8, "k_liveness": 16, "k_exchange": 8, "k_count": 8}
+KIND = {"k_pass1": "pass1", "k_pack_slice": "pack", "k_liveness": "liveness", "k_exchange": "pass1", "k_count": "count"}
 CAL_BYTES = 1 << 30
 
 
