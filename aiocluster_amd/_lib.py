@@ -51,7 +51,7 @@ def fd_sum_bits(window: int) -> int:
 REGIONS = [
     "HB", "MV", "GC", "HELD", "FD", "FD_STATE", "TS", "RING", "POS", "ORD", "ROW",
     "LAST_W", "HIST", "HIST_VID", "NID_SIZE", "KEY_LEN", "STAMP", "COUNTERS", "SLICE_BITS", "PEND", "PEND_STAMP", "LATEST",
-    "SELF_HB", "CAND", "CAND_N",
+    "SELF_HB", "CAND", "CAND_N", "FD_TOD",
 ]
 REGION = {n: i for i, n in enumerate(REGIONS)}
 
@@ -70,10 +70,10 @@ EXPORTS = [
     "gs_read_counters", "gs_reset_counters", "gs_sync", "gs_shard_columns", "gs_phase_count", "gs_phase_pack", "gs_materialize_held", "gs_fd_census",
     "gs_select_peers", "gs_schedule_phases", "gs_set_events", "gs_emit_scratch_bytes", "gs_emit_digest", "gs_emit_delta",
     "gs_check_heartbeat_lag", "gs_stream_copy", "gs_stream_read", "gs_stream_write", "gs_set_timing", "gs_kernel_times",
-    "gs_phase_overflow", "gs_phase_chain",
+    "gs_phase_overflow", "gs_phase_chain", "gs_comm_id", "gs_comm_init", "gs_run_phase_group", "gs_read_rows",
 ]
 
-API_VERSION = 9
+API_VERSION = 10
 MAX_PHASES = 64  # GS_MAX_PHASES
 
 
@@ -127,7 +127,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
     os.makedirs(LIB_DIR, exist_ok=True)
     newest = max(os.path.getmtime(SRC), os.path.getmtime(HEADER))
     if force or not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < newest:
-        cmd = ["hipcc", *HIPCC_FLAGS, "-o", LIB_PATH, SRC]
+        cmd = ["hipcc", *HIPCC_FLAGS, "-o", LIB_PATH, SRC, "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
         if verbose:
             print(" ".join(cmd))
         subprocess.run(cmd, check=True)
@@ -168,6 +168,10 @@ def load():
         "gs_set_timing": (C.c_int, [P, C.c_int]),
         "gs_phase_overflow": (C.c_int, [P, u32, P, P, P, P, C.POINTER(u32)]),
         "gs_phase_chain": (C.c_int, [P, P, P, u32, u32, u32, P, u32, P, P, P]),
+        "gs_comm_id": (C.c_int, [P]),
+        "gs_comm_init": (C.c_int, [P, P, u32, u32]),
+        "gs_run_phase_group": (C.c_int, [P, u32, P, P, u32, u32]),
+        "gs_read_rows": (C.c_int, [P, C.c_int, u32, u32, P, u64, C.POINTER(u64)]),
         "gs_kernel_times": (C.c_int, [P, C.POINTER(GsKtimes)]),
         "gs_sync": (C.c_int, [P]),
         "gs_shard_columns": (C.c_int, [P, C.POINTER(u32), C.POINTER(u32)]),

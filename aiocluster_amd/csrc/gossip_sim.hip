@@ -28,6 +28,7 @@
 //   failure detector  failure_detector.py:12-128
 
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <cstdarg>
 #include <cstdlib>
@@ -80,7 +81,9 @@ struct Dev {
     uint16_t *mv;  // max_version | MV_INEXACT (u16: versions <= K * (C - 1) <= 16,256)
     uint8_t *held;
     uint64_t *fd;  // sampling window: (last tick + 1) | (sum | cnt << sum_bits) << 32; 0 = no window
-    uint32_t *fd_state, *ts;
+    uint8_t *fd_state;  // 0 unknown, 1 live, 2 dead (FailureDetector._live_nodes / _dead_nodes)
+    uint32_t *tod;      // time of death of a dead pair (read only for rows whose row word 2 has passed)
+    uint32_t *ts;
     uint16_t *ring;
     uint32_t *pos, *ord, *row;
     uint8_t *last_w;
@@ -105,9 +108,11 @@ struct Dev {
     // first phase after that replay; plane p holds the phase at tick t_round + 1 + p
     uint32_t t_round;
     // event stream (gs_set_events): records {observer, owner, key | kind << 8, old version, new version,
-    // tick}; kind 0 = on_key_change, 1 = node join, 2 = node leave.  ev == nullptr: off
+    // tick, seq, 0}; kind 0 = on_key_change, 1 = node join, 2 = node leave; seq orders them (gossip_sim.h,
+// gs_set_events).  ev == nullptr: off
     uint32_t *ev, *ev_count;
     uint32_t ev_cap;
+    uint32_t ev_wseq;  // owner-write ops issued since gs_set_events (the seq of the next call's op 0)
 };
 
 // ------------------------------------------------------------------ protobuf sizes
@@ -131,9 +136,12 @@ __device__ inline uint32_t make_meta(uint32_t kvlen, uint32_t status, uint32_t v
 }
 
 // FailureDetector.scheduled_for_deletion_nodes (failure_detector.py:121-128): now >= tod + grace/2.
-__device__ inline bool is_sched(uint32_t st, uint32_t t, uint32_t delay) {
-    return st >= 2u && (t - (st - 2u)) >= delay;
+// dt = the pair's time of death if it is dead, NONE otherwise (dead_tod).
+__device__ inline bool is_sched(uint32_t dt, uint32_t t, uint32_t delay) {
+    return dt != NONE && (t - dt) >= delay;
 }
+enum FdSt { FD_UNKNOWN = 0, FD_LIVE = 1, FD_DEAD = 2 };
+__device__ inline uint32_t dead_tod(const Dev &d, size_t p) { return d.fd_state[p] == FD_DEAD ? d.tod[p] : NONE; }
 
 // One sampling window (SamplingWindow + BoundedArrayStats, failure_detector.py:12-53, 131-162) per
 // pair in 8 bytes: low word = _last_heartbeat tick + 1 (0 = no window), high word = _sum in ticks
@@ -176,11 +184,23 @@ __device__ inline void shard_add(const Dev &d, int c, unsigned long long v) {
 
 enum EvKind { EV_KEY = 0, EV_JOIN = 1, EV_LEAVE = 2 };
 __device__ inline void emit_event(const Dev &d, uint32_t o, uint32_t j, uint32_t kk, uint32_t v_old, uint32_t v_new,
-                                  uint32_t t) {
+                                  uint32_t t, uint32_t seq) {
     const uint32_t i = atomicAdd(d.ev_count, 1u);
     if (i >= d.ev_cap) return;  // overflow: the count says how many were lost
-    uint32_t *r = d.ev + (size_t)i * 6;
-    r[0] = o; r[1] = j; r[2] = kk; r[3] = v_old; r[4] = v_new; r[5] = t;
+    uint4 *r = reinterpret_cast<uint4 *>(d.ev + (size_t)i * 8);
+    r[0] = make_uint4(o, j, kk, v_old);
+    r[1] = make_uint4(v_new, t, seq, 0u);
+}
+
+// on_key_change of apply_delta (state.py:228-231), out of line: the event path stays off the register
+// budget of the packing kernels.  seq = the sender's dict position of the owner (NodeDelta order).
+__device__ __noinline__ void emit_apply_event(uint32_t *ev, uint32_t *evc, uint32_t cap, const uint32_t *pos_s, uint32_t r,
+                                              uint32_t jg, uint32_t j, uint32_t q, uint32_t v_old, uint32_t v, uint32_t t) {
+    const uint32_t i = atomicAdd(evc, 1u);
+    if (i >= cap) return;
+    uint4 *rec = reinterpret_cast<uint4 *>(ev + (size_t)i * 8);
+    rec[0] = make_uint4(r, jg, q | (EV_KEY << 8), v_old);
+    rec[1] = make_uint4(v, t, pos_s ? pos_s[j] : jg, 0u);
 }
 
 // ------------------------------------------------------------------ packing / apply
@@ -270,7 +290,7 @@ __device__ __forceinline__ void eval_cand(const Dev &d, uint32_t s, uint32_t r, 
     const uint32_t ms = msw & MV_MASK, mr = mrw & MV_MASK;
     const uint32_t gs = gct ? d.gc[ps] : 0u, gr = gct ? d.gc[pr] : 0u;
     const uint32_t pos_r = GENM ? d.pos[pr] : 0u;
-    const uint32_t fst = ds.sched ? d.fd_state[pr] : 0u;
+    const uint32_t fst = ds.sched ? dead_tod(d, pr) : NONE;
     const bool sx = !gct && !(msw & MV_INEXACT), rx = !gct && !(mrw & MV_INEXACT);
     // GS_NO_HELD: no view may have holes (counted as err_holes when one would); never read HELD
     const uint32_t *hsp = reinterpret_cast<const uint32_t *>(
@@ -360,8 +380,8 @@ __device__ __forceinline__ void eval_cand(const Dev &d, uint32_t s, uint32_t r, 
 // independent (kvs arrive in version order, so "version <= max_version" only ever compares
 // against the view's max_version before the delta, 209-210).
 template <int KW>
-__device__ __forceinline__ void apply_cand(const Dev &d, uint32_t r, const Cand<KW> &c, uint32_t vmax, uint32_t t, bool &tomb,
-                                  uint32_t &alg) {
+__device__ __forceinline__ void apply_cand(const Dev &d, uint32_t s, uint32_t r, const Cand<KW> &c, uint32_t vmax, uint32_t t,
+                                  bool &tomb, uint32_t &alg) {
     const size_t pr = pix(d, r, c.j);
     if (c.fast && vmax == NONE && !d.ev) {
         // prefix sender, prefix receiver, whole NodeDelta: the view becomes S_j(max(mr, ms)) (keys
@@ -405,8 +425,9 @@ __device__ __forceinline__ void apply_cand(const Dev &d, uint32_t r, const Cand<
             if (!(st != 0u && v <= g)) {
                 // on_key_change(node, key, existing, new) for every stored kv (state.py:228-231)
                 if (d.ev)
-                    emit_event(d, r, d.col_lo + c.j, (uint32_t)q | (EV_KEY << 8),
-                               wr ? (uint32_t)d.hist[hix(d, c.j, wr, q)] : 0u, v, t);
+                    emit_apply_event(d.ev, d.ev_count, d.ev_cap, (d.flags & GS_CANONICAL) ? nullptr : d.pos + pix(d, s, 0),
+                                     r, d.col_lo + c.j, c.j, (uint32_t)q, wr ? (uint32_t)d.hist[hix(d, c.j, wr, q)] : 0u,
+                                     v, t);
                 wr = ws;
                 if (tt) { tsr[q] = st ? t : NONE; alg += 4; }
                 if (st) tomb = true;
@@ -459,7 +480,7 @@ struct PackState {
 // REC: record the selected NodeDeltas {owner, vsel} in sender order into rec[] (nr so far)
 // instead of applying them (the wire-format emitter, gs_emit_delta).
 template <int KW, bool COUNT, bool REC>
-__device__ __forceinline__ void pack_group(const Dev &d, uint32_t r, uint32_t t, const Cand<KW> &c, bool cand,
+__device__ __forceinline__ void pack_group(const Dev &d, uint32_t s, uint32_t r, uint32_t t, const Cand<KW> &c, bool cand,
                                            uint32_t &S, bool &tail, bool &stop, WStats &st, bool &tomb, uint2 *rec,
                                            uint32_t &nr) {
     const int lane = lane_id();
@@ -547,7 +568,7 @@ __device__ __forceinline__ void pack_group(const Dev &d, uint32_t r, uint32_t t,
     }
     // apply_delta at the receiver: one lane per NodeDelta, distinct owners, any order
     if (vsel) {
-        apply_cand<KW>(d, r, c, vsel, t, tomb, st.alg);
+        apply_cand<KW>(d, s, r, c, vsel, t, tomb, st.alg);
         st.nd++;
         if (vsel == NONE) {
             st.kvs += c.nkv;
@@ -636,7 +657,7 @@ __device__ __forceinline__ void pack_dir(const Dev &d, uint32_t s, uint32_t r, c
                 eval_cand<KW, GENM>(d, s, r, ds, j, t, c, st.alg);
                 st.cand++;
             }
-            pack_group<KW, COUNT, REC>(d, r, t, c, cand, S, tail, stop, st, tomb, rec, nr);
+            pack_group<KW, COUNT, REC>(d, s, r, t, c, cand, S, tail, stop, st, tomb, rec, nr);
         }
         if (!last) {  // carry the rest (< 64): entry lim + i to lane i
             const uint32_t rem = total - lim, idx = lim + lane;
@@ -683,7 +704,7 @@ __device__ __forceinline__ void pack_list(const Dev &d, uint32_t s, uint32_t r, 
             eval_cand<KW, false, true>(d, s, r, ds, cr.x, t, c, st.alg, cr.y);
             st.cand++;
         }
-        pack_group<KW, COUNT, false>(d, r, t, c, cand, S, tail, stop, st, tomb, nullptr, nr);
+        pack_group<KW, COUNT, false>(d, s, r, t, c, cand, S, tail, stop, st, tomb, nullptr, nr);
     }
     pst.S = S;
     pst.tail = tail;
@@ -713,7 +734,8 @@ __device__ __forceinline__ void pack_records(const Dev &d, uint32_t snd, uint32_
 // Pass-1 work of one group of 4 consecutive owners (one 16-byte load per array and row), held
 // as scalar arrays so every element stays in a register after unrolling.
 struct Grp {
-    uint32_t hA[4], hB[4], mA[4], mB[4], pA[4], pB[4], fA[4], fB[4];
+    uint32_t hA[4], hB[4], mA[4], mB[4], pA[4], pB[4];
+    uint32_t sA, sB;  // bit i: column c0 + i is scheduled for deletion in that row (only if the row may have one)
 };
 
 // Report bit planes (Dev::pend): column c of a plane row sits in word (c / 256) * 4 + c % 4, bit
@@ -747,9 +769,22 @@ __device__ __forceinline__ void st4w(uint64_t *p, const uint64_t (&v)[4]) {
     reinterpret_cast<ulonglong2 *>(p)[0] = make_ulonglong2(v[0], v[1]);
     reinterpret_cast<ulonglong2 *>(p)[1] = make_ulonglong2(v[2], v[3]);
 }
+// scheduled-for-deletion mask of 4 consecutive pairs (p a multiple of 4): their 4 state bytes, then the
+// times of death if any is dead (rows whose earliest scheduled tick has passed only)
+__device__ __forceinline__ uint32_t sched4(const Dev &d, size_t p, uint32_t t) {
+    const uint32_t s4 = *reinterpret_cast<const uint32_t *>(d.fd_state + p);
+    if (!(s4 & 0x02020202u)) return 0u;
+    uint32_t td[4];
+    ld4(d.tod + p, td);
+    uint32_t m = 0u;
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+        m |= (uint32_t)(((s4 >> (8 * i)) & 0xFFu) == FD_DEAD && is_sched(td[i], t, d.sched_delay)) << i;
+    return m;
+}
 template <bool GENM>
-__device__ __forceinline__ void load_grp(const Dev &d, size_t ra, size_t rb, uint32_t c0, bool schA, bool schB,
-                                         Grp &g) {
+__device__ __forceinline__ void load_grp(const Dev &d, size_t ra, size_t rb, uint32_t c0, uint32_t t, bool schA,
+                                         bool schB, Grp &g) {
     uint32_t R[4];
     ld4(d.self_hb + c0, R);
     ld4h(d.hb + ra + c0, g.hA);
@@ -761,10 +796,11 @@ __device__ __forceinline__ void load_grp(const Dev &d, size_t ra, size_t rb, uin
     // raw max_version words (prefix-view flag included): pass 1 masks them where it compares, and the
     // split path hands them to the packer in its candidate records
 #pragma unroll
-    for (int i = 0; i < 4; i++) { g.pA[i] = g.pB[i] = g.fA[i] = g.fB[i] = 0u; }
+    for (int i = 0; i < 4; i++) { g.pA[i] = g.pB[i] = 0u; }
+    g.sA = g.sB = 0u;
     if (GENM) { ld4(d.pos + ra + c0, g.pA); ld4(d.pos + rb + c0, g.pB); }
-    if (schA) ld4(d.fd_state + ra + c0, g.fA);
-    if (schB) ld4(d.fd_state + rb + c0, g.fB);
+    if (schA) g.sA = sched4(d, ra + c0, t);
+    if (schB) g.sB = sched4(d, rb + c0, t);
 }
 
 // FailureDetector.report_heartbeat -> SamplingWindow.report_heartbeat on one unpacked window
@@ -812,7 +848,7 @@ __device__ __forceinline__ void pass1_grp(const Dev &d, size_t ra, size_t rb, ui
     rmA = rmB = 0u;
     nBA = nAB = nNB = nNA = 0u;
     // HBM-resident elements only: the SELF_HB row (16 B per group, 256 KiB per row, L2-resident) is not counted
-    alg += 32 + (GENM ? 32 : 0) + (schA ? 16 : 0) + (schB ? 16 : 0);
+    alg += 32 + (GENM ? 32 : 0) + (schA ? 4 : 0) + (schB ? 4 : 0);
     // Branch-free (selects, no exec-mask juggling per column): the per-column rules of the reference,
     // restated as predicates.  _report_heartbeat (server.py:599-604, state.py:280-287) of a known view
     // stores the larger heartbeat and reports only if the old one was non-zero; an unknown owner is
@@ -823,8 +859,8 @@ __device__ __forceinline__ void pass1_grp(const Dev &d, size_t ra, size_t rb, ui
         const bool valid = j < d.ncol;
         const bool pa = GENM ? g.pA[i] != NONE : true;
         const bool pb = GENM ? g.pB[i] != NONE : true;
-        const bool sa = SCH && schA && pa && is_sched(g.fA[i], t, d.sched_delay);
-        const bool sb = SCH && schB && pb && is_sched(g.fB[i], t, d.sched_delay);
+        const bool sa = SCH && schA && pa && ((g.sA >> i) & 1u);
+        const bool sb = SCH && schB && pb && ((g.sB >> i) & 1u);
         const bool inA = pa && !sa;  // j is in a's digest (compute_digest, state.py:324-331)
         uint32_t hA = g.hA[i], hB = g.hB[i];
         // responder inc_heartbeat (server.py:524): b's view of itself
@@ -998,10 +1034,10 @@ __global__ __launch_bounds__(XB, (KW == 4 ? P1_WAVES : 1)) void k_pass1(Dev d, c
         constexpr bool SCH = decltype(sch)::value;
         uint32_t c0 = c0s;
         Grp g0, g1;
-        if (c0 < hi) load_grp<false>(d, ra, rb, c0, SCH && schA, SCH && schB, g0);
+        if (c0 < hi) load_grp<false>(d, ra, rb, c0, t, SCH && schA, SCH && schB, g0);
         while (c0 < hi) {
             const uint32_t c1 = c0 + WAVE * 4u;
-            if (c1 < hi) load_grp<false>(d, ra, rb, c1, SCH && schA, SCH && schB, g1);
+            if (c1 < hi) load_grp<false>(d, ra, rb, c1, t, SCH && schA, SCH && schB, g1);
             uint32_t rmA, rmB, nBA, nAB, nNB, nNA;
             const uint32_t mA[4] = {g0.mA[0], g0.mA[1], g0.mA[2], g0.mA[3]};
             const uint32_t mB[4] = {g0.mB[0], g0.mB[1], g0.mB[2], g0.mB[3]};
@@ -1107,10 +1143,10 @@ __global__ __launch_bounds__(XB, (KW == 4 ? XB_WAVES : 1)) void k_exchange(Dev d
     // (different owners, so the early loads never read a location this group writes)
     uint32_t c0 = (uint32_t)tid * 4u;
     Grp g0, g1;
-    if (c0 < d.ncol) load_grp<GENM>(d, ra, rb, c0, schA, schB, g0);
+    if (c0 < d.ncol) load_grp<GENM>(d, ra, rb, c0, t, schA, schB, g0);
     while (c0 < d.ncol) {
         const uint32_t c1 = c0 + XB * 4u;
-        if (c1 < d.ncol) load_grp<GENM>(d, ra, rb, c1, schA, schB, g1);
+        if (c1 < d.ncol) load_grp<GENM>(d, ra, rb, c1, t, schA, schB, g1);
         uint32_t rmA, rmB, nBA, nAB, nNB, nNA;
         pass1_grp<GENM>(d, ra, rb, c0, a, b, t, schA, schB, g0, nBA, nAB, nNB, nNA, alg, reports, hbw, rmA, rmB);
         // one LDS atomic per lane and bitmap (4 consecutive columns sit in one word); stale owners are sparse
@@ -1445,9 +1481,19 @@ __global__ __launch_bounds__(LB) void k_begin_round(Dev d, const uint8_t *up, ui
 }
 
 // ------------------------------------------------------------------ liveness
-__global__ __launch_bounds__(LB) void k_reset_sched(Dev d, const uint8_t *up) {
+// Row word 2 is a lower bound of the row's earliest scheduled-for-deletion tick (tod + grace/2 over its
+// dead targets): a new death lowers it, a revival or FD GC leaves it.  Only a row whose bound has passed
+// (so that a target may be scheduled, or due for FD GC: grace >= grace/2) is recomputed exactly, by the
+// sweep that follows (flag bit 1), which is then the only one to read its times of death.
+__global__ __launch_bounds__(LB) void k_reset_sched(Dev d, const uint8_t *up, uint32_t t) {
     const uint32_t o = blockIdx.x * LB + threadIdx.x;
-    if (o < d.N && up[o]) d.row[o * 4 + 2] = NONE;
+    if (o >= d.N || !up[o]) return;
+    uint32_t f = d.row[o * 4 + 3] & ~2u;
+    if (t >= d.row[o * 4 + 2]) {
+        d.row[o * 4 + 2] = NONE;
+        f |= 2u;
+    }
+    d.row[o * 4 + 3] = f;
 }
 
 // First the round's deferred heartbeat reports (pass 1 of k_exchange) are replayed into the
@@ -1468,6 +1514,7 @@ __global__ __launch_bounds__(LB) void k_liveness(Dev d, const uint8_t *up, uint3
     const uint32_t groups = (chunks + per - 1) / per;
     const uint32_t o = blockIdx.x / groups, cb0 = (blockIdx.x % groups) * per;
     const bool upo = decide && up[o] != 0;
+    const bool exact = upo && (d.row[o * 4 + 3] & 2u);  // recompute row word 2 (k_reset_sched)
     const bool genm = !(d.flags & GS_CANONICAL);
     uint32_t minS = NONE, live = 0, gcdue = 0, ovf = 0, alg = 0;
     // phases of the current round in which row o was in an exchange (its plane rows are valid);
@@ -1486,11 +1533,11 @@ __global__ __launch_bounds__(LB) void k_liveness(Dev d, const uint8_t *up, uint3
     // node was in no exchange), so it loads windows only for up observers, as before
     const uint32_t c0 = (cb * LB + threadIdx.x) * 4u;
     uint64_t w[4] = {0ull, 0ull, 0ull, 0ull};
-    uint32_t st[4] = {0u, 0u, 0u, 0u}, ps[4] = {0u, 0u, 0u, 0u};
+    uint32_t s4 = 0u, ps[4] = {0u, 0u, 0u, 0u};  // s4: the four pairs' states, one byte each
     if (c0 < d.ncol) {
         const size_t p = pix(d, o, c0);
         if (upo || vm) ld4w(d.fd + p, w);
-        if (upo) ld4(d.fd_state + p, st);
+        if (upo) s4 = *reinterpret_cast<const uint32_t *>(d.fd_state + p);
         if (upo && genm) ld4(d.pos + p, ps);
     }
     if (vm) {
@@ -1510,7 +1557,10 @@ __global__ __launch_bounds__(LB) void k_liveness(Dev d, const uint8_t *up, uint3
             for (int i = 0; i < 4; i++) q[i] |= (uint32_t)((s_pl[ph][wb + i] >> lb) & 1ull) << ph;
         }
         const bool rep = (q[0] | q[1] | q[2] | q[3]) != 0u;  // only if vm != 0: then w was loaded
-        bool dw = false, ds = false;
+        bool dw = false;
+        uint32_t td[4] = {NONE, NONE, NONE, NONE};
+        if (exact && (s4 & 0x02020202u)) ld4(d.tod + p, td);
+        uint32_t s4n = s4;
         if (rep) {
 #pragma unroll
             for (int i = 0; i < 4; i++) {
@@ -1540,23 +1590,27 @@ __global__ __launch_bounds__(LB) void k_liveness(Dev d, const uint8_t *up, uint3
                     const double phi = ((double)(t - f.last) * TICK_S) / mean;
                     alive = phi <= d.phi_thr;
                 }
+                const uint32_t st = (s4 >> (8 * i)) & 0xFFu;
                 // node join / leave: the live set against the previous call's (server.py:611-616)
-                if (d.ev && alive != (st[i] == 1u))
-                    emit_event(d, o, d.col_lo + j, (alive ? EV_JOIN : EV_LEAVE) << 8, 0u, 0u, t);
-                if (alive) {
-                    if (st[i] != 1u) { st[i] = 1u; ds = true; }
-                } else {
-                    if (st[i] < 2u) { st[i] = 2u + t; ds = true; }  // time_of_death recorded once
+                if (d.ev && alive != (st == FD_LIVE))
+                    emit_event(d, o, d.col_lo + j, (alive ? EV_JOIN : EV_LEAVE) << 8, 0u, 0u, t, 0u);
+                uint32_t sn = FD_LIVE;
+                if (!alive) {
+                    sn = FD_DEAD;
+                    uint32_t tod = td[i];  // loaded for the dead pairs of a row being recomputed
+                    if (st != FD_DEAD) { tod = t; d.tod[p + i] = t; }  // time_of_death recorded once
                     if (has && (f.sum | f.cnt)) { w[i] = fd_pack(d, Fd{f.last, 0u, 0u}); dw = true; }  // reset
-                    const uint32_t tod = st[i] - 2u;
-                    const uint32_t sat = tod + d.sched_delay;
-                    if (sat < minS) minS = sat;
-                    if ((uint64_t)t >= (uint64_t)tod + d.dead_grace) gcdue++;
+                    if (st != FD_DEAD || exact) {
+                        const uint32_t sat = tod + d.sched_delay;
+                        if (sat < minS) minS = sat;
+                    }
+                    if (exact && (uint64_t)t >= (uint64_t)tod + d.dead_grace) gcdue++;
                 }
+                s4n = (s4n & ~(0xFFu << (8 * i))) | (sn << (8 * i));
             }
         }
         if (dw) st4w(d.fd + p, w);
-        if (ds) st4(d.fd_state + p, st);
+        if (s4n != s4) *reinterpret_cast<uint32_t *>(d.fd_state + p) = s4n;
     }
     }
     // earliest scheduled-for-deletion tick of this row
@@ -1570,7 +1624,7 @@ __global__ __launch_bounds__(LB) void k_liveness(Dev d, const uint8_t *up, uint3
         if (sl) shard_add(d, C_LIVE, sl);
         if (so) shard_add(d, C_E_FDOVF, so);
         if (sg) {
-            if (genm) d.row[o * 4 + 3] = 1u;  // k_fd_gc collects this row
+            if (genm) atomicOr(&d.row[o * 4 + 3], 1u);  // k_fd_gc collects this row
             else shard_add(d, C_E_FDGC, sg);  // removal would break the canonical layout
         }
     }
@@ -1588,16 +1642,16 @@ __global__ __launch_bounds__(LB) void k_fd_gc(Dev d, const uint8_t *up, uint32_t
     __shared__ uint32_t s_wsum[LB / WAVE];
     extern __shared__ __attribute__((aligned(16))) uint32_t rmv[];  // removal bitmap, NP bits
     const uint32_t o = blockIdx.x;
-    if (!up[o] || !d.row[o * 4 + 3]) return;
+    if (!up[o] || !(d.row[o * 4 + 3] & 1u)) return;
     const int tid = threadIdx.x, lane = tid & (WAVE - 1), wid = tid >> 6;
     const size_t ro = (size_t)o * d.NP;
     const uint32_t cnt = d.row[o * 4 + 0];
     // 1. earliest expired target (in dead-dict order) that has no window
     unsigned long long fkey = ~0ull;
     for (uint32_t j = tid; j < d.ncol; j += LB) {
-        const uint32_t st = d.fd_state[ro + j], pos = d.pos[ro + j];
-        if (st >= 2u && pos != NONE && (uint64_t)t >= (uint64_t)(st - 2u) + d.dead_grace && d.fd[ro + j] == 0ull) {
-            const unsigned long long key = ((unsigned long long)(st - 2u) << 32) | pos;
+        const uint32_t tod = dead_tod(d, ro + j), pos = d.pos[ro + j];
+        if (tod != NONE && pos != NONE && (uint64_t)t >= (uint64_t)tod + d.dead_grace && d.fd[ro + j] == 0ull) {
+            const unsigned long long key = ((unsigned long long)tod << 32) | pos;
             if (key < fkey) fkey = key;
         }
     }
@@ -1614,9 +1668,9 @@ __global__ __launch_bounds__(LB) void k_fd_gc(Dev d, const uint8_t *up, uint32_t
     // 2. drop dead entries / windows; mark dict removals
     uint32_t gcn = 0;
     for (uint32_t j = tid; j < d.ncol; j += LB) {
-        const uint32_t st = d.fd_state[ro + j], pos = d.pos[ro + j];
-        if (!(st >= 2u && pos != NONE && (uint64_t)t >= (uint64_t)(st - 2u) + d.dead_grace)) continue;
-        const unsigned long long key = ((unsigned long long)(st - 2u) << 32) | pos;
+        const uint32_t tod = dead_tod(d, ro + j), pos = d.pos[ro + j];
+        if (!(tod != NONE && pos != NONE && (uint64_t)t >= (uint64_t)tod + d.dead_grace)) continue;
+        const unsigned long long key = ((unsigned long long)tod << 32) | pos;
         if (q9 && key > fkey) continue;
         d.fd_state[ro + j] = 0u;  // del self._dead_nodes[gossip_id]
         if (q9 && key == fkey) continue;
@@ -1663,7 +1717,7 @@ __global__ __launch_bounds__(LB) void k_fd_gc(Dev d, const uint8_t *up, uint32_t
         if (tid == 0) d.row[o * 4 + 0] = base;
     }
     if (tid == 0) {
-        d.row[o * 4 + 3] = 0u;
+        d.row[o * 4 + 3] &= ~1u;
         if (q9) shard_add(d, C_Q9, 1);
     }
     const unsigned long long sg = wave_sum(gcn);
@@ -1785,7 +1839,8 @@ __global__ __launch_bounds__(LB) void k_owner_writes(Dev d, const gs_write *ops,
     // delete_after_ttl mutate the stored VersionedValue in place, so old and new are the same
     // object and nothing is emitted (server.py:199-203, 211-215)
     if (d.ev && (op.op == GS_OP_SET || op.op == GS_OP_SET_WITH_TTL))
-        emit_event(d, op.owner, op.owner, k | (EV_KEY << 8), w ? (uint32_t)d.hist[hix(d, j, w, k)] : 0u, ver, t);
+        emit_event(d, op.owner, op.owner, k | (EV_KEY << 8), w ? (uint32_t)d.hist[hix(d, j, w, k)] : 0u, ver, t,
+                   d.ev_wseq + i);
     if (d.flags & GS_TOMBSTONES) {
         d.ts[pj * d.KP + k] = st ? t : NONE;
         if (st) d.row[op.owner * 4 + 1] = 1u;
@@ -1889,7 +1944,7 @@ __device__ inline uint8_t *put_u(uint8_t *p, uint32_t tag, uint32_t x) {
 __device__ inline uint32_t digest_owner(const Dev &d, uint32_t o, uint32_t q, uint32_t t, bool sch) {
     const uint32_t j = (d.flags & GS_CANONICAL) ? q : d.ord[(size_t)o * d.NP + q];
     if (j == NONE) return NONE;
-    if (sch && is_sched(d.fd_state[pix(d, o, j)], t, d.sched_delay)) return NONE;
+    if (sch && is_sched(dead_tod(d, pix(d, o, j)), t, d.sched_delay)) return NONE;
     return j;
 }
 __device__ inline void view_hgm(const Dev &d, uint32_t o, uint32_t j, uint32_t &H, uint32_t &G, uint32_t &M) {
@@ -1970,9 +2025,9 @@ __global__ __launch_bounds__(WAVE) void k_delta_plan(Dev d, uint32_t s, uint32_t
         if (j < d.ncol) {
             const size_t ps = pix(d, s, j), pr = pix(d, r, j);
             const bool has = GENM ? d.pos[ps] != NONE : true;
-            if (has && !(schS && is_sched(d.fd_state[ps], t, d.sched_delay))) {
+            if (has && !(schS && is_sched(dead_tod(d, ps), t, d.sched_delay))) {
                 bool in_d = GENM ? d.pos[pr] < cntR : true;
-                if (in_d && schR && is_sched(d.fd_state[pr], t, d.sched_delay)) in_d = false;
+                if (in_d && schR && is_sched(dead_tod(d, pr), t, d.sched_delay)) in_d = false;
                 const uint32_t dm = in_d ? (d.mv[pr] & MV_MASK) : 0u;
                 stale = (d.mv[ps] & MV_MASK) > dm;  // state.py:347-357
             }
@@ -2364,6 +2419,14 @@ struct gs_handle {
     std::vector<std::pair<hipEvent_t, hipEvent_t>> tev[4];
     std::vector<hipEvent_t> evpool;
     std::string err;
+    // sliced phases driven by the library (gs_comm_init: RCCL across processes; gs_run_phase_group:
+    // the slices of one process): device scratch for the gathered totals and chain states
+    ncclComm_t comm = nullptr;
+    struct {
+        uint64_t *tot = nullptr, *tot_all = nullptr, *chain = nullptr, *chainc = nullptr, *chain_all = nullptr;
+        uint32_t *list = nullptr;
+        uint32_t cap = 0;  // exchanges the buffers hold
+    } sc;
 };
 
 namespace {
@@ -2417,7 +2480,8 @@ int check_bound(gs_handle *h) {
     d.gc = (uint32_t *)h->reg[GS_R_GC];
     d.held = (uint8_t *)h->reg[GS_R_HELD];
     d.fd = (uint64_t *)h->reg[GS_R_FD];
-    d.fd_state = (uint32_t *)h->reg[GS_R_FD_STATE];
+    d.fd_state = (uint8_t *)h->reg[GS_R_FD_STATE];
+    d.tod = (uint32_t *)h->reg[GS_R_FD_TOD];
     d.ts = (uint32_t *)h->reg[GS_R_TS];
     d.ring = (uint16_t *)h->reg[GS_R_RING];
     d.pos = (uint32_t *)h->reg[GS_R_POS];
@@ -2582,7 +2646,8 @@ int gs_create(const gs_config *cfg, gs_handle **out) {
     b[GS_R_GC] = (c.flags & GS_TOMBSTONES) ? pairs * 4 : 0;  // last_gc_version stays 0 without tombstone GC
     b[GS_R_HELD] = (c.flags & GS_NO_HELD) ? 0 : pairs * KP;
     b[GS_R_FD] = pairs * 8;
-    b[GS_R_FD_STATE] = pairs * 4;
+    b[GS_R_FD_STATE] = pairs;
+    b[GS_R_FD_TOD] = pairs * 4;
     b[GS_R_TS] = (c.flags & GS_TOMBSTONES) ? pairs * KP * 4 : 0;
     b[GS_R_RING] = (c.flags & GS_FD_RING) ? pairs * W * 2 : 0;
     b[GS_R_POS] = b[GS_R_ORD] = genm ? pairs * 4 : 0;
@@ -2638,6 +2703,10 @@ void gs_destroy(gs_handle *h) {
     for (auto &v : h->tev)
         for (auto &pr : v) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
     for (hipEvent_t e : h->evpool) (void)hipEventDestroy(e);
+    for (void *p : {(void *)h->sc.tot, (void *)h->sc.tot_all, (void *)h->sc.chain, (void *)h->sc.chainc,
+                    (void *)h->sc.chain_all, (void *)h->sc.list})
+        if (p) (void)hipFree(p);
+    if (h->comm) (void)ncclCommDestroy(h->comm);
     delete h;
 }
 
@@ -2667,7 +2736,7 @@ int gs_boot(gs_handle *h, const uint16_t *nid_size, const uint8_t *key_len) {
     if (rc) return rc;
     hipStream_t s = h->stream;
     // regions that start at zero
-    const int zero[] = {GS_R_HB, GS_R_SELF_HB, GS_R_MV, GS_R_GC, GS_R_HELD, GS_R_FD, GS_R_FD_STATE,
+    const int zero[] = {GS_R_HB, GS_R_SELF_HB, GS_R_MV, GS_R_GC, GS_R_HELD, GS_R_FD, GS_R_FD_STATE, GS_R_FD_TOD,
                         GS_R_RING, GS_R_ROW, GS_R_LAST_W, GS_R_HIST, GS_R_HIST_VID,
                         GS_R_STAMP, GS_R_COUNTERS, GS_R_SLICE_BITS, GS_R_PEND, GS_R_PEND_STAMP, GS_R_LATEST};
     for (int r : zero)
@@ -2724,6 +2793,7 @@ int gs_owner_writes(gs_handle *h, const gs_write *ops, uint32_t n, uint32_t tick
     if (!n) return GS_OK;
     k_owner_writes<<<(n + LB - 1) / LB, LB, 0, h->stream>>>(h->d, ops, n, tick);
     HIPCHK(h, hipGetLastError());
+    if (h->d.ev) h->d.ev_wseq += n;
     return GS_OK;
 }
 
@@ -2754,10 +2824,20 @@ int gs_check_heartbeat_lag(gs_handle *h) {
     return GS_OK;
 }
 
+extern "C++" {
+namespace {
+int sliced_phase(gs_handle *const *hs, uint32_t nh, const int32_t *ini, const int32_t *res, uint32_t n, uint32_t tick);
+}
+}
+
 int gs_run_phase(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t n, uint32_t tick) {
     int rc = check_phase(h, ini, res, n, tick);
     if (rc) return rc;
-    if (h->G > 1) return fail(h, GS_E_UNSUPPORTED, "sliced handle: use gs_phase_count / gs_phase_pack");
+    if (h->G > 1) {
+        if (!h->comm)
+            return fail(h, GS_E_UNSUPPORTED, "sliced handle without gs_comm_init: use gs_run_phase_group or gs_phase_*");
+        return n ? sliced_phase(&h, 1, ini, res, n, tick) : GS_OK;
+    }
     if (!n) return GS_OK;
     if ((rc = advance_planes(h, tick))) return rc;
     const bool genm = !(h->cfg.flags & GS_CANONICAL);
@@ -2873,11 +2953,125 @@ int gs_phase_chain(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_
     return time_end(h, GS_KT_PACK, e0);
 }
 
+// ---- sliced phases driven by the library
+extern "C++" {
+namespace {
+int ensure_scratch(gs_handle *h, uint32_t n) {
+    if (h->sc.cap >= n) return GS_OK;
+    for (void *p : {(void *)h->sc.tot, (void *)h->sc.tot_all, (void *)h->sc.chain, (void *)h->sc.chainc,
+                    (void *)h->sc.chain_all, (void *)h->sc.list})
+        if (p) HIPCHK(h, hipFree(p));
+    const uint32_t cap = std::max(n, 1024u);
+    const size_t s2 = (size_t)2 * cap * 8, G = h->G;
+    HIPCHK(h, hipMalloc(&h->sc.tot, s2));
+    HIPCHK(h, hipMalloc(&h->sc.chain, s2));
+    HIPCHK(h, hipMalloc(&h->sc.chainc, s2));
+    HIPCHK(h, hipMalloc(&h->sc.tot_all, G * s2));
+    HIPCHK(h, hipMalloc(&h->sc.chain_all, G * s2));
+    HIPCHK(h, hipMalloc(&h->sc.list, ((size_t)2 * cap + 256) * 4));
+    h->sc.cap = cap;
+    return GS_OK;
+}
+
+// all-gather of `count` u64 per slice (src of slice g -> dst[g * count ..], on every slice): one RCCL
+// all-gather when this process drives one slice of a communicator, device copies when it drives them all
+int gather_u64(gs_handle *const *hs, uint32_t nh, uint64_t *(*src)(gs_handle *), uint64_t *(*dst)(gs_handle *),
+               size_t count) {
+    if (!count) return GS_OK;
+    if (nh == 1) {
+        gs_handle *h = hs[0];
+        const ncclResult_t r = ncclAllGather(src(h), dst(h), count, ncclUint64, h->comm, h->stream);
+        if (r != ncclSuccess) return fail(h, GS_E_HIP, "ncclAllGather: %s", ncclGetErrorString(r));
+        return GS_OK;
+    }
+    for (uint32_t i = 0; i < nh; i++)
+        for (uint32_t g = 0; g < nh; g++)
+            HIPCHK(hs[i], hipMemcpyAsync(dst(hs[i]) + (size_t)g * count, src(hs[g]), count * 8, hipMemcpyDeviceToDevice,
+                                         hs[i]->stream));
+    return GS_OK;
+}
+
+// One phase of a sliced cluster: pass 1 + slice totals on every slice, all-gather of the
+// totals (16 B per exchange and slice), packing step 0, then -- only for the (exchange, direction) slots
+// whose totals sum past the MTU, listed on the device, one host read -- G - 1 chain steps, each an
+// all-gather of those slots' chain states (8 B per slot and slice) and a resume on the next slice.
+int sliced_phase(gs_handle *const *hs, uint32_t nh, const int32_t *ini, const int32_t *res, uint32_t n, uint32_t tick) {
+    int rc;
+    for (uint32_t i = 0; i < nh; i++) {
+        if (!hs[i]->d.cand) return fail(hs[i], GS_E_UNSUPPORTED, "library-driven sliced phases need candidate records");
+        if ((rc = ensure_scratch(hs[i], n))) return rc;
+    }
+    for (uint32_t i = 0; i < nh; i++)
+        if ((rc = gs_phase_count(hs[i], ini, res, n, tick, hs[i]->sc.tot))) return rc;
+    if ((rc = gather_u64(hs, nh, [](gs_handle *h) { return h->sc.tot; }, [](gs_handle *h) { return h->sc.tot_all; },
+                         (size_t)2 * n)))
+        return rc;
+    for (uint32_t i = 0; i < nh; i++)
+        if ((rc = gs_phase_pack(hs[i], ini, res, n, tick, 0, hs[i]->sc.tot_all, nullptr, hs[i]->sc.chain))) return rc;
+    uint32_t count = 0;
+    for (uint32_t i = nh; i-- > 0;)  // the same gathered totals give every slice the same list: read it once
+        if ((rc = gs_phase_overflow(hs[i], n, hs[i]->sc.tot_all, hs[i]->sc.chain, hs[i]->sc.list, hs[i]->sc.chainc,
+                                    i == 0 ? &count : nullptr)))
+            return rc;
+    if (!count) return GS_OK;
+    const uint32_t G = hs[0]->G;
+    for (uint32_t step = 1; step < G; step++) {
+        if ((rc = gather_u64(hs, nh, [](gs_handle *h) { return h->sc.chainc; },
+                             [](gs_handle *h) { return h->sc.chain_all; }, count)))
+            return rc;
+        for (uint32_t i = 0; i < nh; i++)
+            if ((rc = gs_phase_chain(hs[i], ini, res, n, tick, step, hs[i]->sc.list, count, hs[i]->sc.chain_all,
+                                     hs[i]->sc.chain, hs[i]->sc.chainc)))
+                return rc;
+    }
+    return GS_OK;
+}
+}  // namespace
+}
+
+int gs_comm_id(void *id) {
+    if (!id) return GS_E_INVALID;
+    ncclUniqueId u;
+    if (ncclGetUniqueId(&u) != ncclSuccess) return GS_E_HIP;
+    static_assert(sizeof u == GS_COMM_ID_BYTES, "ncclUniqueId size");
+    memcpy(id, &u, sizeof u);
+    return GS_OK;
+}
+
+int gs_comm_init(gs_handle *h, const void *id, uint32_t nranks, uint32_t rank) {
+    if (!h || !id) return GS_E_INVALID;
+    if (h->comm) return fail(h, GS_E_INVALID, "gs_comm_init: this handle already has a communicator");
+    if (nranks != h->G || rank != h->shard)
+        return fail(h, GS_E_INVALID, "gs_comm_init: %u ranks / rank %u for slice %u of %u", nranks, rank, h->shard, h->G);
+    ncclUniqueId u;
+    memcpy(&u, id, sizeof u);
+    const ncclResult_t r = ncclCommInitRank(&h->comm, (int)nranks, u, (int)rank);
+    if (r != ncclSuccess) {
+        h->comm = nullptr;
+        return fail(h, GS_E_HIP, "ncclCommInitRank: %s", ncclGetErrorString(r));
+    }
+    return GS_OK;
+}
+
+int gs_run_phase_group(gs_handle *const *hs, uint32_t n_handles, const int32_t *ini, const int32_t *res, uint32_t n,
+                       uint32_t tick) {
+    if (!hs || !n_handles || !hs[0]) return GS_E_INVALID;
+    gs_handle *h0 = hs[0];
+    if (n_handles != h0->G) return fail(h0, GS_E_INVALID, "gs_run_phase_group: %u handles for %u slices", n_handles, h0->G);
+    for (uint32_t i = 0; i < n_handles; i++) {
+        if (!hs[i] || hs[i]->shard != i || hs[i]->G != h0->G || hs[i]->N != h0->N || hs[i]->stream != h0->stream)
+            return fail(h0, GS_E_INVALID, "gs_run_phase_group: handle %u is not slice %u of this cluster on one stream", i, i);
+    }
+    if (h0->G == 1) return gs_run_phase(h0, ini, res, n, tick);
+    if (!n) return check_phase(h0, ini, res, n, tick);
+    return sliced_phase(hs, n_handles, ini, res, n, tick);
+}
+
 int gs_liveness(gs_handle *h, const uint8_t *up, uint32_t tick) {
     if (!h || !h->booted || !up) return GS_E_INVALID;
     if (h->reports_pending && tick < h->last_phase_tick)
         return fail(h, GS_E_INVALID, "gs_liveness at tick %u precedes a phase at tick %u", tick, h->last_phase_tick);
-    k_reset_sched<<<(h->N + LB - 1) / LB, LB, 0, h->stream>>>(h->d, up);
+    k_reset_sched<<<(h->N + LB - 1) / LB, LB, 0, h->stream>>>(h->d, up, tick);
     HIPCHK(h, hipGetLastError());
     int rc = launch_liveness(h, up, tick, h->reports_pending, true);
     if (rc) return rc;
@@ -2887,6 +3081,26 @@ int gs_liveness(gs_handle *h, const uint8_t *up, uint32_t tick) {
         k_fd_gc<<<h->N, LB, (h->NP / 32) * 4, h->stream>>>(h->d, up, tick);
         HIPCHK(h, hipGetLastError());
     }
+    return GS_OK;
+}
+
+int gs_read_rows(gs_handle *h, int region, uint32_t row_lo, uint32_t row_hi, void *out, uint64_t cap, uint64_t *len) {
+    static const int rows_major[] = {GS_R_HB, GS_R_MV, GS_R_GC, GS_R_HELD, GS_R_FD, GS_R_FD_STATE, GS_R_FD_TOD,
+                                     GS_R_TS, GS_R_RING, GS_R_POS, GS_R_ORD, GS_R_ROW};
+    if (!h || !h->booted || !out || !len || row_lo > row_hi || row_hi > h->N) return GS_E_INVALID;
+    if (std::find(std::begin(rows_major), std::end(rows_major), region) == std::end(rows_major))
+        return fail(h, GS_E_INVALID, "gs_read_rows: region %d is not indexed by observer row", region);
+    if (!h->bytes[region]) return fail(h, GS_E_UNSUPPORTED, "gs_read_rows: region %d is not allocated", region);
+    const uint64_t rb = h->bytes[region] / h->N, nb = rb * (row_hi - row_lo);
+    *len = nb;
+    if (nb > cap) return fail(h, GS_E_INVALID, "gs_read_rows: %llu bytes > capacity %llu", (unsigned long long)nb,
+                              (unsigned long long)cap);
+    if (region == GS_R_HELD) {  // prefix views do not keep their held ordinals: derive them first
+        int rc = gs_materialize_held(h, row_lo, row_hi);
+        if (rc) return rc;
+    }
+    HIPCHK(h, hipMemcpyAsync(out, (const uint8_t *)h->reg[region] + rb * row_lo, nb, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
     return GS_OK;
 }
 
@@ -3062,6 +3276,7 @@ int gs_set_events(gs_handle *h, uint32_t *records, uint32_t capacity, uint32_t *
     h->d.ev = records;
     h->d.ev_count = records ? count : nullptr;
     h->d.ev_cap = records ? capacity : 0u;
+    h->d.ev_wseq = 0u;
     return GS_OK;
 }
 

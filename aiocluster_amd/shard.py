@@ -134,7 +134,10 @@ def run_sliced_phase(slices, comm, mtu: int, t: int, ini, res) -> int:
 class ShardGroup:
     """The owner-column slices of one simulated cluster, driven like one ``GossipSim``."""
 
-    def __init__(self, slices, comm, mtu: int):
+    def __init__(self, slices, comm, mtu: int, native: bool = False):
+        """``native``: the library drives each phase (gs_run_phase_group for the slices of this process,
+        or gs_run_phase over the RCCL communicator of gs_comm_init, one slice per rank); otherwise this
+        module does (run_sliced_phase, gathers through ``comm``)."""
         if not slices:
             raise GsError("ShardGroup needs at least one slice")
         self.slices = list(slices)
@@ -142,21 +145,37 @@ class ShardGroup:
         self.mtu = int(mtu)
         self.n = self.slices[0].n
         self.chain_phases = 0
+        self.native = native
+        if native and len(self.slices) == 1 and isinstance(comm, DistComm):
+            self._comm_init()
+
+    def _comm_init(self):
+        """gs_comm_id on rank 0, broadcast over the process group, gs_comm_init on every rank."""
+        import ctypes as C
+
+        s = self.slices[0]
+        uid = (C.c_uint8 * 128)()
+        if self.comm.rank == 0:
+            s._chk(s.L.gs_comm_id(uid), "gs_comm_id")
+        box = [bytes(uid)]
+        self.comm.dist.broadcast_object_list(box, src=0, group=self.comm.group)
+        uid = (C.c_uint8 * 128).from_buffer_copy(box[0])
+        s._chk(s.L.gs_comm_init(s.h, uid, self.comm.world, self.comm.rank), "gs_comm_init")
 
     @classmethod
-    def in_process(cls, node_ids, keys, cfg, shards: int, **kw):
+    def in_process(cls, node_ids, keys, cfg, shards: int, native: bool = False, **kw):
         from .sim import GossipSim
 
         sl = [GossipSim(node_ids, keys, cfg, shards=shards, shard=g, **kw) for g in range(shards)]
-        return cls(sl, LocalComm(shards), cfg["mtu"])
+        return cls(sl, LocalComm(shards), cfg["mtu"], native=native)
 
     @classmethod
-    def distributed(cls, node_ids, keys, cfg, group=None, **kw):
+    def distributed(cls, node_ids, keys, cfg, group=None, native: bool = False, **kw):
         from .sim import GossipSim
 
         comm = DistComm(group)
         s = GossipSim(node_ids, keys, cfg, shards=comm.world, shard=comm.rank, **kw)
-        return cls([s], comm, cfg["mtu"])
+        return cls([s], comm, cfg["mtu"], native=native)
 
     # -- owner writes / round driver: every slice sees every call (each keeps its own columns)
     def write(self, t, j, k, op, value):
@@ -182,6 +201,18 @@ class ShardGroup:
         for s in self.slices:
             s._flush()
         ini, res = s0._pairs_dev(initiators, responders)
+        if self.native:
+            import ctypes as C
+
+            n = int(ini.numel())
+            if len(self.slices) == 1:
+                s0._chk(s0.L.gs_run_phase(s0.h, C.c_void_p(ini.data_ptr()), C.c_void_p(res.data_ptr()), n, t),
+                        "gs_run_phase")
+            else:
+                hs = (C.c_void_p * len(self.slices))(*[s.h for s in self.slices])
+                s0._chk(s0.L.gs_run_phase_group(hs, len(self.slices), C.c_void_p(ini.data_ptr()),
+                                                C.c_void_p(res.data_ptr()), n, t), "gs_run_phase_group")
+            return
         if run_sliced_phase(self.slices, self.comm, self.mtu, t, ini, res) > 1:
             self.chain_phases += 1
 

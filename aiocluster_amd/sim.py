@@ -61,6 +61,47 @@ def sched_delay_ticks(dead_grace_s: float) -> int:
     return -(-half // TICK_US)
 
 
+def fd_state_word(st8: np.ndarray, tod: np.ndarray) -> np.ndarray:
+    """GS_R_FD_STATE (u8: 0 unknown, 1 live, 2 dead) + GS_R_FD_TOD (time of death) as one u32 per pair:
+    0 unknown, 1 live, tick of death + 2 for a dead pair (the readback format of export / snapshot)."""
+    st8 = np.asarray(st8).view(np.uint8)
+    tod = np.asarray(tod).view(np.uint32)
+    return np.where(st8 == 2, tod + np.uint32(2), st8.astype(np.uint32)).astype(np.uint32)
+
+
+def order_events(ev: np.ndarray, n: int, phases: dict, wmap: list) -> np.ndarray:
+    """Permutation putting device event records (uint32 [m, 8], gs_set_events) in the reference's order:
+    by tick; owner writes by call order (``wmap``: record seq -> call index); in a phase (``phases``:
+    tick -> (initiators, responders)) by exchange index, the initiator's apply (SynAck delta,
+    server.py:351-353) before the responder's (Ack delta, 372-376), then the NodeDelta order (seq = the
+    sender's dict position, state.py:346-413), then kv version; join / leave by observer, joins first,
+    then node (the reference iterates sets there, server.py:611-614)."""
+    m = len(ev)
+    t = ev[:, 5].astype(np.int64)
+    kind = (ev[:, 2] >> 8).astype(np.int64)
+    seq = ev[:, 6].astype(np.int64)
+    obs = ev[:, 0].astype(np.int64)
+    k1, k2, k3, k4 = (np.zeros(m, np.int64) for _ in range(4))
+    lv = kind != 0
+    k1[lv], k2[lv], k3[lv] = obs[lv], kind[lv], ev[lv, 1]
+    kc = ~lv
+    wm = np.asarray(wmap, dtype=np.int64)
+    for tick in np.unique(t[kc]).tolist():
+        sel = kc & (t == tick)
+        ph = phases.get(tick)
+        if ph is None:  # owner writes
+            k1[sel] = wm[seq[sel]] if len(wm) else seq[sel]
+            continue
+        a, b = (np.asarray(x, dtype=np.int64) for x in ph)
+        ex = np.full(n, -1, np.int64)
+        side = np.zeros(n, np.int64)
+        ex[a] = np.arange(len(a))
+        ex[b] = np.arange(len(b))
+        side[b] = 1
+        k1[sel], k2[sel], k3[sel], k4[sel] = ex[obs[sel]], side[obs[sel]], seq[sel], ev[sel, 4]
+    return np.lexsort((k4, k3, k2, k1, t))
+
+
 def make_config(n: int, k: int, cfg: dict, flags: int, hist_cap: int, shards: int = 1,
                 shard: int = 0) -> _lib.GsConfig:
     c = _lib.GsConfig()
@@ -180,7 +221,11 @@ class GossipSim:
             raise
         self.values = [""]
         self.value_ids = {"": 0}
-        self._pending: list[tuple[int, int, int, int, str]] = []
+        self._pending: list[tuple] = []
+        self._ev = self._ev_count = None  # hook events off (enable_events)
+        self._ev_phases: dict = {}
+        self._ev_wmap: list[int] = []
+        self._ev_writes = 0
         self.last_tick = 0
         self.q9_events: list = []
         if initial_values:
@@ -231,7 +276,8 @@ class GossipSim:
         if op in (1, 2, 3) and not self.flags & GS_TOMBSTONES:
             raise GsError("deletes / TTL writes need tombstones=True (GS_TOMBSTONES)")
         # interned at call time, so ids follow the caller's write order (as the oracle's do)
-        self._pending.append((t, j, k, op, self.intern(value), len(value.encode())))
+        self._pending.append((t, j, k, op, self.intern(value), len(value.encode()), self._ev_writes))
+        self._ev_writes += 1
 
     def set(self, t: int, owner: int, key: str, value: str):
         self.write(t, owner, self.keys.index(key), 0, value)
@@ -253,8 +299,10 @@ class GossipSim:
         for batch in batches:
             ticks = {x[0] for x in batch}
             for tick in sorted(ticks):
-                rows = [[j, k, op, vid, vl] for t, j, k, op, vid, vl in batch if t == tick]
+                rows = [[j, k, op, vid, vl] for t, j, k, op, vid, vl, _ in batch if t == tick]
                 self.owner_writes(np.asarray(rows, dtype=np.uint32), tick)
+                if self._ev is not None:  # gs_set_events: op i of this call has seq = ops issued before + i
+                    self._ev_wmap += [w for t, *_, w in batch if t == tick]
 
     def owner_writes(self, ops: np.ndarray, tick: int):
         """Device batch of owner writes; ``ops`` is uint32 [m, 5] (owner, key, op, value_id, value_len)."""
@@ -293,6 +341,8 @@ class GossipSim:
         n = int(ini.numel())
         if n == 0:
             return
+        if self._ev is not None:
+            self._ev_phases[t] = (ini.cpu().numpy().astype(np.int64), res.cpu().numpy().astype(np.int64))
         self._chk(self.L.gs_run_phase(self.h, C.c_void_p(ini.data_ptr()), C.c_void_p(res.data_ptr()), n, t),
                   "gs_run_phase")
 
@@ -389,7 +439,10 @@ class GossipSim:
     def enable_events(self, capacity: int = 1 << 20):
         """gs_set_events: record on_key_change / on_node_join / on_node_leave (see drain_events)."""
         torch = self.torch
-        self._ev = torch.empty((capacity, 6), dtype=torch.int32, device=self.device)
+        self._ev = torch.empty((capacity, 8), dtype=torch.int32, device=self.device)
+        self._ev_phases = {}  # phase tick -> (initiators, responders): the exchange order of that phase
+        self._ev_wmap = []    # owner-write seq -> index among the caller's writes since enable_events
+        self._ev_writes = 0
         self._ev_count = torch.zeros(1, dtype=torch.int32, device=self.device)
         self._chk(self.L.gs_set_events(self.h, C.c_void_p(self._ev.data_ptr()), capacity,
                                        C.c_void_p(self._ev_count.data_ptr())), "gs_set_events")
@@ -400,7 +453,10 @@ class GossipSim:
 
     def drain_events(self) -> np.ndarray:
         """The events since the last drain, uint32 [n, 6] = observer, owner (node index), key | kind << 8,
-        old version (0 = none), new version, tick; sorted.  Raises if the buffer overflowed."""
+        old version (0 = none), new version, tick; in the reference's order (gossip_sim.h, gs_set_events):
+        by tick; owner writes in call order; within a phase by exchange (its index in the phase), the
+        initiator's apply before the responder's, the NodeDelta order (sender's dict position), kv version;
+        liveness by observer, joins before leaves, then node.  Raises if the buffer overflowed."""
         self.sync()
         n = int(self._ev_count.item())
         if n > self._ev.shape[0]:
@@ -411,8 +467,10 @@ class GossipSim:
                           f"(the records of this drain are lost; enable_events with a larger capacity)")
         ev = self._ev[:n].cpu().numpy().view(np.uint32)
         self._ev_count.zero_()
-        order = np.lexsort(ev.T[::-1])
-        return ev[order]
+        out = ev[order_events(ev, self.n, self._ev_phases, self._ev_wmap), :6]
+        self._ev_phases.clear()
+        return out
+
 
     def fd_census(self, up) -> dict:
         """gs_fd_census: live / dead sets of every up observer against the up mask (config 5's
@@ -465,9 +523,10 @@ class GossipSim:
 
         g = {"rows": np.arange(n) if rows is None else rows}
         g["HB"] = self.decode_heartbeats(rd("HB", torch.int16, (n, NP)))
-        for name in ("GC", "FD_STATE", "POS"):
+        for name in ("GC", "POS"):
             if name in self.regions:
                 g[name] = rd(name, torch.int32, (n, NP)).view(np.uint32)
+        g["FD_STATE"] = fd_state_word(rd("FD_STATE", torch.uint8, (n, NP)), rd("FD_TOD", torch.int32, (n, NP)))
         mv = rd("MV", torch.int16, (n, NP)).view(np.uint16).astype(np.uint32)
         g["MV_INEXACT"] = (mv >> np.uint32(15)).astype(np.uint8)  # prefix-view flag (GS_MV_INEXACT)
         g["MV"] = mv & np.uint32(0x7FFF)
@@ -548,6 +607,16 @@ class GossipSim:
         sb = _lib.fd_sum_bits(int(self.cfg["window"]))
         last = (lo - np.uint32(1)).astype(np.uint32)  # 0 - 1 wraps to GS_NONE
         return last, hi & np.uint32((1 << sb) - 1), hi >> np.uint32(sb)
+
+    def read_rows(self, region: str, row_lo: int, row_hi: int) -> bytes:
+        """gs_read_rows: the bytes of observer rows [row_lo, row_hi) of ``region`` (blocking copy-out)."""
+        n = C.c_uint64()
+        t = self.regions.get(region)
+        rb = t.numel() * t.element_size() // self.n if t is not None else 0
+        buf = (C.c_uint8 * max(1, rb * (row_hi - row_lo)))()
+        self._chk(self.L.gs_read_rows(self.h, REGION[region], row_lo, row_hi, buf, len(buf), C.byref(n)),
+                  "gs_read_rows")
+        return bytes(buf)[: n.value]
 
     def phi_row(self, observer: int, tick: int | None = None) -> np.ndarray:
         """Device-computed phi (binary64) of every target of ``observer``; NaN = None."""
@@ -663,7 +732,7 @@ class GossipSim:
         hb = self.decode_heartbeats(self.region("HB", torch.int16, (n, self.np_))[o].cpu().numpy())[:n]
         mv = row("MV", torch.int16).view(np.uint16).astype(np.uint32) & np.uint32(0x7FFF)
         gc = row("GC").view(np.uint32) if "GC" in self.regions else np.zeros(n, np.uint32)
-        st = row("FD_STATE").view(np.uint32)
+        st = fd_state_word(row("FD_STATE", torch.uint8), row("FD_TOD"))
         hist = self.region("HIST", torch.int64, (n, Cc, K)).cpu().numpy().view(np.uint64)
         if "HELD" in self.regions:
             held = self.region("HELD", torch.uint8, (n, self.np_, KP))[o, :n, :K].cpu().numpy()
@@ -705,13 +774,13 @@ class GossipSim:
 
     def live_nodes(self, observer: int) -> list[NodeId]:
         self._whole()
-        st = self.region("FD_STATE", self.torch.int32, (self.n, self.np_))[observer, : self.n].cpu().numpy()
+        st = self.region("FD_STATE", self.torch.uint8, (self.n, self.np_))[observer, : self.n].cpu().numpy()
         return [self.node_ids[j] for j in np.flatnonzero(st == 1)]
 
     def dead_nodes(self, observer: int) -> list[NodeId]:
         self._whole()
-        st = self.region("FD_STATE", self.torch.int32, (self.n, self.np_))[observer, : self.n].cpu().numpy()
-        return [self.node_ids[j] for j in np.flatnonzero(st >= 2)]
+        st = self.region("FD_STATE", self.torch.uint8, (self.n, self.np_))[observer, : self.n].cpu().numpy()
+        return [self.node_ids[j] for j in np.flatnonzero(st == 2)]
 
     def phi(self, observer: int, target: int, tick: int | None = None) -> float | None:
         v = float(self.phi_row(observer, tick)[target])

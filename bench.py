@@ -403,6 +403,10 @@ def main():
                          "as the line's peer_select object (0 = skip)")
     ap.add_argument("--rehearse-slices", type=int, default=0,
                     help="hold only slice 0 of G owner-column slices (one GPU's share of a G-GPU run; timing only)")
+    ap.add_argument("--native-comm", action="store_true",
+                    help="--gpus N: the library drives each sliced phase over its own RCCL communicator "
+                         "(gs_comm_init + gs_run_phase) instead of aiocluster_amd/shard.py over torch.distributed; "
+                         "--slices G: gs_run_phase_group")
     ap.add_argument("--no-held", action="store_true",
                     help="version-only layout (GS_NO_HELD, config 4): needs an mtu no delta reaches")
     args = ap.parse_args()
@@ -452,13 +456,13 @@ def main():
     group = None
     if world > 1:
         sims = [GossipSim(ids, key_names(K), cfg, shards=world, shard=rank, **kw)]
-        group = ShardGroup(sims, DistComm(), cfg["mtu"])
+        group = ShardGroup(sims, DistComm(), cfg["mtu"], native=args.native_comm)
     elif args.rehearse_slices > 1:
         sims = [GossipSim(ids, key_names(K), cfg, shards=args.rehearse_slices, shard=0, **kw)]
         group = ShardGroup(sims, RehearsalComm(args.rehearse_slices), cfg["mtu"])
     elif args.slices > 1:
         sims = [GossipSim(ids, key_names(K), cfg, shards=args.slices, shard=g, **kw) for g in range(args.slices)]
-        group = ShardGroup(sims, LocalComm(args.slices), cfg["mtu"])
+        group = ShardGroup(sims, LocalComm(args.slices), cfg["mtu"], native=args.native_comm)
     else:
         sims = [GossipSim(ids, key_names(K), cfg, **kw)]
     sim = sims[0]
@@ -542,7 +546,8 @@ def main():
                 "keys": K,
                 "fanout": args.fanout,
                 "exchanges_per_step": exch / args.steps,
-                "parallelism": (f"owner-column slices x{world} (RCCL all-gather of slice totals)" if world > 1
+                "parallelism": (f"owner-column slices x{world} (RCCL all-gather of slice totals"
+                                + (", library-driven: gs_comm_init)" if args.native_comm else ")") if world > 1
                                 else f"slice 0 of {args.rehearse_slices} (rehearsal)" if args.rehearse_slices > 1
                                 else f"owner-column slices x{args.slices} in one process" if group is not None
                                 else "1 GPU"),

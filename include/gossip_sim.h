@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define GS_API_VERSION 9
+#define GS_API_VERSION 10
 #define GS_MAX_PHASES 64  /* gs_schedule_phases: phases per round */
 #define GS_TICK_US 15625u
 #define GS_NONE 0xFFFFFFFFu
@@ -95,13 +95,16 @@ enum gs_region {
                                         window); high word = _sum in ticks | intervals appended since
                                         the last reset << sum_bits (len = min(cnt, W)); sum_bits =
                                         32 - bits(2W) (gs_create rejects W * max_interval >= 2^sum_bits) */
-    GS_R_FD_STATE,    /* u32 [N][NP]   0 = unknown, 1 = live, >= 2: dead since tick (v - 2) */
+    GS_R_FD_STATE,    /* u8  [N][NP]   0 = unknown, 1 = live (in _live_nodes), 2 = dead (in _dead_nodes,
+                                        time of death in GS_R_FD_TOD) */
     GS_R_TS,          /* u32 [N][NP][KP] tombstone receive tick, GS_NONE for SET entries (GS_TOMBSTONES) */
     GS_R_RING,        /* u16 [N][NP][W] interval ring in ticks (GS_FD_RING) */
     GS_R_POS,         /* u32 [N][NP]   insertion index of owner j in observer o's dict, GS_NONE = absent (general) */
     GS_R_ORD,         /* u32 [N][NP]   owner at insertion index q (general) */
-    GS_R_ROW,         /* u32 [N][4]    {dict size, tombstone-present flag, first tick a dead target of
-                                        this slice is scheduled for deletion, FD-GC-due flag} */
+    GS_R_ROW,         /* u32 [N][4]    {dict size, tombstone-present flag, a lower bound of the first tick a
+                                        dead target of this slice is scheduled for deletion (exact after a
+                                        liveness sweep that found the row due), flags: bit 0 FD-GC due,
+                                        bit 1 the current sweep recomputes word 2} */
     GS_R_LAST_W,      /* u8  [NC][KP]  owner's latest write ordinal per key */
     GS_R_HIST,        /* u64 [NC][C][K] write w of (owner, key): version | meta << 32, where
                                         meta = KeyValueUpdatePb size | status << 16 | value bytes << 18 */
@@ -127,6 +130,8 @@ enum gs_region {
                                         by pass 1 for the packer (the first GS_CAND_CAP of each half) */
     GS_R_CAND_N,      /* u32 [N/2][2][2] stale owners found per exchange, direction and row half (may exceed
                                         GS_CAND_CAP: the packer then walks GS_R_SLICE_BITS for that half) */
+    GS_R_FD_TOD,      /* u32 [N][NP]   time of death (tick) of a GS_R_FD_STATE = 2 pair; read only for rows
+                                        whose word 2 of GS_R_ROW has passed */
     GS_NUM_REGIONS
 };
 
@@ -252,6 +257,20 @@ int gs_phase_chain(gs_handle *h, const int32_t *initiators, const int32_t *respo
                    uint32_t step, const uint32_t *list, uint32_t count, const uint64_t *chain_all, uint64_t *chain,
                    uint64_t *chainc);
 
+/* ---- Multi-GPU: one handle per device, each holding one owner-column
+ * slice; the library drives the sliced phase itself (count, all-gather of the slice totals, packing,
+ * the overflow chain) over an RCCL communicator.  Rank 0 calls gs_comm_id and hands the
+ * GS_COMM_ID_BYTES bytes to every rank (e.g. a torch.distributed broadcast); each rank then calls
+ * gs_comm_init(h, id, n_shards, shard) on its slice (ncclCommInitRank), and gs_run_phase on a sliced
+ * handle runs the whole phase (one blocking host read of the overflow count, as gs_phase_overflow).
+ * gs_run_phase_group: the same phase for all G slices of one cluster held by this process (one device,
+ * one stream; the gathers are device copies) -- the one-GPU rehearsal and test of the same driver. */
+#define GS_COMM_ID_BYTES 128
+int gs_comm_id(void *id);
+int gs_comm_init(gs_handle *h, const void *id, uint32_t nranks, uint32_t rank);
+int gs_run_phase_group(gs_handle *const *handles, uint32_t n_handles, const int32_t *initiators,
+                       const int32_t *responders, uint32_t n, uint32_t tick);
+
 /* _update_node_liveness for every up node (server.py:606-620; failure_detector.py:89-128),
  * including garbage_collect + remove_node (general layout only). */
 int gs_liveness(gs_handle *h, const uint8_t *up, uint32_t tick);
@@ -269,14 +288,24 @@ int gs_phi_row(gs_handle *h, uint32_t observer, uint32_t tick, double *out);
 int gs_check_heartbeat_lag(gs_handle *h);
 
 /* Batched hook events (Cluster.on_key_change / on_node_join / on_node_leave, server.py:217-257).
- * When enabled, every kernel that changes what a hook reports appends 6 x u32 records
- * {observer, owner, key | kind << 8, old version (0 = none), new version, tick} to the DEVICE array
- * records[capacity][6], counting in the DEVICE u32 *count (records beyond capacity are dropped but
- * counted; the caller resets *count).  kind 0 = on_key_change: a kv stored by apply_delta
+ * When enabled, every kernel that changes what a hook reports appends 8 x u32 records
+ * {observer, owner, key | kind << 8, old version (0 = none), new version, tick, seq, 0} to the DEVICE
+ * array records[capacity][8], counting in the DEVICE u32 *count (records beyond capacity are dropped
+ * but counted; the caller resets *count).  kind 0 = on_key_change: a kv stored by apply_delta
  * (state.py:228-231) or an owner set / set_with_ttl (owner deletes mutate the stored value in
  * place and emit nothing, server.py:199-215); 1 = node join, 2 = node leave: the live set of
- * _update_node_liveness against the previous one (server.py:611-616).  Order is unspecified.
- * Exchanges between prefix views take the per-key apply path while enabled.  records = NULL: off. */
+ * _update_node_liveness against the previous one (server.py:611-616).  Records are appended in no
+ * particular order; seq makes the reference's order recoverable:
+ *   owner write:  the write's index among all gs_owner_writes ops since gs_set_events (counting every
+ *                 op of every call, in call order; a write's index within its call is its row in ops);
+ *   apply_delta:  the sender's dict position of the owner (the NodeDelta order of the delta,
+ *                 state.py:346-413); a NodeDelta's kvs are applied in version order;
+ *   join / leave: 0 (the reference iterates Python sets there: no order to reproduce).
+ * So the reference's order (oracle/gen_events_fixture.py) is: by tick; owner writes by seq; in a
+ * phase by exchange (its index in the phase), the initiator's apply (SynAck delta) before the
+ * responder's (Ack delta), then seq, then new version; liveness by observer, joins before leaves,
+ * then owner.  Exchanges between prefix views take the per-key apply path while enabled.
+ * records = NULL: off. */
 int gs_set_events(gs_handle *h, uint32_t *records, uint32_t capacity, uint32_t *count);
 
 /* select_nodes_for_gossip (server.py:656-717) for every up node at round start (server.py:442-469),
@@ -360,6 +389,12 @@ int gs_kernel_times(gs_handle *h, gs_ktimes *out);
 int gs_read_counters(gs_handle *h, gs_counters *out);
 int gs_reset_counters(gs_handle *h);
 int gs_sync(gs_handle *h);
+
+/* Copy-out (blocking, SURVEY §8(b) gs_read_*): observer rows [row_lo, row_hi) of a region indexed by
+ * observer row (GS_R_HB, MV, GC, HELD, FD, FD_STATE, FD_TOD, TS, RING, POS, ORD, ROW) into host memory
+ * `out` of `cap` bytes, in the region's layout; *len = the bytes of those rows (set even when they exceed
+ * cap, which fails).  GS_R_HELD rows are complete: the prefix views' ordinals are materialized first. */
+int gs_read_rows(gs_handle *h, int region, uint32_t row_lo, uint32_t row_hi, void *out, uint64_t cap, uint64_t *len);
 
 #ifdef __cplusplus
 }

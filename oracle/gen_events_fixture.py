@@ -2,9 +2,12 @@
 aiocluster/server.py:217-257, 611-616) per round of golden scenarios, for the event-stream parity tests.
 Build container only (imports /root/reference via refharness).
 
-Output: tests/golden/events_<name>.json.gz = per round the sorted list of
+Output: tests/golden/events_<name>.json.gz = per round the list of
 [observer, owner, key | kind << 8, old version (0 = None), new version, tick], kind 0/1/2 =
-key change / node join / node leave.
+key change / node join / node leave, in the order the reference's hooks were called.  One
+canonicalisation: _update_node_liveness emits its joins, then its leaves, by iterating Python sets
+(server.py:611-614), whose order follows the hash-seeded NodeId hashes and so differs from run to
+run; within each observer's join block and leave block the fixture orders by node index.
 """
 
 from __future__ import annotations
@@ -24,6 +27,20 @@ from refharness import RefSim, dt_tick  # noqa: E402
 from aiocluster_amd.scenario import initial_by_owner, replay_round, scenario_node_ids  # noqa: E402
 
 NAMES = ["trunc8", "fdgc12", "simple3", "cold64"]
+
+
+def canonical_liveness(events):
+    """Each maximal run of join / leave events (one or more consecutive _update_node_liveness calls)
+    ordered by (observer, kind, node); key-change events keep their positions."""
+    out, run = [], []
+    for e in events:
+        if e[2] >> 8:
+            run.append(e)
+            continue
+        out += sorted(run, key=lambda x: (x[0], x[2] >> 8, x[1]))
+        run = []
+        out.append(e)
+    return out + sorted(run, key=lambda x: (x[0], x[2] >> 8, x[1]))
 
 
 def capture(name):
@@ -56,7 +73,7 @@ def capture(name):
     per_round = []
     for r in range(len(scen["rounds"])):
         replay_round(ref, scen, r)
-        per_round.append(sorted(events))
+        per_round.append(canonical_liveness(events))
         events.clear()
     return per_round
 

@@ -594,13 +594,22 @@ int32_t orc_liveness(orc *o, int32_t node, int64_t now) {
     int32_t cnt = b->cnt;
     int32_t *snap = xcalloc(cnt, sizeof(int32_t));
     memcpy(snap, b->order, sizeof(int32_t) * cnt);                   /* nodes() is a tuple */
+    /* live-set changes, emitted joins first, then leaves (server.py:611-616); the reference iterates
+     * Python sets there (hash order), so each group goes out in node-index order */
+    uint8_t *chg = o->ev_on ? xcalloc(o->N, 1) : NULL;
     for (int32_t q = 0; q < cnt; q++)
         if (snap[q] != node) {
             const int32_t j = snap[q];
             const int was = b->live[j];
             fd_update(o, b, j, now);
-            if (b->live[j] != was) emit(o, node, j, (b->live[j] ? 1 : 2) << 8, 0u, 0u, now); /* 611-616 */
+            if (chg && b->live[j] != was) chg[j] = b->live[j] ? 1 : 2;
         }
+    if (chg) {
+        for (int kind = 1; kind <= 2; kind++)
+            for (int32_t j = 0; j < o->N; j++)
+                if (chg[j] == kind) emit(o, node, j, kind << 8, 0u, 0u, now);
+        free(chg);
+    }
     free(snap);
     /* FailureDetector.garbage_collect (108-119) */
     int32_t *res = xcalloc(b->ndead + 1, sizeof(int32_t));

@@ -194,14 +194,15 @@ class OracleSim:
         self.L.orc_enable_events(self.h, 1)
 
     def drain_events(self) -> np.ndarray:
-        """Events since the last drain in the device's format (times in ticks), sorted."""
+        """Events since the last drain in the device's format (times in ticks), in the reference's order
+        (the oracle runs the reference's calls one at a time; join / leave in node order, see
+        gossip_oracle.c orc_liveness)."""
         buf = np.zeros((1 << 22, 6), dtype=np.int64)
         n = self.L.orc_drain_events(self.h, buf.ctypes.data_as(C.c_void_p), buf.shape[0])
         assert n <= buf.shape[0]
         ev = buf[:n].copy()
         ev[:, 5] //= TICK_US
-        ev = ev.astype(np.uint32)
-        return ev[np.lexsort(ev.T[::-1])]
+        return ev.astype(np.uint32)
 
     def stats(self) -> dict:
         s = _Stats()

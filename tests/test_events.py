@@ -62,3 +62,71 @@ def test_device_events_prefix_views():
     scen = load_scenario("fdgc12")
     kinds = _check(make_backend(GossipSim, scen, tombstones=False), "fdgc12")
     assert {0, 1, 2} <= kinds
+
+
+class _SeqRecorder:
+    """Proxies an OracleSim and turns its (reference-ordered) events into device-format records
+    (gs_set_events: 8 words, seq as the device computes it) call by call."""
+
+    def __init__(self, orc):
+        self.orc, self.recs, self.phases, self.writes = orc, [], {}, 0
+
+    def _take(self, seq_of):
+        for e in self.orc.drain_events().astype(np.int64).tolist():
+            self.recs.append(e + [seq_of(e), 0])
+
+    def write(self, t, j, k, op, v):
+        self.orc.write(t, j, k, op, v)
+
+    def begin_round(self, t, up):
+        w0 = self.writes
+
+        def seq(e):  # the write's index among all writes (call order)
+            nonlocal w0
+            w0 += 1
+            return w0 - 1
+
+        self.orc.begin_round(t, up)  # flushes the writes
+        self._take(seq)
+        self.writes = w0
+
+    def run_phase(self, t, pairs):
+        self.orc.run_phase(t, pairs)
+        peer = {}
+        for a, b in pairs:
+            peer[a], peer[b] = b, a
+        self.phases[t] = ([a for a, _ in pairs], [b for _, b in pairs])
+        order = {}
+
+        def seq(e):  # the sender's dict position of the owner
+            s = peer[e[0]]
+            if s not in order:
+                order[s] = {j: q for q, j in enumerate(self.orc.order(s))}
+            return order[s][e[1]]
+
+        self._take(seq)
+
+    def liveness(self, t, up, r):
+        self.orc.liveness(t, up, r)
+        self._take(lambda e: 0)
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_order_events_restores_reference_order(name):
+    """aiocluster_amd.sim.order_events (the device stream's host-side order) puts shuffled records,
+    carrying the seq words the kernels write, back into the reference's hook order."""
+    from aiocluster_amd.sim import order_events
+
+    scen = load_scenario(name)
+    rec = _SeqRecorder(make_backend(OracleSim, scen))
+    rec.orc.enable_events()
+    want = golden_events(name)
+    rng = np.random.default_rng(7)
+    for r in range(len(scen["rounds"])):
+        rec.recs, rec.phases = [], {}
+        replay_round(rec, scen, r)
+        ev = np.asarray(rec.recs, dtype=np.int64).reshape(-1, 8)
+        assert ev[:, :6].tolist() == want[r]
+        shuf = ev[rng.permutation(len(ev))].astype(np.uint32)
+        got = shuf[order_events(shuf, rec.orc.n, rec.phases, list(range(rec.writes)))]
+        assert got[:, :6].astype(np.int64).tolist() == want[r], f"{name} round {r}"

@@ -142,6 +142,16 @@ def test_config2_cold_1024x64_converges_bit_exact():
     assert np.all(ex["mv"] == owner_mv[None, :]), "version matrix did not converge"
 
 
+def test_config2_matches_reference_digests():
+    """BASELINE config 2 (1,024 x 64, cold) against the REAL reference: per-round SHA-256 of every export
+    field and the final max_version matrix (tests/golden/scen_config2.json.gz, the rounds it pins)."""
+    from test_oracle_golden import replay_digests
+
+    scen = load_scenario("config2")
+    for tomb in (True, False):  # tombstone layout and prefix views
+        replay_digests(make_backend(GossipSim, scen, tombstones=tomb, fd_ring=False), scen)
+
+
 def test_config5_partition_heal_small_vs_oracle():
     """BASELINE config 5 in miniature: MTU-truncated deltas, deletes + tombstone GC, a partition into
     halves that heals; every round vs the oracle, and the device's failure-detector census (false-

@@ -47,6 +47,55 @@ def test_slices_match_single_handle(n, G, mtu, tomb):
     assert np.array_equal(grp.phi_row(o), one.phi_row(o), equal_nan=True)
 
 
+@pytest.mark.parametrize("n,G,mtu", [(256, 2, 1800), (384, 3, 3000), (512, 4, 1200)])
+def test_native_group_matches_single_handle(n, G, mtu):
+    """The library-driven sliced phase (gs_run_phase_group: the driver gs_run_phase runs over RCCL after
+    gs_comm_init, with device-copy gathers) vs one handle, MTU cuts across slices included."""
+    spec = WorkloadSpec(n=n, k=8, fanout=3, seed=n * G, init="warm", write_frac=0.3, delete_frac=0.1,
+                        ttl_frac=0.05, down_frac=0.05, down_rounds=2)
+    scen = make_scenario(f"native{n}x{G}", spec, 8, {"mtu": mtu, "tombstone_grace_s": 2})
+    kw = dict(tombstones=True, fd_ring=False)
+    one = make_backend(GossipSim, scen, **kw)
+    grp = sharded(scen, G, native=True, **kw)
+    for r in range(len(scen["rounds"])):
+        replay_round(one, scen, r)
+        replay_round(grp, scen, r)
+        diff = compare_exports(grp.export(), one.export())
+        assert diff is None, f"round {r}: {diff}"
+    c1, cg = one.check(), grp.check()
+    for k in ("exchanges", "hb_reports", "node_deltas", "kvs_sent", "truncated", "delta_bytes", "hb_writes"):
+        assert cg[k] == c1[k], (k, cg[k], c1[k])
+    assert c1["truncated"] > 0
+
+
+def test_read_rows_copies_out_regions():
+    """gs_read_rows (blocking copy-out of observer rows) returns the bytes of the bound regions, and
+    complete HELD rows for prefix views (materialized first)."""
+    import torch
+
+    from aiocluster_amd import _lib
+
+    spec = WorkloadSpec(n=160, k=8, fanout=3, seed=3, init="warm", write_frac=0.3, down_frac=0.05, down_rounds=2)
+    scen = make_scenario("rows160", spec, 6, {"mtu": 1500})
+    sim = make_backend(GossipSim, scen, tombstones=False, fd_ring=False)
+    for r in range(len(scen["rounds"])):
+        replay_round(sim, scen, r)
+    lo, hi = 17, 45
+    for name, dt in (("HB", torch.int16), ("MV", torch.int16), ("FD", torch.int64), ("FD_STATE", torch.uint8),
+                     ("FD_TOD", torch.int32), ("ROW", torch.int32)):
+        got = sim.read_rows(name, lo, hi)
+        t = sim.regions[name]
+        rb = t.numel() * t.element_size() // sim.n
+        want = t.view(torch.uint8).reshape(sim.n, rb)[lo:hi].cpu().numpy().tobytes()
+        assert got == want, name
+    held = np.frombuffer(sim.read_rows("HELD", lo, hi), np.uint8).reshape(hi - lo, sim.np_, sim.kp)
+    g = sim._host(list(range(lo, hi)))
+    assert np.array_equal(held, g["HELD"])
+    assert held.any()
+    with pytest.raises(_lib.GsError):
+        sim.read_rows("HIST", 0, 1)  # indexed by owner, not observer row
+
+
 def test_slices_match_oracle_with_ring():
     spec = WorkloadSpec(n=192, k=16, fanout=3, seed=5, init="warm", write_frac=0.2, delete_frac=0.1,
                         down_frac=0.1, down_rounds=3)
