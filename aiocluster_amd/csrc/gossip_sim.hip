@@ -88,7 +88,7 @@ struct Dev {
     uint32_t *pos, *ord, *row;
     uint8_t *last_w;
     uint64_t *hist;  // version | meta << 32
-    uint64_t *lat;   // [NC][KP] copy of each key's latest HIST entry (prefix views, no GS_TOMBSTONES)
+    uint32_t *lat;   // [NC][KP] each key's latest write: version | DeltaPb bytes of its kv << 16 (prefix views)
     uint32_t *hist_vid;
     uint16_t *nid_size;
     uint8_t *key_len;
@@ -276,14 +276,16 @@ __device__ __forceinline__ void eval_cand(const Dev &d, uint32_t s, uint32_t r, 
     const bool gct = (d.flags & GS_TOMBSTONES) != 0;
     // prefix views: the owner's latest write of every key is loaded with round trip 1, before it is
     // known whether the sender's view is a prefix, so a prefix sender costs one round trip, not two
-    uint64_t lat[4 * KW];
+    uint32_t lat[4 * KW];
     if (!gct) {
-        const ulonglong2 *lp = reinterpret_cast<const ulonglong2 *>(d.lat + (size_t)j * d.KP);
+        const uint4 *lp = reinterpret_cast<const uint4 *>(d.lat + (size_t)j * d.KP);
 #pragma unroll
-        for (int q = 0; q < 2 * KW; q++) {
-            const ulonglong2 v = (uint32_t)(2 * q) < d.KP ? lp[q] : make_ulonglong2(0ull, 0ull);
-            lat[2 * q] = v.x;
-            lat[2 * q + 1] = v.y;
+        for (int q = 0; q < KW; q++) {
+            const uint4 v = (uint32_t)q < kw ? lp[q] : make_uint4(0u, 0u, 0u, 0u);
+            lat[4 * q] = v.x;
+            lat[4 * q + 1] = v.y;
+            lat[4 * q + 2] = v.z;
+            lat[4 * q + 3] = v.w;
         }
     }
     const uint32_t msw = HAVE_MV ? (mvw & 0xFFFFu) : d.mv[ps], mrw = HAVE_MV ? (mvw >> 16) : d.mv[pr];
@@ -316,18 +318,22 @@ __device__ __forceinline__ void eval_cand(const Dev &d, uint32_t s, uint32_t r, 
             c.km[q] = 0u;
             uint32_t w = byte_of(c.hs, q);
             if (!w || (uint32_t)q >= d.K) continue;
-            uint64_t e = lat[q];  // counted below only for the kvs sent
-            if ((uint32_t)e > ms) {
+            const uint32_t e32 = lat[q];  // counted below only for the kvs sent
+            if ((e32 & 0xFFFFu) > ms) {
+                uint64_t e = 0;
                 do {
                     w--;
                     if (w) { e = d.hist[hix(d, j, w, q)]; alg += 8; }
                 } while (w && (uint32_t)e > ms);
                 set_byte(c.hs, q, w);
                 if (!w) continue;
+                const uint32_t meta = (uint32_t)(e >> 32);
+                c.ver[q] = (uint32_t)e;
+                c.km[q] = msgf(meta_kvlen(meta)) | (meta_status(meta) << 16);
+            } else {  // the latest write (a prefix view: status SET)
+                c.ver[q] = e32 & 0xFFFFu;
+                c.km[q] = e32 >> 16;
             }
-            const uint32_t meta = (uint32_t)(e >> 32);
-            c.ver[q] = (uint32_t)e;
-            c.km[q] = msgf(meta_kvlen(meta)) | (meta_status(meta) << 16);
         }
     } else {
         // round trip 2: the sender's kv history entries.  Every version a view holds is <= its
@@ -360,7 +366,7 @@ __device__ __forceinline__ void eval_cand(const Dev &d, uint32_t s, uint32_t r, 
             if (c.ver[q] < minv) { minv = c.ver[q]; minkv = kvm; }
         }
     }
-    if (sx) alg += 8 * nk;  // the history entries of the NodeDelta's kvs
+    if (sx) alg += 4 * nk;  // the latest-write words of the NodeDelta's kvs
     c.j = j;
     c.from = from;
     c.gs = gs;
@@ -782,25 +788,46 @@ __device__ __forceinline__ uint32_t sched4(const Dev &d, size_t p, uint32_t t) {
         m |= (uint32_t)(((s4 >> (8 * i)) & 0xFFu) == FD_DEAD && is_sched(td[i], t, d.sched_delay)) << i;
     return m;
 }
+// One group's loads as they arrive (packed u16 pairs, not yet decoded): the loop keeps the next group in
+// this form while the current one computes, so nothing waits on the prefetch until it is decoded one
+// iteration later (and the packed form holds 12 VGPRs instead of 20).
+struct GrpRaw {
+    uint4 R;
+    uint2 hA, hB, mA, mB;
+    uint4 pA, pB;
+    uint32_t sA, sB;
+};
 template <bool GENM>
 __device__ __forceinline__ void load_grp(const Dev &d, size_t ra, size_t rb, uint32_t c0, uint32_t t, bool schA,
-                                         bool schB, Grp &g) {
-    uint32_t R[4];
-    ld4(d.self_hb + c0, R);
-    ld4h(d.hb + ra + c0, g.hA);
-    ld4h(d.hb + rb + c0, g.hB);
-#pragma unroll
-    for (int i = 0; i < 4; i++) { g.hA[i] = hb_dec(g.hA[i], R[i]); g.hB[i] = hb_dec(g.hB[i], R[i]); }
-    ld4h(d.mv + ra + c0, g.mA);
-    ld4h(d.mv + rb + c0, g.mB);
-    // raw max_version words (prefix-view flag included): pass 1 masks them where it compares, and the
-    // split path hands them to the packer in its candidate records
-#pragma unroll
-    for (int i = 0; i < 4; i++) { g.pA[i] = g.pB[i] = 0u; }
+                                         bool schB, GrpRaw &g) {
+    g.R = *reinterpret_cast<const uint4 *>(d.self_hb + c0);
+    g.hA = *reinterpret_cast<const uint2 *>(d.hb + ra + c0);
+    g.hB = *reinterpret_cast<const uint2 *>(d.hb + rb + c0);
+    g.mA = *reinterpret_cast<const uint2 *>(d.mv + ra + c0);
+    g.mB = *reinterpret_cast<const uint2 *>(d.mv + rb + c0);
+    g.pA = g.pB = make_uint4(0u, 0u, 0u, 0u);
     g.sA = g.sB = 0u;
-    if (GENM) { ld4(d.pos + ra + c0, g.pA); ld4(d.pos + rb + c0, g.pB); }
+    if (GENM) {
+        g.pA = *reinterpret_cast<const uint4 *>(d.pos + ra + c0);
+        g.pB = *reinterpret_cast<const uint4 *>(d.pos + rb + c0);
+    }
     if (schA) g.sA = sched4(d, ra + c0, t);
     if (schB) g.sB = sched4(d, rb + c0, t);
+}
+// decode: heartbeats against the owners' own (hb_dec); raw max_version words (prefix-view flag included):
+// pass 1 masks them where it compares, and the split path hands them to the packer in its records
+__device__ __forceinline__ void dec_grp(const GrpRaw &r, Grp &g) {
+    const uint32_t R[4] = {r.R.x, r.R.y, r.R.z, r.R.w};
+    const uint32_t hA[4] = {r.hA.x & 0xFFFFu, r.hA.x >> 16, r.hA.y & 0xFFFFu, r.hA.y >> 16};
+    const uint32_t hB[4] = {r.hB.x & 0xFFFFu, r.hB.x >> 16, r.hB.y & 0xFFFFu, r.hB.y >> 16};
+#pragma unroll
+    for (int i = 0; i < 4; i++) { g.hA[i] = hb_dec(hA[i], R[i]); g.hB[i] = hb_dec(hB[i], R[i]); }
+    g.mA[0] = r.mA.x & 0xFFFFu; g.mA[1] = r.mA.x >> 16; g.mA[2] = r.mA.y & 0xFFFFu; g.mA[3] = r.mA.y >> 16;
+    g.mB[0] = r.mB.x & 0xFFFFu; g.mB[1] = r.mB.x >> 16; g.mB[2] = r.mB.y & 0xFFFFu; g.mB[3] = r.mB.y >> 16;
+    g.pA[0] = r.pA.x; g.pA[1] = r.pA.y; g.pA[2] = r.pA.z; g.pA[3] = r.pA.w;
+    g.pB[0] = r.pB.x; g.pB[1] = r.pB.y; g.pB[2] = r.pB.z; g.pB[3] = r.pB.w;
+    g.sA = r.sA;
+    g.sB = r.sB;
 }
 
 // FailureDetector.report_heartbeat -> SamplingWindow.report_heartbeat on one unpacked window
@@ -1033,11 +1060,13 @@ __global__ __launch_bounds__(XB, (KW == 4 ? P1_WAVES : 1)) void k_pass1(Dev d, c
     auto loop = [&](auto sch) {
         constexpr bool SCH = decltype(sch)::value;
         uint32_t c0 = c0s;
-        Grp g0, g1;
-        if (c0 < hi) load_grp<false>(d, ra, rb, c0, t, SCH && schA, SCH && schB, g0);
+        GrpRaw r0, r1;
+        if (c0 < hi) load_grp<false>(d, ra, rb, c0, t, SCH && schA, SCH && schB, r0);
         while (c0 < hi) {
             const uint32_t c1 = c0 + WAVE * 4u;
-            if (c1 < hi) load_grp<false>(d, ra, rb, c1, t, SCH && schA, SCH && schB, g1);
+            if (c1 < hi) load_grp<false>(d, ra, rb, c1, t, SCH && schA, SCH && schB, r1);
+            Grp g0;
+            dec_grp(r0, g0);
             uint32_t rmA, rmB, nBA, nAB, nNB, nNA;
             const uint32_t mA[4] = {g0.mA[0], g0.mA[1], g0.mA[2], g0.mA[3]};
             const uint32_t mB[4] = {g0.mB[0], g0.mB[1], g0.mB[2], g0.mB[3]};
@@ -1048,7 +1077,7 @@ __global__ __launch_bounds__(XB, (KW == 4 ? P1_WAVES : 1)) void k_pass1(Dev d, c
             store_plane(planeB, c0, rmB, alg);
             emit_dir(gBA, LBA, nBAc, c0, nBA, mB, mA, alg);  // b -> a: sender b, receiver a
             emit_dir(gAB, LAB, nABc, c0, nAB, mA, mB, alg);
-            g0 = g1;
+            r0 = r1;
             c0 = c1;
         }
     };
@@ -1142,11 +1171,13 @@ __global__ __launch_bounds__(XB, (KW == 4 ? XB_WAVES : 1)) void k_exchange(Dev d
     // software-pipelined: the next group's loads are in flight while this group computes and stores
     // (different owners, so the early loads never read a location this group writes)
     uint32_t c0 = (uint32_t)tid * 4u;
-    Grp g0, g1;
-    if (c0 < d.ncol) load_grp<GENM>(d, ra, rb, c0, t, schA, schB, g0);
+    GrpRaw r0, r1;
+    if (c0 < d.ncol) load_grp<GENM>(d, ra, rb, c0, t, schA, schB, r0);
     while (c0 < d.ncol) {
         const uint32_t c1 = c0 + XB * 4u;
-        if (c1 < d.ncol) load_grp<GENM>(d, ra, rb, c1, t, schA, schB, g1);
+        if (c1 < d.ncol) load_grp<GENM>(d, ra, rb, c1, t, schA, schB, r1);
+        Grp g0;
+        dec_grp(r0, g0);
         uint32_t rmA, rmB, nBA, nAB, nNB, nNA;
         pass1_grp<GENM>(d, ra, rb, c0, a, b, t, schA, schB, g0, nBA, nAB, nNB, nNA, alg, reports, hbw, rmA, rmB);
         // one LDS atomic per lane and bitmap (4 consecutive columns sit in one word); stale owners are sparse
@@ -1159,7 +1190,7 @@ __global__ __launch_bounds__(XB, (KW == 4 ? XB_WAVES : 1)) void k_exchange(Dev d
             store_plane(planeA, c0, rmA, alg);
             store_plane(planeB, c0, rmB, alg);
         }
-        g0 = g1;
+        r0 = r1;
         c0 = c1;
     }
     // no static LDS: the 20 KB of dynamic LDS per workgroup (N = 65,536, canonical) then fits 8
@@ -1831,7 +1862,7 @@ __global__ __launch_bounds__(LB) void k_owner_writes(Dev d, const gs_write *ops,
     d.hist[h] = (uint64_t)ver |
                 ((uint64_t)make_meta(sfield(d.key_len[k]) + sfield(vl) + ufield(ver) + ufield(st), st, vl) << 32);
     d.hist_vid[h] = vid;
-    if (d.lat) d.lat[(size_t)j * d.KP + k] = d.hist[h];
+    if (d.lat) d.lat[(size_t)j * d.KP + k] = ver | (msgf(meta_kvlen((uint32_t)(d.hist[h] >> 32))) << 16);
     d.last_w[(size_t)j * d.KP + k] = (uint8_t)nw;
     *held = (uint8_t)nw;
     d.mv[pj] = (uint16_t)ver;
@@ -2489,7 +2520,7 @@ int check_bound(gs_handle *h) {
     d.row = (uint32_t *)h->reg[GS_R_ROW];
     d.last_w = (uint8_t *)h->reg[GS_R_LAST_W];
     d.hist = (uint64_t *)h->reg[GS_R_HIST];
-    d.lat = (uint64_t *)h->reg[GS_R_LATEST];
+    d.lat = (uint32_t *)h->reg[GS_R_LATEST];
     d.hist_vid = (uint32_t *)h->reg[GS_R_HIST_VID];
     d.nid_size = (uint16_t *)h->reg[GS_R_NID_SIZE];
     d.key_len = (uint8_t *)h->reg[GS_R_KEY_LEN];
@@ -2655,7 +2686,7 @@ int gs_create(const gs_config *cfg, gs_handle **out) {
     b[GS_R_LAST_W] = NC * KP;
     b[GS_R_HIST] = NC * C * K * 8;
     b[GS_R_HIST_VID] = NC * C * K * 4;
-    b[GS_R_LATEST] = (c.flags & GS_TOMBSTONES) ? 0 : NC * KP * 8;
+    b[GS_R_LATEST] = (c.flags & GS_TOMBSTONES) ? 0 : NC * KP * 4;
     b[GS_R_NID_SIZE] = NP * 2;
     b[GS_R_KEY_LEN] = KP;
     b[GS_R_STAMP] = NR * 4;

@@ -122,7 +122,8 @@ enum gs_region {
                                         replayed into GS_R_FD by gs_liveness */
     GS_R_PEND_STAMP,  /* u32 [N][16]   tick of the phase that last wrote plane row (o, p): the row is
                                         valid for the current round only if it equals round tick + 1 + p */
-    GS_R_LATEST,      /* u64 [NC][KP]  the HIST entry of each key's latest write (no GS_TOMBSTONES only) */
+    GS_R_LATEST,      /* u32 [NC][KP]  each key's latest write: version | DeltaPb bytes of its KeyValueUpdatePb
+                                        field << 16 (no GS_TOMBSTONES only: versions <= 16,256, values < 16 KiB) */
     GS_R_SELF_HB,     /* u32 [NP]      each owner column's own heartbeat (the diagonal of GS_R_HB, full width) */
     GS_R_CAND,        /* u64 [N/2][2][2][GS_CAND_CAP] canonical one-slice phases: each exchange's stale owners
                                         per direction and row half, in column order, as {local column,
