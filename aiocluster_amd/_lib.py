@@ -51,7 +51,7 @@ def fd_sum_bits(window: int) -> int:
 REGIONS = [
     "HB", "MV", "GC", "HELD", "FD", "FD_STATE", "TS", "RING", "POS", "ORD", "ROW",
     "LAST_W", "HIST", "HIST_VID", "NID_SIZE", "KEY_LEN", "STAMP", "COUNTERS", "SLICE_BITS", "PEND", "PEND_STAMP", "LATEST",
-    "SELF_HB", "CAND", "CAND_N", "FD_TOD",
+    "SELF_HB", "CAND", "CAND_N", "FD_TOD", "FD_LAST",
 ]
 REGION = {n: i for i, n in enumerate(REGIONS)}
 
@@ -71,6 +71,7 @@ EXPORTS = [
     "gs_select_peers", "gs_schedule_phases", "gs_set_events", "gs_emit_scratch_bytes", "gs_emit_digest", "gs_emit_delta",
     "gs_check_heartbeat_lag", "gs_stream_copy", "gs_stream_read", "gs_stream_write", "gs_set_timing", "gs_kernel_times",
     "gs_phase_overflow", "gs_phase_chain", "gs_comm_id", "gs_comm_init", "gs_run_phase_group", "gs_read_rows",
+    "gs_latest_tick",
 ]
 
 API_VERSION = 10
@@ -172,6 +173,7 @@ def load():
         "gs_comm_init": (C.c_int, [P, P, u32, u32]),
         "gs_run_phase_group": (C.c_int, [P, u32, P, P, u32, u32]),
         "gs_read_rows": (C.c_int, [P, C.c_int, u32, u32, P, u64, C.POINTER(u64)]),
+        "gs_latest_tick": (C.c_int, [P, C.POINTER(u32)]),
         "gs_kernel_times": (C.c_int, [P, C.POINTER(GsKtimes)]),
         "gs_sync": (C.c_int, [P]),
         "gs_shard_columns": (C.c_int, [P, C.POINTER(u32), C.POINTER(u32)]),

@@ -75,13 +75,15 @@ struct Dev {
     uint32_t max_iv, tomb_grace, dead_grace, sched_delay, lb_min, sum_bits;
     uint32_t ablate;  // profiling only (env GS_ABLATE): 1 = skip packing, 2 = skip pass-1 stores; results invalid
     double phi_thr, prior5;
+    double prior5t;  // prior5 in ticks (x 64): the liveness sweep's division-free phi test
     uint16_t *hb;       // heartbeat mod 2^16 (hb_dec: exact while a view lags its owner by < 2^16)
     uint32_t *self_hb;  // [NP] each owner column's own heartbeat, full width
     uint32_t *gc;
     uint16_t *mv;  // max_version | MV_INEXACT (u16: versions <= K * (C - 1) <= 16,256)
     uint8_t *held;
-    uint64_t *fd;  // sampling window: (last tick + 1) | (sum | cnt << sum_bits) << 32; 0 = no window
-    uint8_t *fd_state;  // 0 unknown, 1 live, 2 dead (FailureDetector._live_nodes / _dead_nodes)
+    uint32_t *fd;       // sampling window: _sum in ticks | intervals appended since the last reset << sum_bits
+    uint16_t *fd_last;  // _last_heartbeat tick mod 2^16 (decoded against the operation's tick: fd_get)
+    uint8_t *fd_state;  // bits 0-1: 0 unknown, 1 live, 2 dead (_live_nodes / _dead_nodes); FD_WIN, FD_OLD
     uint32_t *tod;      // time of death of a dead pair (read only for rows whose row word 2 has passed)
     uint32_t *ts;
     uint16_t *ring;
@@ -140,22 +142,33 @@ __device__ inline uint32_t make_meta(uint32_t kvlen, uint32_t status, uint32_t v
 __device__ inline bool is_sched(uint32_t dt, uint32_t t, uint32_t delay) {
     return dt != NONE && (t - dt) >= delay;
 }
-enum FdSt { FD_UNKNOWN = 0, FD_LIVE = 1, FD_DEAD = 2 };
-__device__ inline uint32_t dead_tod(const Dev &d, size_t p) { return d.fd_state[p] == FD_DEAD ? d.tod[p] : NONE; }
+// FD_STATE byte: membership in bits 0-1 (FD_MEMB), FD_WIN = the pair has a sampling window (its
+// _last_heartbeat is set), FD_OLD = that last report is >= FD_OLD_AGE ticks old (k_fd_age)
+enum FdSt { FD_UNKNOWN = 0, FD_LIVE = 1, FD_DEAD = 2, FD_MEMB = 3, FD_WIN = 4, FD_OLD = 8 };
+constexpr uint32_t FD_OLD_AGE = 1u << 15;
+__device__ inline uint32_t dead_tod(const Dev &d, size_t p) {
+    return (d.fd_state[p] & FD_MEMB) == FD_DEAD ? d.tod[p] : NONE;
+}
 
-// One sampling window (SamplingWindow + BoundedArrayStats, failure_detector.py:12-53, 131-162) per
-// pair in 8 bytes: low word = _last_heartbeat tick + 1 (0 = no window), high word = _sum in ticks
-// (sum_bits wide, exact: every interval is a whole number of 1/64 s) | intervals appended since the
-// last reset << sum_bits.
+// One sampling window (SamplingWindow + BoundedArrayStats, failure_detector.py:12-53, 131-162) per pair
+// in 6 bytes + 2 state bits: the _last_heartbeat tick mod 2^16 (GS_R_FD_LAST) and one word (GS_R_FD) =
+// _sum in ticks (sum_bits wide, exact: every interval is a whole number of 1/64 s) | intervals appended
+// since the last reset << sum_bits.  Decoding the tick against the operation's tick t is exact while the
+// report is < 2^16 ticks old; k_fd_age marks windows FD_OLD once it is 2^15 old (the host runs it at
+// least every 2^14 ticks), and an FD_OLD window's tick only ever enters as "more than max_interval
+// ago" (no interval appended, gs_create: max_interval < 2^14) and "phi above the threshold" (gs_create:
+// threshold x max(max_interval, prior) < 2^15), so it is decoded as t - 2^15.
 struct Fd {
     uint32_t last, sum, cnt;  // last = NONE when there is no window
 };
-__device__ inline Fd fd_unpack(const Dev &d, uint64_t v) {
-    const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
-    return Fd{lo - 1u, hi & ((1u << d.sum_bits) - 1u), hi >> d.sum_bits};
+__device__ inline Fd fd_get(const Dev &d, uint32_t st, uint32_t l16, uint32_t sc, uint32_t t) {
+    const uint32_t last = !(st & FD_WIN) ? NONE : (st & FD_OLD) ? t - FD_OLD_AGE : t - ((t - l16) & 0xFFFFu);
+    return Fd{last, sc & ((1u << d.sum_bits) - 1u), sc >> d.sum_bits};
 }
-__device__ inline uint64_t fd_pack(const Dev &d, Fd f) {
-    return (uint64_t)(f.last + 1u) | ((uint64_t)(f.sum | (f.cnt << d.sum_bits)) << 32);
+__device__ inline uint32_t fd_sc(const Dev &d, const Fd &f) { return f.sum | (f.cnt << d.sum_bits); }
+// the state byte after storing f (a window from its first report on; its tick is current again)
+__device__ inline uint32_t fd_st(uint32_t st, const Fd &f) {
+    return f.last == NONE ? (st & ~(uint32_t)(FD_WIN | FD_OLD)) : ((st | FD_WIN) & ~(uint32_t)FD_OLD);
 }
 
 __device__ inline int lane_id() { return (int)__lane_id(); }
@@ -785,7 +798,7 @@ __device__ __forceinline__ uint32_t sched4(const Dev &d, size_t p, uint32_t t) {
     uint32_t m = 0u;
 #pragma unroll
     for (int i = 0; i < 4; i++)
-        m |= (uint32_t)(((s4 >> (8 * i)) & 0xFFu) == FD_DEAD && is_sched(td[i], t, d.sched_delay)) << i;
+        m |= (uint32_t)(((s4 >> (8 * i)) & FD_MEMB) == FD_DEAD && is_sched(td[i], t, d.sched_delay)) << i;
     return m;
 }
 // One group's loads as they arrive (packed u16 pairs, not yet decoded): the loop keeps the next group in
@@ -1010,6 +1023,9 @@ __device__ inline PackState chain_unpack(uint64_t v) {
 #ifndef P1_WAVES
 #define P1_WAVES 4
 #endif
+#ifndef P1_AHEAD
+#define P1_AHEAD 1  // pass-1 groups loaded ahead of the one being computed (1 or 2: 2 measured slower, r2o)
+#endif
 // FUSE: the same workgroup then packs and applies both directions from the records (wave 0: b -> a,
 // wave 1: a -> b) right after streaming the rows, while the receivers' max_version lines are still in L2
 // (the applies are one scattered 2-byte store per NodeDelta; tools/membench.hip prices those at 25 G/s
@@ -1060,11 +1076,18 @@ __global__ __launch_bounds__(XB, (KW == 4 ? P1_WAVES : 1)) void k_pass1(Dev d, c
     auto loop = [&](auto sch) {
         constexpr bool SCH = decltype(sch)::value;
         uint32_t c0 = c0s;
-        GrpRaw r0, r1;
+        // P1_AHEAD groups in flight ahead of the one being computed
+        GrpRaw r0, r1, r2;
+        constexpr uint32_t STEP = WAVE * 4u;
         if (c0 < hi) load_grp<false>(d, ra, rb, c0, t, SCH && schA, SCH && schB, r0);
+        if (P1_AHEAD > 1 && c0 + STEP < hi) load_grp<false>(d, ra, rb, c0 + STEP, t, SCH && schA, SCH && schB, r1);
         while (c0 < hi) {
-            const uint32_t c1 = c0 + WAVE * 4u;
-            if (c1 < hi) load_grp<false>(d, ra, rb, c1, t, SCH && schA, SCH && schB, r1);
+            const uint32_t c1 = c0 + STEP;
+            if (P1_AHEAD > 1) {
+                if (c1 + STEP < hi) load_grp<false>(d, ra, rb, c1 + STEP, t, SCH && schA, SCH && schB, r2);
+            } else if (c1 < hi) {
+                load_grp<false>(d, ra, rb, c1, t, SCH && schA, SCH && schB, r1);
+            }
             Grp g0;
             dec_grp(r0, g0);
             uint32_t rmA, rmB, nBA, nAB, nNB, nNA;
@@ -1078,6 +1101,7 @@ __global__ __launch_bounds__(XB, (KW == 4 ? P1_WAVES : 1)) void k_pass1(Dev d, c
             emit_dir(gBA, LBA, nBAc, c0, nBA, mB, mA, alg);  // b -> a: sender b, receiver a
             emit_dir(gAB, LAB, nABc, c0, nAB, mA, mB, alg);
             r0 = r1;
+            if (P1_AHEAD > 1) r1 = r2;
             c0 = c1;
         }
     };
@@ -1540,7 +1564,9 @@ template <bool RING>
 // more than 16 ticks after its plane base: the planes are emptied mid-round)
 __global__ __launch_bounds__(LB) void k_liveness(Dev d, const uint8_t *up, uint32_t t, uint32_t chunks,
                                                  uint32_t per, bool replay, bool decide) {
-    __shared__ uint64_t s_pl[16][16];  // [phase][the 16 plane words of this chunk's 1024 columns]
+    // [wave][phase][the wave's 4 plane words of this chunk]: each wave stages and reads only its own
+    // words (lane l: phase l / 4, word l % 4), so the chunks need no workgroup barrier
+    __shared__ uint64_t s_pl[LB / WAVE][16][4];
     __shared__ uint32_t s_vm;
     const uint32_t groups = (chunks + per - 1) / per;
     const uint32_t o = blockIdx.x / groups, cb0 = (blockIdx.x % groups) * per;
@@ -1561,86 +1587,106 @@ __global__ __launch_bounds__(LB) void k_liveness(Dev d, const uint8_t *up, uint3
     for (uint32_t cb = cb0; cb < cb1; cb++) {
     // this chunk's windows and states are loaded before the plane staging (they do not depend on
     // it), so the two global round trips of a chunk overlap; a down row has no valid planes (its
-    // node was in no exchange), so it loads windows only for up observers, as before
+    // node was in no exchange), so it loads windows only for up observers
     const uint32_t c0 = (cb * LB + threadIdx.x) * 4u;
-    uint64_t w[4] = {0ull, 0ull, 0ull, 0ull};
-    uint32_t s4 = 0u, ps[4] = {0u, 0u, 0u, 0u};  // s4: the four pairs' states, one byte each
+    uint4 sc4 = make_uint4(0u, 0u, 0u, 0u);  // the four windows' sum | cnt words
+    uint2 l4 = make_uint2(0u, 0u);           // ... and their last-report ticks, u16 pairs
+    uint32_t s4 = 0u, ps[4] = {0u, 0u, 0u, 0u};  // s4: the four pairs' state bytes
     if (c0 < d.ncol) {
         const size_t p = pix(d, o, c0);
-        if (upo || vm) ld4w(d.fd + p, w);
-        if (upo) s4 = *reinterpret_cast<const uint32_t *>(d.fd_state + p);
+        if (upo || vm) {
+            sc4 = *reinterpret_cast<const uint4 *>(d.fd + p);
+            l4 = *reinterpret_cast<const uint2 *>(d.fd_last + p);
+            s4 = *reinterpret_cast<const uint32_t *>(d.fd_state + p);
+        }
         if (upo && genm) ld4(d.pos + p, ps);
     }
+    const uint32_t wv = threadIdx.x >> 6, ln = threadIdx.x & 63u;
     if (vm) {
-        if (cb != cb0) __syncthreads();  // every thread is done with the previous chunk's planes
-        const uint32_t ph = threadIdx.x >> 4, wi = cb * 16u + (threadIdx.x & 15u);
-        if ((vm >> ph) & 1u) s_pl[ph][threadIdx.x & 15u] = wi < d.PW ? d.pend[((size_t)o * 16u + ph) * d.PW + wi] : 0ull;
-        __syncthreads();
+        __builtin_amdgcn_wave_barrier();  // this wave is done with the previous chunk's words
+        const uint32_t ph = ln >> 2, wi = cb * 16u + wv * 4u + (ln & 3u);
+        if ((vm >> ph) & 1u) s_pl[wv][ph][ln & 3u] = wi < d.PW ? d.pend[((size_t)o * 16u + ph) * d.PW + wi] : 0ull;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
     }
     if (c0 < d.ncol) {
         const size_t p = pix(d, o, c0);
         // this thread's four columns: bit ph of q[i] = a report in phase ph
         uint32_t q[4] = {0u, 0u, 0u, 0u};
-        const uint32_t wb = (threadIdx.x >> 6) * 4u, lb = plane_bit(c0);
+        const uint32_t lb = plane_bit(c0);
         for (uint32_t m = vm; m; m &= m - 1u) {
             const uint32_t ph = (uint32_t)__builtin_ctz(m);
 #pragma unroll
-            for (int i = 0; i < 4; i++) q[i] |= (uint32_t)((s_pl[ph][wb + i] >> lb) & 1ull) << ph;
+            for (int i = 0; i < 4; i++) q[i] |= (uint32_t)((s_pl[wv][ph][i] >> lb) & 1ull) << ph;
         }
-        const bool rep = (q[0] | q[1] | q[2] | q[3]) != 0u;  // only if vm != 0: then w was loaded
+        uint32_t sc[4] = {sc4.x, sc4.y, sc4.z, sc4.w};
+        uint32_t lt[4] = {l4.x & 0xFFFFu, l4.x >> 16, l4.y & 0xFFFFu, l4.y >> 16};
         bool dw = false;
         uint32_t td[4] = {NONE, NONE, NONE, NONE};
         if (exact && (s4 & 0x02020202u)) ld4(d.tod + p, td);
         uint32_t s4n = s4;
-        if (rep) {
 #pragma unroll
-            for (int i = 0; i < 4; i++) {
-                uint32_t m = q[i];
-                if (!m) continue;
-                Fd f = fd_unpack(d, w[i]);
+        for (int i = 0; i < 4; i++) {
+            uint32_t st = (s4 >> (8 * i)) & 0xFFu;
+            Fd f = fd_get(d, st, lt[i], sc[i], t);  // t is at or after every report tick of this round
+            uint32_t m = q[i];  // only if vm != 0: then the window was loaded
+            if (m) {
                 while (m) {
                     const uint32_t bb = (uint32_t)__builtin_ctz(m);
                     m &= m - 1u;
                     f = fd_report_val<RING>(d, p + i, d.t_round + 1u + bb, f, alg, ovf);
                 }
-                w[i] = fd_pack(d, f);
+                dw = true;
             }
-            dw = true;
-        }
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
             const uint32_t j = c0 + i;
             if (upo && j < d.ncol && d.col_lo + j != o && !(genm && ps[i] == NONE)) {
                 live++;
-                const Fd f = fd_unpack(d, w[i]);
                 const bool has = f.last != NONE;
                 const uint32_t len = RING ? (f.cnt < d.W ? f.cnt : d.W) : f.cnt;
                 bool alive = false;
                 if (has && len) {
-                    const double mean = ((double)f.sum * TICK_S + d.prior5) / ((double)len + 5.0);
-                    const double phi = ((double)(t - f.last) * TICK_S) / mean;
-                    alive = phi <= d.phi_thr;
+                    // phi <= threshold (failure_detector.py:43-53, 97-98) decided without the two binary64
+                    // divisions when it is clear by a margin (2^-30 relative, far above their rounding):
+                    // phi ~ elapsed (len + 5) / (sum + 5 prior) in ticks; the exact expression otherwise
+                    const double lhs = (double)(t - f.last) * (double)(len + 5u);  // exact: < 2^43
+                    const double rhs = d.phi_thr * ((double)f.sum + d.prior5t);
+                    if (lhs < rhs * (1.0 - 0x1p-30)) {
+                        alive = true;
+                    } else if (!(lhs > rhs * (1.0 + 0x1p-30))) {
+                        const double mean = ((double)f.sum * TICK_S + d.prior5) / ((double)len + 5.0);
+                        const double phi = ((double)(t - f.last) * TICK_S) / mean;
+                        alive = phi <= d.phi_thr;
+                    }
                 }
-                const uint32_t st = (s4 >> (8 * i)) & 0xFFu;
+                const uint32_t mb = st & FD_MEMB;
                 // node join / leave: the live set against the previous call's (server.py:611-616)
-                if (d.ev && alive != (st == FD_LIVE))
+                if (d.ev && alive != (mb == FD_LIVE))
                     emit_event(d, o, d.col_lo + j, (alive ? EV_JOIN : EV_LEAVE) << 8, 0u, 0u, t, 0u);
                 uint32_t sn = FD_LIVE;
                 if (!alive) {
                     sn = FD_DEAD;
                     uint32_t tod = td[i];  // loaded for the dead pairs of a row being recomputed
-                    if (st != FD_DEAD) { tod = t; d.tod[p + i] = t; }  // time_of_death recorded once
-                    if (has && (f.sum | f.cnt)) { w[i] = fd_pack(d, Fd{f.last, 0u, 0u}); dw = true; }  // reset
-                    if (st != FD_DEAD || exact) {
+                    if (mb != FD_DEAD) { tod = t; d.tod[p + i] = t; }  // time_of_death recorded once
+                    if (has && (f.sum | f.cnt)) { f.sum = f.cnt = 0u; dw = true; }  // reset
+                    if (mb != FD_DEAD || exact) {
                         const uint32_t sat = tod + d.sched_delay;
                         if (sat < minS) minS = sat;
                     }
                     if (exact && (uint64_t)t >= (uint64_t)tod + d.dead_grace) gcdue++;
                 }
-                s4n = (s4n & ~(0xFFu << (8 * i))) | (sn << (8 * i));
+                st = (st & ~(uint32_t)FD_MEMB) | sn;
             }
+            // a window whose last report is >= FD_OLD_AGE old keeps only that fact (fd_get)
+            if ((st & (FD_WIN | FD_OLD)) == FD_WIN && t - f.last >= FD_OLD_AGE) st |= FD_OLD;
+            if (q[i]) st = fd_st(st, f);
+            sc[i] = fd_sc(d, f);
+            lt[i] = f.last & 0xFFFFu;
+            s4n = (s4n & ~(0xFFu << (8 * i))) | (st << (8 * i));
         }
-        if (dw) st4w(d.fd + p, w);
+        if (dw) {
+            *reinterpret_cast<uint4 *>(d.fd + p) = make_uint4(sc[0], sc[1], sc[2], sc[3]);
+            *reinterpret_cast<uint2 *>(d.fd_last + p) = make_uint2(lt[0] | (lt[1] << 16), lt[2] | (lt[3] << 16));
+        }
         if (s4n != s4) *reinterpret_cast<uint32_t *>(d.fd_state + p) = s4n;
     }
     }
@@ -1681,7 +1727,7 @@ __global__ __launch_bounds__(LB) void k_fd_gc(Dev d, const uint8_t *up, uint32_t
     unsigned long long fkey = ~0ull;
     for (uint32_t j = tid; j < d.ncol; j += LB) {
         const uint32_t tod = dead_tod(d, ro + j), pos = d.pos[ro + j];
-        if (tod != NONE && pos != NONE && (uint64_t)t >= (uint64_t)tod + d.dead_grace && d.fd[ro + j] == 0ull) {
+        if (tod != NONE && pos != NONE && (uint64_t)t >= (uint64_t)tod + d.dead_grace && !(d.fd_state[ro + j] & FD_WIN)) {
             const unsigned long long key = ((unsigned long long)tod << 32) | pos;
             if (key < fkey) fkey = key;
         }
@@ -1703,9 +1749,12 @@ __global__ __launch_bounds__(LB) void k_fd_gc(Dev d, const uint8_t *up, uint32_t
         if (!(tod != NONE && pos != NONE && (uint64_t)t >= (uint64_t)tod + d.dead_grace)) continue;
         const unsigned long long key = ((unsigned long long)tod << 32) | pos;
         if (q9 && key > fkey) continue;
-        d.fd_state[ro + j] = 0u;  // del self._dead_nodes[gossip_id]
-        if (q9 && key == fkey) continue;
-        d.fd[ro + j] = 0ull;  // del self._node_samples[gossip_id]
+        if (q9 && key == fkey) {
+            d.fd_state[ro + j] &= (uint8_t)~FD_MEMB;  // del self._dead_nodes[gossip_id]
+            continue;
+        }
+        d.fd_state[ro + j] = 0u;  // ... and del self._node_samples[gossip_id]
+        d.fd[ro + j] = 0u;
         gcn++;
         if (!q9) atomicOr(&rmv[j >> 5], 1u << (j & 31u));
     }
@@ -1763,7 +1812,7 @@ __global__ __launch_bounds__(LB) void k_fd_census(Dev d, const uint8_t *up) {
     const uint32_t j = blockIdx.x * LB + threadIdx.x;
     uint32_t c[5] = {0u, 0u, 0u, 0u, 0u};
     if (up[o] && j < d.ncol && d.col_lo + j != o) {
-        const uint32_t st = d.fd_state[pix(d, o, j)];
+        const uint32_t st = d.fd_state[pix(d, o, j)] & FD_MEMB;
         if (up[d.col_lo + j]) {
             c[0] = 1u;
             c[1] = st >= 2u;
@@ -1789,7 +1838,10 @@ __global__ void k_zero_slots(Dev d, uint32_t lo, uint32_t n) {
 __global__ __launch_bounds__(LB) void k_phi_row(Dev d, uint32_t o, uint32_t t, double *out) {
     const uint32_t j = blockIdx.x * LB + threadIdx.x;
     if (j >= d.ncol) return;
-    const Fd f = fd_unpack(d, d.fd[pix(d, o, j)]);
+    const size_t p = pix(d, o, j);
+    const uint32_t st = d.fd_state[p];
+    const Fd f = fd_get(d, st, d.fd_last[p], d.fd[p], t);
+    if ((st & FD_OLD) && f.cnt) shard_add(d, C_E_FDOVF, 1);  // phi of a window silent for >= 2^15 ticks: inexact
     const uint32_t len = (d.flags & GS_FD_RING) ? (f.cnt < d.W ? f.cnt : d.W) : f.cnt;
     double phi = __builtin_nan("");
     if (f.last != NONE && len) {
@@ -1797,6 +1849,26 @@ __global__ __launch_bounds__(LB) void k_phi_row(Dev d, uint32_t o, uint32_t t, d
         phi = ((double)(t - f.last) * TICK_S) / mean;
     }
     out[j] = phi;
+}
+
+// Marks every window whose last report is >= FD_OLD_AGE ticks before t FD_OLD (all rows; the host runs
+// it at least every 2^14 ticks, so an unmarked window is < 2^15 + 2^14 ticks old and decodes exactly).
+__global__ __launch_bounds__(LB) void k_fd_age(Dev d, uint32_t t) {
+    const uint64_t total = (uint64_t)d.N * d.NP / 4;
+    for (uint64_t x = (uint64_t)blockIdx.x * LB + threadIdx.x; x < total; x += (uint64_t)gridDim.x * LB) {
+        const size_t p = x * 4;
+        const uint32_t s4 = *reinterpret_cast<const uint32_t *>(d.fd_state + p);
+        if (!(s4 & 0x04040404u)) continue;
+        const uint2 l4 = *reinterpret_cast<const uint2 *>(d.fd_last + p);
+        const uint32_t lt[4] = {l4.x & 0xFFFFu, l4.x >> 16, l4.y & 0xFFFFu, l4.y >> 16};
+        uint32_t s4n = s4;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const uint32_t st = (s4 >> (8 * i)) & 0xFFu;
+            if ((st & (FD_WIN | FD_OLD)) == FD_WIN && ((t - lt[i]) & 0xFFFFu) >= FD_OLD_AGE) s4n |= (uint32_t)FD_OLD << (8 * i);
+        }
+        if (s4n != s4) *reinterpret_cast<uint32_t *>(d.fd_state + p) = s4n;
+    }
 }
 
 // 16-bit heartbeats (hb_dec) are exact while every view lags its owner's own heartbeat by < 2^16.  An
@@ -2184,7 +2256,7 @@ __global__ __launch_bounds__(LB) void k_sel_count(Dev d, const uint8_t *up, uint
     for (uint32_t j = threadIdx.x; j < d.ncol; j += LB) {
         const size_t p = pix(d, o, j);
         if (j == o || (genm && d.pos[p] == NONE)) continue;
-        const uint32_t st = d.fd_state[p];
+        const uint32_t st = d.fd_state[p] & FD_MEMB;
         P++;
         L += st == 1u;
         D += st >= 2u;
@@ -2258,7 +2330,7 @@ __global__ __launch_bounds__(LB) void k_sel_resolve(Dev d, const uint8_t *up, co
             const size_t p = pix(d, o, j);
             known = !genm || d.pos[p] != NONE;
             if (known) {
-                const uint32_t st = d.fd_state[p];
+                const uint32_t st = d.fd_state[p] & FD_MEMB;
                 live = st == 1u;
                 dead = st >= 2u;
             }
@@ -2437,6 +2509,8 @@ struct gs_handle {
     uint32_t last_phase_tick;
     uint64_t plane_flushes;           // mid-round report replays (rounds with phases > 16 ticks after the base)
     uint32_t hb_incs;                 // rounds + phases since the last heartbeat-lag check (gs_check_heartbeat_lag)
+    uint32_t age_tick = 0;            // tick of the last window-age sweep (k_fd_age)
+    uint32_t max_tick = 0;            // latest tick of any operation (gs_latest_tick: decodes GS_R_FD_LAST)
     void *reg[GS_NUM_REGIONS];
     uint64_t bytes[GS_NUM_REGIONS];
     hipStream_t stream;
@@ -2501,6 +2575,10 @@ int time_end(gs_handle *h, int kind, hipEvent_t e0) {
     return GS_OK;
 }
 
+// k_fd_age at least every 2^14 ticks of the operations that decode 16-bit report ticks (phases: the
+// mid-round replay; liveness; phi), so every unmarked window is < 2^15 + 2^14 ticks old when decoded
+int fd_age(gs_handle *h, uint32_t tick);
+
 int check_bound(gs_handle *h) {
     for (int r = 0; r < GS_NUM_REGIONS; r++)
         if (h->bytes[r] && !h->reg[r]) return fail(h, GS_E_UNBOUND, "region %d not bound", r);
@@ -2510,7 +2588,8 @@ int check_bound(gs_handle *h) {
     d.mv = (uint16_t *)h->reg[GS_R_MV];
     d.gc = (uint32_t *)h->reg[GS_R_GC];
     d.held = (uint8_t *)h->reg[GS_R_HELD];
-    d.fd = (uint64_t *)h->reg[GS_R_FD];
+    d.fd = (uint32_t *)h->reg[GS_R_FD];
+    d.fd_last = (uint16_t *)h->reg[GS_R_FD_LAST];
     d.fd_state = (uint8_t *)h->reg[GS_R_FD_STATE];
     d.tod = (uint32_t *)h->reg[GS_R_FD_TOD];
     d.ts = (uint32_t *)h->reg[GS_R_TS];
@@ -2651,6 +2730,12 @@ int gs_create(const gs_config *cfg, gs_handle **out) {
     while ((1ull << cnt_bits) <= 2ull * c.window) cnt_bits++;
     const uint32_t sum_bits = 32 - cnt_bits;
     if (cnt_bits > 31 || (uint64_t)c.window * c.max_interval_ticks >= (1ull << sum_bits)) return GS_E_INVALID;
+    // 16-bit last-report ticks (GS_R_FD_LAST): a window silent for >= 2^15 ticks must be past max_interval
+    // and past the phi threshold whatever its exact age (fd_get)
+    const double prior_ticks = c.prior_weighted / 5.0 * 64.0;
+    if (c.max_interval_ticks >= (1u << 14) ||
+        c.phi_threshold * std::max((double)c.max_interval_ticks, prior_ticks) >= (double)(1u << 15))
+        return GS_E_INVALID;
     gs_handle *h = new gs_handle();
     h->cfg = c;
     h->N = c.n_nodes;
@@ -2676,7 +2761,8 @@ int gs_create(const gs_config *cfg, gs_handle **out) {
     b[GS_R_MV] = pairs * 2;
     b[GS_R_GC] = (c.flags & GS_TOMBSTONES) ? pairs * 4 : 0;  // last_gc_version stays 0 without tombstone GC
     b[GS_R_HELD] = (c.flags & GS_NO_HELD) ? 0 : pairs * KP;
-    b[GS_R_FD] = pairs * 8;
+    b[GS_R_FD] = pairs * 4;
+    b[GS_R_FD_LAST] = pairs * 2;
     b[GS_R_FD_STATE] = pairs;
     b[GS_R_FD_TOD] = pairs * 4;
     b[GS_R_TS] = (c.flags & GS_TOMBSTONES) ? pairs * KP * 4 : 0;
@@ -2725,6 +2811,7 @@ int gs_create(const gs_config *cfg, gs_handle **out) {
     if (const char *ab = getenv("GS_ABLATE")) d.ablate = (uint32_t)atoi(ab);
     d.phi_thr = c.phi_threshold;
     d.prior5 = c.prior_weighted;
+    d.prior5t = c.prior_weighted * 64.0;
     *out = h;
     return GS_OK;
 }
@@ -2767,7 +2854,7 @@ int gs_boot(gs_handle *h, const uint16_t *nid_size, const uint8_t *key_len) {
     if (rc) return rc;
     hipStream_t s = h->stream;
     // regions that start at zero
-    const int zero[] = {GS_R_HB, GS_R_SELF_HB, GS_R_MV, GS_R_GC, GS_R_HELD, GS_R_FD, GS_R_FD_STATE, GS_R_FD_TOD,
+    const int zero[] = {GS_R_HB, GS_R_SELF_HB, GS_R_MV, GS_R_GC, GS_R_HELD, GS_R_FD, GS_R_FD_LAST, GS_R_FD_STATE, GS_R_FD_TOD,
                         GS_R_RING, GS_R_ROW, GS_R_LAST_W, GS_R_HIST, GS_R_HIST_VID,
                         GS_R_STAMP, GS_R_COUNTERS, GS_R_SLICE_BITS, GS_R_PEND, GS_R_PEND_STAMP, GS_R_LATEST};
     for (int r : zero)
@@ -2838,6 +2925,7 @@ int gs_begin_round(gs_handle *h, const uint8_t *up, uint32_t tick) {
     }
     h->d.t_round = tick;
     h->last_phase_tick = tick;
+    h->max_tick = std::max(h->max_tick, tick);
     k_begin_round<<<h->N, LB, 0, h->stream>>>(h->d, up, tick);
     HIPCHK(h, hipGetLastError());
     h->round_open = true;
@@ -2870,7 +2958,7 @@ int gs_run_phase(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t 
         return n ? sliced_phase(&h, 1, ini, res, n, tick) : GS_OK;
     }
     if (!n) return GS_OK;
-    if ((rc = advance_planes(h, tick))) return rc;
+    if ((rc = fd_age(h, tick)) || (rc = advance_planes(h, tick))) return rc;
     const bool genm = !(h->cfg.flags & GS_CANONICAL);
     const size_t lds = exchange_lds(h);
     const SliceIO io{};
@@ -2902,7 +2990,7 @@ int gs_phase_count(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_
     if (h->G < 2) return fail(h, GS_E_UNSUPPORTED, "gs_phase_count needs a sliced handle (n_shards > 1)");
     if (!n) return GS_OK;
     if (!slice_bytes) return GS_E_INVALID;
-    if ((rc = advance_planes(h, tick))) return rc;
+    if ((rc = fd_age(h, tick)) || (rc = advance_planes(h, tick))) return rc;
     const size_t lds = exchange_lds(h);
     SliceIO io{};
     io.tot = slice_bytes;
@@ -3098,8 +3186,29 @@ int gs_run_phase_group(gs_handle *const *hs, uint32_t n_handles, const int32_t *
     return sliced_phase(hs, n_handles, ini, res, n, tick);
 }
 
+extern "C++" {
+namespace {
+int fd_age(gs_handle *h, uint32_t tick) {
+    h->max_tick = std::max(h->max_tick, tick);
+    const uint32_t dt = tick - h->age_tick;
+    if ((int32_t)dt < 0) return GS_OK;  // an earlier tick (phi of the past): nothing aged since the sweep
+    if (dt >= FD_OLD_AGE)
+        return fail(h, GS_E_INVALID, "tick %u is %u ticks after the last window-age sweep (at most 2^15 between "
+                    "operations: 16-bit report ticks)", tick, dt);
+    if (dt < (FD_OLD_AGE >> 1)) return GS_OK;
+    const uint64_t quads = (uint64_t)h->N * h->NP / 4;
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>((quads + LB - 1) / LB, 1u << 16);
+    k_fd_age<<<blocks, LB, 0, h->stream>>>(h->d, tick);
+    HIPCHK(h, hipGetLastError());
+    h->age_tick = tick;
+    return GS_OK;
+}
+}  // namespace
+}
+
 int gs_liveness(gs_handle *h, const uint8_t *up, uint32_t tick) {
     if (!h || !h->booted || !up) return GS_E_INVALID;
+    if (int rc = fd_age(h, tick)) return rc;
     if (h->reports_pending && tick < h->last_phase_tick)
         return fail(h, GS_E_INVALID, "gs_liveness at tick %u precedes a phase at tick %u", tick, h->last_phase_tick);
     k_reset_sched<<<(h->N + LB - 1) / LB, LB, 0, h->stream>>>(h->d, up, tick);
@@ -3135,8 +3244,15 @@ int gs_read_rows(gs_handle *h, int region, uint32_t row_lo, uint32_t row_hi, voi
     return GS_OK;
 }
 
+int gs_latest_tick(const gs_handle *h, uint32_t *tick) {
+    if (!h || !tick) return GS_E_INVALID;
+    *tick = h->max_tick;
+    return GS_OK;
+}
+
 int gs_phi_row(gs_handle *h, uint32_t observer, uint32_t tick, double *out) {
     if (!h || !h->booted || !out || observer >= h->N) return GS_E_INVALID;
+    if (int rc = fd_age(h, tick)) return rc;
     k_phi_row<<<(h->ncol + LB - 1) / LB, LB, 0, h->stream>>>(h->d, observer, tick, out);
     HIPCHK(h, hipGetLastError());
     return GS_OK;

@@ -61,10 +61,24 @@ def sched_delay_ticks(dead_grace_s: float) -> int:
     return -(-half // TICK_US)
 
 
+FD_WIN, FD_OLD, FD_OLD_AGE = 4, 8, 1 << 15
+
+
+def unpack_fd(st8, last16, sc, tick: int, sum_bits: int):
+    """Host restatement of the device's fd_get (gossip_sim.hip): see GossipSim.unpack_fd."""
+    st8 = np.asarray(st8).view(np.uint8).astype(np.uint32)
+    l16 = np.asarray(last16).view(np.uint16).astype(np.int64)
+    sc = np.asarray(sc).view(np.uint32)
+    t = np.int64(tick)
+    last = np.where(st8 & FD_OLD, t - FD_OLD_AGE, t - ((t - l16) & 0xFFFF)) & 0xFFFFFFFF
+    last = np.where(st8 & FD_WIN, last, GS_NONE).astype(np.uint32)
+    return last, sc & np.uint32((1 << sum_bits) - 1), sc >> np.uint32(sum_bits)
+
+
 def fd_state_word(st8: np.ndarray, tod: np.ndarray) -> np.ndarray:
     """GS_R_FD_STATE (u8: 0 unknown, 1 live, 2 dead) + GS_R_FD_TOD (time of death) as one u32 per pair:
     0 unknown, 1 live, tick of death + 2 for a dead pair (the readback format of export / snapshot)."""
-    st8 = np.asarray(st8).view(np.uint8)
+    st8 = np.asarray(st8).view(np.uint8) & np.uint8(3)
     tod = np.asarray(tod).view(np.uint32)
     return np.where(st8 == 2, tod + np.uint32(2), st8.astype(np.uint32)).astype(np.uint32)
 
@@ -526,14 +540,16 @@ class GossipSim:
         for name in ("GC", "POS"):
             if name in self.regions:
                 g[name] = rd(name, torch.int32, (n, NP)).view(np.uint32)
-        g["FD_STATE"] = fd_state_word(rd("FD_STATE", torch.uint8, (n, NP)), rd("FD_TOD", torch.int32, (n, NP)))
+        st8 = rd("FD_STATE", torch.uint8, (n, NP))
+        g["FD_STATE"] = fd_state_word(st8, rd("FD_TOD", torch.int32, (n, NP)))
         mv = rd("MV", torch.int16, (n, NP)).view(np.uint16).astype(np.uint32)
         g["MV_INEXACT"] = (mv >> np.uint32(15)).astype(np.uint8)  # prefix-view flag (GS_MV_INEXACT)
         g["MV"] = mv & np.uint32(0x7FFF)
         nr = g["MV"].shape[0]
         if "GC" not in g:  # no tombstone GC: last_gc_version is 0 everywhere
             g["GC"] = np.zeros((nr, NP), dtype=np.uint32)
-        g["FD_LAST"], g["FD_SUM"], g["FD_CNT"] = self.unpack_fd(rd("FD", torch.int64, (n, NP)))
+        g["FD_LAST"], g["FD_SUM"], g["FD_CNT"] = self.unpack_fd(st8, rd("FD_LAST", torch.int16, (n, NP)),
+                                                                rd("FD", torch.int32, (n, NP)), self.latest_tick())
         nc = self.ncol
         hist = self.region("HIST", torch.int64, (nc, Cc, K)).cpu().numpy().view(np.uint64)
         g["HIST_VER"] = (hist & 0xFFFFFFFF).astype(np.uint32)
@@ -599,14 +615,17 @@ class GossipSim:
         65,536-node matrix)."""
         return self.export(self._host(rows))
 
-    def unpack_fd(self, packed: np.ndarray):
-        """Split packed windows (GS_R_FD) into (last tick or GS_NONE, sum in ticks, appended count)."""
-        v = packed.view(np.uint64)
-        lo = (v & 0xFFFFFFFF).astype(np.uint32)
-        hi = (v >> 32).astype(np.uint32)
-        sb = _lib.fd_sum_bits(int(self.cfg["window"]))
-        last = (lo - np.uint32(1)).astype(np.uint32)  # 0 - 1 wraps to GS_NONE
-        return last, hi & np.uint32((1 << sb) - 1), hi >> np.uint32(sb)
+    def latest_tick(self) -> int:
+        """gs_latest_tick: the latest tick any operation on the handle used (decodes GS_R_FD_LAST)."""
+        t = C.c_uint32()
+        self._chk(self.L.gs_latest_tick(self.h, C.byref(t)), "gs_latest_tick")
+        return int(t.value)
+
+    def unpack_fd(self, st8: np.ndarray, last16: np.ndarray, sc: np.ndarray, tick: int):
+        """Windows (GS_R_FD_STATE bits, GS_R_FD_LAST, GS_R_FD) as (last tick or GS_NONE, sum in ticks,
+        appended count); 16-bit ticks decoded against ``tick`` (at or after every report recorded), a
+        window marked old (>= 2^15 ticks) as tick - 2^15, as the device does (fd_get)."""
+        return unpack_fd(st8, last16, sc, tick, _lib.fd_sum_bits(int(self.cfg["window"])))
 
     def read_rows(self, region: str, row_lo: int, row_hi: int) -> bytes:
         """gs_read_rows: the bytes of observer rows [row_lo, row_hi) of ``region`` (blocking copy-out)."""
@@ -775,12 +794,12 @@ class GossipSim:
     def live_nodes(self, observer: int) -> list[NodeId]:
         self._whole()
         st = self.region("FD_STATE", self.torch.uint8, (self.n, self.np_))[observer, : self.n].cpu().numpy()
-        return [self.node_ids[j] for j in np.flatnonzero(st == 1)]
+        return [self.node_ids[j] for j in np.flatnonzero((st & 3) == 1)]
 
     def dead_nodes(self, observer: int) -> list[NodeId]:
         self._whole()
         st = self.region("FD_STATE", self.torch.uint8, (self.n, self.np_))[observer, : self.n].cpu().numpy()
-        return [self.node_ids[j] for j in np.flatnonzero(st == 2)]
+        return [self.node_ids[j] for j in np.flatnonzero((st & 3) == 2)]
 
     def phi(self, observer: int, target: int, tick: int | None = None) -> float | None:
         v = float(self.phi_row(observer, tick)[target])

@@ -91,12 +91,12 @@ enum gs_region {
     GS_R_HELD,        /* u8  [N][NP][KP] write ordinal of each key held (0 = absent), KP = K rounded to 4;
                                         kept only for views with GS_MV_INEXACT or with GS_TOMBSTONES;
                                         not allocated with GS_NO_HELD */
-    GS_R_FD,          /* u64 [N][NP]   sampling window: low word = _last_heartbeat tick + 1 (0 = no
-                                        window); high word = _sum in ticks | intervals appended since
-                                        the last reset << sum_bits (len = min(cnt, W)); sum_bits =
-                                        32 - bits(2W) (gs_create rejects W * max_interval >= 2^sum_bits) */
-    GS_R_FD_STATE,    /* u8  [N][NP]   0 = unknown, 1 = live (in _live_nodes), 2 = dead (in _dead_nodes,
-                                        time of death in GS_R_FD_TOD) */
+    GS_R_FD,          /* u32 [N][NP]   sampling window: _sum in ticks | intervals appended since the last
+                                        reset << sum_bits (len = min(cnt, W)); sum_bits = 32 - bits(2W)
+                                        (gs_create rejects W * max_interval >= 2^sum_bits) */
+    GS_R_FD_STATE,    /* u8  [N][NP]   bits 0-1: 0 = unknown, 1 = live (in _live_nodes), 2 = dead (in
+                                        _dead_nodes, time of death in GS_R_FD_TOD); bit 2: the pair has a
+                                        sampling window; bit 3: its last report is >= 2^15 ticks old */
     GS_R_TS,          /* u32 [N][NP][KP] tombstone receive tick, GS_NONE for SET entries (GS_TOMBSTONES) */
     GS_R_RING,        /* u16 [N][NP][W] interval ring in ticks (GS_FD_RING) */
     GS_R_POS,         /* u32 [N][NP]   insertion index of owner j in observer o's dict, GS_NONE = absent (general) */
@@ -133,6 +133,10 @@ enum gs_region {
                                         GS_CAND_CAP: the packer then walks GS_R_SLICE_BITS for that half) */
     GS_R_FD_TOD,      /* u32 [N][NP]   time of death (tick) of a GS_R_FD_STATE = 2 pair; read only for rows
                                         whose word 2 of GS_R_ROW has passed */
+    GS_R_FD_LAST,     /* u16 [N][NP]   the window's _last_heartbeat tick mod 2^16 (decoded against the
+                                        operation's tick; exact until 2^15 old, then only "old": bit 3 above;
+                                        gs_create requires max_interval < 2^14 and
+                                        phi_threshold * max(max_interval, prior) < 2^15 ticks) */
     GS_NUM_REGIONS
 };
 
@@ -396,6 +400,10 @@ int gs_sync(gs_handle *h);
  * `out` of `cap` bytes, in the region's layout; *len = the bytes of those rows (set even when they exceed
  * cap, which fails).  GS_R_HELD rows are complete: the prefix views' ordinals are materialized first. */
 int gs_read_rows(gs_handle *h, int region, uint32_t row_lo, uint32_t row_hi, void *out, uint64_t cap, uint64_t *len);
+
+/* The latest tick any operation on h has used: GS_R_FD_LAST rows read with gs_read_rows are decoded against
+ * it (tick - ((tick - s) mod 2^16); a window with bit 3 of GS_R_FD_STATE set as tick - 2^15). */
+int gs_latest_tick(const gs_handle *h, uint32_t *tick);
 
 #ifdef __cplusplus
 }

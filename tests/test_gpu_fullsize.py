@@ -122,8 +122,9 @@ def test_fullsize_check_detects_a_corrupted_row():
     hb[o, j] += 1
     st = sim.region("FD_STATE", torch.uint8, (n, sim.np_))
     tod = sim.region("FD_TOD", torch.int32, (n, sim.np_))
-    st[rows[12], (rows[12] + 5) % n] = 2  # dead since t
-    tod[rows[12], (rows[12] + 5) % n] = t
+    o, j = rows[12], (rows[12] + 5) % n
+    st[o, j] = (st[o, j] & 0xFC) | 2  # dead since t (membership bits only; the window bits stay)
+    tod[o, j] = t
     d = rowcheck.compare_exports(sim.export_rows(rows), want)
     assert d is not None and d.startswith("live[12, "), d
     ro.close()

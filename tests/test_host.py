@@ -24,27 +24,28 @@ def test_split_owner_batches_keeps_per_owner_order():
     assert flat == {1: ["a", "c", "d"], 2: ["b", "f"], 3: ["e"]}
 
 
-def test_fd_packing_roundtrip():
-    """GS_R_FD: (last + 1) | (sum | cnt << sum_bits) << 32, 0 = no window."""
+def test_fd_window_decode():
+    """GS_R_FD (sum | cnt << sum_bits) + GS_R_FD_LAST (tick mod 2^16) + GS_R_FD_STATE bits (window, old):
+    the host decode restates the device's fd_get; exact while the last report is < 2^16 ticks old."""
+    from aiocluster_amd.sim import FD_OLD, FD_OLD_AGE, FD_WIN, unpack_fd
+
     W = 1000
     sb = _lib.fd_sum_bits(W)
     assert sb == 21 and W * 640 < (1 << sb)
-
-    class Dummy:
-        cfg = {"window": W}
-
-    from aiocluster_amd.sim import GossipSim
-
     rng = np.random.default_rng(0)
-    last = rng.integers(0, 1 << 31, 100, dtype=np.uint64)
+    t = 5_000_000
+    last = t - rng.integers(0, 1 << 16, 100, dtype=np.int64)
     sm = rng.integers(0, 1 << sb, 100, dtype=np.uint64)
     cnt = rng.integers(0, 2 * W, 100, dtype=np.uint64)
-    packed = (last + 1) | ((sm | (cnt << np.uint64(sb))) << np.uint64(32))
-    packed[:3] = 0  # no window
-    l2, s2, c2 = GossipSim.unpack_fd(Dummy(), packed.view(np.int64))
-    assert np.all(l2[:3] == _lib.GS_NONE) and np.all(s2[:3] == 0) and np.all(c2[:3] == 0)
-    assert np.array_equal(l2[3:], last[3:].astype(np.uint32))
-    assert np.array_equal(s2[3:], sm[3:].astype(np.uint32)) and np.array_equal(c2[3:], cnt[3:].astype(np.uint32))
+    sc = (sm | (cnt << np.uint64(sb))).astype(np.uint32)
+    st = np.full(100, FD_WIN | 1, np.uint8)
+    st[:3] = 0  # no window
+    st[3:6] |= FD_OLD
+    l2, s2, c2 = unpack_fd(st, (last & 0xFFFF).astype(np.uint16), sc, t, sb)
+    assert np.all(l2[:3] == _lib.GS_NONE)
+    assert np.all(l2[3:6] == t - FD_OLD_AGE)
+    assert np.array_equal(l2[6:], last[6:].astype(np.uint32))
+    assert np.array_equal(s2, sm.astype(np.uint32)) and np.array_equal(c2, cnt.astype(np.uint32))
 
 
 def test_make_config_ticks_and_rejects_fractional_ticks():
