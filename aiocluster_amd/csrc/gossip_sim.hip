@@ -1562,7 +1562,10 @@ template <bool RING>
 // the per-workgroup plane staging, stamp check and counter atomics are paid once per `per` chunks).
 // decide = false: only replay the pending reports into the windows, for every row (a round with phases
 // more than 16 ticks after its plane base: the planes are emptied mid-round)
-__global__ __launch_bounds__(LB) void k_liveness(Dev d, const uint8_t *up, uint32_t t, uint32_t chunks,
+#ifndef LIVE_WAVES
+#define LIVE_WAVES 8  // waves per SIMD k_liveness is compiled for (<= 64 VGPRs)
+#endif
+__global__ __launch_bounds__(LB, LIVE_WAVES) void k_liveness(Dev d, const uint8_t *up, uint32_t t, uint32_t chunks,
                                                  uint32_t per, bool replay, bool decide) {
     // [wave][phase][the wave's 4 plane words of this chunk]: each wave stages and reads only its own
     // words (lane l: phase l / 4, word l % 4), so the chunks need no workgroup barrier
