@@ -1030,8 +1030,11 @@ __device__ inline PackState chain_unpack(uint64_t v) {
 // wave 1: a -> b) right after streaming the rows, while the receivers' max_version lines are still in L2
 // (the applies are one scattered 2-byte store per NodeDelta; tools/membench.hip prices those at 25 G/s
 // from HBM).
+#ifndef P1S_WAVES
+#define P1S_WAVES 4  // waves per SIMD of the pass-1-only kernel (split phases, sliced count pass); 5 spills and measured slower (r2r)
+#endif
 template <int KW, bool FUSE>
-__global__ __launch_bounds__(XB, (KW == 4 ? P1_WAVES : 1)) void k_pass1(Dev d, const int32_t *ini, const int32_t *res,
+__global__ __launch_bounds__(XB, (KW == 4 ? (FUSE ? P1_WAVES : P1S_WAVES) : 1)) void k_pass1(Dev d, const int32_t *ini, const int32_t *res,
                                                                        uint32_t n, uint32_t t, uint32_t seq,
                                                                        uint32_t e0) {
     const uint32_t e = e0 + blockIdx.x;  // exchanges [e0, e0 + grid) of the phase (one chunk)
@@ -2635,7 +2638,12 @@ size_t exchange_lds(const gs_handle *h) {
 
 int launch_liveness(gs_handle *h, const uint8_t *up, uint32_t tick, bool replay, bool decide) {
     const uint32_t chunks = (h->ncol + 4 * LB - 1) / (4 * LB);
-    const uint32_t per = LIVE_PER, groups = (chunks + per - 1) / per;
+    static const uint32_t live_per = [] {  // env GS_LIVE_PER: chunks per workgroup (tuning sweeps)
+        const char *e = getenv("GS_LIVE_PER");
+        const int v = e ? atoi(e) : 0;
+        return v >= 1 && v <= 64 ? (uint32_t)v : (uint32_t)LIVE_PER;
+    }();
+    const uint32_t per = live_per, groups = (chunks + per - 1) / per;
     hipEvent_t e0 = nullptr;
     int rc = time_begin(h, e0);
     if (rc) return rc;
