@@ -235,10 +235,16 @@ template <int KW>
 struct Cand {
     uint32_t j, from, gs, ms, gr, mr, base, emsg, min1, nkv;
     uint32_t hs[KW], hr[KW];  // held write ordinals, 4 keys per word (sender / receiver)
-    uint32_t ver[4 * KW];     // version of each key the sender holds (0 = absent)
-    uint32_t km[4 * KW];      // DeltaPb bytes of that kv | status << 16
     bool rx;                  // prefix views (no GS_TOMBSTONES): the receiver's view is S_j(mr)
     bool fast;                // ... and so is the sender's: hr was not loaded
+};
+// The sender's kvs of one candidate, per key: eval_cand's working set, not kept in Cand (32 VGPRs at
+// KW = 4): the packer re-reads a key's history entry (the sender's held ordinal hs) in the rare paths
+// that need it (a truncated NodeDelta, a per-key apply) -- lanes = keys, one load.
+template <int KW>
+struct CandKeys {
+    uint32_t ver[4 * KW];  // version of each key the sender holds (0 = absent)
+    uint32_t km[4 * KW];   // DeltaPb bytes of that kv | status << 16
 };
 
 __device__ inline void set_byte(uint32_t *w, int q, uint32_t v) {
@@ -280,7 +286,7 @@ __device__ __forceinline__ void derive_held(const Dev &d, uint32_t j, uint32_t M
 // HAVE_MV: both views' max_version words come from pass 1's candidate record (mvw = sender | receiver << 16)
 template <int KW, bool GENM, bool HAVE_MV = false>
 __device__ __forceinline__ void eval_cand(const Dev &d, uint32_t s, uint32_t r, const DigestSide &ds, uint32_t j,
-                                          uint32_t t, Cand<KW> &c, uint32_t &alg, uint32_t mvw = 0) {
+                                          uint32_t t, Cand<KW> &c, CandKeys<KW> &k, uint32_t &alg, uint32_t mvw = 0) {
     const size_t ps = pix(d, s, j), pr = pix(d, r, j);
     const uint32_t kw = d.KP >> 2;
     // round trip 1
@@ -327,8 +333,8 @@ __device__ __forceinline__ void eval_cand(const Dev &d, uint32_t s, uint32_t r, 
         // latest write of every key, stepping back for the keys written after ms
 #pragma unroll
         for (int q = 0; q < 4 * KW; q++) {
-            c.ver[q] = 0u;
-            c.km[q] = 0u;
+            k.ver[q] = 0u;
+            k.km[q] = 0u;
             uint32_t w = byte_of(c.hs, q);
             if (!w || (uint32_t)q >= d.K) continue;
             const uint32_t e32 = lat[q];  // counted below only for the kvs sent
@@ -341,11 +347,11 @@ __device__ __forceinline__ void eval_cand(const Dev &d, uint32_t s, uint32_t r, 
                 set_byte(c.hs, q, w);
                 if (!w) continue;
                 const uint32_t meta = (uint32_t)(e >> 32);
-                c.ver[q] = (uint32_t)e;
-                c.km[q] = msgf(meta_kvlen(meta)) | (meta_status(meta) << 16);
+                k.ver[q] = (uint32_t)e;
+                k.km[q] = msgf(meta_kvlen(meta)) | (meta_status(meta) << 16);
             } else {  // the latest write (a prefix view: status SET)
-                c.ver[q] = e32 & 0xFFFFu;
-                c.km[q] = e32 >> 16;
+                k.ver[q] = e32 & 0xFFFFu;
+                k.km[q] = e32 >> 16;
             }
         }
     } else {
@@ -358,13 +364,13 @@ __device__ __forceinline__ void eval_cand(const Dev &d, uint32_t s, uint32_t r, 
 #pragma unroll
         for (int q = 0; q < 4 * KW; q++) {
             const uint32_t w = byte_of(c.hs, q);
-            c.ver[q] = 0u;
-            c.km[q] = 0u;
+            k.ver[q] = 0u;
+            k.km[q] = 0u;
             if (w && (uint32_t)q < d.K && (all_keys || (rx ? true : w > byte_of(c.hr, q)))) {
                 const uint64_t e = d.hist[hix(d, j, w, q)];
                 const uint32_t meta = (uint32_t)(e >> 32);
-                c.ver[q] = (uint32_t)e;
-                c.km[q] = msgf(meta_kvlen(meta)) | (meta_status(meta) << 16);
+                k.ver[q] = (uint32_t)e;
+                k.km[q] = msgf(meta_kvlen(meta)) | (meta_status(meta) << 16);
                 alg += 8;
             }
         }
@@ -372,11 +378,11 @@ __device__ __forceinline__ void eval_cand(const Dev &d, uint32_t s, uint32_t r, 
     uint32_t sum = 0, nk = 0, minv = NONE, minkv = 0;
 #pragma unroll
     for (int q = 0; q < 4 * KW; q++) {
-        if (c.ver[q] > from) {
-            const uint32_t kvm = c.km[q] & 0xFFFFu;
+        if (k.ver[q] > from) {
+            const uint32_t kvm = k.km[q] & 0xFFFFu;
             sum += kvm;
             nk += 1;
-            if (c.ver[q] < minv) { minv = c.ver[q]; minkv = kvm; }
+            if (k.ver[q] < minv) { minv = k.ver[q]; minkv = kvm; }
         }
     }
     if (sx) alg += 4 * nk;  // the latest-write words of the NodeDelta's kvs
@@ -437,10 +443,13 @@ __device__ __forceinline__ void apply_cand(const Dev &d, uint32_t s, uint32_t r,
             if (tt) tsr[q] = NONE;
             alg += 8;
         }
-        const uint32_t v = c.ver[q];
+        // the sender's entry of key q (its held ordinal ws), re-read: Cand keeps no per-key arrays
+        uint64_t e = 0;
+        if (ws) { e = d.hist[hix(d, c.j, ws, q)]; alg += 8; }
+        const uint32_t v = (uint32_t)e;
         // skip: not in the delta / version <= max_version / existing >= / GC'd tombstone (209-220)
         if (ws && v > c.from && v <= vmax && v > m0 && wr < ws) {
-            const uint32_t st = c.km[q] >> 16;
+            const uint32_t st = meta_status((uint32_t)(e >> 32));
             if (!(st != 0u && v <= g)) {
                 // on_key_change(node, key, existing, new) for every stored kv (state.py:228-231)
                 if (d.ev)
@@ -546,12 +555,22 @@ __device__ __forceinline__ void pack_group(const Dev &d, uint32_t s, uint32_t r,
             // truncated NodeDelta: lanes = keys, rank kvs by version, longest fitting prefix
             const uint32_t fx = __shfl(c.from, x, WAVE);
             const uint32_t bx = __shfl(c.base, x, WAVE);
+            // lanes = keys: lane q re-reads candidate x's entry of key q (its held ordinal)
             uint32_t v = 0, kvm = 0;
+            {
+                const uint32_t jx = __shfl(c.j, x, WAVE);
+                uint32_t hsx[KW];
 #pragma unroll
-            for (int q = 0; q < 4 * KW; q++) {
-                const uint32_t vq = __shfl(c.ver[q], x, WAVE);
-                const uint32_t kq = __shfl(c.km[q], x, WAVE);
-                if (lane == q) { v = vq; kvm = kq & 0xFFFFu; }
+                for (int w = 0; w < KW; w++) hsx[w] = __shfl(c.hs[w], x, WAVE);
+                uint32_t wq = 0;
+#pragma unroll
+                for (int w = 0; w < KW; w++)
+                    if ((lane >> 2) == w) wq = (hsx[w] >> (8 * (lane & 3))) & 0xFFu;
+                if (lane < (int)d.K && wq) {
+                    const uint64_t e = d.hist[hix(d, jx, wq, (uint32_t)lane)];
+                    v = (uint32_t)e;
+                    kvm = msgf(meta_kvlen((uint32_t)(e >> 32)));
+                }
             }
             const bool inc = lane < (int)d.K && v > fx;
             const unsigned long long im = __ballot(inc);
@@ -673,7 +692,8 @@ __device__ __forceinline__ void pack_dir(const Dev &d, uint32_t s, uint32_t r, c
             if (cand) {
                 const uint32_t p = ci < pend ? rv : win + wbuf[ci - pend];
                 const uint32_t j = GENM ? order[p] : p;
-                eval_cand<KW, GENM>(d, s, r, ds, j, t, c, st.alg);
+                CandKeys<KW> ck;
+                eval_cand<KW, GENM>(d, s, r, ds, j, t, c, ck, st.alg);
                 st.cand++;
             }
             pack_group<KW, COUNT, REC>(d, s, r, t, c, cand, S, tail, stop, st, tomb, rec, nr);
@@ -720,7 +740,8 @@ __device__ __forceinline__ void pack_list(const Dev &d, uint32_t s, uint32_t r, 
         c.emsg = 0;
         c.min1 = 0;
         if (cand) {
-            eval_cand<KW, false, true>(d, s, r, ds, cr.x, t, c, st.alg, cr.y);
+            CandKeys<KW> ck;
+            eval_cand<KW, false, true>(d, s, r, ds, cr.x, t, c, ck, st.alg, cr.y);
             st.cand++;
         }
         pack_group<KW, COUNT, false>(d, s, r, t, c, cand, S, tail, stop, st, tomb, nullptr, nr);
@@ -2156,15 +2177,16 @@ __global__ __launch_bounds__(WAVE) void k_delta_plan(Dev d, uint32_t s, uint32_t
 
 // one recorded NodeDelta: the sender's candidate (eval_cand) and its NodeDeltaPb body size
 template <int KW, bool GENM>
-__device__ inline uint32_t nd_eval(const Dev &d, uint32_t s, uint32_t r, uint32_t t, uint2 rc, Cand<KW> &c) {
+__device__ inline uint32_t nd_eval(const Dev &d, uint32_t s, uint32_t r, uint32_t t, uint2 rc, Cand<KW> &c,
+                                   CandKeys<KW> &k) {
     const bool schR = t >= d.row[r * 4 + 2];
     const DigestSide ds{r, GENM ? d.row[r * 4 + 0] : d.ncol, schR};
     uint32_t alg = 0;
-    eval_cand<KW, GENM>(d, s, r, ds, rc.x, t, c, alg);
+    eval_cand<KW, GENM>(d, s, r, ds, rc.x, t, c, k, alg);
     uint32_t sum = 0;
 #pragma unroll
     for (int q = 0; q < 4 * KW; q++)
-        if (c.ver[q] > c.from && c.ver[q] <= rc.y) sum += c.km[q] & 0xFFFFu;
+        if (k.ver[q] > c.from && k.ver[q] <= rc.y) sum += k.km[q] & 0xFFFFu;
     return c.base + sum;
 }
 template <int KW, bool GENM>
@@ -2173,7 +2195,8 @@ __global__ __launch_bounds__(LB) void k_delta_size(Dev d, uint32_t s, uint32_t r
     const uint32_t i = blockIdx.x * LB + threadIdx.x;
     if (i >= n) return;
     Cand<KW> c;
-    sz[i] = msgf(nd_eval<KW, GENM>(d, s, r, t, rec[i], c));
+    CandKeys<KW> k;
+    sz[i] = msgf(nd_eval<KW, GENM>(d, s, r, t, rec[i], c, k));
 }
 template <int KW, bool GENM>
 __global__ __launch_bounds__(LB) void k_delta_write(Dev d, Wire w, uint32_t s, uint32_t r, uint32_t t,
@@ -2181,8 +2204,9 @@ __global__ __launch_bounds__(LB) void k_delta_write(Dev d, Wire w, uint32_t s, u
     const uint32_t i = blockIdx.x * LB + threadIdx.x;
     if (i >= n) return;
     Cand<KW> c;
+    CandKeys<KW> k;
     const uint2 rc = rec[i];
-    const uint32_t body = nd_eval<KW, GENM>(d, s, r, t, rc, c);
+    const uint32_t body = nd_eval<KW, GENM>(d, s, r, t, rc, c, k);
     const uint32_t j = rc.x, jg = d.col_lo + j, nl = w.nid_off[jg + 1] - w.nid_off[jg];
     uint8_t *p = out + off[i];
     *p++ = 0x0Au;  // DeltaPb.node_deltas (1)
@@ -2198,7 +2222,7 @@ __global__ __launch_bounds__(LB) void k_delta_write(Dev d, Wire w, uint32_t s, u
         int qm = -1;
         uint32_t vm = NONE;
         for (int q = 0; q < 4 * KW; q++)
-            if (c.ver[q] > last && c.ver[q] <= rc.y && c.ver[q] < vm) { vm = c.ver[q]; qm = q; }
+            if (k.ver[q] > last && k.ver[q] <= rc.y && k.ver[q] < vm) { vm = k.ver[q]; qm = q; }
         if (qm < 0) break;
         last = vm;
         const size_t hx = hix(d, j, byte_of(c.hs, qm), (uint32_t)qm);
