@@ -57,6 +57,34 @@ def test_create_validates_config_without_gpu():
     assert lib.gs_create(ctypes.byref(bad), ctypes.byref(h)) == -1
 
 
+def test_window_layout_and_16_bit_tick_bounds():
+    """Sampling windows: u32 sum|count + u16 last-report tick + state byte (+ u32 time of death); gs_create
+    refuses configs under which a window silent for 2^15 ticks could still append an interval
+    (max_interval >= 2^14 ticks) or still be alive (threshold x max(max_interval, prior) >= 2^15 ticks)."""
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("library not built")
+    from aiocluster_amd.scenario import DEFAULT_CFG
+    from aiocluster_amd.sim import make_config
+
+    lib = _lib.load()
+    h = ctypes.c_void_p()
+    cfg = make_config(1000, 16, DEFAULT_CFG, _lib.GS_CANONICAL, 32)
+    assert lib.gs_create(ctypes.byref(cfg), ctypes.byref(h)) == 0
+    pairs = 1000 * 1024
+    for name, per in (("FD", 4), ("FD_LAST", 2), ("FD_STATE", 1), ("FD_TOD", 4)):
+        nb = ctypes.c_uint64()
+        assert lib.gs_region_bytes(h, _lib.REGION[name], ctypes.byref(nb)) == 0 and nb.value == pairs * per, name
+    nb = ctypes.c_uint64()
+    assert lib.gs_region_bytes(h, _lib.REGION["LATEST"], ctypes.byref(nb)) == 0 and nb.value == 1000 * 16 * 4
+    lib.gs_destroy(h)
+    for over in ({"max_interval_s": 256.0}, {"phi_threshold": 200.0}, {"phi_threshold": 60.0, "max_interval_s": 9.0}):
+        bad = make_config(1000, 16, dict(DEFAULT_CFG, **over), 0, 32)
+        assert lib.gs_create(ctypes.byref(bad), ctypes.byref(h)) == -1, over
+    ok = make_config(1000, 16, dict(DEFAULT_CFG, max_interval_s=255.0, phi_threshold=2.0, window=100), 0, 32)
+    assert lib.gs_create(ctypes.byref(ok), ctypes.byref(h)) == 0
+    lib.gs_destroy(h)
+
+
 def test_sched_delay_rounding():
     from aiocluster_amd.sim import sched_delay_ticks
 
