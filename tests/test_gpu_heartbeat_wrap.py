@@ -87,3 +87,43 @@ def test_heartbeat_lag_sweep_flags_views_near_the_16_bit_bound():
     gpu.check_heartbeat_lag()
     with pytest.raises(GsError, match="err_hb_lag"):
         gpu.check()
+
+
+def test_windows_silent_past_2_15_ticks_decide_exactly():
+    """16-bit last-report ticks (GS_R_FD_LAST): node 7 is down for 700 rounds (44,800 ticks > 2^15), so
+    every window about it and every window of its own row goes unreported past the 2^15-tick bound and
+    is marked old (k_fd_age); liveness decisions (dead while silent, a report after the silence appends
+    no interval) stay exact, and once node 7 is back every window is fresh again: the export matches
+    the C oracle array for array.  Windows are compared mid-silence too, with the old windows' report
+    tick left out (it reads back only as "2^15 ticks or more ago")."""
+    import torch
+
+    n, down0, down1, rounds = 8, 10, 710, 740
+    ids, keys = synthetic_node_ids(n), key_names(2)
+    init = {j: [(0, f"v{j}")] for j in range(n)}
+    gpu = GossipSim(ids, keys, dict(DEFAULT_CFG), "warm", init, tombstones=False, fd_ring=False, hist_cap=8)
+    orc = OracleSim(ids, keys, dict(DEFAULT_CFG), "warm", init)
+    for r in range(rounds):
+        up = np.ones(n, np.uint8)
+        if down0 <= r < down1:
+            up[7] = 0
+        up_dev = torch.from_numpy(up).to(gpu.device)
+        t = round_tick(r)
+        gpu.begin_round(t, up_dev)
+        orc.begin_round(t, up)
+        for p in range(2):
+            pairs = [(a, b) for a, b in SCHED[(r + p) % len(SCHED)] if up[a] and up[b]]
+            gpu.run_phase(phase_tick(r, p), pairs)
+            orc.run_phase(phase_tick(r, p), pairs)
+        gpu.liveness(liveness_tick(r, 2), up_dev)
+        orc.liveness(liveness_tick(r, 2), up)
+        if r == down1 - 1:  # mid-silence: the old windows' tick is the only thing not kept
+            got, want = gpu.export(), orc.export()
+            old = (want["fd_last"] >= 0) & (liveness_tick(r, 2) - want["fd_last"] >= 1 << 15)
+            assert old[:, 7].sum() == n - 1 and old[7].sum() == n - 1
+            got["fd_last"] = np.where(old, want["fd_last"], got["fd_last"])
+            diff = compare_exports(got, want)
+            assert diff is None, f"round {r}: {diff}"
+    diff = compare_exports(gpu.export(), orc.export())
+    assert diff is None, f"after the silence: {diff}"
+    assert gpu.check()["exchanges"] == orc.stats()["exchanges"]
