@@ -103,8 +103,9 @@ def order_events(ev: np.ndarray, n: int, phases: dict, wmap: list) -> np.ndarray
     for tick in np.unique(t[kc]).tolist():
         sel = kc & (t == tick)
         ph = phases.get(tick)
-        if ph is None:  # owner writes
-            k1[sel] = wm[seq[sel]] if len(wm) else seq[sel]
+        if ph is None:  # owner writes (a seq the map does not cover: after every mapped write, in seq order)
+            sq = seq[sel]
+            k1[sel] = np.where(sq < len(wm), wm[np.minimum(sq, len(wm) - 1)], len(wm) + sq) if len(wm) else sq
             continue
         a, b = (np.asarray(x, dtype=np.int64) for x in ph)
         ex = np.full(n, -1, np.int64)
@@ -314,12 +315,13 @@ class GossipSim:
             ticks = {x[0] for x in batch}
             for tick in sorted(ticks):
                 rows = [[j, k, op, vid, vl] for t, j, k, op, vid, vl, _ in batch if t == tick]
-                self.owner_writes(np.asarray(rows, dtype=np.uint32), tick)
-                if self._ev is not None:  # gs_set_events: op i of this call has seq = ops issued before + i
-                    self._ev_wmap += [w for t, *_, w in batch if t == tick]
+                self.owner_writes(np.asarray(rows, dtype=np.uint32), tick,
+                                  order=[w for t, *_, w in batch if t == tick])
 
-    def owner_writes(self, ops: np.ndarray, tick: int):
-        """Device batch of owner writes; ``ops`` is uint32 [m, 5] (owner, key, op, value_id, value_len)."""
+    def owner_writes(self, ops: np.ndarray, tick: int, order: list[int] | None = None):
+        """Device batch of owner writes; ``ops`` is uint32 [m, 5] (owner, key, op, value_id, value_len).
+        ``order``: each op's index among the caller's writes (hook-event order); default: after every
+        write so far, in row order."""
         if len(ops) == 0:
             return
         ops = np.ascontiguousarray(ops, dtype=np.uint32)
@@ -327,6 +329,11 @@ class GossipSim:
             raise GsError("owner_writes: owners must be distinct within one batch")
         d = self._dev(ops.view(np.int32), self.torch.int32)
         self._chk(self.L.gs_owner_writes(self.h, C.c_void_p(d.data_ptr()), len(ops), tick), "gs_owner_writes")
+        if self._ev is not None:  # gs_set_events: op i of this call has seq = ops issued before + i
+            if order is None:
+                order = list(range(self._ev_writes, self._ev_writes + len(ops)))
+                self._ev_writes += len(ops)
+            self._ev_wmap += list(order)
 
     # --------------------------------------------------------------- round driver
     def begin_round(self, t: int, up):
