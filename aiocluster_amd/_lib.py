@@ -41,6 +41,11 @@ def slice_columns(n: int, shards: int, shard: int) -> tuple[int, int]:
     return lo, min(blk, n - lo)
 
 
+def overflow_list_len(n: int) -> int:
+    """u32 words of gs_phase_overflow's list for a phase of ``n`` exchanges (GS_OVERFLOW_LIST_LEN)."""
+    return 2 * n + (2 * n + 1023) // 1024 + 1
+
+
 def fd_sum_bits(window: int) -> int:
     """Bits of the packed window's interval sum (include/gossip_sim.h, GS_R_FD)."""
     cnt_bits = 1
@@ -51,7 +56,7 @@ def fd_sum_bits(window: int) -> int:
 REGIONS = [
     "HB", "MV", "GC", "HELD", "FD", "FD_STATE", "TS", "RING", "POS", "ORD", "ROW",
     "LAST_W", "HIST", "HIST_VID", "NID_SIZE", "KEY_LEN", "STAMP", "COUNTERS", "SLICE_BITS", "PEND", "PEND_STAMP", "LATEST",
-    "SELF_HB", "CAND", "CAND_N", "FD_TOD", "FD_LAST",
+    "SELF_HB", "CAND", "CAND_N", "FD_TOD", "FD_LAST", "SLOT_STAT", "RING_SLOT",
 ]
 REGION = {n: i for i, n in enumerate(REGIONS)}
 
@@ -61,6 +66,7 @@ COUNTER_FIELDS = [
     "exchanges", "hb_reports", "node_deltas", "kvs_sent", "truncated", "delta_bytes", "alg_bytes", "hb_writes",
     "candidates", "live_pairs", "tomb_gc", "err_fd_overflow", "err_hist_full", "err_bad_index", "err_conflict",
     "err_fd_gc", "err_insert", "fd_gc", "q9", "pack_bytes", "err_holes", "err_hb_lag", "plane_flushes",
+    "fd_saturated",
 ]
 
 # Every symbol include/gossip_sim.h declares (checked by tests/test_abi.py).
@@ -71,10 +77,10 @@ EXPORTS = [
     "gs_select_peers", "gs_schedule_phases", "gs_set_events", "gs_emit_scratch_bytes", "gs_emit_digest", "gs_emit_delta",
     "gs_check_heartbeat_lag", "gs_stream_copy", "gs_stream_read", "gs_stream_write", "gs_set_timing", "gs_kernel_times",
     "gs_phase_overflow", "gs_phase_chain", "gs_comm_id", "gs_comm_init", "gs_run_phase_group", "gs_read_rows",
-    "gs_latest_tick",
+    "gs_latest_tick", "gs_flush_reports", "gs_set_ring_rows",
 ]
 
-API_VERSION = 10
+API_VERSION = 11
 MAX_PHASES = 64  # GS_MAX_PHASES
 
 
@@ -94,6 +100,7 @@ class GsConfig(C.Structure):
         ("prior_weighted", C.c_double),
         ("n_shards", C.c_uint32),
         ("shard", C.c_uint32),
+        ("ring_rows", C.c_uint32),
     ]
 
 
@@ -123,15 +130,33 @@ class GsError(RuntimeError):
     pass
 
 
+def source_hash() -> str:
+    """SHA-256 of the HIP source, the header and the compile flags: what the built library is stamped with."""
+    import hashlib
+
+    h = hashlib.sha256(" ".join(HIPCC_FLAGS).encode())
+    for f in (SRC, HEADER):
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
-    """Compile the HIP library for gfx950 in-tree (cross-compiles without a GPU)."""
+    """Compile the HIP library for gfx950 in-tree (cross-compiles without a GPU).  Rebuilds whenever the
+    sources' hash differs from the one stamped next to the library (LIB_PATH + ".srchash")."""
     os.makedirs(LIB_DIR, exist_ok=True)
-    newest = max(os.path.getmtime(SRC), os.path.getmtime(HEADER))
-    if force or not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < newest:
-        cmd = ["hipcc", *HIPCC_FLAGS, "-o", LIB_PATH, SRC, "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
+    stamp = LIB_PATH + ".srchash"
+    want = source_hash()
+    have = open(stamp).read().strip() if os.path.exists(stamp) else None
+    if force or not os.path.exists(LIB_PATH) or have != want:
+        tmp = LIB_PATH + ".tmp"
+        cmd = ["hipcc", *HIPCC_FLAGS, "-o", tmp, SRC, "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
         if verbose:
             print(" ".join(cmd))
         subprocess.run(cmd, check=True)
+        os.replace(tmp, LIB_PATH)
+        with open(stamp, "w") as fh:
+            fh.write(want + "\n")
     return LIB_PATH
 
 
@@ -174,6 +199,8 @@ def load():
         "gs_run_phase_group": (C.c_int, [P, u32, P, P, u32, u32]),
         "gs_read_rows": (C.c_int, [P, C.c_int, u32, u32, P, u64, C.POINTER(u64)]),
         "gs_latest_tick": (C.c_int, [P, C.POINTER(u32)]),
+        "gs_flush_reports": (C.c_int, [P, u32]),
+        "gs_set_ring_rows": (C.c_int, [P, P, u32]),
         "gs_kernel_times": (C.c_int, [P, C.POINTER(GsKtimes)]),
         "gs_sync": (C.c_int, [P]),
         "gs_shard_columns": (C.c_int, [P, C.POINTER(u32), C.POINTER(u32)]),

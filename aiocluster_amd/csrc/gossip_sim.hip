@@ -55,16 +55,26 @@ constexpr int LB = 256;  // liveness / elementwise workgroups
 #endif
 constexpr int NSHARD = 64;
 constexpr uint32_t WIN = 16 * 64;  // positions per packer window (16 per lane)
+// KW of the kernels for K > 16 keys (up to 64).  Those instantiations take most of the build time; a
+// development build with -DGS_KW4_ONLY (tools/build_dev.sh) leaves them out and refuses K > 16.
+#ifdef GS_KW4_ONLY
+constexpr int KWB = 4;
+#else
+constexpr int KWB = 16;
+#endif
+constexpr uint32_t NPL = GS_PLANES;  // report bit planes per observer row (phases per plane base)
+static_assert(NPL == 16 || NPL == 32, "k_liveness stages 16 or 32 planes");
 constexpr double TICK_S = 1.0 / 64.0;
 constexpr uint32_t HB_LAG_CHECK_EVERY = 1u << 14;  // round starts + phases between heartbeat-lag sweeps
 
 enum Ctr {
     C_EXCH = 0, C_REPORTS, C_ND, C_KVS, C_TRUNC, C_DBYTES, C_ALG, C_HBW, C_CAND, C_LIVE, C_TOMBGC,
     C_E_FDOVF, C_E_HIST, C_E_IDX, C_E_CONFLICT, C_E_FDGC, C_E_INSERT, C_FDGC, C_Q9, C_PACKB, C_E_HOLES,
-    C_E_HBLAG, C_FLUSH /* host-side: plane_flushes */,
+    C_E_HBLAG, C_FLUSH /* host-side: plane_flushes */, C_FDSAT,
     C_CEN0 = 24, C_NUM = C_CEN0 + 6  // gs_fd_census scratch slots (not part of gs_counters)
 };
 static_assert(C_NUM <= 32, "counter region");
+static_assert(C_FDSAT < C_CEN0, "gs_counters fields before the census scratch");
 static_assert(sizeof(gs_counters) == 32 * 8, "gs_counters layout");
 
 struct Dev {
@@ -100,15 +110,25 @@ struct Dev {
     uint2 *cand;       // split phases: stale-owner records [e][dir][half][GS_CAND_CAP] (GS_R_CAND)
     uint32_t *cand_n;  // [e][dir][half] stale owners found (GS_R_CAND_N)
     // heartbeat reports of the current round not yet applied to the windows: one bit plane per phase
-    // p (tick t_round + 1 + p) and observer row, [N][16][PW] u64 in quad-interleaved column order
+    // p (tick t_round + 1 + p) and observer row, [N][NPL][PW] u64 in quad-interleaved column order
     // (plane_word/plane_bit); a plane row is valid only if pstamp[o][p] holds that phase's tick
     uint64_t *pend;
-    uint32_t *pstamp;  // [N][16]
+    uint32_t *pstamp;  // [N][NPL]
     uint32_t PW;       // u64 words per plane row: NP rounded up to 256, / 64
-    // plane base: the tick of the last gs_begin_round, or, once a round has run phases more than 16
+    // plane base: the tick of the last gs_begin_round, or, once a round has run phases more than NPL
     // ticks after it (the planes were replayed into the windows mid-round), the tick before the
     // first phase after that replay; plane p holds the phase at tick t_round + 1 + p
     uint32_t t_round;
+    // speculative max-version merge (canonical record phases): pass 1 already wrote
+    // max(sender, receiver) into the receiver's max_version word of every recorded candidate whose two
+    // views are prefix views; the packers restore the receiver's word of such a candidate when it is not
+    // sent, and skip the store when it is sent whole.  Set per phase by the host (gs_run_phase /
+    // gs_phase_count), identical in every kernel of the phase.
+    uint32_t spec;
+    uint4 *slot_stat;
+    // sampled rings (gs_config.ring_rows): ring slot of each observer row (NONE: a compact row), GS_R_RING
+    // then holds [ring_rows][NP][W]; nullptr otherwise
+    uint32_t *ring_slot;  // sliced phases: per (exchange, direction) {NodeDeltas, kvs, candidates, needs a pack}
     // event stream (gs_set_events): records {observer, owner, key | kind << 8, old version, new version,
     // tick, seq, 0}; kind 0 = on_key_change, 1 = node join, 2 = node leave; seq orders them (gossip_sim.h,
 // gs_set_events).  ev == nullptr: off
@@ -404,16 +424,20 @@ __device__ __forceinline__ void eval_cand(const Dev &d, uint32_t s, uint32_t r, 
 // sender's kvs with from < version <= vmax, last_gc c.gs, max_version c.ms}.  Keys are
 // independent (kvs arrive in version order, so "version <= max_version" only ever compares
 // against the view's max_version before the delta, 209-210).
+// specd: pass 1 already stored max(ms, mr) for this candidate (Dev::spec; its record's words are the
+// pre-exchange ones, which every path below starts from).
 template <int KW>
 __device__ __forceinline__ void apply_cand(const Dev &d, uint32_t s, uint32_t r, const Cand<KW> &c, uint32_t vmax, uint32_t t,
-                                  bool &tomb, uint32_t &alg) {
+                                  bool &tomb, uint32_t &alg, bool specd = false) {
     const size_t pr = pix(d, r, c.j);
     if (c.fast && vmax == NONE && !d.ev) {
         // prefix sender, prefix receiver, whole NodeDelta: the view becomes S_j(max(mr, ms)) (keys
         // above mr move to the sender's latest write <= ms, the others already are), still a prefix.
         // ms <= mr happens when the receiver's digest left j out (scheduled for deletion: from = 0)
-        d.mv[pr] = (uint16_t)(c.ms > c.mr ? c.ms : c.mr);
-        alg += 4;
+        if (!specd) {
+            d.mv[pr] = (uint16_t)(c.ms > c.mr ? c.ms : c.mr);
+            alg += 4;
+        }
         return;
     }
     uint32_t g = c.gr;
@@ -507,10 +531,12 @@ struct PackState {
 // COUNT: only sum the DeltaPb bytes of every candidate (owner-sharded runs: the slice total).
 // REC: record the selected NodeDeltas {owner, vsel} in sender order into rec[] (nr so far)
 // instead of applying them (the wire-format emitter, gs_emit_delta).
+// specd: the group's candidates come from pass 1's records of a speculative phase (Dev::spec): a prefix
+// candidate (c.fast) sent whole is already applied, one not sent gets its receiver's word restored.
 template <int KW, bool COUNT, bool REC>
 __device__ __forceinline__ void pack_group(const Dev &d, uint32_t s, uint32_t r, uint32_t t, const Cand<KW> &c, bool cand,
                                            uint32_t &S, bool &tail, bool &stop, WStats &st, bool &tomb, uint2 *rec,
-                                           uint32_t &nr) {
+                                           uint32_t &nr, bool specd = false) {
     const int lane = lane_id();
     const uint32_t mtu = d.mtu;
     const uint32_t em = cand ? c.emsg : 0u;
@@ -606,7 +632,7 @@ __device__ __forceinline__ void pack_group(const Dev &d, uint32_t s, uint32_t r,
     }
     // apply_delta at the receiver: one lane per NodeDelta, distinct owners, any order
     if (vsel) {
-        apply_cand<KW>(d, s, r, c, vsel, t, tomb, st.alg);
+        apply_cand<KW>(d, s, r, c, vsel, t, tomb, st.alg, specd);
         st.nd++;
         if (vsel == NONE) {
             st.kvs += c.nkv;
@@ -614,6 +640,9 @@ __device__ __forceinline__ void pack_group(const Dev &d, uint32_t s, uint32_t r,
             st.kvs += nsel;
             st.trunc++;
         }
+    } else if (specd && cand && c.fast) {
+        d.mv[pix(d, r, c.j)] = (uint16_t)c.mr;  // not sent: undo pass 1's merge (a prefix view: no flag bit)
+        st.alg += 4;
     }
 }
 
@@ -625,13 +654,13 @@ __device__ __forceinline__ void pack_begin(const Dev &d, bool count, const PackS
     if (!count && !stop && (S >= d.mtu || d.mtu - S < d.lb_min)) stop = true;
 }
 
-// Bitmap source: positions [p0, cnt) of the sender's dict order (p0 = 0 in the general layout; a
-// multiple of 256 otherwise).
+// Bitmap source: positions [max(p0, pmin), cnt) of the sender's dict order (p0 = 0 in the general
+// layout; a multiple of 256 otherwise; pmin > p0: the positions before it came from pass 1's records).
 template <int KW, bool GENM, bool COUNT, bool REC = false>
 __device__ __forceinline__ void pack_dir(const Dev &d, uint32_t s, uint32_t r, const DigestSide ds,
                                          const uint32_t *order, uint32_t cnt, const uint32_t *bits, uint16_t *wbuf,
                                          uint32_t t, WStats &st, bool &tomb, PackState &pst, uint2 *rec = nullptr,
-                                         uint32_t *nrec = nullptr, uint32_t p0 = 0) {
+                                         uint32_t *nrec = nullptr, uint32_t p0 = 0, uint32_t pmin = 0) {
     const int lane = lane_id();
     const uint32_t S0 = pst.S;
     uint32_t S;
@@ -663,6 +692,7 @@ __device__ __forceinline__ void pack_dir(const Dev &d, uint32_t s, uint32_t r, c
             }
             const uint32_t lim = cnt - pb;
             if (lim < 16) m &= (1u << lim) - 1u;
+            if (pb < pmin) m &= pmin - pb >= 16u ? 0u : ~((1u << (pmin - pb)) - 1u);
         }
         const uint32_t cl = (uint32_t)__popc(m);
         const uint32_t incl = wave_incl_scan(cl);
@@ -717,9 +747,14 @@ __device__ __forceinline__ void pack_dir(const Dev &d, uint32_t s, uint32_t r, c
     if (!COUNT && lane == 0) shard_add(d, C_DBYTES, S - S0);  // DeltaPb bytes this call added
 }
 
-// List source (canonical, one slice): the n stale owners pass 1 recorded for one row half, in column
+// both views of a record are prefix views (GS_MV_INEXACT clear in both words): the candidates pass 1
+// merged speculatively (Dev::spec)
+__device__ inline bool rec_fast(uint32_t mvw) { return !(mvw & (MV_INEXACT | (MV_INEXACT << 16))); }
+
+// List source (canonical records): the n stale owners pass 1 recorded for one row half, in column
 // order, each with both views' max_version words (GS_R_CAND), so no row is read again.  The next
-// group's records are loaded one group ahead.
+// group's records are loaded one group ahead.  Dev::spec: once the delta is complete, the remaining
+// prefix candidates' receiver words are restored (pass 1 merged them).
 template <int KW, bool COUNT = false>
 __device__ __forceinline__ void pack_list(const Dev &d, uint32_t s, uint32_t r, const DigestSide ds, const uint2 *L,
                                           uint32_t n, uint32_t t, WStats &st, bool &tomb, PackState &pst) {
@@ -728,14 +763,19 @@ __device__ __forceinline__ void pack_list(const Dev &d, uint32_t s, uint32_t r, 
     uint32_t S;
     bool tail, stop;
     pack_begin(d, COUNT, pst, S, tail, stop);
+    const bool specd = !COUNT && d.spec;
     uint32_t nr = 0;
     uint2 nxt = make_uint2(0u, 0u);
     if ((uint32_t)lane < n) nxt = L[lane];
-    for (uint32_t c0 = 0; c0 < n && !stop; c0 += WAVE) {
+    for (uint32_t c0 = 0; c0 < n && (specd || !stop); c0 += WAVE) {
         const uint32_t ci = c0 + lane;
         const bool cand = ci < n;
         const uint2 cr = nxt;
         if (ci + WAVE < n) nxt = L[ci + WAVE];
+        if (stop) {  // specd only: nothing more is sent
+            if (cand && rec_fast(cr.y)) { d.mv[pix(d, r, cr.x)] = (uint16_t)(cr.y >> 16); st.alg += 4; }
+            continue;
+        }
         Cand<KW> c;
         c.emsg = 0;
         c.min1 = 0;
@@ -744,7 +784,7 @@ __device__ __forceinline__ void pack_list(const Dev &d, uint32_t s, uint32_t r, 
             eval_cand<KW, false, true>(d, s, r, ds, cr.x, t, c, ck, st.alg, cr.y);
             st.cand++;
         }
-        pack_group<KW, COUNT, false>(d, s, r, t, c, cand, S, tail, stop, st, tomb, nullptr, nr);
+        pack_group<KW, COUNT, false>(d, s, r, t, c, cand, S, tail, stop, st, tomb, nullptr, nr, specd);
     }
     pst.S = S;
     pst.tail = tail;
@@ -752,21 +792,24 @@ __device__ __forceinline__ void pack_list(const Dev &d, uint32_t s, uint32_t r, 
     if (!COUNT && lane == 0) shard_add(d, C_DBYTES, S - S0);
 }
 
-// Candidates of one direction of exchange slot from pass 1's records (row half 0, then half 1), or
-// the bitmap walk for a half whose records overflowed GS_CAND_CAP.
+// Candidates of one direction of exchange slot from pass 1's records (row half 0, then half 1); a half
+// with more stale owners than GS_CAND_CAP continues in the bitmap after its last record (those owners
+// were not merged speculatively: the bitmap walk reads their rows).
 template <int KW, bool COUNT>
 __device__ __forceinline__ void pack_records(const Dev &d, uint32_t snd, uint32_t rcv, const DigestSide &ds,
                                              size_t slot, uint16_t *wbuf, uint32_t t, WStats &st, bool &tomb,
                                              PackState &pst) {
     const uint32_t H = ((d.ncol + 1u) / 2u + 255u) & ~255u;
     const uint32_t words = d.NP / 32;
-    for (uint32_t hf = 0; hf < 2 && (COUNT || !pst.stop); hf++) {
+    for (uint32_t hf = 0; hf < 2 && (COUNT || d.spec || !pst.stop); hf++) {
         const uint32_t nh = d.cand_n[slot * 2 + hf];
-        if (nh <= GS_CAND_CAP)
-            pack_list<KW, COUNT>(d, snd, rcv, ds, d.cand + (slot * 2 + hf) * GS_CAND_CAP, nh, t, st, tomb, pst);
-        else
+        const uint2 *L = d.cand + (slot * 2 + hf) * GS_CAND_CAP;
+        pack_list<KW, COUNT>(d, snd, rcv, ds, L, min(nh, GS_CAND_CAP), t, st, tomb, pst);
+        if (nh > GS_CAND_CAP && (COUNT || !pst.stop)) {
+            const uint32_t pmin = L[GS_CAND_CAP - 1].x + 1u;  // wave-uniform load
             pack_dir<KW, false, COUNT>(d, snd, rcv, ds, nullptr, min(H * (hf + 1), d.ncol), d.sbits + (slot * words),
-                                       wbuf, t, st, tomb, pst, nullptr, nullptr, H * hf);
+                                       wbuf, t, st, tomb, pst, nullptr, nullptr, pmin & ~15u, pmin);
+        }
     }
 }
 
@@ -867,13 +910,12 @@ __device__ __forceinline__ void dec_grp(const GrpRaw &r, Grp &g) {
 // FailureDetector.report_heartbeat -> SamplingWindow.report_heartbeat on one unpacked window
 // (failure_detector.py:79-81, 32-38): the first report only records the time; later intervals
 // <= max_interval go to BoundedArrayStats (139-150).
-template <bool RING>
-__device__ __forceinline__ Fd fd_report_val(const Dev &d, size_t p, uint32_t t, Fd f, uint32_t &alg, uint32_t &ovf) {
+// rg: this pair's interval ring (GS_FD_RING, or a sampled ring row), nullptr for a compact window.
+__device__ __forceinline__ Fd fd_report_val(const Dev &d, uint16_t *rg, uint32_t t, Fd f, uint32_t &alg, uint32_t &ovf) {
     if (f.last != NONE) {
         const uint32_t iv = t - f.last;
         if (iv <= d.max_iv) {
-            if (RING) {
-                uint16_t *rg = d.ring + p * d.W;
+            if (rg) {
                 const uint32_t slot = f.cnt % d.W;
                 if (f.cnt >= d.W) f.sum -= rg[slot];  // subtract-then-add (failure_detector.py:140-143)
                 rg[slot] = (uint16_t)iv;
@@ -993,8 +1035,9 @@ __device__ __forceinline__ uint32_t spread8(uint32_t x) {
 //    needs clearing; the first lane of each 8 stores its word: 32 contiguous bytes per wave;
 //  * as records {column, sender max_version word | receiver max_version word << 16} appended in
 //    column order to the wave's list L (the first GS_CAND_CAP of them; cnt counts all, wave-uniform).
-__device__ __forceinline__ void emit_dir(uint32_t *gw, uint2 *L, uint32_t &cnt, uint32_t c0, uint32_t nib,
-                                         const uint32_t (&ms)[4], const uint32_t (&mr)[4], uint32_t &alg) {
+// Returns the lane's recorded columns (bit i: column c0 + i got a record).
+__device__ __forceinline__ uint32_t emit_dir(uint32_t *gw, uint2 *L, uint32_t &cnt, uint32_t c0, uint32_t nib,
+                                             const uint32_t (&ms)[4], const uint32_t (&mr)[4], uint32_t &alg) {
     const uint64_t b0 = __ballot(nib & 1u), b1 = __ballot(nib & 2u), b2 = __ballot(nib & 4u), b3 = __ballot(nib & 8u);
     const int l = lane_id();
     const bool any = (b0 | b1 | b2 | b3) != 0ull;
@@ -1005,17 +1048,47 @@ __device__ __forceinline__ void emit_dir(uint32_t *gw, uint2 *L, uint32_t &cnt, 
         gw[c0 >> 5] = w;
         alg += 4;
     }
-    if (!any) return;
+    if (!any) return 0u;
     const uint64_t lt = (1ull << l) - 1ull;
     uint32_t off = cnt + (uint32_t)(__popcll(b0 & lt) + __popcll(b1 & lt) + __popcll(b2 & lt) + __popcll(b3 & lt));
+    uint32_t recm = 0u;
 #pragma unroll
     for (int i = 0; i < 4; i++) {
         if ((nib >> i) & 1u) {
-            if (off < GS_CAND_CAP) { L[off] = make_uint2(c0 + i, (ms[i] & 0xFFFFu) | (mr[i] << 16)); alg += 8; }
+            if (off < GS_CAND_CAP) {
+                L[off] = make_uint2(c0 + i, (ms[i] & 0xFFFFu) | (mr[i] << 16));
+                alg += 8;
+                recm |= 1u << i;
+            }
             off++;
         }
     }
     cnt += (uint32_t)(__popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3));
+    return recm;
+}
+
+// Speculative apply (Dev::spec): every recorded candidate whose two views are prefix views gets
+// max(sender, receiver) as the receiver's max_version now, in the row group pass 1 just loaded (an
+// 8-byte store into a line still in L2 -- instead of a scattered 2-byte store per NodeDelta later).  A
+// delta that fits the mtu sends all of them whole, which is exactly apply_delta's result for a prefix
+// view (apply_cand's fast path); the packers restore the receiver's word of the others.
+__device__ __forceinline__ void spec_merge(const Dev &d, size_t ra, size_t rb, uint32_t c0, uint32_t recBA,
+                                           uint32_t recAB, const uint32_t (&mA)[4], const uint32_t (&mB)[4],
+                                           uint32_t &alg) {
+    uint32_t nA[4], nB[4];
+    bool wA = false, wB = false;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const bool fast = !((mA[i] | mB[i]) & MV_INEXACT);
+        const uint32_t mx = mA[i] > mB[i] ? mA[i] : mB[i];
+        const bool ba = fast && ((recBA >> i) & 1u), ab = fast && ((recAB >> i) & 1u);
+        nA[i] = ba ? mx : mA[i];
+        nB[i] = ab ? mx : mB[i];
+        wA = wA || ba;
+        wB = wB || ab;
+    }
+    if (wA) { st4h(d.mv + ra + c0, nA); alg += 8; }
+    if (wB) { st4h(d.mv + rb + c0, nB); alg += 8; }
 }
 
 // Owner-column sharded phases ("multi-GPU"): the count pass leaves each exchange's
@@ -1054,10 +1127,13 @@ __device__ inline PackState chain_unpack(uint64_t v) {
 #ifndef P1S_WAVES
 #define P1S_WAVES 4  // waves per SIMD of the pass-1-only kernel (split phases, sliced count pass); 5 spills and measured slower (r2r)
 #endif
-template <int KW, bool FUSE>
+// SPEC (not with FUSE): the speculative max-version merge of the recorded prefix candidates (spec_merge,
+// Dev::spec); k_settle then only settles the deltas that do not fit and the candidates with holes.
+template <int KW, bool FUSE, bool SPEC = false>
 __global__ __launch_bounds__(XB, (KW == 4 ? (FUSE ? P1_WAVES : P1S_WAVES) : 1)) void k_pass1(Dev d, const int32_t *ini, const int32_t *res,
                                                                        uint32_t n, uint32_t t, uint32_t seq,
                                                                        uint32_t e0) {
+    static_assert(!(FUSE && SPEC), "the fused packer applies every NodeDelta itself");
     const uint32_t e = e0 + blockIdx.x;  // exchanges [e0, e0 + grid) of the phase (one chunk)
     if (e >= n) return;
     const int tid = threadIdx.x, lane = tid & (WAVE - 1), wid = tid >> 6;
@@ -1086,11 +1162,11 @@ __global__ __launch_bounds__(XB, (KW == 4 ? (FUSE ? P1_WAVES : P1S_WAVES) : 1)) 
     uint32_t alg = 0, reports = 0, hbw = 0;
     bool anynew = false;
     const uint32_t ph = t - d.t_round - 1u;
-    uint64_t *planeA = d.pend + ((size_t)a * 16u + ph) * d.PW;
-    uint64_t *planeB = d.pend + ((size_t)b * 16u + ph) * d.PW;
+    uint64_t *planeA = d.pend + ((size_t)a * NPL + ph) * d.PW;
+    uint64_t *planeB = d.pend + ((size_t)b * NPL + ph) * d.PW;
     if (tid == 0) {
-        d.pstamp[a * 16u + ph] = t;
-        d.pstamp[b * 16u + ph] = t;
+        d.pstamp[a * NPL + ph] = t;
+        d.pstamp[b * NPL + ph] = t;
     }
     // responder inc_heartbeat (server.py:524): the owner's own heartbeat R is raised once, here; the
     // view hb[b][b] is raised in the loop.  Other exchanges of the phase decode column b against R or
@@ -1122,8 +1198,9 @@ __global__ __launch_bounds__(XB, (KW == 4 ? (FUSE ? P1_WAVES : P1S_WAVES) : 1)) 
             anynew = anynew || (nNB | nNA) != 0u;
             store_plane(planeA, c0, rmA, alg);
             store_plane(planeB, c0, rmB, alg);
-            emit_dir(gBA, LBA, nBAc, c0, nBA, mB, mA, alg);  // b -> a: sender b, receiver a
-            emit_dir(gAB, LAB, nABc, c0, nAB, mA, mB, alg);
+            const uint32_t recBA = emit_dir(gBA, LBA, nBAc, c0, nBA, mB, mA, alg);  // b -> a: sender b, receiver a
+            const uint32_t recAB = emit_dir(gAB, LAB, nABc, c0, nAB, mA, mB, alg);
+            if (SPEC && (recBA | recAB)) spec_merge(d, ra, rb, c0, recBA, recAB, mA, mB, alg);
             r0 = r1;
             if (P1_AHEAD > 1) r1 = r2;
             c0 = c1;
@@ -1209,12 +1286,12 @@ __global__ __launch_bounds__(XB, (KW == 4 ? XB_WAVES : 1)) void k_exchange(Dev d
     const size_t ra = (size_t)a * d.NP, rb = (size_t)b * d.NP;
     uint32_t alg = 0, reports = 0, hbw = 0;
     bool anynew = false;
-    const uint32_t ph = t - d.t_round - 1u;  // phase of this round (host-checked: < 16)
-    uint64_t *planeA = d.pend + ((size_t)a * 16u + ph) * d.PW;
-    uint64_t *planeB = d.pend + ((size_t)b * 16u + ph) * d.PW;
+    const uint32_t ph = t - d.t_round - 1u;  // phase of this round (host-checked: < NPL)
+    uint64_t *planeA = d.pend + ((size_t)a * NPL + ph) * d.PW;
+    uint64_t *planeB = d.pend + ((size_t)b * NPL + ph) * d.PW;
     if (tid == 0) {  // both plane rows are rewritten below: valid for this phase
-        d.pstamp[a * 16u + ph] = t;
-        d.pstamp[b * 16u + ph] = t;
+        d.pstamp[a * NPL + ph] = t;
+        d.pstamp[b * NPL + ph] = t;
     }
     // software-pipelined: the next group's loads are in flight while this group computes and stores
     // (different owners, so the early loads never read a location this group writes)
@@ -1403,9 +1480,9 @@ __global__ __launch_bounds__(XB, (KW == 4 ? PK_WAVES : 1)) void k_pack_slice(Dev
 // Overflowing slots of a sliced phase (gs_phase_overflow): every (exchange, direction) slot whose slice
 // totals sum past the mtu, in slot order -- the same list on every slice, since all hold the same
 // gathered totals -- plus this slice's chain state of each listed slot (chainc[i] = chain[list[i]]).
-// Two launches of 1024-thread blocks: per-block counts, then per-block offsets (a sum over at most a
-// few dozen block counts) and a ballot scan inside the block.  scratch = list + 2n: [blocks] counts,
-// then the total.
+// Two launches of 1024-thread blocks: per-block counts, then per-block offsets (a sum over the block
+// counts: ceil(2n / 1024) of them) and a ballot scan inside the block.  scratch = list + 2n: [blocks]
+// counts, then the total -- GS_OVERFLOW_LIST_LEN(n) words in all.
 constexpr uint32_t OVB = 1024;
 __global__ __launch_bounds__(OVB) void k_ov_count(const uint64_t *tot_all, uint32_t slots, uint32_t G, uint32_t mtu,
                                                   uint32_t *blkcnt) {
@@ -1447,6 +1524,20 @@ __global__ __launch_bounds__(OVB) void k_ov_write(const uint64_t *tot_all, uint3
         list[i] = sl;
         chainc[i] = chain[sl];
     }
+}
+
+// In-process all-gather (gs_run_phase_group: every slice on one device and stream): dst[i][g * count + k]
+// = src[g][k] for every destination slice i (grid.y) -- one launch instead of G^2 copies.
+constexpr uint32_t GATHER_MAX = 64;
+struct GatherPtrs {
+    const uint64_t *src[GATHER_MAX];
+    uint64_t *dst[GATHER_MAX];
+};
+__global__ __launch_bounds__(LB) void k_gather_u64(GatherPtrs p, uint32_t G, uint64_t count) {
+    uint64_t *dst = p.dst[blockIdx.y];
+    const uint64_t total = (uint64_t)G * count;
+    for (uint64_t x = (uint64_t)blockIdx.x * LB + threadIdx.x; x < total; x += (uint64_t)gridDim.x * LB)
+        dst[x] = p.src[x / count][x % count];
 }
 
 // Chain step `step` >= 1 over the overflowing slots only (gs_phase_chain): one wave per listed slot; a
@@ -1491,13 +1582,78 @@ __global__ __launch_bounds__(WAVE) void k_chain_step(Dev d, const int32_t *ini, 
     }
 }
 
-// Sharded count pass, after k_pass1 on a sliced handle (gs_phase_count): the DeltaPb bytes of every
-// stale owner of this slice per exchange and direction (wave 0: b -> a, wave 1: a -> b), from pass 1's
-// candidate records, into tot[e][dir].  (Sizing every record with 4 waves per slot and handing the sizes
-// to the packer measured slower at 8 slices: 0.53 vs 0.45 ms per slice and phase, profiles/r2h.)
+// The settle pass of a speculative phase, per (exchange, direction) slot: every record's NodeDelta is
+// evaluated (eval_cand: DeltaPb bytes, kvs), independently -- no sequential budget walk, so the loads of
+// a wave's groups overlap -- giving the slot's DeltaPb total T and, if the delta fits, its statistics.
+// clean: every candidate was recorded and merged by pass 1 (no candidate with holes, no bitmap tail).
+struct SlotSum {
+    unsigned long long T;
+    uint32_t nd, kvs, cand;
+    bool clean;
+};
 template <int KW>
-__global__ __launch_bounds__(XB, (KW == 4 ? PK_WAVES : 1)) void k_count(Dev d, const int32_t *ini, const int32_t *res,
-                                                                       uint32_t n, uint32_t t, uint64_t *tot) {
+__device__ __forceinline__ SlotSum settle_sum(const Dev &d, uint32_t snd, uint32_t rcv, const DigestSide &ds,
+                                              size_t slot, uint16_t *wbuf, uint32_t t, uint32_t &alg) {
+    const int lane = lane_id();
+    uint32_t T = 0, nd = 0, kvs = 0, cand = 0;
+    bool clean = true;
+    unsigned long long tail = 0;
+    for (uint32_t hf = 0; hf < 2; hf++) {
+        const uint32_t nh = d.cand_n[slot * 2 + hf], m = min(nh, GS_CAND_CAP);
+        const uint2 *L = d.cand + (slot * 2 + hf) * GS_CAND_CAP;
+#pragma unroll 2
+        for (uint32_t c0 = 0; c0 < m; c0 += WAVE) {
+            const uint32_t ci = c0 + lane;
+            if (ci < m) {
+                const uint2 cr = L[ci];
+                Cand<KW> c;
+                CandKeys<KW> ck;
+                eval_cand<KW, false, true>(d, snd, rcv, ds, cr.x, t, c, ck, alg, cr.y);
+                T += c.emsg;
+                nd += c.emsg ? 1u : 0u;
+                kvs += c.nkv;
+                cand++;
+                clean = clean && c.fast;
+            }
+        }
+        if (nh > GS_CAND_CAP) {  // the bitmap tail: its owners are not merged, the pack walks them
+            const uint32_t H = ((d.ncol + 1u) / 2u + 255u) & ~255u, words = d.NP / 32;
+            const uint32_t pmin = L[GS_CAND_CAP - 1].x + 1u;
+            WStats cs{0, 0, 0, 0, 0};
+            bool ctomb = false;
+            PackState pst{0u, false, false};
+            pack_dir<KW, false, true>(d, snd, rcv, ds, nullptr, min(H * (hf + 1), d.ncol), d.sbits + (slot * words),
+                                      wbuf, t, cs, ctomb, pst, nullptr, nullptr, pmin & ~15u, pmin);
+            tail += pst.S;
+            alg += cs.alg;
+            clean = false;
+        }
+    }
+    SlotSum r;
+    r.T = wave_sum(T) + tail;
+    r.nd = (uint32_t)wave_sum(nd);
+    r.kvs = (uint32_t)wave_sum(kvs);
+    r.cand = (uint32_t)wave_sum(cand);
+    r.clean = __ballot(!clean) == 0ull;
+    return r;
+}
+
+// Phase completion after k_pass1 on canonical record handles, one wave per (exchange, direction) slot
+// (wave 0: the SynAck delta b -> a, wave 1: the Ack delta a -> b):
+//   MODE 0 (one slice, gs_run_phase): a speculative phase whose delta fits (T <= mtu) and is clean is
+//          complete -- pass 1 applied it -- and only its statistics are added; any other slot runs the
+//          sequential packer (pack_records: exact first-fit, restores of the merged candidates it does
+//          not send, applies of the rest); a non-speculative phase always does.
+//   MODE 1 (sliced count, gs_phase_count): the slot's DeltaPb total of this slice into io.tot (and, when
+//          speculative, its statistics into slot_stat for MODE 2).
+//   MODE 2 (sliced pack step 0, gs_phase_pack): the slice resumes the sender-order walk at the bytes
+//          its predecessors reach when they all fit whole (pending otherwise: the chain steps); a
+//          speculative slot whose whole delta fits over every slice and is clean here is complete.
+// Sequential semantics over the slices in column (= canonical dict) order, so the result is the
+// single-slice result bit for bit.
+template <int KW, int MODE>
+__global__ __launch_bounds__(XB, (KW == 4 ? PK_WAVES : 1)) void k_settle(Dev d, const int32_t *ini, const int32_t *res,
+                                                                        uint32_t n, uint32_t t, SliceIO io) {
     __shared__ __attribute__((aligned(16))) uint16_t s_wbuf[2 * WIN];
     const uint32_t e = blockIdx.x;
     if (e >= n) return;
@@ -1509,11 +1665,86 @@ __global__ __launch_bounds__(XB, (KW == 4 ? PK_WAVES : 1)) void k_count(Dev d, c
     const bool w0 = wid == 0;
     const uint32_t snd = w0 ? b : a, rcv = w0 ? a : b;
     const DigestSide ds{rcv, d.ncol, t >= d.row[rcv * 4 + 2]};
+    uint16_t *wbuf = s_wbuf + wid * WIN;
     WStats st{0, 0, 0, 0, 0};
     bool tomb = false;
     PackState pst{0u, false, false};
-    pack_records<KW, true>(d, snd, rcv, ds, slot, s_wbuf + wid * WIN, t, st, tomb, pst);
-    if (lane == 0) tot[slot] = pst.S;
+    uint32_t salg = 0;
+    bool done = false;
+    if (MODE == 1) {
+        if (d.spec) {
+            const SlotSum s = settle_sum<KW>(d, snd, rcv, ds, slot, wbuf, t, salg);
+            if (lane == 0) {
+                io.tot[slot] = s.T;
+                d.slot_stat[slot] = make_uint4(s.nd, s.kvs, s.cand, s.clean ? 0u : 1u);
+            }
+        } else {
+            pack_records<KW, true>(d, snd, rcv, ds, slot, wbuf, t, st, tomb, pst);
+            if (lane == 0) io.tot[slot] = pst.S;
+            salg = st.alg;
+        }
+        const unsigned long long s_alg = wave_sum(salg);
+        if (lane == 0) { shard_add(d, C_ALG, s_alg); shard_add(d, C_PACKB, s_alg); }
+        return;
+    }
+    if (MODE == 0) {
+        if (d.spec) {
+            const SlotSum s = settle_sum<KW>(d, snd, rcv, ds, slot, wbuf, t, salg);
+            if (s.clean && s.T <= d.mtu) {
+                done = true;
+                st.nd = s.nd;  // wave totals: added by lane 0 only (below)
+                st.kvs = s.kvs;
+                st.cand = s.cand;
+                if (lane == 0) shard_add(d, C_DBYTES, s.T);
+            }
+        }
+    } else {  // MODE 2
+        unsigned long long P = 0, all = 0;
+        for (uint32_t g = 0; g < d.shards; g++) {
+            const unsigned long long x = io.tot_all[(size_t)g * n * 2 + slot];
+            if (g < d.shard) P += x;
+            all += x;
+        }
+        if (P > d.mtu) {
+            if (lane == 0) io.chain[slot] = CHAIN_PENDING;
+            return;
+        }
+        pst = PackState{(uint32_t)P, false, false};
+        if (d.spec && all <= d.mtu) {
+            const uint4 ss = d.slot_stat[slot];
+            if (!ss.w) {
+                done = true;
+                st.nd = ss.x;
+                st.kvs = ss.y;
+                st.cand = ss.z;
+                if (lane == 0) {
+                    shard_add(d, C_DBYTES, io.tot_all[(size_t)d.shard * n * 2 + slot]);
+                    io.chain[slot] = (uint64_t)(P + io.tot_all[(size_t)d.shard * n * 2 + slot]);  // not listed
+                }
+            }
+        }
+    }
+    if (!done) {
+        pack_records<KW, false>(d, snd, rcv, ds, slot, wbuf, t, st, tomb, pst);
+        if (tomb) d.row[rcv * 4 + 1] = 1u;
+        if (MODE == 2 && lane == 0) io.chain[slot] = chain_pack(pst);
+        st.alg += salg;
+        st.nd = (uint32_t)wave_sum(st.nd);
+        st.kvs = (uint32_t)wave_sum(st.kvs);
+        st.trunc = (uint32_t)wave_sum(st.trunc);
+        st.cand = (uint32_t)wave_sum(st.cand);
+    } else {
+        st.alg = salg;
+    }
+    const unsigned long long s_alg = wave_sum(st.alg);
+    if (lane == 0) {
+        shard_add(d, C_ALG, s_alg);
+        shard_add(d, C_PACKB, s_alg);
+        shard_add(d, C_ND, st.nd);
+        shard_add(d, C_KVS, st.kvs);
+        shard_add(d, C_TRUNC, st.trunc);
+        shard_add(d, C_CAND, st.cand);
+    }
 }
 
 
@@ -1592,19 +1823,27 @@ template <bool RING>
 __global__ __launch_bounds__(LB, LIVE_WAVES) void k_liveness(Dev d, const uint8_t *up, uint32_t t, uint32_t chunks,
                                                  uint32_t per, bool replay, bool decide) {
     // [wave][phase][the wave's 4 plane words of this chunk]: each wave stages and reads only its own
-    // words (lane l: phase l / 4, word l % 4), so the chunks need no workgroup barrier
-    __shared__ uint64_t s_pl[LB / WAVE][16][4];
+    // words (lane l: phase l / 4 (+ 16), word l % 4), so the chunks need no workgroup barrier
+    __shared__ uint64_t s_pl[LB / WAVE][NPL][4];
     __shared__ uint32_t s_vm;
     const uint32_t groups = (chunks + per - 1) / per;
     const uint32_t o = blockIdx.x / groups, cb0 = (blockIdx.x % groups) * per;
     const bool upo = decide && up[o] != 0;
     const bool exact = upo && (d.row[o * 4 + 3] & 2u);  // recompute row word 2 (k_reset_sched)
     const bool genm = !(d.flags & GS_CANONICAL);
+    // this row's interval rings: every row has them (RING: GS_FD_RING), or this is a sampled ring row
+    uint16_t *rrow = nullptr;
+    if (RING) {
+        rrow = d.ring + (size_t)o * d.NP * d.W;
+    } else if (d.ring_slot) {
+        const uint32_t rs = d.ring_slot[o];
+        if (rs != NONE) rrow = d.ring + (size_t)rs * d.NP * d.W;
+    }
     uint32_t minS = NONE, live = 0, gcdue = 0, ovf = 0, alg = 0;
     // phases of the current round in which row o was in an exchange (its plane rows are valid);
     // replay = false once this round's reports were replayed (the host closes the round)
     if (threadIdx.x < 64) {
-        const bool v = replay && threadIdx.x < 16 && d.pstamp[o * 16u + threadIdx.x] == d.t_round + 1u + threadIdx.x;
+        const bool v = replay && threadIdx.x < NPL && d.pstamp[o * NPL + threadIdx.x] == d.t_round + 1u + threadIdx.x;
         const uint32_t m = (uint32_t)__ballot(v);
         if (threadIdx.x == 0) s_vm = m;
     }
@@ -1631,8 +1870,11 @@ __global__ __launch_bounds__(LB, LIVE_WAVES) void k_liveness(Dev d, const uint8_
     const uint32_t wv = threadIdx.x >> 6, ln = threadIdx.x & 63u;
     if (vm) {
         __builtin_amdgcn_wave_barrier();  // this wave is done with the previous chunk's words
-        const uint32_t ph = ln >> 2, wi = cb * 16u + wv * 4u + (ln & 3u);
-        if ((vm >> ph) & 1u) s_pl[wv][ph][ln & 3u] = wi < d.PW ? d.pend[((size_t)o * 16u + ph) * d.PW + wi] : 0ull;
+        const uint32_t wi = cb * 16u + wv * 4u + (ln & 3u);
+        const uint32_t ph = ln >> 2;
+        if ((vm >> ph) & 1u) s_pl[wv][ph][ln & 3u] = wi < d.PW ? d.pend[((size_t)o * NPL + ph) * d.PW + wi] : 0ull;
+        if (NPL > 16 && (vm >> (ph + 16u)) & 1u)
+            s_pl[wv][ph + 16u][ln & 3u] = wi < d.PW ? d.pend[((size_t)o * NPL + ph + 16u) * d.PW + wi] : 0ull;
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         __builtin_amdgcn_wave_barrier();
     }
@@ -1661,7 +1903,8 @@ __global__ __launch_bounds__(LB, LIVE_WAVES) void k_liveness(Dev d, const uint8_
                 while (m) {
                     const uint32_t bb = (uint32_t)__builtin_ctz(m);
                     m &= m - 1u;
-                    f = fd_report_val<RING>(d, p + i, d.t_round + 1u + bb, f, alg, ovf);
+                    f = fd_report_val(d, rrow ? rrow + (size_t)(c0 + i) * d.W : nullptr, d.t_round + 1u + bb, f, alg,
+                                      ovf);
                 }
                 dw = true;
             }
@@ -1669,7 +1912,7 @@ __global__ __launch_bounds__(LB, LIVE_WAVES) void k_liveness(Dev d, const uint8_
             if (upo && j < d.ncol && d.col_lo + j != o && !(genm && ps[i] == NONE)) {
                 live++;
                 const bool has = f.last != NONE;
-                const uint32_t len = RING ? (f.cnt < d.W ? f.cnt : d.W) : f.cnt;
+                const uint32_t len = rrow ? (f.cnt < d.W ? f.cnt : d.W) : f.cnt;
                 bool alive = false;
                 if (has && len) {
                     // phi <= threshold (failure_detector.py:43-53, 97-98) decided without the two binary64
@@ -1726,7 +1969,9 @@ __global__ __launch_bounds__(LB, LIVE_WAVES) void k_liveness(Dev d, const uint8_
     if ((threadIdx.x & 63) == 0) {
         if (minS != NONE) atomicMin(&d.row[o * 4 + 2], minS);
         if (sl) shard_add(d, C_LIVE, sl);
-        if (so) shard_add(d, C_E_FDOVF, so);
+        // a full compact window that needed an eviction: an error, except with sampled rings, where the
+        // compact rows are documented as exact only up to W intervals (fd_saturated)
+        if (so) shard_add(d, d.ring_slot ? C_FDSAT : C_E_FDOVF, so);
         if (sg) {
             if (genm) atomicOr(&d.row[o * 4 + 3], 1u);  // k_fd_gc collects this row
             else shard_add(d, C_E_FDGC, sg);  // removal would break the canonical layout
@@ -1869,7 +2114,8 @@ __global__ __launch_bounds__(LB) void k_phi_row(Dev d, uint32_t o, uint32_t t, d
     const uint32_t st = d.fd_state[p];
     const Fd f = fd_get(d, st, d.fd_last[p], d.fd[p], t);
     if ((st & FD_OLD) && f.cnt) shard_add(d, C_E_FDOVF, 1);  // phi of a window silent for >= 2^15 ticks: inexact
-    const uint32_t len = (d.flags & GS_FD_RING) ? (f.cnt < d.W ? f.cnt : d.W) : f.cnt;
+    // ring windows count up to 2W (len = min(cnt, W)); a compact window never holds more than W
+    const uint32_t len = f.cnt < d.W ? f.cnt : d.W;
     double phi = __builtin_nan("");
     if (f.last != NONE && len) {
         const double mean = ((double)f.sum * TICK_S + d.prior5) / ((double)len + 5.0);
@@ -2546,9 +2792,13 @@ struct gs_handle {
     hipStream_t stream;
     uint32_t seq;
     bool booted;
-    // canonical unsliced handles run a phase as two kernels (k_pass1, k_pack_slice); env GS_FUSED=1
+    // canonical unsliced handles run a phase on candidate records (k_pass1 + k_settle); env GS_FUSED=1
     // selects the single fused k_exchange (and, on sliced handles, the fused count pass) for A/B runs
     bool split;
+    // record phases (env GS_PACK, A/B runs): 0 = k_pass1 with the speculative merge + k_settle (default),
+    // 1 = "fused": k_pass1 packing in the same workgroup, 2 = "split": k_pass1 + k_pack_slice
+    int pack_mode = 0;
+    bool age_init = false;            // age_tick holds the first operation's tick (fd_age)
     // gs_set_timing: HIP events around each kernel launch of a kind (gs_ktimes), on the library's stream
     bool timing;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> tev[4];
@@ -2640,7 +2890,16 @@ int check_bound(gs_handle *h) {
     d.cand_n = (uint32_t *)h->reg[GS_R_CAND_N];
     d.pend = (uint64_t *)h->reg[GS_R_PEND];
     d.pstamp = (uint32_t *)h->reg[GS_R_PEND_STAMP];
+    d.slot_stat = (uint4 *)h->reg[GS_R_SLOT_STAT];
+    d.ring_slot = (uint32_t *)h->reg[GS_R_RING_SLOT];
     return GS_OK;
+}
+
+// A record phase may merge its prefix candidates speculatively in pass 1 (Dev::spec): canonical prefix
+// views (no tombstones), records on, no hook events (they need the per-key applies), packing not ablated.
+bool spec_ok(const gs_handle *h) {
+    return h->pack_mode == 0 && (h->cfg.flags & GS_CANONICAL) && !(h->cfg.flags & GS_TOMBSTONES) && h->d.cand &&
+           !h->d.ev && !(h->d.ablate & 1u);
 }
 
 template <int KW, bool GENM, int MODE>
@@ -2679,11 +2938,11 @@ int launch_liveness(gs_handle *h, const uint8_t *up, uint32_t tick, bool replay,
     return time_end(h, GS_KT_LIVENESS, e0);
 }
 
-// A phase more than 16 ticks after the plane base: replay the pending report planes into the sampling
+// A phase more than NPL ticks after the plane base: replay the pending report planes into the sampling
 // windows now (nothing reads a window before the round's liveness sweep, and the replay applies the
 // same reports in the same tick order), then start a new plane base just before this phase.
 int advance_planes(gs_handle *h, uint32_t tick) {
-    if (tick - h->d.t_round <= 16u) return GS_OK;
+    if (tick - h->d.t_round <= NPL) return GS_OK;
     if (h->reports_pending) {
         int rc = launch_liveness(h, nullptr, tick, true, false);
         if (rc) return rc;
@@ -2709,28 +2968,49 @@ int check_phase(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t n
     return GS_OK;
 }
 
-// One canonical one-slice phase on the caller's stream: k_pass1<FUSE = true> (pass 1, then packing and
-// apply in the same workgroup), or with env GS_PACK=split, k_pass1 then k_pack_slice.
-int run_split_phase(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t n, uint32_t tick) {
-    static const bool split = [] {
-        const char *m = getenv("GS_PACK");
-        return m && !strcmp(m, "split");
-    }();
+// pass 1 of a record phase (k_pass1 without packing), speculative per Dev::spec
+int launch_pass1(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t n, uint32_t tick) {
     hipEvent_t e0 = nullptr;
     int rc = time_begin(h, e0);
     if (rc) return rc;
-    if (!split) {
+    if (h->d.spec) k_pass1<4, false, true><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, h->seq, 0u);
+    else k_pass1<4, false, false><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, h->seq, 0u);
+    HIPCHK(h, hipGetLastError());
+    return time_end(h, GS_KT_PASS1, e0);
+}
+template <int MODE>
+int launch_settle(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t n, uint32_t tick, const SliceIO &io,
+                  int kind) {
+    hipEvent_t e0 = nullptr;
+    int rc = time_begin(h, e0);
+    if (rc) return rc;
+    if (h->KP <= 16) k_settle<4, MODE><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, io);
+    else k_settle<KWB, MODE><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, io);
+    HIPCHK(h, hipGetLastError());
+    return time_end(h, kind, e0);
+}
+
+// One canonical one-slice phase on the caller's stream (GS_PACK, A/B runs): default k_pass1 with the
+// speculative merge, then k_settle; "fused": k_pass1<FUSE = true> (pass 1, then packing and apply in the
+// same workgroup); "split": k_pass1, then k_pack_slice.
+int run_split_phase(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t n, uint32_t tick) {
+    hipEvent_t e0 = nullptr;
+    int rc;
+    h->d.spec = spec_ok(h) ? 1u : 0u;
+    if (h->pack_mode == 1) {
+        if ((rc = time_begin(h, e0))) return rc;
         if (h->KP <= 16) k_pass1<4, true><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, h->seq, 0u);
-        else k_pass1<16, true><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, h->seq, 0u);
+        else k_pass1<KWB, true><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, h->seq, 0u);
         HIPCHK(h, hipGetLastError());
         return time_end(h, GS_KT_PASS1, e0);
     }
+    if ((rc = launch_pass1(h, ini, res, n, tick))) return rc;
+    if (h->d.ablate & 1u) return GS_OK;  // profiling only: no packing (results invalid)
     const SliceIO io{};
-    k_pass1<4, false><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, h->seq, 0u);
-    HIPCHK(h, hipGetLastError());
-    if ((rc = time_end(h, GS_KT_PASS1, e0)) || (rc = time_begin(h, e0))) return rc;
+    if (h->pack_mode == 0) return launch_settle<0>(h, ini, res, n, tick, io, GS_KT_PACK);
+    if ((rc = time_begin(h, e0))) return rc;
     if (h->KP <= 16) k_pack_slice<4><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, io, 0u);
-    else k_pack_slice<16><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, io, 0u);
+    else k_pack_slice<KWB><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, io, 0u);
     HIPCHK(h, hipGetLastError());
     return time_end(h, GS_KT_PACK, e0);
 }
@@ -2756,10 +3036,14 @@ int gs_create(const gs_config *cfg, gs_handle **out) {
     if (G > 1 && (!(c.flags & GS_CANONICAL) || (uint64_t)(G - 1) * blk >= c.n_nodes)) return GS_E_INVALID;
     const uint32_t ncol = G > 1 ? (uint32_t)std::min<uint64_t>(blk, c.n_nodes - col_lo) : c.n_nodes;
     if (c.n_keys < 1 || c.n_keys > 64) return GS_E_INVALID;
+    if (c.n_keys > 4u * KWB) return GS_E_UNSUPPORTED;  // a -DGS_KW4_ONLY development build
     if ((c.flags & GS_NO_HELD) && (c.flags & GS_TOMBSTONES)) return GS_E_INVALID;  // prefix views need no GC
     if (c.hist_cap < 2 || c.hist_cap > 255) return GS_E_INVALID;
     if (c.mtu < 1 || c.window < 1) return GS_E_INVALID;
-    if ((c.flags & GS_FD_RING) && (c.window > (1u << 20) || c.max_interval_ticks > 0xFFFFu)) return GS_E_INVALID;
+    if ((c.flags & GS_FD_RING) && c.ring_rows) return GS_E_INVALID;  // every row has a ring, or a sample does
+    if (c.ring_rows > c.n_nodes) return GS_E_INVALID;
+    if (((c.flags & GS_FD_RING) || c.ring_rows) && (c.window > (1u << 20) || c.max_interval_ticks > 0xFFFFu))
+        return GS_E_INVALID;
     // packed window: cnt < 2W needs cnt_bits, the sum of <= W intervals <= max_interval the rest of 32
     uint32_t cnt_bits = 1;
     while ((1ull << cnt_bits) <= 2ull * c.window) cnt_bits++;
@@ -2801,7 +3085,8 @@ int gs_create(const gs_config *cfg, gs_handle **out) {
     b[GS_R_FD_STATE] = pairs;
     b[GS_R_FD_TOD] = pairs * 4;
     b[GS_R_TS] = (c.flags & GS_TOMBSTONES) ? pairs * KP * 4 : 0;
-    b[GS_R_RING] = (c.flags & GS_FD_RING) ? pairs * W * 2 : 0;
+    b[GS_R_RING] = (c.flags & GS_FD_RING) ? pairs * W * 2 : (uint64_t)c.ring_rows * NP * W * 2;
+    b[GS_R_RING_SLOT] = c.ring_rows ? N * 4 : 0;
     b[GS_R_POS] = b[GS_R_ORD] = genm ? pairs * 4 : 0;
     b[GS_R_ROW] = N * 16;
     b[GS_R_LAST_W] = NC * KP;
@@ -2820,9 +3105,11 @@ int gs_create(const gs_config *cfg, gs_handle **out) {
     const bool recs = (c.flags & GS_CANONICAL) && !fused;
     b[GS_R_CAND] = recs ? (N / 2) * 4 * GS_CAND_CAP * 8 : 0;
     b[GS_R_CAND_N] = recs ? (N / 2) * 4 * 4 : 0;
+    b[GS_R_SLOT_STAT] = (recs && G > 1) ? (N / 2) * 2 * 16 : 0;
+    if (const char *m = getenv("GS_PACK")) h->pack_mode = !strcmp(m, "fused") ? 1 : !strcmp(m, "split") ? 2 : 0;
     const uint64_t PW = round_up(h->NP, 256) / 64;
-    b[GS_R_PEND] = N * 16 * PW * 8;  // 16 phase bit planes per observer row
-    b[GS_R_PEND_STAMP] = N * 16 * 4;
+    b[GS_R_PEND] = N * NPL * PW * 8;  // one phase bit plane per observer row and phase slot
+    b[GS_R_PEND_STAMP] = N * NPL * 4;
     Dev &d = h->d;
     memset(&d, 0, sizeof d);
     d.N = h->N;
@@ -2891,12 +3178,14 @@ int gs_boot(gs_handle *h, const uint16_t *nid_size, const uint8_t *key_len) {
     // regions that start at zero
     const int zero[] = {GS_R_HB, GS_R_SELF_HB, GS_R_MV, GS_R_GC, GS_R_HELD, GS_R_FD, GS_R_FD_LAST, GS_R_FD_STATE, GS_R_FD_TOD,
                         GS_R_RING, GS_R_ROW, GS_R_LAST_W, GS_R_HIST, GS_R_HIST_VID,
-                        GS_R_STAMP, GS_R_COUNTERS, GS_R_SLICE_BITS, GS_R_PEND, GS_R_PEND_STAMP, GS_R_LATEST};
+                        GS_R_STAMP, GS_R_COUNTERS, GS_R_SLICE_BITS, GS_R_PEND, GS_R_PEND_STAMP, GS_R_LATEST,
+                        GS_R_SLOT_STAT};
     for (int r : zero)
         if (h->bytes[r]) HIPCHK(h, hipMemsetAsync(h->reg[r], 0, h->bytes[r], s));
     if (h->bytes[GS_R_TS]) HIPCHK(h, hipMemsetAsync(h->reg[GS_R_TS], 0xFF, h->bytes[GS_R_TS], s));
     if (h->bytes[GS_R_POS]) HIPCHK(h, hipMemsetAsync(h->reg[GS_R_POS], 0xFF, h->bytes[GS_R_POS], s));
     if (h->bytes[GS_R_ORD]) HIPCHK(h, hipMemsetAsync(h->reg[GS_R_ORD], 0xFF, h->bytes[GS_R_ORD], s));
+    if (h->bytes[GS_R_RING_SLOT]) HIPCHK(h, hipMemsetAsync(h->reg[GS_R_RING_SLOT], 0xFF, h->bytes[GS_R_RING_SLOT], s));
     // tables
     // nid_size covers all n_nodes (the packer's stop bound must hold across slices); keep this slice's
     std::vector<uint16_t> ns(h->NP, 0);
@@ -2919,6 +3208,21 @@ int gs_boot(gs_handle *h, const uint16_t *nid_size, const uint8_t *key_len) {
     HIPCHK(h, hipGetLastError());
     HIPCHK(h, hipStreamSynchronize(s));
     h->booted = true;
+    return GS_OK;
+}
+
+int gs_set_ring_rows(gs_handle *h, const uint32_t *rows, uint32_t n) {
+    if (!h || !h->booted || (n && !rows)) return GS_E_INVALID;
+    if (n > h->cfg.ring_rows)
+        return fail(h, GS_E_INVALID, "gs_set_ring_rows: %u rows for %u ring slots (gs_config.ring_rows)", n, h->cfg.ring_rows);
+    std::vector<uint32_t> slot(h->N, NONE);
+    for (uint32_t i = 0; i < n; i++) {
+        if (rows[i] >= h->N || slot[rows[i]] != NONE)
+            return fail(h, GS_E_INVALID, "gs_set_ring_rows: row %u out of range or repeated", rows[i]);
+        slot[rows[i]] = i;
+    }
+    HIPCHK(h, hipMemcpyAsync(h->reg[GS_R_RING_SLOT], slot.data(), (size_t)h->N * 4, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
     return GS_OK;
 }
 
@@ -2958,9 +3262,9 @@ int gs_begin_round(gs_handle *h, const uint8_t *up, uint32_t tick) {
         int rc = gs_check_heartbeat_lag(h);
         if (rc) return rc;
     }
+    if (int rc = fd_age(h, tick)) return rc;  // the tick axis of the 16-bit report ticks (and gs_latest_tick)
     h->d.t_round = tick;
     h->last_phase_tick = tick;
-    h->max_tick = std::max(h->max_tick, tick);
     k_begin_round<<<h->N, LB, 0, h->stream>>>(h->d, up, tick);
     HIPCHK(h, hipGetLastError());
     h->round_open = true;
@@ -3002,12 +3306,13 @@ int gs_run_phase(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t 
     h->last_phase_tick = tick;
     h->hb_incs++;
     if (h->split) return run_split_phase(h, ini, res, n, tick);
+    h->d.spec = 0u;
     hipEvent_t e0 = nullptr;
     if ((rc = time_begin(h, e0))) return rc;
     if (h->KP <= 16) rc = genm ? launch_exchange<4, true, 0>(h, ini, res, n, tick, lds, io)
                                : launch_exchange<4, false, 0>(h, ini, res, n, tick, lds, io);
-    else rc = genm ? launch_exchange<16, true, 0>(h, ini, res, n, tick, lds, io)
-                   : launch_exchange<16, false, 0>(h, ini, res, n, tick, lds, io);
+    else rc = genm ? launch_exchange<KWB, true, 0>(h, ini, res, n, tick, lds, io)
+                   : launch_exchange<KWB, false, 0>(h, ini, res, n, tick, lds, io);
     return rc ? rc : time_end(h, GS_KT_PASS1, e0);
 }
 
@@ -3033,20 +3338,18 @@ int gs_phase_count(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_
     h->reports_pending = true;
     h->last_phase_tick = tick;
     h->hb_incs++;
-    hipEvent_t e0 = nullptr;
-    if ((rc = time_begin(h, e0))) return rc;
     if (!h->d.cand) {  // GS_FUSED: the fused count pass (LDS bitmaps)
+        h->d.spec = 0u;
+        hipEvent_t e0 = nullptr;
+        if ((rc = time_begin(h, e0))) return rc;
         rc = h->KP <= 16 ? launch_exchange<4, false, 1>(h, ini, res, n, tick, lds, io)
-                         : launch_exchange<16, false, 1>(h, ini, res, n, tick, lds, io);
+                         : launch_exchange<KWB, false, 1>(h, ini, res, n, tick, lds, io);
         return rc ? rc : time_end(h, GS_KT_PASS1, e0);
     }
-    k_pass1<4, false><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, h->seq, 0u);
-    HIPCHK(h, hipGetLastError());
-    if ((rc = time_end(h, GS_KT_PASS1, e0)) || (rc = time_begin(h, e0))) return rc;
-    if (h->KP <= 16) k_count<4><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, slice_bytes);
-    else k_count<16><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, slice_bytes);
-    HIPCHK(h, hipGetLastError());
-    return time_end(h, GS_KT_COUNT, e0);
+    // the speculative merge is decided here for the whole phase (gs_phase_pack / gs_phase_chain use it)
+    h->d.spec = spec_ok(h) ? 1u : 0u;
+    if ((rc = launch_pass1(h, ini, res, n, tick))) return rc;
+    return launch_settle<1>(h, ini, res, n, tick, io, GS_KT_COUNT);
 }
 
 int gs_phase_pack(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t n, uint32_t tick, uint32_t step,
@@ -3063,10 +3366,11 @@ int gs_phase_pack(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t
     io.chain = chain;
     io.step = step;
     if (step && h->shard == 0) return GS_OK;  // slice 0 always finishes at step 0
+    if (step == 0 && h->d.cand) return launch_settle<2>(h, ini, res, n, tick, io, GS_KT_PACK);
     hipEvent_t e0 = nullptr;
     if ((rc = time_begin(h, e0))) return rc;
     if (h->KP <= 16) k_pack_slice<4><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, io, 0u);
-    else k_pack_slice<16><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, io, 0u);
+    else k_pack_slice<KWB><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, io, 0u);
     HIPCHK(h, hipGetLastError());
     return time_end(h, GS_KT_PACK, e0);
 }
@@ -3102,7 +3406,7 @@ int gs_phase_chain(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_
     if ((rc = time_begin(h, e0))) return rc;
     const uint32_t grid = std::min<uint32_t>(count, 2048u);
     if (h->KP <= 16) k_chain_step<4><<<grid, WAVE, 0, h->stream>>>(h->d, ini, res, tick, list, count, chain_all, chain, chainc);
-    else k_chain_step<16><<<grid, WAVE, 0, h->stream>>>(h->d, ini, res, tick, list, count, chain_all, chain, chainc);
+    else k_chain_step<KWB><<<grid, WAVE, 0, h->stream>>>(h->d, ini, res, tick, list, count, chain_all, chain, chainc);
     HIPCHK(h, hipGetLastError());
     return time_end(h, GS_KT_PACK, e0);
 }
@@ -3122,13 +3426,14 @@ int ensure_scratch(gs_handle *h, uint32_t n) {
     HIPCHK(h, hipMalloc(&h->sc.chainc, s2));
     HIPCHK(h, hipMalloc(&h->sc.tot_all, G * s2));
     HIPCHK(h, hipMalloc(&h->sc.chain_all, G * s2));
-    HIPCHK(h, hipMalloc(&h->sc.list, ((size_t)2 * cap + 256) * 4));
+    HIPCHK(h, hipMalloc(&h->sc.list, (size_t)GS_OVERFLOW_LIST_LEN(cap) * 4));
     h->sc.cap = cap;
     return GS_OK;
 }
 
 // all-gather of `count` u64 per slice (src of slice g -> dst[g * count ..], on every slice): one RCCL
-// all-gather when this process drives one slice of a communicator, device copies when it drives them all
+// all-gather when this process drives one slice of a communicator, one gather kernel (k_gather_u64)
+// when it drives them all
 int gather_u64(gs_handle *const *hs, uint32_t nh, uint64_t *(*src)(gs_handle *), uint64_t *(*dst)(gs_handle *),
                size_t count) {
     if (!count) return GS_OK;
@@ -3138,10 +3443,16 @@ int gather_u64(gs_handle *const *hs, uint32_t nh, uint64_t *(*src)(gs_handle *),
         if (r != ncclSuccess) return fail(h, GS_E_HIP, "ncclAllGather: %s", ncclGetErrorString(r));
         return GS_OK;
     }
-    for (uint32_t i = 0; i < nh; i++)
-        for (uint32_t g = 0; g < nh; g++)
-            HIPCHK(hs[i], hipMemcpyAsync(dst(hs[i]) + (size_t)g * count, src(hs[g]), count * 8, hipMemcpyDeviceToDevice,
-                                         hs[i]->stream));
+    if (nh > GATHER_MAX) return fail(hs[0], GS_E_INVALID, "gather over %u slices (at most %u)", nh, GATHER_MAX);
+    GatherPtrs p{};
+    for (uint32_t g = 0; g < nh; g++) {
+        p.src[g] = src(hs[g]);
+        p.dst[g] = dst(hs[g]);
+    }
+    const uint64_t total = (uint64_t)nh * count;
+    const uint32_t bx = (uint32_t)std::min<uint64_t>((total + LB - 1) / LB, 4096u);
+    k_gather_u64<<<dim3(bx, nh), LB, 0, hs[0]->stream>>>(p, nh, count);
+    HIPCHK(hs[0], hipGetLastError());
     return GS_OK;
 }
 
@@ -3223,19 +3534,35 @@ int gs_run_phase_group(gs_handle *const *hs, uint32_t n_handles, const int32_t *
 
 extern "C++" {
 namespace {
-int fd_age(gs_handle *h, uint32_t tick) {
-    h->max_tick = std::max(h->max_tick, tick);
-    const uint32_t dt = tick - h->age_tick;
-    if ((int32_t)dt < 0) return GS_OK;  // an earlier tick (phi of the past): nothing aged since the sweep
-    if (dt >= FD_OLD_AGE)
-        return fail(h, GS_E_INVALID, "tick %u is %u ticks after the last window-age sweep (at most 2^15 between "
-                    "operations: 16-bit report ticks)", tick, dt);
-    if (dt < (FD_OLD_AGE >> 1)) return GS_OK;
+// Invariant: after a sweep at tick A every unmarked window's report is less than 2^15 ticks older than A,
+// so decodes are exact at every tick below A + 2^15.  An operation at t sweeps once t - A reaches 2^14;
+// when t - A is 2^15 or more it first sweeps at the previous operation's tick (less than 2^14 after A, so
+// exact there), which leaves t - A = the step from that operation.  Only a step of 2^15 or more between
+// two consecutive operations is refused, and a refused tick changes nothing (a later, smaller step works).
+int age_sweep(gs_handle *h, uint32_t tick) {
     const uint64_t quads = (uint64_t)h->N * h->NP / 4;
     const uint32_t blocks = (uint32_t)std::min<uint64_t>((quads + LB - 1) / LB, 1u << 16);
     k_fd_age<<<blocks, LB, 0, h->stream>>>(h->d, tick);
     HIPCHK(h, hipGetLastError());
     h->age_tick = tick;
+    return GS_OK;
+}
+int fd_age(gs_handle *h, uint32_t tick) {
+    if (!h->age_init) {  // no window exists before the first operation: start the clock there
+        h->age_init = true;
+        h->age_tick = h->max_tick = tick;
+        return GS_OK;
+    }
+    if ((int32_t)(tick - h->max_tick) < 0) return GS_OK;  // an earlier tick (phi of the past): nothing aged
+    const uint32_t step = tick - h->max_tick;
+    if (step >= FD_OLD_AGE)
+        return fail(h, GS_E_INVALID, "tick %u is %u ticks after the previous operation (at most 2^15 - 1 between "
+                    "operations: 16-bit report ticks)", tick, step);
+    if (tick - h->age_tick >= FD_OLD_AGE) {
+        if (int rc = age_sweep(h, h->max_tick)) return rc;
+    }
+    h->max_tick = tick;
+    if (tick - h->age_tick >= (FD_OLD_AGE >> 1)) return age_sweep(h, tick);
     return GS_OK;
 }
 }  // namespace
@@ -3259,13 +3586,30 @@ int gs_liveness(gs_handle *h, const uint8_t *up, uint32_t tick) {
     return GS_OK;
 }
 
+int gs_flush_reports(gs_handle *h, uint32_t tick) {
+    if (!h || !h->booted) return GS_E_INVALID;
+    if (!h->round_open) return fail(h, GS_E_INVALID, "gs_flush_reports: no open round");
+    if (tick < h->last_phase_tick)
+        return fail(h, GS_E_INVALID, "gs_flush_reports at tick %u precedes a phase at tick %u", tick, h->last_phase_tick);
+    if (int rc = fd_age(h, tick)) return rc;
+    if (h->reports_pending) {
+        if (int rc = launch_liveness(h, nullptr, tick, true, false)) return rc;
+        h->reports_pending = false;
+    }
+    h->d.t_round = tick;  // the next phase (after tick) starts a new plane base
+    h->last_phase_tick = tick;
+    return GS_OK;
+}
+
 int gs_read_rows(gs_handle *h, int region, uint32_t row_lo, uint32_t row_hi, void *out, uint64_t cap, uint64_t *len) {
-    static const int rows_major[] = {GS_R_HB, GS_R_MV, GS_R_GC, GS_R_HELD, GS_R_FD, GS_R_FD_STATE, GS_R_FD_TOD,
-                                     GS_R_TS, GS_R_RING, GS_R_POS, GS_R_ORD, GS_R_ROW};
+    static const int rows_major[] = {GS_R_HB, GS_R_MV, GS_R_GC, GS_R_HELD, GS_R_FD, GS_R_FD_LAST, GS_R_FD_STATE,
+                                     GS_R_FD_TOD, GS_R_TS, GS_R_RING, GS_R_POS, GS_R_ORD, GS_R_ROW};
     if (!h || !h->booted || !out || !len || row_lo > row_hi || row_hi > h->N) return GS_E_INVALID;
     if (std::find(std::begin(rows_major), std::end(rows_major), region) == std::end(rows_major))
         return fail(h, GS_E_INVALID, "gs_read_rows: region %d is not indexed by observer row", region);
     if (!h->bytes[region]) return fail(h, GS_E_UNSUPPORTED, "gs_read_rows: region %d is not allocated", region);
+    if (region == GS_R_RING && h->cfg.ring_rows)
+        return fail(h, GS_E_UNSUPPORTED, "gs_read_rows: sampled rings are indexed by ring slot, not observer row");
     const uint64_t rb = h->bytes[region] / h->N, nb = rb * (row_hi - row_lo);
     *len = nb;
     if (nb > cap) return fail(h, GS_E_INVALID, "gs_read_rows: %llu bytes > capacity %llu", (unsigned long long)nb,
@@ -3404,8 +3748,8 @@ int gs_emit_delta(gs_handle *h, const gs_wire *w, uint32_t sender, uint32_t rece
     if (h->KP <= 16)
         return genm ? emit_delta<4, true>(h, wr, sender, receiver, tick, out, cap, len, e)
                     : emit_delta<4, false>(h, wr, sender, receiver, tick, out, cap, len, e);
-    return genm ? emit_delta<16, true>(h, wr, sender, receiver, tick, out, cap, len, e)
-                : emit_delta<16, false>(h, wr, sender, receiver, tick, out, cap, len, e);
+    return genm ? emit_delta<KWB, true>(h, wr, sender, receiver, tick, out, cap, len, e)
+                : emit_delta<KWB, false>(h, wr, sender, receiver, tick, out, cap, len, e);
 }
 
 int gs_read_counters(gs_handle *h, gs_counters *out) {

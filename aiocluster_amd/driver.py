@@ -87,6 +87,11 @@ def run_phases(sims, rd, events=None, group=None, phases=None):
     for a, b, n, t in (rd["phases"] if phases is None else phases):
         if not n:
             continue
+        for s_ in sims:
+            if s_._ev is not None:  # hook events: order_events needs each phase's exchange order
+                if group is not None:
+                    raise ValueError("hook events on a sliced cluster are not supported (drain per slice)")
+                s_._ev_phases[t] = (a.cpu().numpy().astype(np.int64), b.cpu().numpy().astype(np.int64))
         if events is not None:
             e0 = s0.torch.cuda.Event(enable_timing=True)
             e1 = s0.torch.cuda.Event(enable_timing=True)
@@ -112,7 +117,7 @@ def run_round(sims, rd, events=None, group=None, sel=None):
     """One gossip round on the slices this process drives (one GossipSim when unsliced).  With ``sel``
     (a PeerSelector) the round's exchanges come from the device's select_nodes_for_gossip + phase
     schedule instead of the workload's explicit schedule (``rd`` gains "exchanges", "unscheduled")."""
-    from .workload import phase_tick
+    from .workload import TICKS_PER_ROUND, phase_tick
 
     begin(sims, rd)
     phases = None
@@ -123,5 +128,7 @@ def run_round(sims, rd, events=None, group=None, sel=None):
         rd["exchanges"] = offs[-1]
         rd["unscheduled"] = left
         rd["t_live"] = rd["t"] + 1 + len(phases)
+    if rd["t_live"] >= rd["t"] + TICKS_PER_ROUND:
+        raise ValueError(f"round {rd['r']}: liveness tick {rd['t_live']} reaches the next round's tick")
     run_phases(sims, rd, events, group, phases)
     end(sims, rd)

@@ -29,9 +29,14 @@ class PeerSelector:
             raise GsError("peer selection needs the whole matrix (one slice)")
         if not 1 <= fanout <= 8:
             raise GsError("fanout must be in 1..8")
+        from .workload import MAX_PHASES_PER_ROUND
+
         torch = sim.torch
-        if not 1 <= max_phases <= MAX_PHASES:
-            raise GsError(f"max_phases must be in 1..{MAX_PHASES}")
+        # the workload's tick model: phase p at round tick + 1 + p, liveness after the last phase, all before
+        # the next round's tick (TICKS_PER_ROUND apart)
+        top = min(MAX_PHASES, MAX_PHASES_PER_ROUND)
+        if not 1 <= max_phases <= top:
+            raise GsError(f"max_phases must be in 1..{top}")
         self.sim, self.fanout, self.seed, self.iters = sim, int(fanout), int(seed), int(iters)
         self.max_phases = int(max_phases)
         n, F = sim.n, self.fanout

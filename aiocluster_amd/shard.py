@@ -30,7 +30,7 @@ from __future__ import annotations
 
 import numpy as np
 
-from ._lib import COUNTER_FIELDS, GsError
+from ._lib import COUNTER_FIELDS, GsError, overflow_list_len
 
 CHAIN_PENDING = -1  # u64 ~0 viewed as int64 (gossip_sim.hip CHAIN_PENDING)
 
@@ -49,6 +49,31 @@ class LocalComm:
 
     def sum_counters(self, per_slice: list[dict]) -> dict:
         return {k: sum(c[k] for c in per_slice) for k in COUNTER_FIELDS}
+
+    def any(self, flag: bool) -> bool:
+        return flag
+
+
+class SoloComm:
+    """Slice ``rank`` of a ``world``-slice cluster held alone (one GPU's share of a multi-GPU run): the
+    other slices' gathered totals are zeros.  Exact for this slice's columns whenever the MTU cannot bind
+    (config 4's contract: mtu above every delta), since a slice's packing then does not depend on the
+    others; otherwise a timing rehearsal only."""
+
+    def __init__(self, world: int, rank: int = 0):
+        self.world = world
+        self.rank = rank
+
+    def gather(self, parts):
+        import torch
+
+        (x,) = parts
+        out = torch.zeros((self.world,) + tuple(x.shape), dtype=x.dtype, device=x.device)
+        out[self.rank] = x
+        return out
+
+    def sum_counters(self, per_slice: list[dict]) -> dict:
+        return per_slice[0]
 
     def any(self, flag: bool) -> bool:
         return flag
@@ -117,7 +142,7 @@ def run_sliced_phase(slices, comm, mtu: int, t: int, ini, res) -> int:
                 s.phase_pack(t, ini, res, step, tot_all, chain_all, ch)
         return comm.world
     dev = tots[0].device
-    lists = [torch.empty(2 * n + 256, dtype=torch.int32, device=dev) for _ in slices]
+    lists = [torch.empty(overflow_list_len(n), dtype=torch.int32, device=dev) for _ in slices]
     chaincs = [torch.empty(2 * n, dtype=torch.int64, device=dev) for _ in slices]
     # the same gathered totals give every slice the same list: one host read per process
     for i in range(len(slices) - 1, -1, -1):
@@ -200,6 +225,8 @@ class ShardGroup:
         s0 = self.slices[0]
         for s in self.slices:
             s._flush()
+            if s._ev is not None:
+                raise GsError("hook events on a sliced cluster are not supported (order_events needs one handle)")
         ini, res = s0._pairs_dev(initiators, responders)
         if self.native:
             import ctypes as C
@@ -215,6 +242,10 @@ class ShardGroup:
             return
         if run_sliced_phase(self.slices, self.comm, self.mtu, t, ini, res) > 1:
             self.chain_phases += 1
+
+    def flush_reports(self, t: int):
+        for s in self.slices:
+            s.flush_reports(t)
 
     def update_node_liveness(self, t: int, up):
         for s in self.slices:

@@ -118,10 +118,11 @@ def order_events(ev: np.ndarray, n: int, phases: dict, wmap: list) -> np.ndarray
 
 
 def make_config(n: int, k: int, cfg: dict, flags: int, hist_cap: int, shards: int = 1,
-                shard: int = 0) -> _lib.GsConfig:
+                shard: int = 0, ring_rows: int = 0) -> _lib.GsConfig:
     c = _lib.GsConfig()
     c.n_shards = shards
     c.shard = shard
+    c.ring_rows = ring_rows
     c.n_nodes = n
     c.n_keys = k
     c.hist_cap = hist_cap
@@ -169,7 +170,8 @@ class GossipSim:
                  initial_values: dict[int, list[tuple[int, str]]] | None = None, *, device: str = "cuda:0",
                  tombstones: bool = True, fd_ring: bool | None = None, hist_cap: int = 64,
                  nid_sizes: list[int] | None = None, initial_ops: list[np.ndarray] | None = None,
-                 canonical: bool | None = None, shards: int = 1, shard: int = 0, held: bool = True):
+                 canonical: bool | None = None, shards: int = 1, shard: int = 0, held: bool = True,
+                 ring_rows=None):
         import torch
 
         if not torch.cuda.is_available():
@@ -202,13 +204,15 @@ class GossipSim:
                 raise GsError("held=False (GS_NO_HELD) needs tombstones=False")
             flags |= GS_NO_HELD
         W = int(cfg["window"])
+        # sampled rings: these observer rows keep interval rings (exact eviction), the others compact windows
+        self.ring_rows = sorted(set(int(x) for x in ring_rows)) if ring_rows else []
         if fd_ring is None:
-            fd_ring = n * ((n + 63) // 64 * 64) * W * 2 <= (1 << 30)  # whole-cluster rule: every slice agrees
+            fd_ring = not self.ring_rows and n * ((n + 63) // 64 * 64) * W * 2 <= (1 << 30)  # whole-cluster rule
         if fd_ring:
             flags |= GS_FD_RING
         self.flags = flags
         self.canonical = bool(flags & GS_CANONICAL)
-        c = make_config(n, k, cfg, flags, hist_cap, shards, shard)
+        c = make_config(n, k, cfg, flags, hist_cap, shards, shard, len(self.ring_rows))
         h = C.c_void_p()
         rc = self.L.gs_create(C.byref(c), C.byref(h))
         if rc:
@@ -231,6 +235,9 @@ class GossipSim:
             ns = np.asarray(nid_sizes, dtype=np.uint16)
             kl = np.asarray([len(s.encode()) for s in self.keys], dtype=np.uint8)
             self._chk(self.L.gs_boot(h, ns.ctypes.data_as(C.c_void_p), kl.ctypes.data_as(C.c_void_p)), "gs_boot")
+            if self.ring_rows:
+                rr = np.asarray(self.ring_rows, dtype=np.uint32)
+                self._chk(self.L.gs_set_ring_rows(h, rr.ctypes.data_as(C.c_void_p), len(rr)), "gs_set_ring_rows")
         except Exception:
             self.close()
             raise
@@ -409,6 +416,11 @@ class GossipSim:
                                         C.c_void_p(chain.data_ptr()), C.c_void_p(chainc.data_ptr())),
                   "gs_phase_chain")
 
+    def flush_reports(self, t: int):
+        """gs_flush_reports: apply the open round's pending heartbeat reports to the windows now (a
+        mid-round readback of GS_R_FD); the next phase must come after ``t``."""
+        self._chk(self.L.gs_flush_reports(self.h, t), "gs_flush_reports")
+
     def update_node_liveness(self, t: int, up):
         self._flush()
         u = up if hasattr(up, "data_ptr") else self._dev(np.asarray(up, dtype=np.uint8), self.torch.uint8)
@@ -463,7 +475,9 @@ class GossipSim:
         self._ev = torch.empty((capacity, 8), dtype=torch.int32, device=self.device)
         self._ev_phases = {}  # phase tick -> (initiators, responders): the exchange order of that phase
         self._ev_wmap = []    # owner-write seq -> index among the caller's writes since enable_events
-        self._ev_writes = 0
+        # writes queued before this call (not yet flushed) are the first ones of the new numbering
+        self._pending = [(*w[:-1], i) for i, w in enumerate(self._pending)]
+        self._ev_writes = len(self._pending)
         self._ev_count = torch.zeros(1, dtype=torch.int32, device=self.device)
         self._chk(self.L.gs_set_events(self.h, C.c_void_p(self._ev.data_ptr()), capacity,
                                        C.c_void_p(self._ev_count.data_ptr())), "gs_set_events")
@@ -505,6 +519,23 @@ class GossipSim:
         """Write out GS_R_HELD for the prefix views of rows [row_lo, row_hi) (readback only)."""
         hi = self.n if row_hi is None else row_hi
         self._chk(self.L.gs_materialize_held(self.h, row_lo, hi), "gs_materialize_held")
+
+    def horizon(self) -> dict:
+        """Headroom to the two bounds of the exact compact layout: the most intervals any
+        sampling window holds since its last reset (compact windows: err_fd_overflow at W; the ring
+        evicts exactly), and the most writes of any (owner, key) of this slice (err_hist_full at
+        hist_cap - 1)."""
+        torch = self.torch
+        sb = _lib.fd_sum_bits(int(self.cfg["window"]))
+        fd = self.region("FD", torch.int32, (self.n, self.np_))
+        mx = 0
+        for r0 in range(0, self.n, 8192):
+            blk = fd[r0:r0 + 8192, : self.ncol]
+            mx = max(mx, int(((blk >> sb) & ((1 << (32 - sb)) - 1)).max().item()))
+        lw = self.region("LAST_W", torch.uint8, (self.ncol, self.kp))[:, : self.k]
+        return {"max_window_count": mx, "window": int(self.cfg["window"]),
+                "fd_ring": "all rows" if self.flags & GS_FD_RING else f"{len(self.ring_rows)} sampled rows",
+                "max_writes_per_owner_key": int(lw.max().item()), "hist_cap_writes": self.hist_cap - 1}
 
     def inexact_views(self) -> int:
         """Views with holes (GS_MV_INEXACT set): those whose HELD row the exchange kernel keeps."""
@@ -610,7 +641,8 @@ class GossipSim:
         out["fd_last"] = np.where(last == GS_NONE, -1, last.astype(np.int64))
         cnt = g["FD_CNT"][:, :n].astype(np.int32)
         W = int(self.cfg["window"])
-        out["fd_len"] = np.where(last == GS_NONE, 0, np.minimum(cnt, W) if self.flags & GS_FD_RING else cnt)
+        # ring windows count appends up to 2W (len = min(cnt, W)); a compact window never holds more than W
+        out["fd_len"] = np.where(last == GS_NONE, 0, np.minimum(cnt, W))
         out["fd_sum"] = np.where(last == GS_NONE, 0.0, g["FD_SUM"][:, :n] / 64.0)
         st = g["FD_STATE"][:, :n]
         out["live"] = (st == 1).astype(np.int32)
@@ -675,8 +707,7 @@ class GossipSim:
         return out
 
     def _window_len(self, cnt: int) -> int:
-        W = int(self.cfg["window"])
-        return min(cnt, W) if self.flags & GS_FD_RING else cnt
+        return min(cnt, int(self.cfg["window"]))
 
     def observer_state(self, o: int, g=None) -> dict:
         """Canonical dump, identical in format to ``oracle/refharness.py`` (golden fixtures)."""

@@ -140,6 +140,7 @@ class WorkloadSpec:
     partition: tuple[int, int] | None = None  # rounds [start, end) with the cluster split in halves
     node_style: str = "synthetic"
     initial_keys: int | None = None  # keys written at boot (default: all k)
+    quiet_from: int | None = None  # rounds >= this: no writes, every node up (convergence checks)
     extra: dict = field(default_factory=dict)
 
 
@@ -175,8 +176,11 @@ class Workload:
             goes_down = up & (rng.random(n) < s.down_frac / max(1, s.down_rounds))
             self._down_until[goes_down] = r + s.down_rounds
             up = self._down_until <= r
+        quiet = s.quiet_from is not None and r >= s.quiet_from
+        if quiet:
+            up = np.ones(n, dtype=bool)
         # -- owner writes (only up nodes write)
-        m_w = int(round(s.write_frac * n))
+        m_w = 0 if quiet else int(round(s.write_frac * n))
         if m_w > 0:
             owners = rng.choice(n, size=m_w, replace=False).astype(np.int64)
             keys = rng.integers(0, s.k, size=m_w).astype(np.int64)

@@ -159,28 +159,6 @@ def cpu_baseline(sim, cfg, rd, sample: int, min_seconds: float = 10.0, threads: 
     }
 
 
-class RehearsalComm:
-    """One slice of a G-slice cluster on this GPU (``--rehearse-slices G``): the other slices' gathered
-    totals are zeros, so the packing is NOT the cluster's -- a timing rehearsal of one GPU's share of a
-    G-GPU run (memory footprint, kernel times), never a result."""
-
-    def __init__(self, world: int):
-        self.world = world
-        self.rank = 0
-
-    def gather(self, parts):
-        import torch
-
-        (x,) = parts
-        return torch.cat([x[None], torch.zeros((self.world - 1,) + tuple(x.shape), dtype=x.dtype, device=x.device)])
-
-    def sum_counters(self, per_slice):
-        return per_slice[0]
-
-    def any(self, flag):
-        return flag
-
-
 def aggregate(exchanges: float, elapsed: float, dist=None, dev=None) -> tuple[float, float]:
     """Whole-job totals: exchanges summed over ranks, time = the slowest rank's."""
     if dist is None:
@@ -257,7 +235,7 @@ def load_traffic(workload: str, kernel: str, units_per_launch: float):
         f"({e.get('calibration')}), x this run's units per launch")
 
 
-KERNEL_OF = {"pass1": "k_pass1", "pack": "k_pack_slice", "liveness": "k_liveness", "count": "k_count"}
+KERNEL_OF = {"pass1": "k_pass1", "pack": "k_settle", "liveness": "k_liveness", "count": "k_settle"}
 
 
 def roofline(sims, local_c, exch, kt, elapsed, torch, dev, rank, group, workload) -> dict:
@@ -321,6 +299,93 @@ def roofline(sims, local_c, exch, kt, elapsed, torch, dev, rank, group, workload
         "kernels": per,
         "survey_formula_bytes_per_phase": survey,
         "survey_formula_gbs_over_pass1": survey / (kt["pass1"][0] / launches / 1e3) / 1e9 if kt["pass1"][0] else None,
+    }
+
+
+C4_NODES, C4_GPUS = 262144, 8
+
+
+def config4_leg(args, world: int, rank: int, dist, dev) -> dict:
+    """BASELINE config 4: 262,144 nodes over 8 GPUs, one owner-column slice of 32,768 columns per rank
+    (all 262,144 observer rows: ~170 GB of HBM per GPU), config 4's contract: warm start, no
+    deletes, version-only views (GS_NO_HELD), mtu 2^30 above every delta (no truncation).  Same workload
+    shape as the headline (K = 16, F = 3, 5 % writes + 5 % up/down churn per round, window 1000).  With 8
+    ranks the slices gather their DeltaPb totals per phase over RCCL (torch.distributed "nccl");
+    ``world == 1`` holds slice 0 of 8 alone (``SoloComm``: exact for its columns under this contract,
+    tests/test_gpu_config4.py) and reports one GPU's share.  Weak in the sense of fixed work per GPU:
+    every rank runs every exchange on its own columns."""
+    import torch
+
+    from aiocluster_amd import driver
+    from aiocluster_amd.scenario import DEFAULT_CFG
+    from aiocluster_amd.shard import DistComm, ShardGroup, SoloComm
+    from aiocluster_amd.sim import GossipSim
+    from aiocluster_amd.workload import WorkloadSpec, key_names, synthetic_node_ids
+
+    n, K = C4_NODES, args.keys
+    cfg = dict(DEFAULT_CFG)
+    cfg["mtu"] = 1 << 30
+    spec = WorkloadSpec(n=n, k=K, fanout=args.fanout, seed=args.seed, init="warm", write_frac=0.05,
+                        down_frac=0.05, down_rounds=3)
+    t0 = time.perf_counter()
+    shard = rank if world == C4_GPUS else 0
+    sim = GossipSim(synthetic_node_ids(n), key_names(K), cfg, init="warm", device=str(dev), tombstones=False,
+                    fd_ring=False, hist_cap=16, initial_ops=driver.boot_ops(n, K), held=False, shards=C4_GPUS,
+                    shard=shard)
+    comm = DistComm() if world == C4_GPUS else SoloComm(C4_GPUS, 0)
+    grp = ShardGroup([sim], comm, cfg["mtu"])
+    S, W, T = args.config4_settle, 1, args.config4_steps
+    plans = driver.prepare(spec, S + W + T, torch, dev)
+    torch.cuda.synchronize(dev)
+    setup = time.perf_counter() - t0
+    for r in range(S + W):
+        driver.run_round([sim], plans[r], group=grp)
+    torch.cuda.synchronize(dev)
+    sim.check()
+    sim.reset_counters()
+    sim.set_timing(True)
+    sim.kernel_times()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    for r in range(S + W, S + W + T):
+        driver.run_round([sim], plans[r], group=grp)
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    el = time.perf_counter() - t1
+    kt = sim.kernel_times()
+    sim.set_timing(False)
+    c = grp.check()
+    exch = sum(plans[r]["exchanges"] for r in range(S + W, S + W + T))
+    assert c["exchanges"] == exch, (c["exchanges"], exch)
+    _, el_max = aggregate(0.0, el, dist, dev)
+    hz = sim.horizon()
+    sim.close()
+    del sim, grp
+    torch.cuda.empty_cache()
+    return {
+        "metric": "simulated gossip exchanges/sec at 262,144 nodes (BASELINE config 4)",
+        "value": exch / el_max if world == C4_GPUS else None,
+        "one_gpu_share_exchanges_per_s": exch / el if world != C4_GPUS else None,
+        "unit": "exchanges/s",
+        "n_gpus": world if world == C4_GPUS else 1,
+        "slices": C4_GPUS,
+        "scope": ("the whole 262,144-node cluster, one slice per GPU" if world == C4_GPUS else
+                  "slice 0 of 8 held alone on one GPU: every exchange of the cluster on 32,768 owner columns "
+                  "(one GPU's share of the 8-GPU run; exact for those columns under config 4's contract)"),
+        "steps": T, "warmup": W, "settle": S,
+        "ms_per_step": el_max / T * 1e3,
+        "exchanges_per_step": exch / T,
+        "setup_s": setup,
+        "config": {"workload": f"N={n} K={K} F={args.fanout} warm, 5% writes + 5% down churn/round, window 1000, "
+                               f"mtu 2^30 (no truncation), version-only views (GS_NO_HELD)",
+                   "parallelism": f"owner-column slices x{C4_GPUS}" + (" (RCCL all-gather of slice totals)"
+                                                                       if world == C4_GPUS else ", slice 0 only")},
+        "kernel_ms_per_step": {k: v[0] / T for k, v in kt.items() if v[1]},
+        "counters": {k: v for k, v in c.items() if not k.startswith("err_")},
+        "exactness": hz,
     }
 
 
@@ -402,7 +467,15 @@ def main():
                          "select_nodes_for_gossip (gs_select_peers) + Luby phases (gs_schedule_phases), reported "
                          "as the line's peer_select object (0 = skip)")
     ap.add_argument("--rehearse-slices", type=int, default=0,
-                    help="hold only slice 0 of G owner-column slices (one GPU's share of a G-GPU run; timing only)")
+                    help="hold only slice 0 of G owner-column slices (one GPU's share of a G-GPU run; timing only "
+                         "unless the mtu cannot bind)")
+    ap.add_argument("--config4-steps", type=int, default=3,
+                    help="with --gpus 8: after the headline, time this many rounds of BASELINE config 4 (262,144 "
+                         "nodes, one owner-column slice of 32,768 columns per GPU, version-only views, mtu 2^30), "
+                         "reported as the line's config4 object (0 = skip)")
+    ap.add_argument("--config4-settle", type=int, default=3, help="untimed config-4 rounds before its warmup")
+    ap.add_argument("--config4", action="store_true",
+                    help="on one GPU: also run the config-4 leg as slice 0 of 8 held alone (one GPU's share)")
     ap.add_argument("--native-comm", action="store_true",
                     help="--gpus N: the library drives each sliced phase over its own RCCL communicator "
                          "(gs_comm_init + gs_run_phase) instead of aiocluster_amd/shard.py over torch.distributed; "
@@ -434,7 +507,7 @@ def main():
 
     from aiocluster_amd import driver
     from aiocluster_amd.scenario import DEFAULT_CFG
-    from aiocluster_amd.shard import DistComm, LocalComm, ShardGroup
+    from aiocluster_amd.shard import DistComm, LocalComm, ShardGroup, SoloComm
     from aiocluster_amd.sim import GossipSim
     from aiocluster_amd.workload import WorkloadSpec, key_names, synthetic_node_ids
 
@@ -459,7 +532,7 @@ def main():
         group = ShardGroup(sims, DistComm(), cfg["mtu"], native=args.native_comm)
     elif args.rehearse_slices > 1:
         sims = [GossipSim(ids, key_names(K), cfg, shards=args.rehearse_slices, shard=0, **kw)]
-        group = ShardGroup(sims, RehearsalComm(args.rehearse_slices), cfg["mtu"])
+        group = ShardGroup(sims, SoloComm(args.rehearse_slices), cfg["mtu"])
     elif args.slices > 1:
         sims = [GossipSim(ids, key_names(K), cfg, shards=args.slices, shard=g, **kw) for g in range(args.slices)]
         group = ShardGroup(sims, LocalComm(args.slices), cfg["mtu"], native=args.native_comm)
@@ -522,6 +595,14 @@ def main():
     ps = None
     if ps_steps:
         ps = peer_select_rounds(sims, plans, R0 + args.steps + 1, ps_steps, args, n, dev)
+    horizon = sims[0].horizon()
+    c4 = None
+    if args.config4_steps and (world == C4_GPUS or args.config4):
+        for s_ in sims:
+            s_.close()
+        del sims, sim, group
+        torch.cuda.empty_cache()
+        c4 = config4_leg(args, world, rank, dist, dev)
     if rank == 0:
         line = {
             "metric": ("REHEARSAL (one GPU's slice of a %d-GPU run, packing not the cluster's): exchanges/s"
@@ -558,6 +639,10 @@ def main():
             "peer_select": ps,
             **({"ABLATION_RESULTS_INVALID": os.environ["GS_ABLATE"]} if os.environ.get("GS_ABLATE") else {}),
             "counters": {**{k: v for k, v in c.items() if not k.startswith("err_")}, "inexact_views": inexact},
+            # headroom to the exact layout's two bounds: err_fd_overflow at a window count of W (compact
+            # windows), err_hist_full at hist_cap - 1 writes of one (owner, key)
+            "exactness": horizon,
+            "config4": c4,
         }
         print(json.dumps(line), flush=True)
     if dist is not None:

@@ -28,11 +28,15 @@
 extern "C" {
 #endif
 
-#define GS_API_VERSION 10
+#define GS_API_VERSION 11
 #define GS_MAX_PHASES 64  /* gs_schedule_phases: phases per round */
 #define GS_TICK_US 15625u
 #define GS_NONE 0xFFFFFFFFu
 #define GS_CAND_CAP 1024u /* GS_R_CAND records per exchange, direction and row half */
+#define GS_PLANES 32u     /* GS_R_PEND report bit planes per observer row: phases per plane base */
+/* u32 words of gs_phase_overflow's DEVICE list for a phase of n exchanges: 2n slots, ceil(2n / 1024)
+ * block counts, the total */
+#define GS_OVERFLOW_LIST_LEN(n) (2u * (n) + (2u * (n) + 1023u) / 1024u + 1u)
 
 /* error codes */
 #define GS_OK 0
@@ -74,6 +78,11 @@ typedef struct gs_config {
                                        G > 1 needs GS_CANONICAL); one handle per slice, usually one per GPU */
     uint32_t shard;                 /* this handle's slice: columns [shard*B, min(N, (shard+1)*B)),
                                        B = ceil(N/G) rounded up to 64 (every slice must be non-empty) */
+    uint32_t ring_rows;             /* sampled rings (not with GS_FD_RING): this many observer rows, chosen by
+                                       gs_set_ring_rows, keep every window's interval ring (exact eviction
+                                       past W intervals, BoundedArrayStats); the other rows keep compact
+                                       windows, exact up to W intervals, and a compact window that would need
+                                       an eviction is counted in fd_saturated (not an error) */
 } gs_config;
 
 /* device regions (all caller-allocated).  [N][NP] regions hold every observer row o and this
@@ -98,7 +107,8 @@ enum gs_region {
                                         _dead_nodes, time of death in GS_R_FD_TOD); bit 2: the pair has a
                                         sampling window; bit 3: its last report is >= 2^15 ticks old */
     GS_R_TS,          /* u32 [N][NP][KP] tombstone receive tick, GS_NONE for SET entries (GS_TOMBSTONES) */
-    GS_R_RING,        /* u16 [N][NP][W] interval ring in ticks (GS_FD_RING) */
+    GS_R_RING,        /* u16 [N][NP][W] interval ring in ticks (GS_FD_RING); [ring_rows][NP][W] by ring slot
+                                        with sampled rings */
     GS_R_POS,         /* u32 [N][NP]   insertion index of owner j in observer o's dict, GS_NONE = absent (general) */
     GS_R_ORD,         /* u32 [N][NP]   owner at insertion index q (general) */
     GS_R_ROW,         /* u32 [N][4]    {dict size, tombstone-present flag, a lower bound of the first tick a
@@ -116,11 +126,11 @@ enum gs_region {
     GS_R_SLICE_BITS,  /* u32 [N/2][2][NP/32] stale-owner bitmaps per exchange and direction: between
                                         gs_phase_count and gs_phase_pack (n_shards > 1), and between the two
                                         kernels of a canonical one-slice gs_run_phase */
-    GS_R_PEND,        /* u64 [N][16][PW] heartbeat reports of the current round: one bit plane per phase
+    GS_R_PEND,        /* u64 [N][GS_PLANES][PW] heartbeat reports of the current round: one bit plane per phase
                                         p (tick = round tick + 1 + p) and observer row, PW = NP rounded up
                                         to 256, / 64; column c at word (c/256)*4 + c%4, bit (c/4)%64;
                                         replayed into GS_R_FD by gs_liveness */
-    GS_R_PEND_STAMP,  /* u32 [N][16]   tick of the phase that last wrote plane row (o, p): the row is
+    GS_R_PEND_STAMP,  /* u32 [N][GS_PLANES] tick of the phase that last wrote plane row (o, p): the row is
                                         valid for the current round only if it equals round tick + 1 + p */
     GS_R_LATEST,      /* u32 [NC][KP]  each key's latest write: version | DeltaPb bytes of its KeyValueUpdatePb
                                         field << 16 (no GS_TOMBSTONES only: versions <= 16,256, values < 16 KiB) */
@@ -137,6 +147,10 @@ enum gs_region {
                                         operation's tick; exact until 2^15 old, then only "old": bit 3 above;
                                         gs_create requires max_interval < 2^14 and
                                         phi_threshold * max(max_interval, prior) < 2^15 ticks) */
+    GS_R_SLOT_STAT,   /* u32 [N/2][2][4] sliced canonical handles: per exchange and direction, this slice's
+                                        {NodeDeltas, kvs, candidates, needs a pack} of a speculative phase,
+                                        between gs_phase_count and gs_phase_pack */
+    GS_R_RING_SLOT,   /* u32 [N]       sampled rings: each observer row's ring slot, GS_NONE = compact windows */
     GS_NUM_REGIONS
 };
 
@@ -173,8 +187,10 @@ typedef struct gs_counters {
     uint64_t err_holes;        /* GS_NO_HELD: a view got holes (a truncated NodeDelta); result inexact */
     uint64_t err_hb_lag;       /* a view lagged its owner's heartbeat by >= 2^15 at a gs_check_heartbeat_lag
                                   sweep: the 16-bit heartbeat store is no longer known to be exact */
-    uint64_t plane_flushes;    /* host count: mid-round report replays (phases > 16 ticks after the round start) */
-    uint64_t reserved[9];
+    uint64_t plane_flushes;    /* host count: mid-round report replays (phases > GS_PLANES ticks after the plane base) */
+    uint64_t fd_saturated;     /* sampled rings: intervals a full compact window could not append (the compact rows'
+                                  windows are exact only up to W intervals; the ring rows are exact) */
+    uint64_t reserved[8];
 } gs_counters;
 
 /* Failure-detector membership census (gs_fd_census): (observer, target) pairs with the observer up and
@@ -209,6 +225,9 @@ int gs_set_stream(gs_handle *h, void *hip_stream);
 int gs_boot(gs_handle *h, const uint16_t *nid_size, const uint8_t *key_len);
 /* Warm start: every observer learns every owner's current state, in index order. */
 int gs_warm(gs_handle *h);
+/* Sampled rings (gs_config.ring_rows > 0): the observer rows (host array, distinct, n <= ring_rows) whose
+ * windows keep interval rings, ring slot i = rows[i].  After gs_boot, before the first phase. */
+int gs_set_ring_rows(gs_handle *h, const uint32_t *rows, uint32_t n);
 
 /* Fill GS_R_HELD of observer rows [row_lo, row_hi) for the views it is not kept for (see
  * GS_MV_INEXACT).  Readback only; no-op with GS_TOMBSTONES. */
@@ -225,9 +244,9 @@ int gs_begin_round(gs_handle *h, const uint8_t *up, uint32_t tick);
  * compute_partial_delta_respecting_mtu and apply_delta on both sides.  At most n_nodes/2 exchanges;
  * the round must still be open (no gs_liveness since the last gs_begin_round) and `tick` must be
  * later than the round start and than the round's previous phase.  The failure detector's
- * report_heartbeat calls are recorded per phase (GS_R_PEND bit planes, 16 per row) and applied to the
+ * report_heartbeat calls are recorded per phase (GS_R_PEND bit planes, GS_PLANES per row) and applied to the
  * sampling windows, in tick order, by the gs_liveness that closes the round (nothing reads a
- * window in between); a phase more than 16 ticks after the planes' base replays the pending planes
+ * window in between); a phase more than GS_PLANES ticks after the planes' base replays the pending planes
  * into the windows first (counted in plane_flushes). */
 int gs_run_phase(gs_handle *h, const int32_t *initiators, const int32_t *responders, uint32_t n, uint32_t tick);
 /* Owner-column sliced phase (n_shards > 1; gs_run_phase refuses sliced handles).  The slices of one
@@ -250,7 +269,7 @@ int gs_phase_pack(gs_handle *h, const int32_t *initiators, const int32_t *respon
                   uint32_t step, const uint64_t *slice_bytes_all, const uint64_t *chain_all, uint64_t *chain);
 /* Compacted chain (replaces step 4 above on canonical handles built with candidate records):
  *   gs_phase_overflow (blocking: one 4-byte read): the slots (2e + dir) whose gathered slice totals sum
- *     past the mtu, in slot order, into DEVICE list[2n + 256] (the tail is scratch), this slice's chain
+ *     past the mtu, in slot order, into DEVICE list[GS_OVERFLOW_LIST_LEN(n)] (the tail is scratch), this slice's chain
  *     state of each into DEVICE chainc[2n], and their number into *count (host; NULL: not read back);
  *   for step = 1 .. G-1: gather every slice's chainc[count] into chain_all[G][count], then
  *     gs_phase_chain(step) (one wave per listed slot; chain and chainc updated).
@@ -275,6 +294,12 @@ int gs_comm_id(void *id);
 int gs_comm_init(gs_handle *h, const void *id, uint32_t nranks, uint32_t rank);
 int gs_run_phase_group(gs_handle *const *handles, uint32_t n_handles, const int32_t *initiators,
                        const int32_t *responders, uint32_t n, uint32_t tick);
+
+/* Apply the open round's pending failure-detector reports (the GS_R_PEND planes of its phases so far) to
+ * the sampling windows now, in tick order, exactly as the closing gs_liveness would (nothing reads a
+ * window in between, so the result is the same); the round stays open and its next phase must come after
+ * `tick` (>= the last phase's tick).  Lets a checker compare GS_R_FD / GS_R_FD_LAST rows mid-round. */
+int gs_flush_reports(gs_handle *h, uint32_t tick);
 
 /* _update_node_liveness for every up node (server.py:606-620; failure_detector.py:89-128),
  * including garbage_collect + remove_node (general layout only). */
@@ -378,12 +403,12 @@ int gs_stream_write(void *dst, uint64_t bytes, uint32_t width, void *stream);
 /* Per-kernel timing (measurement): with timing on, every launch of the kinds below is bracketed by HIP
  * events on the library's stream; gs_kernel_times (blocking) returns the summed milliseconds and launch
  * counts since the previous call and clears them. */
-#define GS_KT_PASS1 0     /* a canonical one-slice phase (k_pass1 fused with packing; with env GS_PACK=split,
-                             pass 1 alone), the general-layout k_exchange, pass 1 of gs_phase_count */
-#define GS_KT_PACK 1      /* delta packing + apply_delta when it runs as its own kernel: k_pack_slice
-                             (GS_PACK=split, gs_phase_pack) and k_chain_step (gs_phase_chain) */
+#define GS_KT_PASS1 0     /* pass 1 of a canonical phase (k_pass1; with env GS_PACK=fused, k_pass1 fused with
+                             packing), the general-layout k_exchange, pass 1 of gs_phase_count */
+#define GS_KT_PACK 1      /* delta packing + apply_delta as their own kernel: k_settle (one-slice phases and
+                             gs_phase_pack step 0), k_pack_slice (GS_PACK=split), k_chain_step (gs_phase_chain) */
 #define GS_KT_LIVENESS 2  /* k_liveness (report replay + liveness sweep) */
-#define GS_KT_COUNT 3     /* the slice byte totals of gs_phase_count (k_count) */
+#define GS_KT_COUNT 3     /* the slice byte totals of gs_phase_count (k_settle, count mode) */
 typedef struct gs_ktimes {
     double ms[4];
     uint64_t launches[4];
@@ -396,7 +421,7 @@ int gs_reset_counters(gs_handle *h);
 int gs_sync(gs_handle *h);
 
 /* Copy-out (blocking, SURVEY §8(b) gs_read_*): observer rows [row_lo, row_hi) of a region indexed by
- * observer row (GS_R_HB, MV, GC, HELD, FD, FD_STATE, FD_TOD, TS, RING, POS, ORD, ROW) into host memory
+ * observer row (GS_R_HB, MV, GC, HELD, FD, FD_LAST, FD_STATE, FD_TOD, TS, RING, POS, ORD, ROW) into host memory
  * `out` of `cap` bytes, in the region's layout; *len = the bytes of those rows (set even when they exceed
  * cap, which fails).  GS_R_HELD rows are complete: the prefix views' ordinals are materialized first. */
 int gs_read_rows(gs_handle *h, int region, uint32_t row_lo, uint32_t row_hi, void *out, uint64_t cap, uint64_t *len);

@@ -764,6 +764,28 @@ void orc_set_row_ts(orc *o, int32_t obs, const uint32_t *ts_tick, int64_t tick_u
     }
 }
 
+/* The interval rings of a row loaded by orc_load_row (sampled ring rows of the device): ring_tick[N][W]
+ * (ticks), cnt[N] = intervals appended since the last reset, kept below 2W (the device's encoding: the
+ * next slot is cnt mod W, and the ring is full once cnt >= W).  BoundedArrayStats (failure_detector.py:
+ * 131-162): _values, _index, _filled; _sum was set by orc_load_row. */
+void orc_set_row_ring(orc *o, int32_t obs, const uint16_t *ring_tick, const uint32_t *cnt, int64_t tick_us) {
+    oobs *b = row(o, obs);
+    const int32_t N = o->N, W = o->c.window;
+    for (int32_t j = 0; j < N; j++) {
+        owin *w = &b->w[j];
+        if (b->pos[j] < 0 || !w->has) continue;
+        if (w->cap_alloc < W) {
+            w->vals = realloc(w->vals, sizeof(double) * (size_t)W);
+            if (!w->vals) abort();
+            w->cap_alloc = W;
+        }
+        for (int32_t k = 0; k < W; k++) w->vals[k] = (double)((int64_t)ring_tick[(size_t)j * W + k] * tick_us) / 1e6;
+        const uint32_t c = cnt[j];
+        w->filled = c >= (uint32_t)W;
+        w->idx = (int32_t)(c % (uint32_t)W);
+    }
+}
+
 /* ------------------------------------------- method-level hooks (KAT ports) */
 void orc_kat_set_view(orc *o, int32_t obs, int32_t owner, uint32_t hb, uint32_t mv, uint32_t gc) {
     oobs *b = row(o, obs);

@@ -113,6 +113,10 @@ void orc_load_row(orc *o, int32_t obs, int32_t cnt, const int32_t *order,
  * ts_tick[N][K] in ticks, 0xFFFFFFFF = none. */
 void orc_set_row_ts(orc *o, int32_t obs, const uint32_t *ts_tick, int64_t tick_us);
 
+/* The interval rings of a row loaded by orc_load_row (device rows with sampled rings): ring_tick[N][W]
+ * in ticks, cnt[N] = appends since the last reset (< 2W: full once >= W, next slot cnt mod W). */
+void orc_set_row_ring(orc *o, int32_t obs, const uint16_t *ring_tick, const uint32_t *cnt, int64_t tick_us);
+
 /* Keep a copy of observer obs's row / put it back (the CPU baseline re-runs the same
  * exchanges on restored rows to accumulate a bounded, repeatable sample). */
 void orc_snapshot_row(orc *o, int32_t obs);

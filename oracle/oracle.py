@@ -80,6 +80,7 @@ def lib():
             "orc_export_row": (None, [P, i32] + [P] * 13),
             "orc_load_row": (None, [P, i32, i32, P, P, P, P, P, i32, P, P, P, P, P, P, P, P, i64]),
             "orc_set_row_ts": (None, [P, i32, P, i64]),
+            "orc_set_row_ring": (None, [P, i32, P, P, i64]),
             "orc_snapshot_row": (None, [P, i32]),
             "orc_restore_row": (None, [P, i32]),
             "orc_kat_set_view": (None, [P, i32, i32, u32, u32, u32]),

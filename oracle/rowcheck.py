@@ -43,7 +43,14 @@ def compare_exports(got: dict, want: dict):
 
 
 class RowOracle:
-    """One oracle handle holding copies of selected observer rows of a ``GossipSim`` (one slice)."""
+    """One oracle handle holding copies of selected observer rows of a ``GossipSim``.
+
+    An owner-column slice (``sim.shards > 1``, canonical) is checked on its own columns: the oracle holds
+    the whole cluster's rows, with the slice's columns copied from the device and every other column
+    *inert* -- known (canonical), heartbeat 0, max_version 0, no keys, no window, on every loaded row --
+    so no exchange between two loaded rows merges, reports or sends anything for it.  That is exact for
+    the slice's columns whenever the MTU cannot bind (config 4's contract: a slice's packing does not
+    depend on the others); ``export_rows`` returns the slice's columns only."""
 
     def __init__(self, sim, cfg: dict):
         from aiocluster_amd.pbsize import nodeid_size
@@ -51,8 +58,9 @@ class RowOracle:
         self.sim = sim
         self.L = orc_mod.lib()
         n, K = sim.n, sim.k
-        if sim.shards > 1:
-            raise ValueError("RowOracle needs the whole matrix (one slice)")
+        if sim.shards > 1 and not sim.canonical:
+            raise ValueError("RowOracle on a slice needs the canonical layout")
+        self.lo, self.nc = sim.col_lo, sim.ncol
         ids = sim.node_ids
         self._ns = (C.c_int32 * n)(*[nodeid_size(x.name, x.generation_id, x.gossip_advertise_addr[0],
                                                   x.gossip_advertise_addr[1], x.tls_name) for x in ids])
@@ -88,9 +96,20 @@ class RowOracle:
         handles = handles or [self.new_handle()]
         g = sim._host(rows)
         n, K, Cc = sim.n, sim.k, sim.hist_cap
-        hist_ver = np.ascontiguousarray(g["HIST_VER"])
-        hist_vid = np.ascontiguousarray(g["HIST_VID"])
-        meta = g["HIST_META"]
+        lo, nc = self.lo, self.nc
+
+        def full(x, fill=0):
+            """owner-indexed array of the slice -> the whole cluster's (inert owners: ``fill``)"""
+            x = np.asarray(x)
+            if nc == n:
+                return np.ascontiguousarray(x[:n])
+            out = np.full((n,) + x.shape[1:], fill, dtype=x.dtype)
+            out[lo:lo + nc] = x[:nc]
+            return out
+
+        hist_ver = full(g["HIST_VER"])
+        hist_vid = full(g["HIST_VID"])
+        meta = full(g["HIST_META"])
         hist_vlen = np.ascontiguousarray((meta >> 18).astype(np.int32))
         hist_st = np.ascontiguousarray(((meta >> 16) & 3).astype(np.uint8))
         P = C.c_void_p
@@ -100,13 +119,15 @@ class RowOracle:
             else:
                 order = np.ascontiguousarray(g["ORD"][i, : g["ROW"][i, 0]].view(np.int32))
 
-            def c(x, dt=np.uint32):
-                return np.ascontiguousarray(np.asarray(x)[:n].astype(dt))
+            def c(x, dt=np.uint32, fill=0):
+                return full(np.asarray(x)[:nc].astype(dt), fill)
 
             hb, mv, gc = c(g["HB"][i]), c(g["MV"][i]), c(g["GC"][i])
-            fl, fs, fc, st = c(g["FD_LAST"][i]), c(g["FD_SUM"][i]), c(g["FD_CNT"][i]), c(g["FD_STATE"][i])
-            held = np.ascontiguousarray(g["HELD"][i, :n, :K])
-            ts = np.ascontiguousarray(g["TS"][i, :n, :K]) if "TS" in g else None
+            fl = c(g["FD_LAST"][i], fill=0xFFFFFFFF)
+            fs, fc, st = c(g["FD_SUM"][i]), c(g["FD_CNT"][i]), c(g["FD_STATE"][i])
+            held = full(g["HELD"][i, :nc, :K])
+            ts = full(g["TS"][i, :nc, :K], 0xFFFFFFFF) if "TS" in g else None
+            ring = self._ring(o)
             for h in (handles if owner is None else [owner[i]]):
                 self.L.orc_load_row(h, o, len(order), order.ctypes.data_as(P), hb.ctypes.data_as(P),
                                     mv.ctypes.data_as(P), gc.ctypes.data_as(P), held.ctypes.data_as(P), Cc,
@@ -115,8 +136,32 @@ class RowOracle:
                                     fs.ctypes.data_as(P), fc.ctypes.data_as(P), st.ctypes.data_as(P), TICK_US)
                 if ts is not None:
                     self.L.orc_set_row_ts(h, o, ts.ctypes.data_as(P), TICK_US)
+                if ring is not None:  # the row's interval rings: exact eviction from here on
+                    self.L.orc_set_row_ring(h, o, ring.ctypes.data_as(P), fc.ctypes.data_as(P), TICK_US)
         self.rows = rows
         return handles
+
+    def _ring(self, o: int):
+        """Observer row o's interval rings as u16 [N][W] ticks (whole-cluster owner indexing), if it has any:
+        every row with GS_FD_RING, the sampled rows with gs_config.ring_rows; else None."""
+        sim = self.sim
+        from aiocluster_amd._lib import GS_FD_RING
+
+        if sim.flags & GS_FD_RING:
+            slot = o
+        elif o in getattr(sim, "ring_rows", []):
+            slot = sim.ring_rows.index(o)
+        else:
+            return None
+        W = int(sim.cfg["window"])
+        t = sim.regions["RING"].view(sim.torch.int16).view(-1, sim.np_, W)[slot, : self.nc]
+        r = t.cpu().numpy().view(np.uint16)
+        n = sim.n
+        if self.nc == n:
+            return np.ascontiguousarray(r)
+        out = np.zeros((n, W), np.uint16)
+        out[self.lo:self.lo + self.nc] = r
+        return out
 
     def exchange(self, h, a: int, b: int, tick: int):
         self.L.orc_exchange(h, int(a), int(b), tick * TICK_US)
@@ -143,7 +188,7 @@ class RowOracle:
                 m = a[k] >= 0
                 a[k][m] //= TICK_US
             for k in out:
-                out[k].append(a[k])
+                out[k].append(a[k][self.lo:self.lo + self.nc])  # a slice: its own columns
         return {k: np.stack(v) for k, v in out.items()}
 
     def stats(self, h) -> dict:
@@ -152,7 +197,64 @@ class RowOracle:
         return {n: getattr(s, n) for n, _ in orc_mod._Stats._fields_}
 
 
-def check_phase_rows(sim, cfg: dict, rd: dict, sample: int = 64, phase: int = 0):
+def check_round_rows(sim, cfg: dict, rd: dict, sample: int = 32, seed: int = 0, group=None, only_rows=None):
+    """Full-size parity over EVERY phase of round ``rd`` (``sim`` has just run its ``gs_begin_round``).
+
+    Phase p: ``sample`` exchanges drawn at random from the phase; their rows are copied into a fresh
+    oracle handle after the device has applied the round's pending reports so far (``gs_flush_reports``:
+    the windows then hold phases 0..p-1), the whole phase runs on the device and the sample in the oracle,
+    the device applies the new reports, and the rows must be bit-identical (every field; membership only
+    changes at liveness).  The last phase is closed by the liveness sweep on both sides instead.  Rows of
+    later phases have been merged by several phases of this round.  ``only_rows``: sample only exchanges
+    with an endpoint in this set and compare only those rows (e.g. the sampled ring rows: the partner's
+    row is loaded to run the exchange, its windows are not compared).  Returns ``(diff, info)``."""
+    from aiocluster_amd import driver
+
+    rng = np.random.default_rng(seed)
+    sims = group.slices if group is not None else [sim]
+    phases = [p for p in rd["phases"] if p[2]]
+    info = {"phases": len(phases), "rows": 0, "node_deltas": 0, "hb_reports": 0, "truncated": 0}
+    keep = None if only_rows is None else set(int(x) for x in only_rows)
+    for i, (a_all, b_all, n, t) in enumerate(phases):
+        last = i == len(phases) - 1
+        an, bn = a_all.cpu().numpy(), b_all.cpu().numpy()
+        pool = np.arange(n) if keep is None else np.flatnonzero(
+            np.isin(an, list(keep)) | np.isin(bn, list(keep)))
+        pick = np.sort(rng.choice(pool, size=min(sample, len(pool)), replace=False))
+        a = an[pick].tolist()
+        b = bn[pick].tolist()
+        rows = a + b
+        cmp_rows = rows if keep is None else [o for o in rows if o in keep]
+        for s_ in sims:
+            s_.flush_reports(t - 1)
+        ro = RowOracle(sim, cfg)
+        (h,) = ro.load(rows)
+        driver.run_phases(sims, rd, phases=[(a_all, b_all, n, t)], group=group)
+        if last:
+            driver.end(sims, rd, tick=t + 1)
+        else:
+            for s_ in sims:
+                s_.flush_reports(t)
+        for x, y in zip(a, b):
+            ro.exchange(h, x, y, t)
+        if last:
+            for o in rows:
+                if rd["up_host"][o]:
+                    ro.liveness(h, o, t + 1)
+        want = ro.export_rows(h, cmp_rows)
+        got = sim.export_rows(cmp_rows)
+        diff = compare_exports(got, want) if cmp_rows else None
+        st = ro.stats(h)
+        ro.close()
+        info["rows"] += len(cmp_rows)
+        for k in ("node_deltas", "hb_reports", "truncated"):
+            info[k] += st[k]
+        if diff is not None:
+            return f"phase {i} (tick {t}): {diff}", info
+    return None, info
+
+
+def check_phase_rows(sim, cfg: dict, rd: dict, sample: int = 64, phase: int = 0, group=None):
     """Full-size parity on a sample: ``sim`` has just run ``gs_begin_round`` of round ``rd``
     (``aiocluster_amd.driver.begin``).  Copies the rows of the first ``sample`` exchanges of phase
     ``phase`` into the oracle, runs that whole phase on the device and closes the round there
@@ -169,9 +271,10 @@ def check_phase_rows(sim, cfg: dict, rd: dict, sample: int = 64, phase: int = 0)
     assert len(set(rows)) == len(rows), "a phase's exchanges are disjoint"
     ro = RowOracle(sim, cfg)
     (h,) = ro.load(rows)
-    driver.run_phases([sim], rd, phases=[rd["phases"][phase]])
+    sims = group.slices if group is not None else [sim]
+    driver.run_phases(sims, rd, phases=[rd["phases"][phase]], group=group)
     t_live = t + 1
-    driver.end([sim], rd, tick=t_live)
+    driver.end(sims, rd, tick=t_live)
     for x, y in zip(a, b):
         ro.exchange(h, x, y, t)
     for o in rows:

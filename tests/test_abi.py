@@ -47,7 +47,7 @@ def test_create_validates_config_without_gpu():
     assert lib.gs_region_bytes(h, _lib.REGION["POS"], ctypes.byref(nb)) == 0 and nb.value == 1000 * 1024 * 4
     # no tombstone GC: last_gc_version is 0 everywhere and not stored
     assert lib.gs_region_bytes(h, _lib.REGION["GC"], ctypes.byref(nb)) == 0 and nb.value == 0
-    assert lib.gs_region_bytes(h, _lib.REGION["PEND"], ctypes.byref(nb)) == 0 and nb.value == 1000 * 1024 * 2
+    assert lib.gs_region_bytes(h, _lib.REGION["PEND"], ctypes.byref(nb)) == 0 and nb.value == 1000 * 1024 * 4  # 32 planes
     lib.gs_destroy(h)
     withgc = make_config(1000, 16, DEFAULT_CFG, _lib.GS_TOMBSTONES, 32)
     assert lib.gs_create(ctypes.byref(withgc), ctypes.byref(h)) == 0

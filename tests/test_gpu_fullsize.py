@@ -1,18 +1,23 @@
 """Full-size parity (GPU only): BASELINE configs 3 and 5 at their real sizes.
 
 The oracle cannot replay a 65,536-node run (N^2 views), but one conflict-free phase touches only
-its own rows: after ~20 settle rounds on the device, the rows of 64 exchanges of the next phase are
+its own rows: after ~20 settle rounds on the device, the rows of sampled exchanges of a phase are
 copied into the C oracle (``oracle/rowcheck.py``), the whole phase runs on the device and in the
-oracle (the 64 exchanges), both close the round with the liveness sweep, and the 128 rows must be
-bit-identical: decoded heartbeats, max versions, last_gc versions, held keys (version, status,
-value, tombstone tick), failure-detector windows (last report, length, binary64 sum), live/dead.
+oracle (the sample), and the rows must be bit-identical: decoded heartbeats, max versions, last_gc
+versions, held keys (version, status, value, tombstone tick), failure-detector windows (last report,
+length, binary64 sum), live/dead.  ``check_round_rows`` does that for EVERY phase of a round (random
+exchanges, the device's pending reports applied before each copy), so rows merged by several phases
+of the round are compared too, closing with the liveness sweep; two rounds per config.  The owner
+tables the row copies carry (HIST / LAST_W / HIST_VID) are first checked against the workload's write
+stream restated on the host (``oracle/owner_tables.py``), so the oracle does not inherit them unchecked.
 The reference semantics checked: ``aiocluster/state.py:190-233, 340-415``, ``server.py:327-376,
 599-620``, ``failure_detector.py:12-128``.
 """
 
 import numpy as np
 import pytest
-from rowcheck import check_phase_rows
+from owner_tables import check_owner_tables, plan_batches
+from rowcheck import check_phase_rows, check_round_rows
 
 from aiocluster_amd import driver
 from aiocluster_amd.scenario import DEFAULT_CFG
@@ -28,36 +33,39 @@ def _run(sim, plans, rounds):
     sim.check()
 
 
-def test_config3_65536_sampled_phase_matches_oracle():
+def test_config3_65536_every_phase_of_two_rounds_matches_oracle():
     """BASELINE config 3 (the bench workload): 65,536 nodes x 16 keys, fanout 3, warm, 5 % writes + 5 %
-    up/down churn, window 1000, mtu 65,507, prefix-view layout; 20 settle rounds, then phase 0 of
-    round 20 on 64 sampled exchanges."""
+    up/down churn, window 1000, mtu 65,507, prefix-view layout; 20 settle rounds, the owner tables vs the
+    write stream, then every phase of rounds 20 and 21 on 16 random exchanges each."""
     import torch
 
     n, K = 65536, 16
     cfg = dict(DEFAULT_CFG)
     spec = WorkloadSpec(n=n, k=K, fanout=3, seed=0, init="warm", write_frac=0.05, down_frac=0.05, down_rounds=3)
+    boot = driver.boot_ops(n, K)
     sim = GossipSim(synthetic_node_ids(n), key_names(K), cfg, init="warm", tombstones=False, fd_ring=False,
-                    hist_cap=16, initial_ops=driver.boot_ops(n, K))
+                    hist_cap=16, initial_ops=boot)
     dev = sim.device
-    plans = driver.prepare(spec, 21, torch, dev)
+    plans = driver.prepare(spec, 22, torch, dev)
     _run(sim, plans, 20)
-    rd = plans[20]
-    driver.begin([sim], rd)
-    diff, info = check_phase_rows(sim, cfg, rd, sample=64)
-    assert diff is None, diff
+    assert check_owner_tables(sim, plan_batches(K, n, plans[:20], boot)) is None
+    for r in (20, 21):
+        rd = plans[r]
+        driver.begin([sim], rd)
+        diff, info = check_round_rows(sim, cfg, rd, sample=16, seed=r)
+        assert diff is None, f"round {r}: {diff}"
+        # the sample did real work: deltas, heartbeat reports (the oracle's counts), every phase
+        assert info["phases"] >= 8 and info["node_deltas"] > 0 and info["hb_reports"] > 0, info
     c = sim.check()
-    # the sample did real work: deltas, heartbeat reports (the oracle's counts)
-    assert info["node_deltas"] > 0 and info["hb_reports"] > 0, info
     assert c["exchanges"] > 0
     sim.close()
 
 
-def test_config5_16384_partition_heal_sampled_phases_match_oracle():
+def test_config5_16384_partition_heal_every_phase_matches_oracle():
     """BASELINE config 5: 16,384 nodes, K = 16, 5 % writes (1 % deletes), tombstone grace 10 rounds,
-    mtu 65,507, partition into halves for rounds 10-29, heal from round 30.  Sampled phases: the last
-    partitioned round (dead-marked peers: false positives) and the first healed round (the heal burst:
-    MTU-truncated NodeDeltas, tombstones collected)."""
+    mtu 65,507, partition into halves for rounds 10-29, heal from round 30.  Every phase of the last
+    partitioned round (dead-marked peers: false positives) and of the first healed round (the heal burst:
+    MTU-truncated NodeDeltas, tombstones collected) on 24 random exchanges each."""
     import torch
 
     n, K = 16384, 16
@@ -69,16 +77,17 @@ def test_config5_16384_partition_heal_sampled_phases_match_oracle():
                     hist_cap=32, initial_ops=driver.boot_ops(n, K))
     plans = driver.prepare(spec, 31, torch, sim.device)
     _run(sim, plans, 29)
+    assert check_owner_tables(sim, plan_batches(K, n, plans[:29], driver.boot_ops(n, K))) is None
     rd = plans[29]
     driver.begin([sim], rd)
-    diff, info = check_phase_rows(sim, cfg, rd, sample=64)
+    diff, info = check_round_rows(sim, cfg, rd, sample=24, seed=29)
     assert diff is None, f"partitioned round: {diff}"
     cen = sim.fd_census(rd["up"])
     assert cen["up_dead"] > 0  # the partition left peers dead-marked
     rd = plans[30]
     driver.begin([sim], rd)
     before = sim.check()
-    diff, info = check_phase_rows(sim, cfg, rd, sample=64)
+    diff, info = check_round_rows(sim, cfg, rd, sample=24, seed=30)
     assert diff is None, f"healed round: {diff}"
     c = sim.check()
     assert c["truncated"] - before["truncated"] > 0 and info["truncated"] > 0, (info, c["truncated"])

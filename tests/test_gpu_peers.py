@@ -133,12 +133,15 @@ def test_run_selected_round_helper():
     gpu.check()
 
 
-def test_rounds_with_more_than_16_phases_match_oracle():
-    """Fanout 8 = 24 phases per round: phases more than 16 ticks after the round start replay the
-    pending report planes into the windows mid-round (plane_flushes); every round vs the oracle."""
-    spec = WorkloadSpec(n=96, k=4, fanout=8, seed=31, init="warm", write_frac=0.1, down_frac=0.1, down_rounds=3)
-    scen = make_scenario("f8", spec, 6, {"initial_interval_s": 1.0, "phi_threshold": 3.0, "mtu": 800})
-    assert max(len(rd["phases"]) for rd in scen["rounds"]) > 16
+@pytest.mark.parametrize("fanout,flushes", [(8, False), (11, True)])
+def test_rounds_with_many_phases_match_oracle(fanout, flushes):
+    """Fanout 8 = 24 phases per round fit the 32 report planes (no mid-round replay); fanout 11 = 33
+    phases: phases more than 32 ticks after the round start replay the pending planes into the windows
+    mid-round (plane_flushes, one per round); every round vs the oracle."""
+    spec = WorkloadSpec(n=96, k=4, fanout=fanout, seed=31, init="warm", write_frac=0.1, down_frac=0.1,
+                        down_rounds=3)
+    scen = make_scenario(f"f{fanout}", spec, 6, {"initial_interval_s": 1.0, "phi_threshold": 3.0, "mtu": 800})
+    assert max(len(rd["phases"]) for rd in scen["rounds"]) > (32 if flushes else 16)
     gpu = make_backend(GossipSim, scen, fd_ring=False)
     orc = make_backend(OracleSim, scen)
     for r in range(len(scen["rounds"])):
@@ -147,4 +150,6 @@ def test_rounds_with_more_than_16_phases_match_oracle():
         diff = compare_exports(gpu.export(), orc.export())
         assert diff is None, f"round {r}: {diff}"
     c = gpu.check()
-    assert c["plane_flushes"] == len(scen["rounds"])
+    # a round replays its planes mid-round when it runs a phase more than 32 ticks after the round start
+    late = sum(1 for rd in scen["rounds"] if any(len(ph) for ph in rd["phases"][32:]))
+    assert c["plane_flushes"] == late and (late > 0) == flushes

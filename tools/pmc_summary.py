@@ -10,6 +10,7 @@ Each kernel's bytes are then (FETCH_SIZE x f_read(width) + WRITE_SIZE x f_write(
 width of the kernel's dominant streams:
     k_pass1       8 B per lane (u16 heartbeat / max_version rows, 4 columns per lane; stores likewise)
     k_pack_slice  8 B (candidate records; the rest are gathers, which no stream calibrates)
+    k_settle      8 B (likewise: candidate records, owner-table gathers)
     k_liveness    16 B per lane (two 16-B window loads + one 16-B state load per 4 columns)
 Only the launches inside bench.py's timed region are averaged (the last N of each kernel, N from the
 bench's JSON line).  The entry written to profiles/pmc_summary.json carries the source hash of the
@@ -30,10 +31,11 @@ from collections import defaultdict
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
-KERNELS = ("k_pass1", "k_pack_slice", "k_liveness", "k_exchange", "k_count", "k_begin_round", "k_owner_writes",
-           "k_reset_sched", "k_warm", "k_boot_self", "k_phi_row")
-WIDTH = {"k_pass1": 8, "k_pack_slice": 8, "k_liveness": 16, "k_exchange": 8, "k_count": 8}
-KIND = {"k_pass1": "pass1", "k_pack_slice": "pack", "k_liveness": "liveness", "k_exchange": "pass1", "k_count": "count"}
+KERNELS = ("k_pass1", "k_pack_slice", "k_settle", "k_liveness", "k_exchange", "k_count", "k_begin_round",
+           "k_owner_writes", "k_reset_sched", "k_warm", "k_boot_self", "k_phi_row")
+WIDTH = {"k_pass1": 8, "k_pack_slice": 8, "k_settle": 8, "k_liveness": 16, "k_exchange": 8, "k_count": 8}
+KIND = {"k_pass1": "pass1", "k_pack_slice": "pack", "k_settle": "pack", "k_liveness": "liveness", "k_exchange": "pass1",
+        "k_count": "count"}
 CAL_BYTES = 1 << 30
 
 
