@@ -1812,7 +1812,9 @@ __global__ __launch_bounds__(LB) void k_reset_sched(Dev d, const uint8_t *up, ui
 // FailureDetector.update_node_liveness for every known node but self (server.py:606-610;
 // failure_detector.py:89-106), phi in binary64 exactly as SamplingWindow.phi (43-53).  Also folds
 // the earliest "scheduled for deletion" tick per row.
-template <bool RING>
+// RING: 0 = compact windows only (no ring pointer at all: k_liveness stays within 64 VGPRs without
+// spills), 1 = every row has interval rings (GS_FD_RING), 2 = the sampled ring rows (gs_config.ring_rows).
+template <int RING>
 // One workgroup sweeps `per` consecutive 1024-column chunks of one row (fewer, longer workgroups:
 // the per-workgroup plane staging, stamp check and counter atomics are paid once per `per` chunks).
 // decide = false: only replay the pending reports into the windows, for every row (a round with phases
@@ -1823,8 +1825,8 @@ template <bool RING>
 __global__ __launch_bounds__(LB, LIVE_WAVES) void k_liveness(Dev d, const uint8_t *up, uint32_t t, uint32_t chunks,
                                                  uint32_t per, bool replay, bool decide) {
     // [wave][phase][the wave's 4 plane words of this chunk]: each wave stages and reads only its own
-    // words (lane l: phase l / 4 (+ 16), word l % 4), so the chunks need no workgroup barrier
-    __shared__ uint64_t s_pl[LB / WAVE][NPL][4];
+    // words (lane l: phase l / 2, words 2 (l % 2) + {0, 1}), so the chunks need no workgroup barrier
+    __shared__ __attribute__((aligned(16))) uint64_t s_pl[LB / WAVE][NPL][4];
     __shared__ uint32_t s_vm;
     const uint32_t groups = (chunks + per - 1) / per;
     const uint32_t o = blockIdx.x / groups, cb0 = (blockIdx.x % groups) * per;
@@ -1833,9 +1835,9 @@ __global__ __launch_bounds__(LB, LIVE_WAVES) void k_liveness(Dev d, const uint8_
     const bool genm = !(d.flags & GS_CANONICAL);
     // this row's interval rings: every row has them (RING: GS_FD_RING), or this is a sampled ring row
     uint16_t *rrow = nullptr;
-    if (RING) {
+    if (RING == 1) {
         rrow = d.ring + (size_t)o * d.NP * d.W;
-    } else if (d.ring_slot) {
+    } else if (RING == 2) {
         const uint32_t rs = d.ring_slot[o];
         if (rs != NONE) rrow = d.ring + (size_t)rs * d.NP * d.W;
     }
@@ -1870,11 +1872,15 @@ __global__ __launch_bounds__(LB, LIVE_WAVES) void k_liveness(Dev d, const uint8_
     const uint32_t wv = threadIdx.x >> 6, ln = threadIdx.x & 63u;
     if (vm) {
         __builtin_amdgcn_wave_barrier();  // this wave is done with the previous chunk's words
-        const uint32_t wi = cb * 16u + wv * 4u + (ln & 3u);
-        const uint32_t ph = ln >> 2;
-        if ((vm >> ph) & 1u) s_pl[wv][ph][ln & 3u] = wi < d.PW ? d.pend[((size_t)o * NPL + ph) * d.PW + wi] : 0ull;
-        if (NPL > 16 && (vm >> (ph + 16u)) & 1u)
-            s_pl[wv][ph + 16u][ln & 3u] = wi < d.PW ? d.pend[((size_t)o * NPL + ph + 16u) * d.PW + wi] : 0ull;
+        // 16 B per lane: NPL = 32 (lane l: phase l / 2, words 2 (l % 2) and 2 (l % 2) + 1), or NPL = 16
+        // (lanes 0-31 only); PW is a multiple of 4 and each wave's 4 words start on a multiple of 4
+        const uint32_t wi = cb * 16u + wv * 4u + (ln & 1u) * 2u;
+        const uint32_t ph = ln >> 1;
+        if (ph < NPL && ((vm >> ph) & 1u)) {
+            ulonglong2 w2 = make_ulonglong2(0ull, 0ull);
+            if (wi < d.PW) w2 = *reinterpret_cast<const ulonglong2 *>(d.pend + ((size_t)o * NPL + ph) * d.PW + wi);
+            *reinterpret_cast<ulonglong2 *>(&s_pl[wv][ph][(ln & 1u) * 2u]) = w2;
+        }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         __builtin_amdgcn_wave_barrier();
     }
@@ -1903,8 +1909,8 @@ __global__ __launch_bounds__(LB, LIVE_WAVES) void k_liveness(Dev d, const uint8_
                 while (m) {
                     const uint32_t bb = (uint32_t)__builtin_ctz(m);
                     m &= m - 1u;
-                    f = fd_report_val(d, rrow ? rrow + (size_t)(c0 + i) * d.W : nullptr, d.t_round + 1u + bb, f, alg,
-                                      ovf);
+                    f = fd_report_val(d, RING && rrow ? rrow + (size_t)(c0 + i) * d.W : nullptr, d.t_round + 1u + bb,
+                                      f, alg, ovf);
                 }
                 dw = true;
             }
@@ -1912,7 +1918,7 @@ __global__ __launch_bounds__(LB, LIVE_WAVES) void k_liveness(Dev d, const uint8_
             if (upo && j < d.ncol && d.col_lo + j != o && !(genm && ps[i] == NONE)) {
                 live++;
                 const bool has = f.last != NONE;
-                const uint32_t len = rrow ? (f.cnt < d.W ? f.cnt : d.W) : f.cnt;
+                const uint32_t len = RING && rrow ? (f.cnt < d.W ? f.cnt : d.W) : f.cnt;
                 bool alive = false;
                 if (has && len) {
                     // phi <= threshold (failure_detector.py:43-53, 97-98) decided without the two binary64
@@ -2931,9 +2937,11 @@ int launch_liveness(gs_handle *h, const uint8_t *up, uint32_t tick, bool replay,
     int rc = time_begin(h, e0);
     if (rc) return rc;
     if (h->cfg.flags & GS_FD_RING)
-        k_liveness<true><<<groups * h->N, LB, 0, h->stream>>>(h->d, up, tick, chunks, per, replay, decide);
+        k_liveness<1><<<groups * h->N, LB, 0, h->stream>>>(h->d, up, tick, chunks, per, replay, decide);
+    else if (h->d.ring_slot)
+        k_liveness<2><<<groups * h->N, LB, 0, h->stream>>>(h->d, up, tick, chunks, per, replay, decide);
     else
-        k_liveness<false><<<groups * h->N, LB, 0, h->stream>>>(h->d, up, tick, chunks, per, replay, decide);
+        k_liveness<0><<<groups * h->N, LB, 0, h->stream>>>(h->d, up, tick, chunks, per, replay, decide);
     HIPCHK(h, hipGetLastError());
     return time_end(h, GS_KT_LIVENESS, e0);
 }

@@ -228,7 +228,7 @@ def check_round_rows(sim, cfg: dict, rd: dict, sample: int = 32, seed: int = 0, 
         for s_ in sims:
             s_.flush_reports(t - 1)
         ro = RowOracle(sim, cfg)
-        (h,) = ro.load(rows)
+        (h,) = ro.load(rows) if rows else (ro.new_handle(),)
         driver.run_phases(sims, rd, phases=[(a_all, b_all, n, t)], group=group)
         if last:
             driver.end(sims, rd, tick=t + 1)
@@ -241,9 +241,8 @@ def check_round_rows(sim, cfg: dict, rd: dict, sample: int = 32, seed: int = 0, 
             for o in rows:
                 if rd["up_host"][o]:
                     ro.liveness(h, o, t + 1)
-        want = ro.export_rows(h, cmp_rows)
-        got = sim.export_rows(cmp_rows)
-        diff = compare_exports(got, want) if cmp_rows else None
+        # a phase with no sampled exchange on ``only_rows`` (a small third matching) still runs on the device
+        diff = compare_exports(sim.export_rows(cmp_rows), ro.export_rows(h, cmp_rows)) if cmp_rows else None
         st = ro.stats(h)
         ro.close()
         info["rows"] += len(cmp_rows)
