@@ -56,7 +56,7 @@ def fd_sum_bits(window: int) -> int:
 REGIONS = [
     "HB", "MV", "GC", "HELD", "FD", "FD_STATE", "TS", "RING", "POS", "ORD", "ROW",
     "LAST_W", "HIST", "HIST_VID", "NID_SIZE", "KEY_LEN", "STAMP", "COUNTERS", "SLICE_BITS", "PEND", "PEND_STAMP", "LATEST",
-    "SELF_HB", "CAND", "CAND_N", "FD_TOD", "FD_LAST", "SLOT_STAT", "RING_SLOT",
+    "SELF_HB", "CAND", "CAND_N", "FD_TOD", "FD_LAST", "SLOT_STAT", "RING_SLOT", "VLOG",
 ]
 REGION = {n: i for i, n in enumerate(REGIONS)}
 
@@ -80,7 +80,7 @@ EXPORTS = [
     "gs_latest_tick", "gs_flush_reports", "gs_set_ring_rows",
 ]
 
-API_VERSION = 11
+API_VERSION = 12
 MAX_PHASES = 64  # GS_MAX_PHASES
 
 
@@ -111,11 +111,12 @@ class GsCounters(C.Structure):
 CENSUS_FIELDS = ["up_pairs", "up_dead", "up_live", "down_pairs", "down_live"]
 
 
-KT_KINDS = ["pass1", "pack", "liveness", "count"]  # GS_KT_PASS1, GS_KT_PACK, GS_KT_LIVENESS, GS_KT_COUNT
+KT_KINDS = ["pass1", "pack", "liveness", "count", "lite"]  # GS_KT_PASS1, GS_KT_PACK, GS_KT_LIVENESS, GS_KT_COUNT, GS_KT_LITE
+KT_SLOTS = 8  # GS_KT_KINDS
 
 
 class GsKtimes(C.Structure):
-    _fields_ = [("ms", C.c_double * 4), ("launches", C.c_uint64 * 4)]
+    _fields_ = [("ms", C.c_double * KT_SLOTS), ("launches", C.c_uint64 * KT_SLOTS)]
 
 
 class GsCensus(C.Structure):

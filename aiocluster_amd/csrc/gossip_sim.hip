@@ -125,10 +125,16 @@ struct Dev {
     // sent, and skip the store when it is sent whole.  Set per phase by the host (gs_run_phase /
     // gs_phase_count), identical in every kernel of the phase.
     uint32_t spec;
-    uint4 *slot_stat;
+    uint4 *slot_stat;  // sliced phases: per (exchange, direction) {NodeDeltas, kvs, candidates, needs a pack}
     // sampled rings (gs_config.ring_rows): ring slot of each observer row (NONE: a compact row), GS_R_RING
     // then holds [ring_rows][NP][W]; nullptr otherwise
-    uint32_t *ring_slot;  // sliced phases: per (exchange, direction) {NodeDeltas, kvs, candidates, needs a pack}
+    uint32_t *ring_slot;
+    // prefix views: each owner's writes by version, [NC][VL] (GS_R_VLOG): DeltaPb bytes of the kv field |
+    // version of the next write of the same key (0xFFFF: none) << 16 -- a prefix candidate's NodeDelta
+    // size from the entries (mr, ms] alone (pack_lite)
+    uint32_t *vlog;
+    uint32_t VL;
+    uint32_t lite;  // this phase runs k_lite before the exact packer (set per phase by the host)
     // event stream (gs_set_events): records {observer, owner, key | kind << 8, old version, new version,
     // tick, seq, 0}; kind 0 = on_key_change, 1 = node join, 2 = node leave; seq orders them (gossip_sim.h,
 // gs_set_events).  ev == nullptr: off
@@ -792,6 +798,95 @@ __device__ __forceinline__ void pack_list(const Dev &d, uint32_t s, uint32_t r, 
     if (!COUNT && lane == 0) shard_add(d, C_DBYTES, S - S0);
 }
 
+// Whole-delta fast path of one direction of a record phase (prefix views, pack_lite): when every stale owner
+// pass 1 recorded is a prefix candidate (both views S_j(M), no GS_MV_INEXACT) and the receiver's digest
+// holds all of them (no scheduled-for-deletion test due), NodeDelta j is {from = mr, last_gc 0,
+// max_version ms, the kvs of S_j(ms) above mr} (state.py:347-390) = the writes v in (mr, ms] that no write
+// <= ms overwrote (GS_R_VLOG: next > ms), so its DeltaPb bytes follow from those entries and the owner's
+// NodeIdPb size alone -- no latest-write row, no history entry.  If the delta then fits from S0, every
+// NodeDelta is sent whole (state.py:392-398) and each apply is apply_cand's fast path, one max_version
+// store.  Returns false with nothing stored otherwise; the caller runs the exact packer (pack_records).
+// Lane l takes candidates l, l + 64, ... of the two halves' lists in order (sums only: order-free); B
+// groups per step, so their record loads, then their log loads, are in flight together.
+// APPLY = false: only the delta's DeltaPb total (a sliced count pass: every candidate, whatever the mtu).
+constexpr int LITE_B = 4;
+// k_lite's per-slot flags (Dev::slot_stat[slot].w): LITE_FULL = the exact packer must size / pack the slot,
+// LITE_DONE = k_lite completed it
+constexpr uint32_t LITE_FULL = 1u, LITE_DONE = 2u;
+template <bool APPLY = true>
+__device__ __forceinline__ bool pack_lite(const Dev &d, uint32_t rcv, size_t slot, uint32_t S0, WStats &st,
+                                          uint32_t &Tout) {
+    const int lane = lane_id();
+    const uint32_t n0 = d.cand_n[slot * 2], n1 = d.cand_n[slot * 2 + 1];
+    if (n0 > GS_CAND_CAP || n1 > GS_CAND_CAP) return false;  // a half continues in its bitmap
+    const uint2 *L0 = d.cand + slot * 2 * GS_CAND_CAP, *L1 = L0 + GS_CAND_CAP;
+    const uint32_t nt = n0 + n1;
+    uint32_t sum = 0, kvs = 0, alg = 0;
+    bool bad = false;
+    for (uint32_t c0 = 0; c0 < nt; c0 += WAVE * LITE_B) {
+        uint2 rc[LITE_B];
+#pragma unroll
+        for (int u = 0; u < LITE_B; u++) {
+            const uint32_t i = c0 + (uint32_t)(u * WAVE + lane);
+            rc[u] = i < nt ? (i < n0 ? L0[i] : L1[i - n0]) : make_uint2(NONE, 0u);
+        }
+        uint32_t ev[LITE_B], ns[LITE_B];
+#pragma unroll
+        for (int u = 0; u < LITE_B; u++) {
+            ev[u] = 0u;
+            ns[u] = 0u;
+            if (rc[u].x == NONE) continue;
+            const uint32_t ms = rc[u].y & 0xFFFFu, mr = rc[u].y >> 16;  // sender / receiver words
+            if (!rec_fast(rc[u].y) || ms <= mr) { bad = true; continue; }
+            ev[u] = d.vlog[(size_t)rc[u].x * d.VL + ms];
+            ns[u] = d.nid_size[rc[u].x];
+        }
+#pragma unroll
+        for (int u = 0; u < LITE_B; u++) {
+            if (rc[u].x == NONE || !ev[u]) continue;
+            const uint32_t j = rc[u].x, ms = rc[u].y & 0xFFFFu, mr = rc[u].y >> 16;
+            uint32_t kv = ev[u] & 0xFFFFu, nk = 1;  // write ms is the latest <= ms of its key
+            for (uint32_t v = mr + 1u; v < ms; v++) {  // lag > 1 (rare): the other writes of (mr, ms)
+                const uint32_t e = d.vlog[(size_t)j * d.VL + v];
+                if ((e >> 16) > ms) { kv += e & 0xFFFFu; nk++; }
+                alg += 4;
+            }
+            sum += msgf(msgf(ns[u]) + ufield(mr) + 1u + vlen(ms) + kv);
+            kvs += nk;
+            alg += 8 + 4 + 2;
+        }
+    }
+    const uint32_t T = (uint32_t)wave_sum(sum);
+    if (__ballot(bad) != 0ull) return false;
+    if (!APPLY) {
+        st.alg += alg;
+        Tout = T;
+        return true;
+    }
+    if ((uint64_t)S0 + T > d.mtu) return false;
+    // apply: every NodeDelta whole (the records are L2-hot from the pass above)
+    for (uint32_t c0 = 0; c0 < nt; c0 += WAVE * LITE_B) {
+        uint2 rc[LITE_B];
+#pragma unroll
+        for (int u = 0; u < LITE_B; u++) {
+            const uint32_t i = c0 + (uint32_t)(u * WAVE + lane);
+            rc[u] = i < nt ? (i < n0 ? L0[i] : L1[i - n0]) : make_uint2(NONE, 0u);
+        }
+#pragma unroll
+        for (int u = 0; u < LITE_B; u++) {
+            if (rc[u].x == NONE) continue;
+            d.mv[pix(d, rcv, rc[u].x)] = (uint16_t)(rc[u].y & 0xFFFFu);  // max(ms, mr) = ms
+            alg += 4;
+            st.nd++;
+            st.cand++;
+        }
+    }
+    st.kvs += kvs;
+    st.alg += alg;
+    Tout = T;
+    return true;
+}
+
 // Candidates of one direction of exchange slot from pass 1's records (row half 0, then half 1); a half
 // with more stale owners than GS_CAND_CAP continues in the bitmap after its last record (those owners
 // were not merged speculatively: the bitmap walk reads their rows).
@@ -1434,6 +1529,7 @@ __global__ __launch_bounds__(XB, (KW == 4 ? PK_WAVES : 1)) void k_pack_slice(Dev
     if (ai < 0 || bi < 0 || (uint32_t)ai >= d.N || (uint32_t)bi >= d.N || ai == bi) return;  // counted already
     const uint32_t a = (uint32_t)ai, b = (uint32_t)bi;
     const size_t slot = (size_t)e * 2 + wid;
+    if (io.step == 0 && d.lite && (d.slot_stat[slot].w & LITE_DONE)) return;  // k_lite completed it
     PackState pst;
     if (io.step == 0) {
         uint64_t P = 0;
@@ -1679,6 +1775,7 @@ __global__ __launch_bounds__(XB, (KW == 4 ? PK_WAVES : 1)) void k_settle(Dev d, 
                 d.slot_stat[slot] = make_uint4(s.nd, s.kvs, s.cand, s.clean ? 0u : 1u);
             }
         } else {
+            if (d.lite && !(d.slot_stat[slot].w & LITE_FULL)) return;  // k_lite wrote the slice total
             pack_records<KW, true>(d, snd, rcv, ds, slot, wbuf, t, st, tomb, pst);
             if (lane == 0) io.tot[slot] = pst.S;
             salg = st.alg;
@@ -1699,6 +1796,7 @@ __global__ __launch_bounds__(XB, (KW == 4 ? PK_WAVES : 1)) void k_settle(Dev d, 
             }
         }
     } else {  // MODE 2
+        if (d.lite && (d.slot_stat[slot].w & LITE_DONE)) return;  // k_lite applied it and wrote its chain state
         unsigned long long P = 0, all = 0;
         for (uint32_t g = 0; g < d.shards; g++) {
             const unsigned long long x = io.tot_all[(size_t)g * n * 2 + slot];
@@ -1747,6 +1845,69 @@ __global__ __launch_bounds__(XB, (KW == 4 ? PK_WAVES : 1)) void k_settle(Dev d, 
     }
 }
 
+
+// Record phases of prefix-view handles (Dev::lite): the whole-delta fast path of every (exchange,
+// direction) slot as a kernel of its own (pack_lite: few registers, 8 waves per SIMD), between k_pass1 and
+// the exact packer, which then only runs the slots flagged here (slot_stat[slot].w):
+//   MODE 0 (one slice): a delta of prefix candidates that fits is applied here (LITE_DONE);
+//   MODE 1 (sliced count): the slice total of a slot whose candidates are all prefix candidates is
+//          written here (else LITE_FULL: k_settle counts it);
+//   MODE 2 (sliced pack step 0): such a slot whose predecessors' totals and its own fit from their sum
+//          is applied here and its chain state written (LITE_DONE); the rest is k_settle's.
+#ifndef LITE_WAVES
+#define LITE_WAVES 8
+#endif
+template <int MODE>
+__global__ __launch_bounds__(XB, LITE_WAVES) void k_lite(Dev d, const int32_t *ini, const int32_t *res, uint32_t n,
+                                                         uint32_t t, SliceIO io) {
+    const uint32_t e = blockIdx.x;
+    if (e >= n) return;
+    const int tid = threadIdx.x, lane = tid & (WAVE - 1), wid = tid >> 6;
+    const int32_t ai = ini[e], bi = res[e];
+    const size_t slot = (size_t)e * 2 + wid;
+    if (ai < 0 || bi < 0 || (uint32_t)ai >= d.N || (uint32_t)bi >= d.N || ai == bi) {  // counted already
+        if (lane == 0) d.slot_stat[slot].w = LITE_DONE;
+        return;
+    }
+    const uint32_t rcv = wid == 0 ? (uint32_t)ai : (uint32_t)bi;
+    const bool sched = t >= d.row[rcv * 4 + 2];  // the receiver's digest may leave owners out: exact packer
+    WStats st{0, 0, 0, 0, 0};
+    uint32_t T = 0, flag = LITE_FULL;
+    if (MODE == 0) {
+        if (!sched && pack_lite<true>(d, rcv, slot, 0u, st, T)) {
+            flag = LITE_DONE;
+            if (lane == 0) shard_add(d, C_DBYTES, T);
+        }
+    } else if (MODE == 1) {
+        if (!sched && pack_lite<false>(d, rcv, slot, 0u, st, T)) {
+            flag = 0u;
+            if (lane == 0) io.tot[slot] = T;
+        }
+    } else {
+        unsigned long long P = 0;
+        for (uint32_t g = 0; g < d.shard; g++) P += io.tot_all[(size_t)g * n * 2 + slot];
+        const unsigned long long own = io.tot_all[(size_t)d.shard * n * 2 + slot];
+        if (!sched && P + own <= d.mtu && pack_lite<true>(d, rcv, slot, (uint32_t)P, st, T)) {
+            flag = LITE_DONE;
+            const uint32_t S = (uint32_t)P + T;  // every NodeDelta whole: pack_group's state after the last one
+            const bool stop = S >= d.mtu || d.mtu - S < d.lb_min;
+            if (lane == 0) {
+                shard_add(d, C_DBYTES, T);
+                io.chain[slot] = (uint64_t)S | ((uint64_t)stop << 33);
+            }
+        }
+    }
+    if (lane == 0) d.slot_stat[slot].w = flag;
+    const unsigned long long s_alg = wave_sum(st.alg), s_nd = wave_sum(st.nd), s_kv = wave_sum(st.kvs);
+    const unsigned long long s_cd = wave_sum(st.cand);
+    if (lane == 0) {
+        shard_add(d, C_ALG, s_alg);
+        shard_add(d, C_PACKB, s_alg);
+        shard_add(d, C_ND, s_nd);
+        shard_add(d, C_KVS, s_kv);
+        shard_add(d, C_CAND, s_cd);
+    }
+}
 
 // ------------------------------------------------------------------ round start
 // inc_heartbeat + ClusterState.gc_marked_for_deletion (server.py:471-474; state.py:253-274, 333-338)
@@ -2213,7 +2374,17 @@ __global__ __launch_bounds__(LB) void k_owner_writes(Dev d, const gs_write *ops,
     d.hist[h] = (uint64_t)ver |
                 ((uint64_t)make_meta(sfield(d.key_len[k]) + sfield(vl) + ufield(ver) + ufield(st), st, vl) << 32);
     d.hist_vid[h] = vid;
-    if (d.lat) d.lat[(size_t)j * d.KP + k] = ver | (msgf(meta_kvlen((uint32_t)(d.hist[h] >> 32))) << 16);
+    if (d.lat) {
+        const uint32_t kvb = msgf(meta_kvlen((uint32_t)(d.hist[h] >> 32)));
+        uint32_t *lk = d.lat + (size_t)j * d.KP + k;
+        if (d.vlog) {  // the key's previous write (if any) now has a next write at ver
+            uint32_t *vl = d.vlog + (size_t)j * d.VL;
+            const uint32_t prev = *lk & 0xFFFFu;
+            if (prev) vl[prev] = (vl[prev] & 0xFFFFu) | (ver << 16);
+            vl[ver] = kvb | 0xFFFF0000u;
+        }
+        *lk = ver | (kvb << 16);
+    }
     d.last_w[(size_t)j * d.KP + k] = (uint8_t)nw;
     *held = (uint8_t)nw;
     d.mv[pj] = (uint16_t)ver;
@@ -2803,11 +2974,11 @@ struct gs_handle {
     bool split;
     // record phases (env GS_PACK, A/B runs): 0 = k_pass1 with the speculative merge + k_settle (default),
     // 1 = "fused": k_pass1 packing in the same workgroup, 2 = "split": k_pass1 + k_pack_slice
-    int pack_mode = 0;
+    int pack_mode = 2;
     bool age_init = false;            // age_tick holds the first operation's tick (fd_age)
     // gs_set_timing: HIP events around each kernel launch of a kind (gs_ktimes), on the library's stream
     bool timing;
-    std::vector<std::pair<hipEvent_t, hipEvent_t>> tev[4];
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> tev[GS_KT_KINDS];
     std::vector<hipEvent_t> evpool;
     std::string err;
     // sliced phases driven by the library (gs_comm_init: RCCL across processes; gs_run_phase_group:
@@ -2898,6 +3069,7 @@ int check_bound(gs_handle *h) {
     d.pstamp = (uint32_t *)h->reg[GS_R_PEND_STAMP];
     d.slot_stat = (uint4 *)h->reg[GS_R_SLOT_STAT];
     d.ring_slot = (uint32_t *)h->reg[GS_R_RING_SLOT];
+    d.vlog = (uint32_t *)h->reg[GS_R_VLOG];
     return GS_OK;
 }
 
@@ -2906,6 +3078,22 @@ int check_bound(gs_handle *h) {
 bool spec_ok(const gs_handle *h) {
     return h->pack_mode == 0 && (h->cfg.flags & GS_CANONICAL) && !(h->cfg.flags & GS_TOMBSTONES) && h->d.cand &&
            !h->d.ev && !(h->d.ablate & 1u);
+}
+
+// k_lite before the exact packer (Dev::lite): canonical prefix views (no tombstones) with records and the
+// version log, no hook events, the default packing mode, packing not ablated.
+bool lite_ok(const gs_handle *h) {
+    return h->pack_mode == 2 && (h->cfg.flags & GS_CANONICAL) && !(h->cfg.flags & GS_TOMBSTONES) && h->d.cand &&
+           h->d.vlog && h->d.slot_stat && !h->d.ev && !(h->d.ablate & 1u);
+}
+template <int MODE>
+int launch_lite(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t n, uint32_t tick, const SliceIO &io) {
+    hipEvent_t e0 = nullptr;
+    int rc = time_begin(h, e0);
+    if (rc) return rc;
+    k_lite<MODE><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, io);
+    HIPCHK(h, hipGetLastError());
+    return time_end(h, GS_KT_LITE, e0);
 }
 
 template <int KW, bool GENM, int MODE>
@@ -3005,6 +3193,7 @@ int run_split_phase(gs_handle *h, const int32_t *ini, const int32_t *res, uint32
     hipEvent_t e0 = nullptr;
     int rc;
     h->d.spec = spec_ok(h) ? 1u : 0u;
+    h->d.lite = lite_ok(h) ? 1u : 0u;
     if (h->pack_mode == 1) {
         if ((rc = time_begin(h, e0))) return rc;
         if (h->KP <= 16) k_pass1<4, true><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, h->seq, 0u);
@@ -3016,6 +3205,7 @@ int run_split_phase(gs_handle *h, const int32_t *ini, const int32_t *res, uint32
     if (h->d.ablate & 1u) return GS_OK;  // profiling only: no packing (results invalid)
     const SliceIO io{};
     if (h->pack_mode == 0) return launch_settle<0>(h, ini, res, n, tick, io, GS_KT_PACK);
+    if (h->d.lite && (rc = launch_lite<0>(h, ini, res, n, tick, io))) return rc;
     if ((rc = time_begin(h, e0))) return rc;
     if (h->KP <= 16) k_pack_slice<4><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, io, 0u);
     else k_pack_slice<KWB><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, io, 0u);
@@ -3101,6 +3291,8 @@ int gs_create(const gs_config *cfg, gs_handle **out) {
     b[GS_R_HIST] = NC * C * K * 8;
     b[GS_R_HIST_VID] = NC * C * K * 4;
     b[GS_R_LATEST] = (c.flags & GS_TOMBSTONES) ? 0 : NC * KP * 4;
+    const uint32_t VL = round_up(h->K * (h->C - 1) + 1, 4);  // versions 1 .. K (C - 1) (ordinals < C per key)
+    b[GS_R_VLOG] = (c.flags & GS_TOMBSTONES) ? 0 : NC * VL * 4;
     b[GS_R_NID_SIZE] = NP * 2;
     b[GS_R_KEY_LEN] = KP;
     b[GS_R_STAMP] = NR * 4;
@@ -3113,8 +3305,8 @@ int gs_create(const gs_config *cfg, gs_handle **out) {
     const bool recs = (c.flags & GS_CANONICAL) && !fused;
     b[GS_R_CAND] = recs ? (N / 2) * 4 * GS_CAND_CAP * 8 : 0;
     b[GS_R_CAND_N] = recs ? (N / 2) * 4 * 4 : 0;
-    b[GS_R_SLOT_STAT] = (recs && G > 1) ? (N / 2) * 2 * 16 : 0;
-    if (const char *m = getenv("GS_PACK")) h->pack_mode = !strcmp(m, "fused") ? 1 : !strcmp(m, "split") ? 2 : 0;
+    b[GS_R_SLOT_STAT] = recs ? (N / 2) * 2 * 16 : 0;  // sliced spec phases; k_lite's per-slot flags
+    if (const char *m = getenv("GS_PACK")) h->pack_mode = !strcmp(m, "fused") ? 1 : !strcmp(m, "spec") ? 0 : 2;
     const uint64_t PW = round_up(h->NP, 256) / 64;
     b[GS_R_PEND] = N * NPL * PW * 8;  // one phase bit plane per observer row and phase slot
     b[GS_R_PEND_STAMP] = N * NPL * 4;
@@ -3138,6 +3330,7 @@ int gs_create(const gs_config *cfg, gs_handle **out) {
     d.dead_grace = c.dead_grace_ticks;
     d.sched_delay = c.sched_delay_ticks;
     d.sum_bits = sum_bits;
+    d.VL = VL;
     if (const char *ab = getenv("GS_ABLATE")) d.ablate = (uint32_t)atoi(ab);
     d.phi_thr = c.phi_threshold;
     d.prior5 = c.prior_weighted;
@@ -3187,7 +3380,7 @@ int gs_boot(gs_handle *h, const uint16_t *nid_size, const uint8_t *key_len) {
     const int zero[] = {GS_R_HB, GS_R_SELF_HB, GS_R_MV, GS_R_GC, GS_R_HELD, GS_R_FD, GS_R_FD_LAST, GS_R_FD_STATE, GS_R_FD_TOD,
                         GS_R_RING, GS_R_ROW, GS_R_LAST_W, GS_R_HIST, GS_R_HIST_VID,
                         GS_R_STAMP, GS_R_COUNTERS, GS_R_SLICE_BITS, GS_R_PEND, GS_R_PEND_STAMP, GS_R_LATEST,
-                        GS_R_SLOT_STAT};
+                        GS_R_SLOT_STAT, GS_R_VLOG};
     for (int r : zero)
         if (h->bytes[r]) HIPCHK(h, hipMemsetAsync(h->reg[r], 0, h->bytes[r], s));
     if (h->bytes[GS_R_TS]) HIPCHK(h, hipMemsetAsync(h->reg[GS_R_TS], 0xFF, h->bytes[GS_R_TS], s));
@@ -3315,6 +3508,7 @@ int gs_run_phase(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t 
     h->hb_incs++;
     if (h->split) return run_split_phase(h, ini, res, n, tick);
     h->d.spec = 0u;
+    h->d.lite = 0u;
     hipEvent_t e0 = nullptr;
     if ((rc = time_begin(h, e0))) return rc;
     if (h->KP <= 16) rc = genm ? launch_exchange<4, true, 0>(h, ini, res, n, tick, lds, io)
@@ -3348,6 +3542,7 @@ int gs_phase_count(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_
     h->hb_incs++;
     if (!h->d.cand) {  // GS_FUSED: the fused count pass (LDS bitmaps)
         h->d.spec = 0u;
+        h->d.lite = 0u;
         hipEvent_t e0 = nullptr;
         if ((rc = time_begin(h, e0))) return rc;
         rc = h->KP <= 16 ? launch_exchange<4, false, 1>(h, ini, res, n, tick, lds, io)
@@ -3356,7 +3551,9 @@ int gs_phase_count(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_
     }
     // the speculative merge is decided here for the whole phase (gs_phase_pack / gs_phase_chain use it)
     h->d.spec = spec_ok(h) ? 1u : 0u;
+    h->d.lite = lite_ok(h) ? 1u : 0u;
     if ((rc = launch_pass1(h, ini, res, n, tick))) return rc;
+    if (h->d.lite && (rc = launch_lite<1>(h, ini, res, n, tick, io))) return rc;
     return launch_settle<1>(h, ini, res, n, tick, io, GS_KT_COUNT);
 }
 
@@ -3374,7 +3571,10 @@ int gs_phase_pack(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t
     io.chain = chain;
     io.step = step;
     if (step && h->shard == 0) return GS_OK;  // slice 0 always finishes at step 0
-    if (step == 0 && h->d.cand) return launch_settle<2>(h, ini, res, n, tick, io, GS_KT_PACK);
+    if (step == 0 && h->d.cand) {
+        if (h->d.lite && (rc = launch_lite<2>(h, ini, res, n, tick, io))) return rc;
+        return launch_settle<2>(h, ini, res, n, tick, io, GS_KT_PACK);
+    }
     hipEvent_t e0 = nullptr;
     if ((rc = time_begin(h, e0))) return rc;
     if (h->KP <= 16) k_pack_slice<4><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, io, 0u);
@@ -3784,7 +3984,7 @@ int gs_kernel_times(gs_handle *h, gs_ktimes *out) {
     if (!h || !out) return GS_E_INVALID;
     HIPCHK(h, hipStreamSynchronize(h->stream));
     memset(out, 0, sizeof *out);
-    for (int k = 0; k < 4; k++) {
+    for (int k = 0; k < GS_KT_KINDS; k++) {
         for (auto &pr : h->tev[k]) {
             float ms = 0.f;
             HIPCHK(h, hipEventElapsedTime(&ms, pr.first, pr.second));

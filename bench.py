@@ -235,7 +235,7 @@ def load_traffic(workload: str, kernel: str, units_per_launch: float):
         f"({e.get('calibration')}), x this run's units per launch")
 
 
-KERNEL_OF = {"pass1": "k_pass1", "pack": "k_settle", "liveness": "k_liveness", "count": "k_settle"}
+KERNEL_OF = {"pass1": "k_pass1", "pack": "k_pack_slice", "liveness": "k_liveness", "count": "k_settle", "lite": "k_lite"}
 
 
 def roofline(sims, local_c, exch, kt, elapsed, torch, dev, rank, group, workload) -> dict:

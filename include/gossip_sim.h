@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define GS_API_VERSION 11
+#define GS_API_VERSION 12
 #define GS_MAX_PHASES 64  /* gs_schedule_phases: phases per round */
 #define GS_TICK_US 15625u
 #define GS_NONE 0xFFFFFFFFu
@@ -151,6 +151,10 @@ enum gs_region {
                                         {NodeDeltas, kvs, candidates, needs a pack} of a speculative phase,
                                         between gs_phase_count and gs_phase_pack */
     GS_R_RING_SLOT,   /* u32 [N]       sampled rings: each observer row's ring slot, GS_NONE = compact windows */
+    GS_R_VLOG,        /* u32 [NC][VL]  each owner's writes by version (no GS_TOMBSTONES only: every write is version
+                                        max_version + 1), VL = K * (hist_cap - 1) + 1 rounded up to 4: entry v =
+                                        DeltaPb bytes of write v's KeyValueUpdatePb field | (version of the
+                                        next write of the same key, 0xFFFF = none) << 16 */
     GS_NUM_REGIONS
 };
 
@@ -409,9 +413,12 @@ int gs_stream_write(void *dst, uint64_t bytes, uint32_t width, void *stream);
                              gs_phase_pack step 0), k_pack_slice (GS_PACK=split), k_chain_step (gs_phase_chain) */
 #define GS_KT_LIVENESS 2  /* k_liveness (report replay + liveness sweep) */
 #define GS_KT_COUNT 3     /* the slice byte totals of gs_phase_count (k_settle, count mode) */
+#define GS_KT_LITE 4      /* k_lite: the whole-delta fast path of prefix-view record phases (before the exact
+                             packer, which then runs only the slots it could not complete) */
+#define GS_KT_KINDS 8
 typedef struct gs_ktimes {
-    double ms[4];
-    uint64_t launches[4];
+    double ms[GS_KT_KINDS];
+    uint64_t launches[GS_KT_KINDS];
 } gs_ktimes;
 int gs_set_timing(gs_handle *h, int on);
 int gs_kernel_times(gs_handle *h, gs_ktimes *out);
