@@ -70,8 +70,8 @@ constexpr uint32_t HB_LAG_CHECK_EVERY = 1u << 14;  // round starts + phases betw
 enum Ctr {
     C_EXCH = 0, C_REPORTS, C_ND, C_KVS, C_TRUNC, C_DBYTES, C_ALG, C_HBW, C_CAND, C_LIVE, C_TOMBGC,
     C_E_FDOVF, C_E_HIST, C_E_IDX, C_E_CONFLICT, C_E_FDGC, C_E_INSERT, C_FDGC, C_Q9, C_PACKB, C_E_HOLES,
-    C_E_HBLAG, C_FLUSH /* host-side: plane_flushes */, C_FDSAT,
-    C_CEN0 = 24, C_NUM = C_CEN0 + 6  // gs_fd_census scratch slots (not part of gs_counters)
+    C_E_HBLAG, C_FLUSH /* host-side: plane_flushes */, C_FDSAT, C_LITE,
+    C_CEN0 = 26, C_NUM = C_CEN0 + 6  // gs_fd_census scratch slots (not part of gs_counters)
 };
 static_assert(C_NUM <= 32, "counter region");
 static_assert(C_FDSAT < C_CEN0, "gs_counters fields before the census scratch");
@@ -660,6 +660,20 @@ __device__ __forceinline__ void pack_begin(const Dev &d, bool count, const PackS
     if (!count && !stop && (S >= d.mtu || d.mtu - S < d.lb_min)) stop = true;
 }
 
+// both views of a record are prefix views (GS_MV_INEXACT clear in both words): the candidates pass 1
+// merged speculatively (Dev::spec)
+__device__ inline bool rec_fast(uint32_t mvw) { return !(mvw & (MV_INEXACT | (MV_INEXACT << 16))); }
+
+// First-fit continuation (tail mode) tests every later candidate's smallest NodeDelta -- its lowest-version
+// kv alone, eval_cand's min1 -- against the budget left, which only shrinks.  For a prefix candidate (no
+// tombstones: last_gc 0) a lower bound of min1 needs no evaluation: the owner's NodeIdPb size, the
+// from / max_version varints and the owner's smallest kv field over all its writes (GS_R_VLOG entry 0,
+// two L2-resident tables).  A candidate whose bound exceeds the budget cannot be sent (not even
+// truncated) and is skipped without its evaluation's round trips (returning nodes scan thousands).
+__device__ __forceinline__ uint32_t min1_lb(const Dev &d, uint32_t j, uint32_t ms, uint32_t from) {
+    return msgf(msgf(d.nid_size[j]) + ufield(from) + 1u + vlen(ms) + (d.vlog[(size_t)j * d.VL] & 0xFFFFu));
+}
+
 // Bitmap source: positions [max(p0, pmin), cnt) of the sender's dict order (p0 = 0 in the general
 // layout; a multiple of 256 otherwise; pmin > p0: the positions before it came from pass 1's records).
 template <int KW, bool GENM, bool COUNT, bool REC = false>
@@ -721,13 +735,23 @@ __device__ __forceinline__ void pack_dir(const Dev &d, uint32_t s, uint32_t r, c
         const uint32_t lim = last ? total : (total & ~(uint32_t)(WAVE - 1));
         for (uint32_t c0 = 0; c0 < lim && !stop; c0 += WAVE) {
             const uint32_t ci = c0 + lane;
-            const bool cand = ci < lim;
+            bool cand = ci < lim;
             Cand<KW> c;
             c.emsg = 0;
             c.min1 = 0;
+            uint32_t j = 0;
             if (cand) {
                 const uint32_t p = ci < pend ? rv : win + wbuf[ci - pend];
-                const uint32_t j = GENM ? order[p] : p;
+                j = GENM ? order[p] : p;
+                if (!GENM && !COUNT && tail && d.vlog) {  // tail mode: skip what cannot fit (min1_lb)
+                    const uint32_t msw = d.mv[pix(d, s, j)], mrw = d.mv[pix(d, r, j)];
+                    st.alg += 4;
+                    if (!((msw | mrw) & MV_INEXACT) &&
+                        min1_lb(d, j, msw, ds.sched ? 0u : mrw) > d.mtu - S)
+                        cand = false;
+                }
+            }
+            if (cand) {
                 CandKeys<KW> ck;
                 eval_cand<KW, GENM>(d, s, r, ds, j, t, c, ck, st.alg);
                 st.cand++;
@@ -753,9 +777,6 @@ __device__ __forceinline__ void pack_dir(const Dev &d, uint32_t s, uint32_t r, c
     if (!COUNT && lane == 0) shard_add(d, C_DBYTES, S - S0);  // DeltaPb bytes this call added
 }
 
-// both views of a record are prefix views (GS_MV_INEXACT clear in both words): the candidates pass 1
-// merged speculatively (Dev::spec)
-__device__ inline bool rec_fast(uint32_t mvw) { return !(mvw & (MV_INEXACT | (MV_INEXACT << 16))); }
 
 // List source (canonical records): the n stale owners pass 1 recorded for one row half, in column
 // order, each with both views' max_version words (GS_R_CAND), so no row is read again.  The next
@@ -775,12 +796,19 @@ __device__ __forceinline__ void pack_list(const Dev &d, uint32_t s, uint32_t r, 
     if ((uint32_t)lane < n) nxt = L[lane];
     for (uint32_t c0 = 0; c0 < n && (specd || !stop); c0 += WAVE) {
         const uint32_t ci = c0 + lane;
-        const bool cand = ci < n;
+        bool cand = ci < n;
         const uint2 cr = nxt;
         if (ci + WAVE < n) nxt = L[ci + WAVE];
         if (stop) {  // specd only: nothing more is sent
             if (cand && rec_fast(cr.y)) { d.mv[pix(d, r, cr.x)] = (uint16_t)(cr.y >> 16); st.alg += 4; }
             continue;
+        }
+        if (!COUNT && cand && tail && d.vlog && rec_fast(cr.y)) {  // tail mode: skip what cannot fit (min1_lb)
+            const uint32_t mr = cr.y >> 16;
+            if (min1_lb(d, cr.x, cr.y & 0xFFFFu, ds.sched ? 0u : mr) > d.mtu - S) {
+                cand = false;
+                if (specd) { d.mv[pix(d, r, cr.x)] = (uint16_t)mr; st.alg += 4; }  // not sent: undo the merge
+            }
         }
         Cand<KW> c;
         c.emsg = 0;
@@ -1031,6 +1059,20 @@ __device__ __forceinline__ Fd fd_report_val(const Dev &d, uint16_t *rg, uint32_t
     return f;
 }
 
+// Partial-line writes: HBM3E has no write data mask, so a dirty line that was only partly written costs the
+// memory a read-modify-write.  P1_LINE bit 0: a changed heartbeat group stores its whole 64-byte line (the
+// 8 lanes covering it store their 8 bytes, changed or not); bit 1: the same for the speculative merge's
+// max_version groups (A/B, tools/build_dev.sh -DP1_LINE=n).
+#ifndef P1_LINE
+#define P1_LINE 0
+#endif
+// any of the 8 lanes sharing this lane's 64-byte line (8 bytes per lane; lines start at a multiple of 8
+// lanes: rows are 128-byte aligned and a wave's groups start at a multiple of 256 columns)
+__device__ __forceinline__ bool line_any8(bool w) {
+    const uint64_t m = __ballot(w);
+    return ((m >> (lane_id() & ~7)) & 0xFFull) != 0ull;
+}
+
 // Reports are deferred: the window of (observer, owner) is only read by phi, i.e. by the liveness
 // sweep at the end of the round, so pass 1 records each report as one bit in the phase's bit plane
 // (rmA/rmB: bit i = column c0 + i) and k_liveness replays them in tick order before computing phi
@@ -1098,6 +1140,10 @@ __device__ __forceinline__ void pass1_grp(const Dev &d, size_t ra, size_t rb, ui
     }
     // only changed 16/32-byte groups are written back (writing whole lines measured slower: r1c vs r1b)
     if (d.ablate & 2u) return;
+    if (P1_LINE & 1) {
+        dA = line_any8(dA);
+        dB = line_any8(dB);
+    }
     if (dA) { st4h(d.hb + ra + c0, g.hA); alg += 8; }
     if (dB) { st4h(d.hb + rb + c0, g.hB); alg += 8; }
 }
@@ -1181,6 +1227,10 @@ __device__ __forceinline__ void spec_merge(const Dev &d, size_t ra, size_t rb, u
         nB[i] = ab ? mx : mB[i];
         wA = wA || ba;
         wB = wB || ab;
+    }
+    if (P1_LINE & 2) {
+        wA = line_any8(wA);
+        wB = line_any8(wB);
     }
     if (wA) { st4h(d.mv + ra + c0, nA); alg += 8; }
     if (wB) { st4h(d.mv + rb + c0, nB); alg += 8; }
@@ -1295,7 +1345,7 @@ __global__ __launch_bounds__(XB, (KW == 4 ? (FUSE ? P1_WAVES : P1S_WAVES) : 1)) 
             store_plane(planeB, c0, rmB, alg);
             const uint32_t recBA = emit_dir(gBA, LBA, nBAc, c0, nBA, mB, mA, alg);  // b -> a: sender b, receiver a
             const uint32_t recAB = emit_dir(gAB, LAB, nABc, c0, nAB, mA, mB, alg);
-            if (SPEC && (recBA | recAB)) spec_merge(d, ra, rb, c0, recBA, recAB, mA, mB, alg);
+            if (SPEC && ((P1_LINE & 2) || (recBA | recAB))) spec_merge(d, ra, rb, c0, recBA, recAB, mA, mB, alg);
             r0 = r1;
             if (P1_AHEAD > 1) r1 = r2;
             c0 = c1;
@@ -1897,7 +1947,10 @@ __global__ __launch_bounds__(XB, LITE_WAVES) void k_lite(Dev d, const int32_t *i
             }
         }
     }
-    if (lane == 0) d.slot_stat[slot].w = flag;
+    if (lane == 0) {
+        d.slot_stat[slot].w = flag;
+        if (flag == LITE_DONE) shard_add(d, C_LITE, 1);
+    }
     const unsigned long long s_alg = wave_sum(st.alg), s_nd = wave_sum(st.nd), s_kv = wave_sum(st.kvs);
     const unsigned long long s_cd = wave_sum(st.cand);
     if (lane == 0) {
@@ -2382,6 +2435,8 @@ __global__ __launch_bounds__(LB) void k_owner_writes(Dev d, const gs_write *ops,
             const uint32_t prev = *lk & 0xFFFFu;
             if (prev) vl[prev] = (vl[prev] & 0xFFFFu) | (ver << 16);
             vl[ver] = kvb | 0xFFFF0000u;
+            const uint32_t kmin = vl[0];  // entry 0: the owner's smallest kv field over all its writes (min1_lb)
+            if (!kmin || kvb < kmin) vl[0] = kvb;
         }
         *lk = ver | (kvb << 16);
     }
@@ -3969,7 +4024,7 @@ int gs_read_counters(gs_handle *h, gs_counters *out) {
     for (int s = 0; s < NSHARD; s++)
         for (int c = 0; c < 32; c++) acc[c] += buf[(size_t)s * 32 + c];
     acc[C_FLUSH] = h->plane_flushes;
-    for (int c = C_CEN0; c < 32; c++) acc[c] = 0;  // census scratch, not counters
+    for (int c = C_CEN0; c < C_NUM; c++) acc[c] = 0;  // census scratch, not counters
     memcpy(out, acc, sizeof acc);
     return GS_OK;
 }

@@ -194,7 +194,9 @@ typedef struct gs_counters {
     uint64_t plane_flushes;    /* host count: mid-round report replays (phases > GS_PLANES ticks after the plane base) */
     uint64_t fd_saturated;     /* sampled rings: intervals a full compact window could not append (the compact rows'
                                   windows are exact only up to W intervals; the ring rows are exact) */
-    uint64_t reserved[8];
+    uint64_t lite_slots;       /* (exchange, direction) slots whose whole delta k_lite sized and applied (the exact
+                                  packer skipped them) */
+    uint64_t reserved[7];
 } gs_counters;
 
 /* Failure-detector membership census (gs_fd_census): (observer, target) pairs with the observer up and
