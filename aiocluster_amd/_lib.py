@@ -24,6 +24,7 @@ GS_CANONICAL = 1
 GS_TOMBSTONES = 2
 GS_FD_RING = 4
 GS_NO_HELD = 8
+GS_HB8 = 16  # 8-bit heartbeat views (include/gossip_sim.h)
 GS_NONE = 0xFFFFFFFF
 GS_E_INVALID = -1
 GS_MV_INEXACT = 0x8000

@@ -66,6 +66,7 @@ constexpr uint32_t NPL = GS_PLANES;  // report bit planes per observer row (phas
 static_assert(NPL == 16 || NPL == 32, "k_liveness stages 16 or 32 planes");
 constexpr double TICK_S = 1.0 / 64.0;
 constexpr uint32_t HB_LAG_CHECK_EVERY = 1u << 14;  // round starts + phases between heartbeat-lag sweeps
+constexpr uint32_t HB8_LAG_CHECK_EVERY = 1u << 6;  // ... with GS_HB8 (checked at round starts: < 2^7 apart)
 
 enum Ctr {
     C_EXCH = 0, C_REPORTS, C_ND, C_KVS, C_TRUNC, C_DBYTES, C_ALG, C_HBW, C_CAND, C_LIVE, C_TOMBGC,
@@ -135,6 +136,7 @@ struct Dev {
     uint32_t *vlog;
     uint32_t VL;
     uint32_t lite;  // this phase runs k_lite before the exact packer (set per phase by the host)
+    uint32_t hb8;   // GS_HB8: hb holds u8 views (mod 2^8), else u16 (mod 2^16)
     // event stream (gs_set_events): records {observer, owner, key | kind << 8, old version, new version,
     // tick, seq, 0}; kind 0 = on_key_change, 1 = node join, 2 = node leave; seq orders them (gossip_sim.h,
 // gs_set_events).  ev == nullptr: off
@@ -957,6 +959,22 @@ __device__ __forceinline__ void ld4(const uint32_t *p, uint32_t (&v)[4]) {
 // Heartbeats are stored mod 2^16 and decoded against the owner's own heartbeat R (every view of
 // owner j is <= R, and views lag R by < 2^16: DESIGN.md §3), so H = R - ((R - s) mod 2^16).
 __device__ __forceinline__ uint32_t hb_dec(uint32_t s, uint32_t R) { return R - ((R - s) & 0xFFFFu); }
+// GS_HB8: views stored mod 2^8 (exact while they lag their owner by < 2^8: k_hb_lag), same decode
+__device__ __forceinline__ uint32_t hb_dec8(uint32_t s, uint32_t R) { return R - ((R - s) & 0xFFu); }
+// one view's stored heartbeat, any width (the small kernels; pass 1 is specialised on the width)
+__device__ __forceinline__ uint32_t hb_raw(const Dev &d, size_t p) {
+    return d.hb8 ? (uint32_t) reinterpret_cast<const uint8_t *>(d.hb)[p] : (uint32_t)d.hb[p];
+}
+__device__ __forceinline__ void hb_put(const Dev &d, size_t p, uint32_t v) {
+    if (d.hb8) reinterpret_cast<uint8_t *>(d.hb)[p] = (uint8_t)v;
+    else d.hb[p] = (uint16_t)v;
+}
+__device__ __forceinline__ uint32_t hb_view(const Dev &d, size_t p, uint32_t R) {
+    return d.hb8 ? hb_dec8(hb_raw(d, p), R) : hb_dec(hb_raw(d, p), R);
+}
+__device__ __forceinline__ void st4b(uint8_t *p, const uint32_t (&v)[4]) {
+    *reinterpret_cast<uint32_t *>(p) = (v[0] & 0xFFu) | ((v[1] & 0xFFu) << 8) | ((v[2] & 0xFFu) << 16) | (v[3] << 24);
+}
 __device__ __forceinline__ void st4h(uint16_t *p, const uint32_t (&v)[4]) {
     *reinterpret_cast<uint2 *>(p) = make_uint2((v[0] & 0xFFFFu) | (v[1] << 16), (v[2] & 0xFFFFu) | (v[3] << 16));
 }
@@ -997,12 +1015,18 @@ struct GrpRaw {
     uint4 pA, pB;
     uint32_t sA, sB;
 };
-template <bool GENM>
+template <bool GENM, bool HB8 = false>
 __device__ __forceinline__ void load_grp(const Dev &d, size_t ra, size_t rb, uint32_t c0, uint32_t t, bool schA,
                                          bool schB, GrpRaw &g) {
     g.R = *reinterpret_cast<const uint4 *>(d.self_hb + c0);
-    g.hA = *reinterpret_cast<const uint2 *>(d.hb + ra + c0);
-    g.hB = *reinterpret_cast<const uint2 *>(d.hb + rb + c0);
+    if (HB8) {  // 4 bytes per lane (4 views)
+        const uint8_t *h8 = reinterpret_cast<const uint8_t *>(d.hb);
+        g.hA = make_uint2(*reinterpret_cast<const uint32_t *>(h8 + ra + c0), 0u);
+        g.hB = make_uint2(*reinterpret_cast<const uint32_t *>(h8 + rb + c0), 0u);
+    } else {
+        g.hA = *reinterpret_cast<const uint2 *>(d.hb + ra + c0);
+        g.hB = *reinterpret_cast<const uint2 *>(d.hb + rb + c0);
+    }
     g.mA = *reinterpret_cast<const uint2 *>(d.mv + ra + c0);
     g.mB = *reinterpret_cast<const uint2 *>(d.mv + rb + c0);
     g.pA = g.pB = make_uint4(0u, 0u, 0u, 0u);
@@ -1016,12 +1040,21 @@ __device__ __forceinline__ void load_grp(const Dev &d, size_t ra, size_t rb, uin
 }
 // decode: heartbeats against the owners' own (hb_dec); raw max_version words (prefix-view flag included):
 // pass 1 masks them where it compares, and the split path hands them to the packer in its records
+template <bool HB8 = false>
 __device__ __forceinline__ void dec_grp(const GrpRaw &r, Grp &g) {
     const uint32_t R[4] = {r.R.x, r.R.y, r.R.z, r.R.w};
-    const uint32_t hA[4] = {r.hA.x & 0xFFFFu, r.hA.x >> 16, r.hA.y & 0xFFFFu, r.hA.y >> 16};
-    const uint32_t hB[4] = {r.hB.x & 0xFFFFu, r.hB.x >> 16, r.hB.y & 0xFFFFu, r.hB.y >> 16};
+    if (HB8) {
 #pragma unroll
-    for (int i = 0; i < 4; i++) { g.hA[i] = hb_dec(hA[i], R[i]); g.hB[i] = hb_dec(hB[i], R[i]); }
+        for (int i = 0; i < 4; i++) {
+            g.hA[i] = hb_dec8((r.hA.x >> (8 * i)) & 0xFFu, R[i]);
+            g.hB[i] = hb_dec8((r.hB.x >> (8 * i)) & 0xFFu, R[i]);
+        }
+    } else {
+        const uint32_t hA[4] = {r.hA.x & 0xFFFFu, r.hA.x >> 16, r.hA.y & 0xFFFFu, r.hA.y >> 16};
+        const uint32_t hB[4] = {r.hB.x & 0xFFFFu, r.hB.x >> 16, r.hB.y & 0xFFFFu, r.hB.y >> 16};
+#pragma unroll
+        for (int i = 0; i < 4; i++) { g.hA[i] = hb_dec(hA[i], R[i]); g.hB[i] = hb_dec(hB[i], R[i]); }
+    }
     g.mA[0] = r.mA.x & 0xFFFFu; g.mA[1] = r.mA.x >> 16; g.mA[2] = r.mA.y & 0xFFFFu; g.mA[3] = r.mA.y >> 16;
     g.mB[0] = r.mB.x & 0xFFFFu; g.mB[1] = r.mB.x >> 16; g.mB[2] = r.mB.y & 0xFFFFu; g.mB[3] = r.mB.y >> 16;
     g.pA[0] = r.pA.x; g.pA[1] = r.pA.y; g.pA[2] = r.pA.z; g.pA[3] = r.pA.w;
@@ -1079,7 +1112,7 @@ __device__ __forceinline__ bool line_any8(bool w) {
 // (same appends, same order).
 // SCH = false: neither row can have a target scheduled for deletion at t (schA = schB = false; the
 // per-column predicates drop out).  SELF = false: the caller stores the responder's own new heartbeat.
-template <bool GENM, bool SCH = true, bool SELF = true>
+template <bool GENM, bool SCH = true, bool SELF = true, bool HB8 = false>
 __device__ __forceinline__ void pass1_grp(const Dev &d, size_t ra, size_t rb, uint32_t c0, uint32_t a, uint32_t b,
                                           uint32_t t, bool schA, bool schB, Grp &g, uint32_t &nBA, uint32_t &nAB,
                                           uint32_t &nNB, uint32_t &nNA, uint32_t &alg, uint32_t &reports,
@@ -1088,7 +1121,7 @@ __device__ __forceinline__ void pass1_grp(const Dev &d, size_t ra, size_t rb, ui
     rmA = rmB = 0u;
     nBA = nAB = nNB = nNA = 0u;
     // HBM-resident elements only: the SELF_HB row (16 B per group, 256 KiB per row, L2-resident) is not counted
-    alg += 32 + (GENM ? 32 : 0) + (schA ? 4 : 0) + (schB ? 4 : 0);
+    alg += (HB8 ? 24 : 32) + (GENM ? 32 : 0) + (schA ? 4 : 0) + (schB ? 4 : 0);
     // Branch-free (selects, no exec-mask juggling per column): the per-column rules of the reference,
     // restated as predicates.  _report_heartbeat (server.py:599-604, state.py:280-287) of a known view
     // stores the larger heartbeat and reports only if the old one was non-zero; an unknown owner is
@@ -1144,8 +1177,14 @@ __device__ __forceinline__ void pass1_grp(const Dev &d, size_t ra, size_t rb, ui
         dA = line_any8(dA);
         dB = line_any8(dB);
     }
-    if (dA) { st4h(d.hb + ra + c0, g.hA); alg += 8; }
-    if (dB) { st4h(d.hb + rb + c0, g.hB); alg += 8; }
+    if (HB8) {
+        uint8_t *h8 = reinterpret_cast<uint8_t *>(d.hb);
+        if (dA) { st4b(h8 + ra + c0, g.hA); alg += 4; }
+        if (dB) { st4b(h8 + rb + c0, g.hB); alg += 4; }
+    } else {
+        if (dA) { st4h(d.hb + ra + c0, g.hA); alg += 8; }
+        if (dB) { st4h(d.hb + rb + c0, g.hB); alg += 8; }
+    }
 }
 
 // The four ballots of one group step are this wave's 32-byte block of the phase's bit plane
@@ -1274,11 +1313,13 @@ __device__ inline PackState chain_unpack(uint64_t v) {
 #endif
 // SPEC (not with FUSE): the speculative max-version merge of the recorded prefix candidates (spec_merge,
 // Dev::spec); k_settle then only settles the deltas that do not fit and the candidates with holes.
-template <int KW, bool FUSE, bool SPEC = false>
+// HB8 (not with FUSE): GS_HB8's 8-bit heartbeat views.
+template <int KW, bool FUSE, bool SPEC = false, bool HB8 = false>
 __global__ __launch_bounds__(XB, (KW == 4 ? (FUSE ? P1_WAVES : P1S_WAVES) : 1)) void k_pass1(Dev d, const int32_t *ini, const int32_t *res,
                                                                        uint32_t n, uint32_t t, uint32_t seq,
                                                                        uint32_t e0) {
     static_assert(!(FUSE && SPEC), "the fused packer applies every NodeDelta itself");
+    static_assert(!(FUSE && HB8), "8-bit heartbeats: record phases only");
     const uint32_t e = e0 + blockIdx.x;  // exchanges [e0, e0 + grid) of the phase (one chunk)
     if (e >= n) return;
     const int tid = threadIdx.x, lane = tid & (WAVE - 1), wid = tid >> 6;
@@ -1324,21 +1365,21 @@ __global__ __launch_bounds__(XB, (KW == 4 ? (FUSE ? P1_WAVES : P1S_WAVES) : 1)) 
         // P1_AHEAD groups in flight ahead of the one being computed
         GrpRaw r0, r1, r2;
         constexpr uint32_t STEP = WAVE * 4u;
-        if (c0 < hi) load_grp<false>(d, ra, rb, c0, t, SCH && schA, SCH && schB, r0);
-        if (P1_AHEAD > 1 && c0 + STEP < hi) load_grp<false>(d, ra, rb, c0 + STEP, t, SCH && schA, SCH && schB, r1);
+        if (c0 < hi) load_grp<false, HB8>(d, ra, rb, c0, t, SCH && schA, SCH && schB, r0);
+        if (P1_AHEAD > 1 && c0 + STEP < hi) load_grp<false, HB8>(d, ra, rb, c0 + STEP, t, SCH && schA, SCH && schB, r1);
         while (c0 < hi) {
             const uint32_t c1 = c0 + STEP;
             if (P1_AHEAD > 1) {
-                if (c1 + STEP < hi) load_grp<false>(d, ra, rb, c1 + STEP, t, SCH && schA, SCH && schB, r2);
+                if (c1 + STEP < hi) load_grp<false, HB8>(d, ra, rb, c1 + STEP, t, SCH && schA, SCH && schB, r2);
             } else if (c1 < hi) {
-                load_grp<false>(d, ra, rb, c1, t, SCH && schA, SCH && schB, r1);
+                load_grp<false, HB8>(d, ra, rb, c1, t, SCH && schA, SCH && schB, r1);
             }
             Grp g0;
-            dec_grp(r0, g0);
+            dec_grp<HB8>(r0, g0);
             uint32_t rmA, rmB, nBA, nAB, nNB, nNA;
             const uint32_t mA[4] = {g0.mA[0], g0.mA[1], g0.mA[2], g0.mA[3]};
             const uint32_t mB[4] = {g0.mB[0], g0.mB[1], g0.mB[2], g0.mB[3]};
-            pass1_grp<false, SCH, false>(d, ra, rb, c0, a, b, t, schA, schB, g0, nBA, nAB, nNB, nNA, alg, reports, hbw,
+            pass1_grp<false, SCH, false, HB8>(d, ra, rb, c0, a, b, t, schA, schB, g0, nBA, nAB, nNB, nNA, alg, reports, hbw,
                                          rmA, rmB);
             anynew = anynew || (nNB | nNA) != 0u;
             store_plane(planeA, c0, rmA, alg);
@@ -1970,7 +2011,7 @@ __global__ __launch_bounds__(LB) void k_begin_round(Dev d, const uint8_t *up, ui
     if (threadIdx.x == 0 && o - d.col_lo < d.ncol) {
         const uint32_t R = d.self_hb[o - d.col_lo] + 1u;
         d.self_hb[o - d.col_lo] = R;
-        d.hb[pix(d, o, o - d.col_lo)] = (uint16_t)R;
+        hb_put(d, pix(d, o, o - d.col_lo), R);
     }
     if (!(d.flags & GS_TOMBSTONES) || !d.row[o * 4 + 1]) return;
     const bool genm = !(d.flags & GS_CANONICAL);
@@ -2278,7 +2319,7 @@ __global__ __launch_bounds__(LB) void k_fd_gc(Dev d, const uint8_t *up, uint32_t
             if (!bit(rmv, j)) continue;
             const size_t p = ro + j;
             d.pos[p] = NONE;
-            d.hb[p] = 0u;
+            hb_put(d, p, 0u);
             d.mv[p] = 0u;
             if (d.flags & GS_TOMBSTONES) d.gc[p] = 0u;
             if (d.held)
@@ -2370,18 +2411,30 @@ __global__ __launch_bounds__(LB) void k_fd_age(Dev d, uint32_t t) {
 // lag is < 2^15 + 2^14 < 2^16 until this one, so every decode in between was exact and this sweep's
 // decoded lags are the true ones -- a view at >= 2^15 is counted in err_hb_lag (the run is reported
 // inexact) before any decode can go wrong.
-__global__ __launch_bounds__(LB) void k_hb_lag(Dev d) {
+// GS_HB8 (views mod 2^8): the same argument with a sweep at least every 64 round starts + phases (checked
+// at gs_begin_round, so at most 64 + 63 increments apart) and lags >= 2^7 counted: < 2^7 + 2^7 < 2^8.
+// One workgroup per (row, chunk of LB x 16 columns); each thread reads 16 views (u8) or 8 (u16).
+__global__ __launch_bounds__(LB) void k_hb_lag(Dev d, uint32_t chunks) {
     const bool genm = !(d.flags & GS_CANONICAL);
-    const uint64_t total = (uint64_t)d.N * d.ncol;
+    const uint32_t o = blockIdx.x / chunks, cb = blockIdx.x % chunks;
+    const uint32_t per = d.hb8 ? 16u : 8u;
+    const uint32_t j0 = (cb * LB + threadIdx.x) * per;
     uint32_t bad = 0;
-    for (uint64_t x = (uint64_t)blockIdx.x * LB + threadIdx.x; x < total; x += (uint64_t)gridDim.x * LB) {
-        const uint32_t o = (uint32_t)(x / d.ncol), j = (uint32_t)(x % d.ncol);
-        const size_t p = pix(d, o, j);
-        if (genm && d.pos[p] == NONE) continue;
-        if (((d.self_hb[j] - (uint32_t)d.hb[p]) & 0xFFFFu) >= 0x8000u) bad++;
+    if (j0 < d.ncol) {
+        const size_t p0 = pix(d, o, j0);
+        const uint4 raw = d.hb8 ? *reinterpret_cast<const uint4 *>(reinterpret_cast<const uint8_t *>(d.hb) + p0)
+                                : *reinterpret_cast<const uint4 *>(d.hb + p0);
+        const uint32_t w[4] = {raw.x, raw.y, raw.z, raw.w};
+        for (uint32_t i = 0; i < per && j0 + i < d.ncol; i++) {
+            const uint32_t j = j0 + i;
+            if (genm && d.pos[p0 + i] == NONE) continue;
+            const uint32_t s = d.hb8 ? (w[i >> 2] >> (8 * (i & 3))) & 0xFFu : (w[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
+            const uint32_t lag = d.hb8 ? (d.self_hb[j] - s) & 0xFFu : (d.self_hb[j] - s) & 0xFFFFu;
+            if (lag >= (d.hb8 ? 0x80u : 0x8000u)) bad++;
+        }
     }
-    const unsigned long long s = wave_sum(bad);
-    if ((threadIdx.x & 63) == 0) shard_add(d, C_E_HBLAG, s);
+    const unsigned long long sb = wave_sum(bad);
+    if ((threadIdx.x & 63) == 0) shard_add(d, C_E_HBLAG, sb);
 }
 
 // ------------------------------------------------------------------ owner writes
@@ -2465,7 +2518,7 @@ __global__ __launch_bounds__(LB) void k_boot_self(Dev d) {
     d.row[o * 4 + 3] = 0u;
     if (o - d.col_lo >= d.ncol) return;
     const size_t p = pix(d, o, o - d.col_lo);
-    d.hb[p] = 1u;  // Cluster.__init__: inc_heartbeat (server.py:95-96)
+    hb_put(d, p, 1u);  // Cluster.__init__: inc_heartbeat (server.py:95-96)
     d.self_hb[o - d.col_lo] = 1u;
     if (!(d.flags & GS_CANONICAL)) {
         d.pos[p] = 0u;
@@ -2486,7 +2539,7 @@ __global__ __launch_bounds__(LB) void k_warm(Dev d) {
         }
         if (jg == o) continue;
         const size_t q = pix(d, jg, j);  // the owner's own view
-        d.hb[p] = d.hb[q];
+        hb_put(d, p, hb_raw(d, q));
         d.mv[p] = d.mv[q];
         if (d.flags & GS_TOMBSTONES) d.gc[p] = d.gc[q];
         if (d.held)
@@ -2557,7 +2610,7 @@ __device__ inline uint32_t digest_owner(const Dev &d, uint32_t o, uint32_t q, ui
 }
 __device__ inline void view_hgm(const Dev &d, uint32_t o, uint32_t j, uint32_t &H, uint32_t &G, uint32_t &M) {
     const size_t p = pix(d, o, j);
-    H = hb_dec(d.hb[p], d.self_hb[j]);
+    H = hb_view(d, p, d.self_hb[j]);
     G = (d.flags & GS_TOMBSTONES) ? d.gc[p] : 0u;
     M = d.mv[p] & MV_MASK;
 }
@@ -3224,8 +3277,13 @@ int launch_pass1(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t 
     hipEvent_t e0 = nullptr;
     int rc = time_begin(h, e0);
     if (rc) return rc;
-    if (h->d.spec) k_pass1<4, false, true><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, h->seq, 0u);
-    else k_pass1<4, false, false><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, h->seq, 0u);
+    if (h->d.hb8) {
+        if (h->d.spec) k_pass1<4, false, true, true><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, h->seq, 0u);
+        else k_pass1<4, false, false, true><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, h->seq, 0u);
+    } else {
+        if (h->d.spec) k_pass1<4, false, true><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, h->seq, 0u);
+        else k_pass1<4, false, false><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, h->seq, 0u);
+    }
     HIPCHK(h, hipGetLastError());
     return time_end(h, GS_KT_PASS1, e0);
 }
@@ -3328,7 +3386,7 @@ int gs_create(const gs_config *cfg, gs_handle **out) {
     const uint64_t pairs = N * NP;
     const bool genm = !(c.flags & GS_CANONICAL);
     uint64_t *b = h->bytes;
-    b[GS_R_HB] = pairs * 2;
+    b[GS_R_HB] = pairs * ((c.flags & GS_HB8) ? 1 : 2);
     b[GS_R_SELF_HB] = NP * 4;
     b[GS_R_MV] = pairs * 2;
     b[GS_R_GC] = (c.flags & GS_TOMBSTONES) ? pairs * 4 : 0;  // last_gc_version stays 0 without tombstone GC
@@ -3362,6 +3420,11 @@ int gs_create(const gs_config *cfg, gs_handle **out) {
     b[GS_R_CAND_N] = recs ? (N / 2) * 4 * 4 : 0;
     b[GS_R_SLOT_STAT] = recs ? (N / 2) * 2 * 16 : 0;  // sliced spec phases; k_lite's per-slot flags
     if (const char *m = getenv("GS_PACK")) h->pack_mode = !strcmp(m, "fused") ? 1 : !strcmp(m, "spec") ? 0 : 2;
+    // 8-bit heartbeats: only the record phases' pass 1 (k_pass1<HB8>) reads them in bulk
+    if ((c.flags & GS_HB8) && (!(c.flags & GS_CANONICAL) || c.n_keys > 16 || fused || h->pack_mode == 1)) {
+        delete h;
+        return GS_E_UNSUPPORTED;
+    }
     const uint64_t PW = round_up(h->NP, 256) / 64;
     b[GS_R_PEND] = N * NPL * PW * 8;  // one phase bit plane per observer row and phase slot
     b[GS_R_PEND_STAMP] = N * NPL * 4;
@@ -3386,6 +3449,7 @@ int gs_create(const gs_config *cfg, gs_handle **out) {
     d.sched_delay = c.sched_delay_ticks;
     d.sum_bits = sum_bits;
     d.VL = VL;
+    d.hb8 = (c.flags & GS_HB8) ? 1u : 0u;
     if (const char *ab = getenv("GS_ABLATE")) d.ablate = (uint32_t)atoi(ab);
     d.phi_thr = c.phi_threshold;
     d.prior5 = c.prior_weighted;
@@ -3514,7 +3578,7 @@ int gs_begin_round(gs_handle *h, const uint8_t *up, uint32_t tick) {
     if (!h || !h->booted || !up) return GS_E_INVALID;
     if (h->reports_pending)
         return fail(h, GS_E_INVALID, "gs_begin_round: the previous round's phases were not closed by gs_liveness");
-    if (h->hb_incs >= HB_LAG_CHECK_EVERY) {
+    if (h->hb_incs >= (h->d.hb8 ? HB8_LAG_CHECK_EVERY : HB_LAG_CHECK_EVERY)) {
         int rc = gs_check_heartbeat_lag(h);
         if (rc) return rc;
     }
@@ -3530,9 +3594,8 @@ int gs_begin_round(gs_handle *h, const uint8_t *up, uint32_t tick) {
 
 int gs_check_heartbeat_lag(gs_handle *h) {
     if (!h || !h->booted) return GS_E_INVALID;
-    const uint64_t pairs = (uint64_t)h->N * h->ncol;
-    const uint32_t blocks = (uint32_t)std::min<uint64_t>((pairs + LB - 1) / LB, 1u << 16);
-    k_hb_lag<<<blocks, LB, 0, h->stream>>>(h->d);
+    const uint32_t per = h->d.hb8 ? 16u : 8u, chunks = (h->ncol + LB * per - 1) / (LB * per);
+    k_hb_lag<<<h->N * chunks, LB, 0, h->stream>>>(h->d, chunks);
     HIPCHK(h, hipGetLastError());
     h->hb_incs = 0;
     return GS_OK;

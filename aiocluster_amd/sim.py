@@ -34,7 +34,7 @@ from datetime import timedelta
 import numpy as np
 
 from . import _lib
-from ._lib import GS_CANONICAL, GS_FD_RING, GS_NO_HELD, GS_NONE, GS_TOMBSTONES, REGION, TICK_US, GsError
+from ._lib import GS_CANONICAL, GS_FD_RING, GS_HB8, GS_NO_HELD, GS_NONE, GS_TOMBSTONES, REGION, TICK_US, GsError
 from .entities import ClusterSnapshot, NodeId, NodeState, VersionedValue, VersionStatusEnum
 from .pbsize import nodeid_size
 
@@ -171,7 +171,7 @@ class GossipSim:
                  tombstones: bool = True, fd_ring: bool | None = None, hist_cap: int = 64,
                  nid_sizes: list[int] | None = None, initial_ops: list[np.ndarray] | None = None,
                  canonical: bool | None = None, shards: int = 1, shard: int = 0, held: bool = True,
-                 ring_rows=None):
+                 ring_rows=None, hb8: bool = False):
         import torch
 
         if not torch.cuda.is_available():
@@ -203,6 +203,11 @@ class GossipSim:
             if tombstones:
                 raise GsError("held=False (GS_NO_HELD) needs tombstones=False")
             flags |= GS_NO_HELD
+        # 8-bit heartbeat views (GS_HB8: canonical record phases, K <= 16; exact while every view lags its owner
+        # by < 2^8, swept every <= 64 round starts + phases, err_hb_lag at 128)
+        self.hb8 = bool(hb8)
+        if hb8:
+            flags |= GS_HB8
         W = int(cfg["window"])
         # sampled rings: these observer rows keep interval rings (exact eviction), the others compact windows
         self.ring_rows = sorted(set(int(x) for x in ring_rows)) if ring_rows else []
@@ -542,11 +547,19 @@ class GossipSim:
         mv = self.region("MV", self.torch.int16, (self.n, self.np_))[:, : self.ncol]
         return int((mv < 0).sum().item())
 
-    def decode_heartbeats(self, hb16: np.ndarray) -> np.ndarray:
-        """NodeState.heartbeat of host rows of GS_R_HB (u16, any leading shape [..., NP]): the stored
-        value is the heartbeat mod 2^16, decoded against the owner's own heartbeat R (GS_R_SELF_HB)."""
+    def hb_region(self):
+        """GS_R_HB as a device tensor [N, NP]: int16 views (mod 2^16), or uint8 with GS_HB8 (mod 2^8)."""
+        return self.region("HB", self.torch.uint8 if self.hb8 else self.torch.int16, (self.n, self.np_))
+
+    def decode_heartbeats(self, hb: np.ndarray) -> np.ndarray:
+        """NodeState.heartbeat of host rows of GS_R_HB (u16, or u8 with GS_HB8; any leading shape [..., NP]):
+        the stored value is the heartbeat mod 2^16 (2^8), decoded against the owner's own heartbeat R
+        (GS_R_SELF_HB)."""
         R = self.region("SELF_HB", self.torch.int32, (self.np_,)).cpu().numpy().view(np.uint32)
-        s = np.asarray(hb16).view(np.uint16).astype(np.uint32)
+        if self.hb8:
+            s = np.asarray(hb).view(np.uint8).astype(np.uint32)
+            return (R - ((R - s) & np.uint32(0xFF))).astype(np.uint32)
+        s = np.asarray(hb).view(np.uint16).astype(np.uint32)
         return (R - ((R - s) & np.uint32(0xFFFF))).astype(np.uint32)
 
     def max_versions(self):
@@ -574,7 +587,7 @@ class GossipSim:
             return (t if rows is None else t.index_select(0, sel)).cpu().numpy()
 
         g = {"rows": np.arange(n) if rows is None else rows}
-        g["HB"] = self.decode_heartbeats(rd("HB", torch.int16, (n, NP)))
+        g["HB"] = self.decode_heartbeats(rd("HB", torch.uint8 if self.hb8 else torch.int16, (n, NP)))
         for name in ("GC", "POS"):
             if name in self.regions:
                 g[name] = rd(name, torch.int32, (n, NP)).view(np.uint32)
@@ -746,8 +759,9 @@ class GossipSim:
         self.materialize_held(o, o + 1)
         self.sync()
         R = int(self.region("SELF_HB", torch.int32, (self.np_,))[j].item()) & 0xFFFFFFFF
-        s = int(self.region("HB", torch.int16, (n, self.np_))[o, j].item()) & 0xFFFF
-        hb = (R - ((R - s) & 0xFFFF)) & 0xFFFFFFFF
+        s = int(self.hb_region()[o, j].item()) & 0xFFFF
+        m = 0xFF if self.hb8 else 0xFFFF
+        hb = (R - ((R - s) & m)) & 0xFFFFFFFF
         mv = int(self.region("MV", torch.int16, (n, self.np_))[o, j].item()) & 0x7FFF
         gc = int(self.region("GC", torch.int32, (n, self.np_))[o, j].item()) & 0xFFFFFFFF \
             if "GC" in self.regions else 0
@@ -786,7 +800,7 @@ class GossipSim:
         def row(name, dt=torch.int32):
             return self.region(name, dt, (n, self.np_))[o, :n].cpu().numpy()
 
-        hb = self.decode_heartbeats(self.region("HB", torch.int16, (n, self.np_))[o].cpu().numpy())[:n]
+        hb = self.decode_heartbeats(self.hb_region()[o].cpu().numpy())[:n]
         mv = row("MV", torch.int16).view(np.uint16).astype(np.uint32) & np.uint32(0x7FFF)
         gc = row("GC").view(np.uint32) if "GC" in self.regions else np.zeros(n, np.uint32)
         st = fd_state_word(row("FD_STATE", torch.uint8), row("FD_TOD"))

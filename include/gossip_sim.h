@@ -53,6 +53,11 @@ extern "C" {
 #define GS_NO_HELD 8u     /* no GS_R_HELD at all (needs !GS_TOMBSTONES): exact only while every view is a
                              prefix S_j(max_version), i.e. no NodeDelta is ever truncated; a view that would
                              get holes is counted in err_holes.  16 B less per pair at K = 16 (config 4) */
+#define GS_HB8 16u        /* 8-bit heartbeat views: GS_R_HB is u8 [N][NP] (mod 2^8, decoded against the owner's
+                             own heartbeat like the 16-bit store), exact while every view lags its owner by < 2^8;
+                             gs_begin_round sweeps the lags at least every 64 round starts + phases and counts
+                             a lag >= 128 in err_hb_lag.  Needs GS_CANONICAL, n_keys <= 16 and the record phases
+                             (not env GS_FUSED / GS_PACK=fused): half the heartbeat bytes of every exchange */
 
 /* owner write ops (NodeState.set/delete/set_with_ttl/delete_after_ttl, state.py:137-180) */
 #define GS_OP_SET 0u

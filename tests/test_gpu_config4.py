@@ -1,7 +1,8 @@
 """BASELINE config 4 at its real size, on one GPU: 262,144 nodes, one owner-column slice of 8 (GPU only).
 
 Config 4's contract: warm start, no deletes, version-only views
-(GS_NO_HELD) and an mtu above every delta, so no NodeDelta is ever truncated.  Then a slice's packing
+(GS_NO_HELD; 8-bit heartbeat views, GS_HB8, as bench.py runs it) and an mtu above every delta, so no
+NodeDelta is ever truncated.  Then a slice's packing
 does not depend on the other slices (every stale owner is sent whole), and slice 0 of 8 held alone
 (``SoloComm``: the others' totals are zeros) is exact for its 32,768 owner columns over all 262,144
 observer rows -- 152+ GB of the 288 GB HBM, the share one GPU of the 8-GPU run holds.  Checked:
@@ -57,7 +58,7 @@ def test_config4_262144_slice0_of_8():
                         quiet_from=settle + 1)
     boot = driver.boot_ops(n, K)
     sim = GossipSim(synthetic_node_ids(n), key_names(K), cfg, init="warm", tombstones=False, fd_ring=False,
-                    hist_cap=16, initial_ops=boot, held=False, shards=G, shard=0)
+                    hist_cap=16, initial_ops=boot, held=False, shards=G, shard=0, hb8=True)  # bench.py's layout
     assert (sim.col_lo, sim.ncol) == (0, 32768)
     grp = ShardGroup([sim], SoloComm(G), cfg["mtu"])
     plans = driver.prepare(spec, settle + 1 + quiet, torch, sim.device)

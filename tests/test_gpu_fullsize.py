@@ -33,10 +33,12 @@ def _run(sim, plans, rounds):
     sim.check()
 
 
-def test_config3_65536_every_phase_of_two_rounds_matches_oracle():
+@pytest.mark.parametrize("hb8", [True, False], ids=["hb8", "hb16"])
+def test_config3_65536_every_phase_of_two_rounds_matches_oracle(hb8):
     """BASELINE config 3 (the bench workload): 65,536 nodes x 16 keys, fanout 3, warm, 5 % writes + 5 %
-    up/down churn, window 1000, mtu 65,507, prefix-view layout; 20 settle rounds, the owner tables vs the
-    write stream, then every phase of rounds 20 and 21 on 16 random exchanges each."""
+    up/down churn, window 1000, mtu 65,507, prefix-view layout, 8-bit (the bench's) or 16-bit heartbeat
+    views; 20 settle rounds, the owner tables vs the write stream, then every phase of rounds 20 and 21 on
+    16 random exchanges each."""
     import torch
 
     n, K = 65536, 16
@@ -44,7 +46,7 @@ def test_config3_65536_every_phase_of_two_rounds_matches_oracle():
     spec = WorkloadSpec(n=n, k=K, fanout=3, seed=0, init="warm", write_frac=0.05, down_frac=0.05, down_rounds=3)
     boot = driver.boot_ops(n, K)
     sim = GossipSim(synthetic_node_ids(n), key_names(K), cfg, init="warm", tombstones=False, fd_ring=False,
-                    hist_cap=16, initial_ops=boot)
+                    hist_cap=16, initial_ops=boot, hb8=hb8)
     dev = sim.device
     plans = driver.prepare(spec, 22, torch, dev)
     _run(sim, plans, 20)

@@ -1,0 +1,108 @@
+"""8-bit heartbeat views (GS_HB8, GPU only).
+
+GS_R_HB holds each view's heartbeat mod 2^8, decoded against the owner's own heartbeat (GS_R_SELF_HB):
+exact while no view lags its owner by 2^8 or more.  gs_begin_round sweeps the lags at least every 64
+round starts + phases and counts a lag >= 2^7 in err_hb_lag, so a run either decodes
+exactly or is reported inexact.  The headline and config 4 run with it (bench.py; its lag census,
+tools/hb_lag.py, peaks at 49 there).
+"""
+
+import numpy as np
+import pytest
+from helpers import compare_exports, load_scenario, make_backend, replay_and_compare
+from oracle import OracleSim
+
+from aiocluster_amd.scenario import DEFAULT_CFG
+from aiocluster_amd.sim import GossipSim
+from aiocluster_amd.workload import key_names, liveness_tick, phase_tick, round_tick, synthetic_node_ids
+
+pytestmark = pytest.mark.gpu
+
+SCHED = [[(0, 1), (2, 3), (4, 5), (6, 7)], [(1, 2), (3, 4), (5, 6), (7, 0)], [(0, 4), (1, 5), (2, 6), (3, 7)],
+         [(5, 0), (6, 1), (7, 2), (4, 3)]]
+
+
+@pytest.mark.parametrize("name", ["sched16", "warm128"])
+def test_hb8_matches_reference_golden(name):
+    """The warm golden scenarios (MTU truncation, holes, churn) in the 8-bit layout: the reference's
+    canonical state after every round."""
+    scen = load_scenario(name)
+    exp = scen["expect"]
+    sim = make_backend(GossipSim, scen, tombstones=False, hb8=True)
+    res = replay_and_compare(sim, scen, exp["states"], exp["hashes"])
+    assert res is None, f"{name}: first mismatch at round {res[0]}: {res[1]}"
+    assert sim.check()["err_hb_lag"] == 0
+
+
+def test_hb8_heartbeats_past_2_8_with_a_long_absence_match_oracle():
+    """Eight nodes, 400 rounds: every heartbeat wraps mod 2^8 several times, and node 7 is down for 25
+    rounds (its views of the others fall ~75 behind, its windows go silent), then returns; the device
+    matches the C oracle (unbounded heartbeats) array for array, and the automatic lag sweeps ran clean."""
+    import torch
+
+    n, rounds, down0, down1 = 8, 400, 150, 175
+    ids, keys = synthetic_node_ids(n), key_names(2)
+    init = {j: [(0, f"v{j}")] for j in range(n)}
+    gpu = GossipSim(ids, keys, dict(DEFAULT_CFG), "warm", init, tombstones=False, fd_ring=True, hist_cap=8, hb8=True)
+    orc = OracleSim(ids, keys, dict(DEFAULT_CFG), "warm", init)
+    for r in range(rounds):
+        up = np.ones(n, np.uint8)
+        if down0 <= r < down1:
+            up[7] = 0
+        up_dev = torch.from_numpy(up).to(gpu.device)
+        t = round_tick(r)
+        gpu.begin_round(t, up_dev)
+        orc.begin_round(t, up)
+        for p in range(2):
+            pairs = [(a, b) for a, b in SCHED[(r + p) % len(SCHED)] if up[a] and up[b]]
+            gpu.run_phase(phase_tick(r, p), pairs)
+            orc.run_phase(phase_tick(r, p), pairs)
+        gpu.liveness(liveness_tick(r, 2), up_dev)
+        orc.liveness(liveness_tick(r, 2), up)
+        if r in (20, down1 - 1, down1 + 5, rounds - 1):
+            want = orc.export()
+            diff = compare_exports(gpu.export(), want)
+            assert diff is None, f"round {r}: {diff}"
+    assert np.asarray(want["hb"]).min() > 256, "every heartbeat must have wrapped mod 2^8"
+    c = gpu.check()
+    assert c["err_hb_lag"] == 0
+
+
+def test_hb8_lag_sweep_flags_views_at_2_7():
+    """A view lagging its owner by >= 2^7 heartbeats (injected) trips err_hb_lag; 2^7 - 1 does not."""
+    import torch
+
+    from aiocluster_amd._lib import GsError
+
+    n = 8
+    ids, keys = synthetic_node_ids(n), key_names(2)
+    init = {j: [(0, f"v{j}")] for j in range(n)}
+    gpu = GossipSim(ids, keys, dict(DEFAULT_CFG), "warm", init, tombstones=False, fd_ring=True, hist_cap=8, hb8=True)
+    up_dev = torch.ones(n, dtype=torch.uint8, device=gpu.device)
+    gpu.begin_round(round_tick(0), up_dev)
+    gpu.liveness(liveness_tick(0, 0), up_dev)
+    R = gpu.region("SELF_HB", torch.int32, (gpu.np_,))
+    hb = gpu.hb_region()
+    R[3] = 1000
+    for o in range(n):
+        hb[o, 3] = (1000 - 10) & 0xFF
+    hb[3, 3] = 1000 & 0xFF
+    hb[5, 3] = (1000 - 127) & 0xFF  # lag 2^7 - 1: exact, not flagged
+    gpu.check_heartbeat_lag()
+    assert gpu.check()["err_hb_lag"] == 0
+    assert gpu.node_state(5, 3).heartbeat == 1000 - 127
+    hb[6, 3] = (1000 - 128) & 0xFF  # lag 2^7
+    gpu.check_heartbeat_lag()
+    with pytest.raises(GsError, match="err_hb_lag"):
+        gpu.check()
+
+
+def test_hb8_refused_outside_the_record_phases():
+    """GS_HB8 needs the canonical layout and K <= 16 (the record phases' pass 1 reads it)."""
+    from aiocluster_amd._lib import GsError
+
+    ids = synthetic_node_ids(8)
+    with pytest.raises(GsError):
+        GossipSim(ids, key_names(2), dict(DEFAULT_CFG), "cold", None, tombstones=False, hb8=True)
+    with pytest.raises(GsError):
+        GossipSim(ids, key_names(20), dict(DEFAULT_CFG), "warm", None, tombstones=False, hb8=True)
