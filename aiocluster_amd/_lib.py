@@ -25,6 +25,7 @@ GS_TOMBSTONES = 2
 GS_FD_RING = 4
 GS_NO_HELD = 8
 GS_HB8 = 16  # 8-bit heartbeat views (include/gossip_sim.h)
+GS_MV8 = 32  # 8-bit max_version views
 GS_NONE = 0xFFFFFFFF
 GS_E_INVALID = -1
 GS_MV_INEXACT = 0x8000
@@ -57,7 +58,7 @@ def fd_sum_bits(window: int) -> int:
 REGIONS = [
     "HB", "MV", "GC", "HELD", "FD", "FD_STATE", "TS", "RING", "POS", "ORD", "ROW",
     "LAST_W", "HIST", "HIST_VID", "NID_SIZE", "KEY_LEN", "STAMP", "COUNTERS", "SLICE_BITS", "PEND", "PEND_STAMP", "LATEST",
-    "SELF_HB", "CAND", "CAND_N", "FD_TOD", "FD_LAST", "SLOT_STAT", "RING_SLOT", "VLOG",
+    "SELF_HB", "CAND", "CAND_N", "FD_TOD", "FD_LAST", "SLOT_STAT", "RING_SLOT", "SELF_MV", "VLOG",
 ]
 REGION = {n: i for i, n in enumerate(REGIONS)}
 
@@ -81,7 +82,7 @@ EXPORTS = [
     "gs_latest_tick", "gs_flush_reports", "gs_set_ring_rows",
 ]
 
-API_VERSION = 12
+API_VERSION = 13
 MAX_PHASES = 64  # GS_MAX_PHASES
 
 

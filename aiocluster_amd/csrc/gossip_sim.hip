@@ -137,6 +137,8 @@ struct Dev {
     uint32_t VL;
     uint32_t lite;  // this phase runs k_lite before the exact packer (set per phase by the host)
     uint32_t hb8;   // GS_HB8: hb holds u8 views (mod 2^8), else u16 (mod 2^16)
+    uint32_t mv8;   // GS_MV8: mv holds u8 views (version mod 2^7 | inexact << 7), else u16 words
+    uint32_t *self_mv;  // [NP] each owner column's own max_version (GS_R_SELF_MV)
     // event stream (gs_set_events): records {observer, owner, key | kind << 8, old version, new version,
     // tick, seq, 0}; kind 0 = on_key_change, 1 = node join, 2 = node leave; seq orders them (gossip_sim.h,
 // gs_set_events).  ev == nullptr: off
@@ -289,6 +291,21 @@ __device__ inline void set_byte(uint32_t *w, int q, uint32_t v) {
 constexpr uint32_t MV_INEXACT = GS_MV_INEXACT;
 constexpr uint32_t MV_MASK = GS_MV_INEXACT - 1u;
 
+// GS_MV8: a view's max_version in one byte, version mod 2^7 | MV_INEXACT >> 8, decoded against the owner's
+// own max_version M (every view is <= M; exact while it lags M by < 2^7: k_hb_lag) into the u16 word form
+// (version | MV_INEXACT) every consumer uses.  mv_word / mv_put: one view, either width.
+__device__ __forceinline__ uint32_t mv_dec8(uint32_t s, uint32_t M) {
+    return (M - ((M - (s & 0x7Fu)) & 0x7Fu)) | ((s & 0x80u) << 8);
+}
+__device__ __forceinline__ uint32_t mv_enc8(uint32_t w) { return (w & 0x7Fu) | ((w >> 8) & 0x80u); }
+__device__ __forceinline__ uint32_t mv_word(const Dev &d, size_t p, uint32_t j) {  // j: local owner column
+    return d.mv8 ? mv_dec8(reinterpret_cast<const uint8_t *>(d.mv)[p], d.self_mv[j]) : (uint32_t)d.mv[p];
+}
+__device__ __forceinline__ void mv_put(const Dev &d, size_t p, uint32_t w) {
+    if (d.mv8) reinterpret_cast<uint8_t *>(d.mv)[p] = (uint8_t)mv_enc8(w);
+    else d.mv[p] = (uint16_t)w;
+}
+
 // held ordinals of S_j(M) (local owner column j): start from the owner's latest write of each key
 // and step back while the write is newer than M (versions of one key increase with the ordinal)
 template <int KW>
@@ -335,7 +352,7 @@ __device__ __forceinline__ void eval_cand(const Dev &d, uint32_t s, uint32_t r, 
             lat[4 * q + 3] = v.w;
         }
     }
-    const uint32_t msw = HAVE_MV ? (mvw & 0xFFFFu) : d.mv[ps], mrw = HAVE_MV ? (mvw >> 16) : d.mv[pr];
+    const uint32_t msw = HAVE_MV ? (mvw & 0xFFFFu) : mv_word(d, ps, j), mrw = HAVE_MV ? (mvw >> 16) : mv_word(d, pr, j);
     const uint32_t ms = msw & MV_MASK, mr = mrw & MV_MASK;
     const uint32_t gs = gct ? d.gc[ps] : 0u, gr = gct ? d.gc[pr] : 0u;
     const uint32_t pos_r = GENM ? d.pos[pr] : 0u;
@@ -443,7 +460,7 @@ __device__ __forceinline__ void apply_cand(const Dev &d, uint32_t s, uint32_t r,
         // above mr move to the sender's latest write <= ms, the others already are), still a prefix.
         // ms <= mr happens when the receiver's digest left j out (scheduled for deletion: from = 0)
         if (!specd) {
-            d.mv[pr] = (uint16_t)(c.ms > c.mr ? c.ms : c.mr);
+            mv_put(d, pr, c.ms > c.mr ? c.ms : c.mr);
             alg += 4;
         }
         return;
@@ -510,14 +527,14 @@ __device__ __forceinline__ void apply_cand(const Dev &d, uint32_t s, uint32_t r,
     const bool keep_held = tt || (mvw & MV_INEXACT);  // a prefix view's HELD is not kept
     if (keep_held && !d.held) {  // GS_NO_HELD: a view with holes cannot be represented
         shard_add(d, C_E_HOLES, 1);
-        d.mv[pr] = (uint16_t)mvw;
+        mv_put(d, pr, mvw);
         return;
     }
     uint32_t *hrp = reinterpret_cast<uint32_t *>(d.held + pr * d.KP);
 #pragma unroll
     for (int q = 0; q < KW; q++)
         if (keep_held && (hr[q] != hr0[q] || c.rx)) { hrp[q] = hr[q]; alg += 4; }
-    d.mv[pr] = (uint16_t)mvw;
+    mv_put(d, pr, mvw);
     if (g != c.gr) d.gc[pr] = g;
     alg += 8;
 }
@@ -649,7 +666,7 @@ __device__ __forceinline__ void pack_group(const Dev &d, uint32_t s, uint32_t r,
             st.trunc++;
         }
     } else if (specd && cand && c.fast) {
-        d.mv[pix(d, r, c.j)] = (uint16_t)c.mr;  // not sent: undo pass 1's merge (a prefix view: no flag bit)
+        mv_put(d, pix(d, r, c.j), c.mr);  // not sent: undo pass 1's merge (a prefix view: no flag bit)
         st.alg += 4;
     }
 }
@@ -746,7 +763,7 @@ __device__ __forceinline__ void pack_dir(const Dev &d, uint32_t s, uint32_t r, c
                 const uint32_t p = ci < pend ? rv : win + wbuf[ci - pend];
                 j = GENM ? order[p] : p;
                 if (!GENM && !COUNT && tail && d.vlog) {  // tail mode: skip what cannot fit (min1_lb)
-                    const uint32_t msw = d.mv[pix(d, s, j)], mrw = d.mv[pix(d, r, j)];
+                    const uint32_t msw = mv_word(d, pix(d, s, j), j), mrw = mv_word(d, pix(d, r, j), j);
                     st.alg += 4;
                     if (!((msw | mrw) & MV_INEXACT) &&
                         min1_lb(d, j, msw, ds.sched ? 0u : mrw) > d.mtu - S)
@@ -802,14 +819,14 @@ __device__ __forceinline__ void pack_list(const Dev &d, uint32_t s, uint32_t r, 
         const uint2 cr = nxt;
         if (ci + WAVE < n) nxt = L[ci + WAVE];
         if (stop) {  // specd only: nothing more is sent
-            if (cand && rec_fast(cr.y)) { d.mv[pix(d, r, cr.x)] = (uint16_t)(cr.y >> 16); st.alg += 4; }
+            if (cand && rec_fast(cr.y)) { mv_put(d, pix(d, r, cr.x), cr.y >> 16); st.alg += 4; }
             continue;
         }
         if (!COUNT && cand && tail && d.vlog && rec_fast(cr.y)) {  // tail mode: skip what cannot fit (min1_lb)
             const uint32_t mr = cr.y >> 16;
             if (min1_lb(d, cr.x, cr.y & 0xFFFFu, ds.sched ? 0u : mr) > d.mtu - S) {
                 cand = false;
-                if (specd) { d.mv[pix(d, r, cr.x)] = (uint16_t)mr; st.alg += 4; }  // not sent: undo the merge
+                if (specd) { mv_put(d, pix(d, r, cr.x), mr); st.alg += 4; }  // not sent: undo the merge
             }
         }
         Cand<KW> c;
@@ -905,7 +922,7 @@ __device__ __forceinline__ bool pack_lite(const Dev &d, uint32_t rcv, size_t slo
 #pragma unroll
         for (int u = 0; u < LITE_B; u++) {
             if (rc[u].x == NONE) continue;
-            d.mv[pix(d, rcv, rc[u].x)] = (uint16_t)(rc[u].y & 0xFFFFu);  // max(ms, mr) = ms
+            mv_put(d, pix(d, rcv, rc[u].x), rc[u].y & 0xFFFFu);  // max(ms, mr) = ms
             alg += 4;
             st.nd++;
             st.cand++;
@@ -1010,12 +1027,12 @@ __device__ __forceinline__ uint32_t sched4(const Dev &d, size_t p, uint32_t t) {
 // this form while the current one computes, so nothing waits on the prefetch until it is decoded one
 // iteration later (and the packed form holds 12 VGPRs instead of 20).
 struct GrpRaw {
-    uint4 R;
+    uint4 R, M;  // the owners' own heartbeats; with MV8 their own max_versions
     uint2 hA, hB, mA, mB;
     uint4 pA, pB;
     uint32_t sA, sB;
 };
-template <bool GENM, bool HB8 = false>
+template <bool GENM, bool HB8 = false, bool MV8 = false>
 __device__ __forceinline__ void load_grp(const Dev &d, size_t ra, size_t rb, uint32_t c0, uint32_t t, bool schA,
                                          bool schB, GrpRaw &g) {
     g.R = *reinterpret_cast<const uint4 *>(d.self_hb + c0);
@@ -1027,8 +1044,15 @@ __device__ __forceinline__ void load_grp(const Dev &d, size_t ra, size_t rb, uin
         g.hA = *reinterpret_cast<const uint2 *>(d.hb + ra + c0);
         g.hB = *reinterpret_cast<const uint2 *>(d.hb + rb + c0);
     }
-    g.mA = *reinterpret_cast<const uint2 *>(d.mv + ra + c0);
-    g.mB = *reinterpret_cast<const uint2 *>(d.mv + rb + c0);
+    if (MV8) {  // 4 bytes per lane, decoded against the owners' own max_versions
+        const uint8_t *m8 = reinterpret_cast<const uint8_t *>(d.mv);
+        g.M = *reinterpret_cast<const uint4 *>(d.self_mv + c0);
+        g.mA = make_uint2(*reinterpret_cast<const uint32_t *>(m8 + ra + c0), 0u);
+        g.mB = make_uint2(*reinterpret_cast<const uint32_t *>(m8 + rb + c0), 0u);
+    } else {
+        g.mA = *reinterpret_cast<const uint2 *>(d.mv + ra + c0);
+        g.mB = *reinterpret_cast<const uint2 *>(d.mv + rb + c0);
+    }
     g.pA = g.pB = make_uint4(0u, 0u, 0u, 0u);
     g.sA = g.sB = 0u;
     if (GENM) {
@@ -1040,7 +1064,7 @@ __device__ __forceinline__ void load_grp(const Dev &d, size_t ra, size_t rb, uin
 }
 // decode: heartbeats against the owners' own (hb_dec); raw max_version words (prefix-view flag included):
 // pass 1 masks them where it compares, and the split path hands them to the packer in its records
-template <bool HB8 = false>
+template <bool HB8 = false, bool MV8 = false>
 __device__ __forceinline__ void dec_grp(const GrpRaw &r, Grp &g) {
     const uint32_t R[4] = {r.R.x, r.R.y, r.R.z, r.R.w};
     if (HB8) {
@@ -1055,8 +1079,17 @@ __device__ __forceinline__ void dec_grp(const GrpRaw &r, Grp &g) {
 #pragma unroll
         for (int i = 0; i < 4; i++) { g.hA[i] = hb_dec(hA[i], R[i]); g.hB[i] = hb_dec(hB[i], R[i]); }
     }
-    g.mA[0] = r.mA.x & 0xFFFFu; g.mA[1] = r.mA.x >> 16; g.mA[2] = r.mA.y & 0xFFFFu; g.mA[3] = r.mA.y >> 16;
-    g.mB[0] = r.mB.x & 0xFFFFu; g.mB[1] = r.mB.x >> 16; g.mB[2] = r.mB.y & 0xFFFFu; g.mB[3] = r.mB.y >> 16;
+    if (MV8) {
+        const uint32_t M[4] = {r.M.x, r.M.y, r.M.z, r.M.w};
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            g.mA[i] = mv_dec8((r.mA.x >> (8 * i)) & 0xFFu, M[i]);
+            g.mB[i] = mv_dec8((r.mB.x >> (8 * i)) & 0xFFu, M[i]);
+        }
+    } else {
+        g.mA[0] = r.mA.x & 0xFFFFu; g.mA[1] = r.mA.x >> 16; g.mA[2] = r.mA.y & 0xFFFFu; g.mA[3] = r.mA.y >> 16;
+        g.mB[0] = r.mB.x & 0xFFFFu; g.mB[1] = r.mB.x >> 16; g.mB[2] = r.mB.y & 0xFFFFu; g.mB[3] = r.mB.y >> 16;
+    }
     g.pA[0] = r.pA.x; g.pA[1] = r.pA.y; g.pA[2] = r.pA.z; g.pA[3] = r.pA.w;
     g.pB[0] = r.pB.x; g.pB[1] = r.pB.y; g.pB[2] = r.pB.z; g.pB[3] = r.pB.w;
     g.sA = r.sA;
@@ -1112,7 +1145,7 @@ __device__ __forceinline__ bool line_any8(bool w) {
 // (same appends, same order).
 // SCH = false: neither row can have a target scheduled for deletion at t (schA = schB = false; the
 // per-column predicates drop out).  SELF = false: the caller stores the responder's own new heartbeat.
-template <bool GENM, bool SCH = true, bool SELF = true, bool HB8 = false>
+template <bool GENM, bool SCH = true, bool SELF = true, bool HB8 = false, bool MV8 = false>
 __device__ __forceinline__ void pass1_grp(const Dev &d, size_t ra, size_t rb, uint32_t c0, uint32_t a, uint32_t b,
                                           uint32_t t, bool schA, bool schB, Grp &g, uint32_t &nBA, uint32_t &nAB,
                                           uint32_t &nNB, uint32_t &nNA, uint32_t &alg, uint32_t &reports,
@@ -1121,7 +1154,7 @@ __device__ __forceinline__ void pass1_grp(const Dev &d, size_t ra, size_t rb, ui
     rmA = rmB = 0u;
     nBA = nAB = nNB = nNA = 0u;
     // HBM-resident elements only: the SELF_HB row (16 B per group, 256 KiB per row, L2-resident) is not counted
-    alg += (HB8 ? 24 : 32) + (GENM ? 32 : 0) + (schA ? 4 : 0) + (schB ? 4 : 0);
+    alg += (HB8 ? 8 : 16) + (MV8 ? 8 : 16) + (GENM ? 32 : 0) + (schA ? 4 : 0) + (schB ? 4 : 0);
     // Branch-free (selects, no exec-mask juggling per column): the per-column rules of the reference,
     // restated as predicates.  _report_heartbeat (server.py:599-604, state.py:280-287) of a known view
     // stores the larger heartbeat and reports only if the old one was non-zero; an unknown owner is
@@ -1212,7 +1245,8 @@ __device__ __forceinline__ uint32_t spread8(uint32_t x) {
 // Split path (k_pass1): one wave step's stale owners of one direction (a nibble of 4 consecutive
 // columns per lane) go out twice, from the same four ballots (inactive lanes contribute zeros):
 //  * as natural-order bitmap words (bit c % 32 of word c / 32), zeros included, so the buffer never
-//    needs clearing; the first lane of each 8 stores its word: 32 contiguous bytes per wave;
+//    needs clearing; the first lane of each 8 stores its word: 32 contiguous bytes per wave -- only from
+//    the step whose owners overflow the list on (the packers walk the bitmap past the last record only);
 //  * as records {column, sender max_version word | receiver max_version word << 16} appended in
 //    column order to the wave's list L (the first GS_CAND_CAP of them; cnt counts all, wave-uniform).
 // Returns the lane's recorded columns (bit i: column c0 + i got a record).
@@ -1221,7 +1255,8 @@ __device__ __forceinline__ uint32_t emit_dir(uint32_t *gw, uint2 *L, uint32_t &c
     const uint64_t b0 = __ballot(nib & 1u), b1 = __ballot(nib & 2u), b2 = __ballot(nib & 4u), b3 = __ballot(nib & 8u);
     const int l = lane_id();
     const bool any = (b0 | b1 | b2 | b3) != 0ull;
-    if ((l & 7) == 0) {
+    const uint32_t tot = (uint32_t)(__popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3));
+    if ((l & 7) == 0 && cnt + tot > GS_CAND_CAP) {
         const uint32_t w = !any ? 0u
                                 : spread8((uint32_t)(b0 >> l)) | (spread8((uint32_t)(b1 >> l)) << 1) |
                                       (spread8((uint32_t)(b2 >> l)) << 2) | (spread8((uint32_t)(b3 >> l)) << 3);
@@ -1243,7 +1278,7 @@ __device__ __forceinline__ uint32_t emit_dir(uint32_t *gw, uint2 *L, uint32_t &c
             off++;
         }
     }
-    cnt += (uint32_t)(__popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3));
+    cnt += tot;
     return recm;
 }
 
@@ -1252,6 +1287,7 @@ __device__ __forceinline__ uint32_t emit_dir(uint32_t *gw, uint2 *L, uint32_t &c
 // 8-byte store into a line still in L2 -- instead of a scattered 2-byte store per NodeDelta later).  A
 // delta that fits the mtu sends all of them whole, which is exactly apply_delta's result for a prefix
 // view (apply_cand's fast path); the packers restore the receiver's word of the others.
+template <bool MV8 = false>
 __device__ __forceinline__ void spec_merge(const Dev &d, size_t ra, size_t rb, uint32_t c0, uint32_t recBA,
                                            uint32_t recAB, const uint32_t (&mA)[4], const uint32_t (&mB)[4],
                                            uint32_t &alg) {
@@ -1271,8 +1307,16 @@ __device__ __forceinline__ void spec_merge(const Dev &d, size_t ra, size_t rb, u
         wA = line_any8(wA);
         wB = line_any8(wB);
     }
-    if (wA) { st4h(d.mv + ra + c0, nA); alg += 8; }
-    if (wB) { st4h(d.mv + rb + c0, nB); alg += 8; }
+    if (MV8) {
+        uint8_t *m8 = reinterpret_cast<uint8_t *>(d.mv);
+        const uint32_t eA[4] = {mv_enc8(nA[0]), mv_enc8(nA[1]), mv_enc8(nA[2]), mv_enc8(nA[3])};
+        const uint32_t eB[4] = {mv_enc8(nB[0]), mv_enc8(nB[1]), mv_enc8(nB[2]), mv_enc8(nB[3])};
+        if (wA) { st4b(m8 + ra + c0, eA); alg += 4; }
+        if (wB) { st4b(m8 + rb + c0, eB); alg += 4; }
+    } else {
+        if (wA) { st4h(d.mv + ra + c0, nA); alg += 8; }
+        if (wB) { st4h(d.mv + rb + c0, nB); alg += 8; }
+    }
 }
 
 // Owner-column sharded phases ("multi-GPU"): the count pass leaves each exchange's
@@ -1314,7 +1358,7 @@ __device__ inline PackState chain_unpack(uint64_t v) {
 // SPEC (not with FUSE): the speculative max-version merge of the recorded prefix candidates (spec_merge,
 // Dev::spec); k_settle then only settles the deltas that do not fit and the candidates with holes.
 // HB8 (not with FUSE): GS_HB8's 8-bit heartbeat views.
-template <int KW, bool FUSE, bool SPEC = false, bool HB8 = false>
+template <int KW, bool FUSE, bool SPEC = false, bool HB8 = false, bool MV8 = false>
 __global__ __launch_bounds__(XB, (KW == 4 ? (FUSE ? P1_WAVES : P1S_WAVES) : 1)) void k_pass1(Dev d, const int32_t *ini, const int32_t *res,
                                                                        uint32_t n, uint32_t t, uint32_t seq,
                                                                        uint32_t e0) {
@@ -1365,28 +1409,28 @@ __global__ __launch_bounds__(XB, (KW == 4 ? (FUSE ? P1_WAVES : P1S_WAVES) : 1)) 
         // P1_AHEAD groups in flight ahead of the one being computed
         GrpRaw r0, r1, r2;
         constexpr uint32_t STEP = WAVE * 4u;
-        if (c0 < hi) load_grp<false, HB8>(d, ra, rb, c0, t, SCH && schA, SCH && schB, r0);
-        if (P1_AHEAD > 1 && c0 + STEP < hi) load_grp<false, HB8>(d, ra, rb, c0 + STEP, t, SCH && schA, SCH && schB, r1);
+        if (c0 < hi) load_grp<false, HB8, MV8>(d, ra, rb, c0, t, SCH && schA, SCH && schB, r0);
+        if (P1_AHEAD > 1 && c0 + STEP < hi) load_grp<false, HB8, MV8>(d, ra, rb, c0 + STEP, t, SCH && schA, SCH && schB, r1);
         while (c0 < hi) {
             const uint32_t c1 = c0 + STEP;
             if (P1_AHEAD > 1) {
-                if (c1 + STEP < hi) load_grp<false, HB8>(d, ra, rb, c1 + STEP, t, SCH && schA, SCH && schB, r2);
+                if (c1 + STEP < hi) load_grp<false, HB8, MV8>(d, ra, rb, c1 + STEP, t, SCH && schA, SCH && schB, r2);
             } else if (c1 < hi) {
-                load_grp<false, HB8>(d, ra, rb, c1, t, SCH && schA, SCH && schB, r1);
+                load_grp<false, HB8, MV8>(d, ra, rb, c1, t, SCH && schA, SCH && schB, r1);
             }
             Grp g0;
-            dec_grp<HB8>(r0, g0);
+            dec_grp<HB8, MV8>(r0, g0);
             uint32_t rmA, rmB, nBA, nAB, nNB, nNA;
             const uint32_t mA[4] = {g0.mA[0], g0.mA[1], g0.mA[2], g0.mA[3]};
             const uint32_t mB[4] = {g0.mB[0], g0.mB[1], g0.mB[2], g0.mB[3]};
-            pass1_grp<false, SCH, false, HB8>(d, ra, rb, c0, a, b, t, schA, schB, g0, nBA, nAB, nNB, nNA, alg, reports, hbw,
+            pass1_grp<false, SCH, false, HB8, MV8>(d, ra, rb, c0, a, b, t, schA, schB, g0, nBA, nAB, nNB, nNA, alg, reports, hbw,
                                          rmA, rmB);
             anynew = anynew || (nNB | nNA) != 0u;
             store_plane(planeA, c0, rmA, alg);
             store_plane(planeB, c0, rmB, alg);
             const uint32_t recBA = emit_dir(gBA, LBA, nBAc, c0, nBA, mB, mA, alg);  // b -> a: sender b, receiver a
             const uint32_t recAB = emit_dir(gAB, LAB, nABc, c0, nAB, mA, mB, alg);
-            if (SPEC && ((P1_LINE & 2) || (recBA | recAB))) spec_merge(d, ra, rb, c0, recBA, recAB, mA, mB, alg);
+            if (SPEC && ((P1_LINE & 2) || (recBA | recAB))) spec_merge<MV8>(d, ra, rb, c0, recBA, recAB, mA, mB, alg);
             r0 = r1;
             if (P1_AHEAD > 1) r1 = r2;
             c0 = c1;
@@ -2320,7 +2364,7 @@ __global__ __launch_bounds__(LB) void k_fd_gc(Dev d, const uint8_t *up, uint32_t
             const size_t p = ro + j;
             d.pos[p] = NONE;
             hb_put(d, p, 0u);
-            d.mv[p] = 0u;
+            mv_put(d, p, 0u);
             if (d.flags & GS_TOMBSTONES) d.gc[p] = 0u;
             if (d.held)
                 for (uint32_t k = 0; k < d.KP; k += 4) *reinterpret_cast<uint32_t *>(d.held + p * d.KP + k) = 0u;
@@ -2413,6 +2457,9 @@ __global__ __launch_bounds__(LB) void k_fd_age(Dev d, uint32_t t) {
 // inexact) before any decode can go wrong.
 // GS_HB8 (views mod 2^8): the same argument with a sweep at least every 64 round starts + phases (checked
 // at gs_begin_round, so at most 64 + 63 increments apart) and lags >= 2^7 counted: < 2^7 + 2^7 < 2^8.
+// GS_MV8 (max_version views mod 2^7): a view only falls behind when its owner writes (one version per
+// gs_owner_writes call at most), gs_owner_writes sweeps at least every 64 calls, and lags >= 2^6 are
+// counted: < 2^6 + 2^6 = 2^7 between sweeps.
 // One workgroup per (row, chunk of LB x 16 columns); each thread reads 16 views (u8) or 8 (u16).
 __global__ __launch_bounds__(LB) void k_hb_lag(Dev d, uint32_t chunks) {
     const bool genm = !(d.flags & GS_CANONICAL);
@@ -2431,6 +2478,13 @@ __global__ __launch_bounds__(LB) void k_hb_lag(Dev d, uint32_t chunks) {
             const uint32_t s = d.hb8 ? (w[i >> 2] >> (8 * (i & 3))) & 0xFFu : (w[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
             const uint32_t lag = d.hb8 ? (d.self_hb[j] - s) & 0xFFu : (d.self_hb[j] - s) & 0xFFFFu;
             if (lag >= (d.hb8 ? 0x80u : 0x8000u)) bad++;
+        }
+        if (d.mv8) {  // GS_MV8: max_version views lag their owner by < 2^6 at every sweep
+            const uint8_t *m8 = reinterpret_cast<const uint8_t *>(d.mv);
+            for (uint32_t i = 0; i < per && j0 + i < d.ncol; i++) {
+                const uint32_t s = m8[p0 + i];
+                if (((d.self_mv[j0 + i] - (s & 0x7Fu)) & 0x7Fu) >= 0x40u) bad++;
+            }
         }
     }
     const unsigned long long sb = wave_sum(bad);
@@ -2455,7 +2509,7 @@ __global__ __launch_bounds__(LB) void k_owner_writes(Dev d, const gs_write *ops,
     // with GS_NO_HELD its held ordinals are the latest-write table
     uint8_t *held = d.held ? d.held + pj * d.KP + k : d.last_w + (size_t)j * d.KP + k;
     const uint32_t w = *held;
-    const uint32_t M = d.mv[pj];
+    const uint32_t M = mv_word(d, pj, j);
     uint32_t st, vid, vl;
     if (op.op == GS_OP_SET || op.op == GS_OP_SET_WITH_TTL) {
         st = op.op == GS_OP_SET ? 0u : 2u;
@@ -2495,7 +2549,8 @@ __global__ __launch_bounds__(LB) void k_owner_writes(Dev d, const gs_write *ops,
     }
     d.last_w[(size_t)j * d.KP + k] = (uint8_t)nw;
     *held = (uint8_t)nw;
-    d.mv[pj] = (uint16_t)ver;
+    mv_put(d, pj, ver);
+    d.self_mv[j] = ver;
     // Cluster.set / set_with_ttl emit on_key_change (server.py:193-215, 238-252); delete and
     // delete_after_ttl mutate the stored VersionedValue in place, so old and new are the same
     // object and nothing is emitted (server.py:199-203, 211-215)
@@ -2540,7 +2595,8 @@ __global__ __launch_bounds__(LB) void k_warm(Dev d) {
         if (jg == o) continue;
         const size_t q = pix(d, jg, j);  // the owner's own view
         hb_put(d, p, hb_raw(d, q));
-        d.mv[p] = d.mv[q];
+        if (d.mv8) reinterpret_cast<uint8_t *>(d.mv)[p] = reinterpret_cast<const uint8_t *>(d.mv)[q];
+        else d.mv[p] = d.mv[q];
         if (d.flags & GS_TOMBSTONES) d.gc[p] = d.gc[q];
         if (d.held)
             for (uint32_t k = 0; k < d.KP; k += 4)
@@ -2565,7 +2621,7 @@ __global__ __launch_bounds__(LB) void k_materialize(Dev d, uint32_t r0, uint32_t
     for (uint64_t x = (uint64_t)blockIdx.x * LB + threadIdx.x; x < total; x += (uint64_t)gridDim.x * LB) {
         const uint32_t o = r0 + (uint32_t)(x / d.ncol), j = (uint32_t)(x % d.ncol);
         const size_t p = pix(d, o, j);
-        const uint32_t mv = d.mv[p];
+        const uint32_t mv = mv_word(d, p, j);
         if (mv & MV_INEXACT) continue;
         uint32_t h[16], alg = 0;
         derive_held<16>(d, j, mv, h, alg);
@@ -2612,7 +2668,7 @@ __device__ inline void view_hgm(const Dev &d, uint32_t o, uint32_t j, uint32_t &
     const size_t p = pix(d, o, j);
     H = hb_view(d, p, d.self_hb[j]);
     G = (d.flags & GS_TOMBSTONES) ? d.gc[p] : 0u;
-    M = d.mv[p] & MV_MASK;
+    M = mv_word(d, p, j) & MV_MASK;
 }
 __global__ __launch_bounds__(LB) void k_digest_size(Dev d, Wire w, uint32_t o, uint32_t t, bool sch, uint32_t cnt,
                                                     uint64_t *sz) {
@@ -2689,8 +2745,8 @@ __global__ __launch_bounds__(WAVE) void k_delta_plan(Dev d, uint32_t s, uint32_t
             if (has && !(schS && is_sched(dead_tod(d, ps), t, d.sched_delay))) {
                 bool in_d = GENM ? d.pos[pr] < cntR : true;
                 if (in_d && schR && is_sched(dead_tod(d, pr), t, d.sched_delay)) in_d = false;
-                const uint32_t dm = in_d ? (d.mv[pr] & MV_MASK) : 0u;
-                stale = (d.mv[ps] & MV_MASK) > dm;  // state.py:347-357
+                const uint32_t dm = in_d ? (mv_word(d, pr, j) & MV_MASK) : 0u;
+                stale = (mv_word(d, ps, j) & MV_MASK) > dm;  // state.py:347-357
             }
         }
         const unsigned long long m = __ballot(stale);
@@ -3070,6 +3126,7 @@ struct gs_handle {
     uint32_t last_phase_tick;
     uint64_t plane_flushes;           // mid-round report replays (rounds with phases > 16 ticks after the base)
     uint32_t hb_incs;                 // rounds + phases since the last heartbeat-lag check (gs_check_heartbeat_lag)
+    uint32_t mv_incs = 0;             // GS_MV8: gs_owner_writes calls since the last lag check
     uint32_t age_tick = 0;            // tick of the last window-age sweep (k_fd_age)
     uint32_t max_tick = 0;            // latest tick of any operation (gs_latest_tick: decodes GS_R_FD_LAST)
     void *reg[GS_NUM_REGIONS];
@@ -3178,6 +3235,7 @@ int check_bound(gs_handle *h) {
     d.slot_stat = (uint4 *)h->reg[GS_R_SLOT_STAT];
     d.ring_slot = (uint32_t *)h->reg[GS_R_RING_SLOT];
     d.vlog = (uint32_t *)h->reg[GS_R_VLOG];
+    d.self_mv = (uint32_t *)h->reg[GS_R_SELF_MV];
     return GS_OK;
 }
 
@@ -3277,7 +3335,10 @@ int launch_pass1(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t 
     hipEvent_t e0 = nullptr;
     int rc = time_begin(h, e0);
     if (rc) return rc;
-    if (h->d.hb8) {
+    if (h->d.mv8) {  // GS_MV8 implies GS_HB8
+        if (h->d.spec) k_pass1<4, false, true, true, true><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, h->seq, 0u);
+        else k_pass1<4, false, false, true, true><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, h->seq, 0u);
+    } else if (h->d.hb8) {
         if (h->d.spec) k_pass1<4, false, true, true><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, h->seq, 0u);
         else k_pass1<4, false, false, true><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, h->seq, 0u);
     } else {
@@ -3388,7 +3449,8 @@ int gs_create(const gs_config *cfg, gs_handle **out) {
     uint64_t *b = h->bytes;
     b[GS_R_HB] = pairs * ((c.flags & GS_HB8) ? 1 : 2);
     b[GS_R_SELF_HB] = NP * 4;
-    b[GS_R_MV] = pairs * 2;
+    b[GS_R_MV] = pairs * ((c.flags & GS_MV8) ? 1 : 2);
+    b[GS_R_SELF_MV] = NP * 4;
     b[GS_R_GC] = (c.flags & GS_TOMBSTONES) ? pairs * 4 : 0;  // last_gc_version stays 0 without tombstone GC
     b[GS_R_HELD] = (c.flags & GS_NO_HELD) ? 0 : pairs * KP;
     b[GS_R_FD] = pairs * 4;
@@ -3421,7 +3483,8 @@ int gs_create(const gs_config *cfg, gs_handle **out) {
     b[GS_R_SLOT_STAT] = recs ? (N / 2) * 2 * 16 : 0;  // sliced spec phases; k_lite's per-slot flags
     if (const char *m = getenv("GS_PACK")) h->pack_mode = !strcmp(m, "fused") ? 1 : !strcmp(m, "spec") ? 0 : 2;
     // 8-bit heartbeats: only the record phases' pass 1 (k_pass1<HB8>) reads them in bulk
-    if ((c.flags & GS_HB8) && (!(c.flags & GS_CANONICAL) || c.n_keys > 16 || fused || h->pack_mode == 1)) {
+    if (((c.flags & GS_HB8) && (!(c.flags & GS_CANONICAL) || c.n_keys > 16 || fused || h->pack_mode == 1)) ||
+        ((c.flags & GS_MV8) && (!(c.flags & GS_HB8) || (c.flags & GS_TOMBSTONES)))) {
         delete h;
         return GS_E_UNSUPPORTED;
     }
@@ -3450,6 +3513,7 @@ int gs_create(const gs_config *cfg, gs_handle **out) {
     d.sum_bits = sum_bits;
     d.VL = VL;
     d.hb8 = (c.flags & GS_HB8) ? 1u : 0u;
+    d.mv8 = (c.flags & GS_MV8) ? 1u : 0u;
     if (const char *ab = getenv("GS_ABLATE")) d.ablate = (uint32_t)atoi(ab);
     d.phi_thr = c.phi_threshold;
     d.prior5 = c.prior_weighted;
@@ -3499,7 +3563,7 @@ int gs_boot(gs_handle *h, const uint16_t *nid_size, const uint8_t *key_len) {
     const int zero[] = {GS_R_HB, GS_R_SELF_HB, GS_R_MV, GS_R_GC, GS_R_HELD, GS_R_FD, GS_R_FD_LAST, GS_R_FD_STATE, GS_R_FD_TOD,
                         GS_R_RING, GS_R_ROW, GS_R_LAST_W, GS_R_HIST, GS_R_HIST_VID,
                         GS_R_STAMP, GS_R_COUNTERS, GS_R_SLICE_BITS, GS_R_PEND, GS_R_PEND_STAMP, GS_R_LATEST,
-                        GS_R_SLOT_STAT, GS_R_VLOG};
+                        GS_R_SLOT_STAT, GS_R_VLOG, GS_R_SELF_MV};
     for (int r : zero)
         if (h->bytes[r]) HIPCHK(h, hipMemsetAsync(h->reg[r], 0, h->bytes[r], s));
     if (h->bytes[GS_R_TS]) HIPCHK(h, hipMemsetAsync(h->reg[GS_R_TS], 0xFF, h->bytes[GS_R_TS], s));
@@ -3568,6 +3632,11 @@ int gs_materialize_held(gs_handle *h, uint32_t row_lo, uint32_t row_hi) {
 int gs_owner_writes(gs_handle *h, const gs_write *ops, uint32_t n, uint32_t tick) {
     if (!h || !h->booted) return GS_E_INVALID;
     if (!n) return GS_OK;
+    if (h->d.mv8 && h->mv_incs >= 64) {  // 8-bit max_version views: at most 64 owner versions between sweeps
+        int rc = gs_check_heartbeat_lag(h);
+        if (rc) return rc;
+    }
+    h->mv_incs++;
     k_owner_writes<<<(n + LB - 1) / LB, LB, 0, h->stream>>>(h->d, ops, n, tick);
     HIPCHK(h, hipGetLastError());
     if (h->d.ev) h->d.ev_wseq += n;
@@ -3598,6 +3667,7 @@ int gs_check_heartbeat_lag(gs_handle *h) {
     k_hb_lag<<<h->N * chunks, LB, 0, h->stream>>>(h->d, chunks);
     HIPCHK(h, hipGetLastError());
     h->hb_incs = 0;
+    h->mv_incs = 0;
     return GS_OK;
 }
 

@@ -34,7 +34,7 @@ from datetime import timedelta
 import numpy as np
 
 from . import _lib
-from ._lib import GS_CANONICAL, GS_FD_RING, GS_HB8, GS_NO_HELD, GS_NONE, GS_TOMBSTONES, REGION, TICK_US, GsError
+from ._lib import GS_CANONICAL, GS_FD_RING, GS_HB8, GS_MV8, GS_NO_HELD, GS_NONE, GS_TOMBSTONES, REGION, TICK_US, GsError
 from .entities import ClusterSnapshot, NodeId, NodeState, VersionedValue, VersionStatusEnum
 from .pbsize import nodeid_size
 
@@ -171,7 +171,7 @@ class GossipSim:
                  tombstones: bool = True, fd_ring: bool | None = None, hist_cap: int = 64,
                  nid_sizes: list[int] | None = None, initial_ops: list[np.ndarray] | None = None,
                  canonical: bool | None = None, shards: int = 1, shard: int = 0, held: bool = True,
-                 ring_rows=None, hb8: bool = False):
+                 ring_rows=None, hb8: bool = False, mv8: bool = False):
         import torch
 
         if not torch.cuda.is_available():
@@ -208,6 +208,11 @@ class GossipSim:
         self.hb8 = bool(hb8)
         if hb8:
             flags |= GS_HB8
+        # 8-bit max_version views (GS_MV8, with GS_HB8 and no tombstones; exact while every view lags its owner
+        # by < 2^7 versions, swept every <= 64 owner-write calls, err_hb_lag at 64)
+        self.mv8 = bool(mv8)
+        if mv8:
+            flags |= GS_MV8
         W = int(cfg["window"])
         # sampled rings: these observer rows keep interval rings (exact eviction), the others compact windows
         self.ring_rows = sorted(set(int(x) for x in ring_rows)) if ring_rows else []
@@ -544,8 +549,23 @@ class GossipSim:
 
     def inexact_views(self) -> int:
         """Views with holes (GS_MV_INEXACT set): those whose HELD row the exchange kernel keeps."""
+        if self.mv8:
+            mv = self.region("MV", self.torch.uint8, (self.n, self.np_))[:, : self.ncol]
+            return int((mv >= 128).sum().item())
         mv = self.region("MV", self.torch.int16, (self.n, self.np_))[:, : self.ncol]
         return int((mv < 0).sum().item())
+
+    def mv_words(self, rows=None):
+        """Device int32 [rows, NP] max_version words (version | GS_MV_INEXACT) of observer rows ``rows`` (a
+        slice or index tensor; default all): GS_R_MV as stored (u16), or decoded from GS_MV8's bytes (version
+        mod 2^7 | inexact << 7) against the owners' own max_versions (GS_R_SELF_MV)."""
+        torch = self.torch
+        sel = slice(None) if rows is None else rows
+        if not self.mv8:
+            return self.region("MV", torch.int16, (self.n, self.np_))[sel].to(torch.int32) & 0xFFFF
+        s = self.region("MV", torch.uint8, (self.n, self.np_))[sel].to(torch.int32)
+        M = self.region("SELF_MV", torch.int32, (self.np_,))
+        return (M - ((M - (s & 0x7F)) & 0x7F)) | ((s & 0x80) << 8)
 
     def hb_region(self):
         """GS_R_HB as a device tensor [N, NP]: int16 views (mod 2^16), or uint8 with GS_HB8 (mod 2^8)."""
@@ -563,9 +583,8 @@ class GossipSim:
         return (R - ((R - s) & np.uint32(0xFFFF))).astype(np.uint32)
 
     def max_versions(self):
-        """Device int32 [N, NP] NodeState.max_version of every view (GS_R_MV is u16 | GS_MV_INEXACT)."""
-        mv = self.region("MV", self.torch.int16, (self.n, self.np_))
-        return mv.to(self.torch.int32) & 0x7FFF
+        """Device int32 [N, NP] NodeState.max_version of every view (GS_R_MV words: version | GS_MV_INEXACT)."""
+        return self.mv_words() & 0x7FFF
 
     # --------------------------------------------------------------- readback
     def _host(self, rows=None):
@@ -593,7 +612,7 @@ class GossipSim:
                 g[name] = rd(name, torch.int32, (n, NP)).view(np.uint32)
         st8 = rd("FD_STATE", torch.uint8, (n, NP))
         g["FD_STATE"] = fd_state_word(st8, rd("FD_TOD", torch.int32, (n, NP)))
-        mv = rd("MV", torch.int16, (n, NP)).view(np.uint16).astype(np.uint32)
+        mv = (self.mv_words(None if rows is None else sel).cpu().numpy().astype(np.uint32))
         g["MV_INEXACT"] = (mv >> np.uint32(15)).astype(np.uint8)  # prefix-view flag (GS_MV_INEXACT)
         g["MV"] = mv & np.uint32(0x7FFF)
         nr = g["MV"].shape[0]
@@ -762,7 +781,7 @@ class GossipSim:
         s = int(self.hb_region()[o, j].item()) & 0xFFFF
         m = 0xFF if self.hb8 else 0xFFFF
         hb = (R - ((R - s) & m)) & 0xFFFFFFFF
-        mv = int(self.region("MV", torch.int16, (n, self.np_))[o, j].item()) & 0x7FFF
+        mv = int(self.mv_words(slice(o, o + 1))[0, j].item()) & 0x7FFF
         gc = int(self.region("GC", torch.int32, (n, self.np_))[o, j].item()) & 0xFFFFFFFF \
             if "GC" in self.regions else 0
         hist = self.region("HIST", torch.int64, (n, Cc, K))[j].cpu().numpy().view(np.uint64)
@@ -801,7 +820,7 @@ class GossipSim:
             return self.region(name, dt, (n, self.np_))[o, :n].cpu().numpy()
 
         hb = self.decode_heartbeats(self.hb_region()[o].cpu().numpy())[:n]
-        mv = row("MV", torch.int16).view(np.uint16).astype(np.uint32) & np.uint32(0x7FFF)
+        mv = self.mv_words(slice(o, o + 1))[0, :n].cpu().numpy().astype(np.uint32) & np.uint32(0x7FFF)
         gc = row("GC").view(np.uint32) if "GC" in self.regions else np.zeros(n, np.uint32)
         st = fd_state_word(row("FD_STATE", torch.uint8), row("FD_TOD"))
         hist = self.region("HIST", torch.int64, (n, Cc, K)).cpu().numpy().view(np.uint64)

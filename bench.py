@@ -331,7 +331,7 @@ def config4_leg(args, world: int, rank: int, dist, dev) -> dict:
     shard = rank if world == C4_GPUS else 0
     sim = GossipSim(synthetic_node_ids(n), key_names(K), cfg, init="warm", device=str(dev), tombstones=False,
                     fd_ring=False, hist_cap=16, initial_ops=driver.boot_ops(n, K), held=False, shards=C4_GPUS,
-                    shard=shard, hb8=not args.hb16)
+                    shard=shard, hb8=not args.wide_views, mv8=not args.wide_views)
     comm = DistComm() if world == C4_GPUS else SoloComm(C4_GPUS, 0)
     grp = ShardGroup([sim], comm, cfg["mtu"])
     S, W, T = args.config4_settle, 1, args.config4_steps
@@ -480,8 +480,9 @@ def main():
                     help="--gpus N: the library drives each sliced phase over its own RCCL communicator "
                          "(gs_comm_init + gs_run_phase) instead of aiocluster_amd/shard.py over torch.distributed; "
                          "--slices G: gs_run_phase_group")
-    ap.add_argument("--hb16", action="store_true",
-                    help="16-bit heartbeat views (default: GS_HB8, exact while every view lags < 2^8; swept)")
+    ap.add_argument("--wide-views", action="store_true", default=bool(os.environ.get("GS_WIDE_VIEWS")),
+                    help="16-bit heartbeat and max_version views (default: GS_HB8 + GS_MV8, 8-bit views decoded "
+                         "against the owner's own values, exact while every view lags < 2^8 / 2^7; swept)")
     ap.add_argument("--no-held", action="store_true",
                     help="version-only layout (GS_NO_HELD, config 4): needs an mtu no delta reaches")
     args = ap.parse_args()
@@ -520,13 +521,14 @@ def main():
                         down_frac=0.05, down_rounds=3)
     workload = (f"N={n} K={K} F={args.fanout} warm, 5% writes + 5% down churn/round, window 1000, mtu {args.mtu}"
                 + (", version-only views (GS_NO_HELD)" if args.no_held else "")
-                + ("" if args.hb16 else ", 8-bit heartbeat views (GS_HB8)")
+                + ("" if args.wide_views else ", 8-bit heartbeat + max_version views (GS_HB8 + GS_MV8)")
                 + (", device peer selection (select_nodes_for_gossip, 8 seeds) + Luby phases" if args.peer_select
                    else ""))
     t_setup = time.perf_counter()
     ids = synthetic_node_ids(n)
     kw = dict(init="warm", device=str(dev), tombstones=False, fd_ring=False, hist_cap=16,
-              initial_ops=driver.boot_ops(n, K), held=not args.no_held, hb8=not args.hb16)
+              initial_ops=driver.boot_ops(n, K), held=not args.no_held, hb8=not args.wide_views,
+              mv8=not args.wide_views)
     if world > 1 and args.slices > 1:
         raise SystemExit("--slices is a one-process rehearsal; with --gpus N each rank holds one slice")
     group = None
@@ -620,9 +622,9 @@ def main():
             "higher_is_better": True,
             "scaling": "strong" if group is not None else "weak",
             "vs_baseline": None,
-            # the state is integer: heartbeats stored as u8 (GS_HB8) and max versions as u16 (exact decode,
-            # guarded: DESIGN.md §3), computed in u32; phi in binary64
-            "dtype": ("u16" if args.hb16 else "u8/u16") + "/u32 int (phi f64)",
+            # the state is integer: heartbeat and max_version views stored as u8 (GS_HB8 + GS_MV8; exact
+            # decode against the owners' own values, guarded: DESIGN.md §3), computed in u32; phi in binary64
+            "dtype": ("u16" if args.wide_views else "u8") + "/u32 int (phi f64)",
             "data": "synthetic (seeded workload generator; no dataset)",
             "config": {
                 "workload": workload,

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define GS_API_VERSION 12
+#define GS_API_VERSION 13
 #define GS_MAX_PHASES 64  /* gs_schedule_phases: phases per round */
 #define GS_TICK_US 15625u
 #define GS_NONE 0xFFFFFFFFu
@@ -58,6 +58,11 @@ extern "C" {
                              gs_begin_round sweeps the lags at least every 64 round starts + phases and counts
                              a lag >= 128 in err_hb_lag.  Needs GS_CANONICAL, n_keys <= 16 and the record phases
                              (not env GS_FUSED / GS_PACK=fused): half the heartbeat bytes of every exchange */
+#define GS_MV8 32u        /* 8-bit max_version views (needs GS_HB8 and !GS_TOMBSTONES): GS_R_MV is u8 [N][NP] =
+                             version mod 2^7 | GS_MV_INEXACT >> 8, decoded against the owner's own max_version
+                             (GS_R_SELF_MV); exact while every view lags its owner by < 2^7 versions:
+                             gs_owner_writes sweeps the lags at least every 64 calls and counts a lag >= 2^6
+                             in err_hb_lag */
 
 /* owner write ops (NodeState.set/delete/set_with_ttl/delete_after_ttl, state.py:137-180) */
 #define GS_OP_SET 0u
@@ -156,6 +161,7 @@ enum gs_region {
                                         {NodeDeltas, kvs, candidates, needs a pack} of a speculative phase,
                                         between gs_phase_count and gs_phase_pack */
     GS_R_RING_SLOT,   /* u32 [N]       sampled rings: each observer row's ring slot, GS_NONE = compact windows */
+    GS_R_SELF_MV,     /* u32 [NP]      each owner column's own max_version (its latest write's version) */
     GS_R_VLOG,        /* u32 [NC][VL]  each owner's writes by version (no GS_TOMBSTONES only: every write is version
                                         max_version + 1), VL = K * (hist_cap - 1) + 1 rounded up to 4: entry v =
                                         DeltaPb bytes of write v's KeyValueUpdatePb field | (version of the

@@ -1,7 +1,7 @@
 """BASELINE config 4 at its real size, on one GPU: 262,144 nodes, one owner-column slice of 8 (GPU only).
 
 Config 4's contract: warm start, no deletes, version-only views
-(GS_NO_HELD; 8-bit heartbeat views, GS_HB8, as bench.py runs it) and an mtu above every delta, so no
+(GS_NO_HELD; 8-bit heartbeat and max_version views, GS_HB8 + GS_MV8, as bench.py runs it) and an mtu above every delta, so no
 NodeDelta is ever truncated.  Then a slice's packing
 does not depend on the other slices (every stale owner is sent whole), and slice 0 of 8 held alone
 (``SoloComm``: the others' totals are zeros) is exact for its 32,768 owner columns over all 262,144
@@ -32,15 +32,16 @@ pytestmark = pytest.mark.gpu
 
 
 def _max_version_checks(sim, converged: bool) -> tuple[int, int]:
-    """(views above their owner's max_version, views below it); row chunks keep the temporaries small."""
+    """(views above their owner's max_version, views below it); row chunks keep the temporaries small.
+    The owner's max_version is GS_R_SELF_MV (its own latest write).  With GS_MV8 a view decodes to at most
+    that by construction, and the bound that keeps the decode exact (lag < 2^7) is the lag sweep's
+    (err_hb_lag, checked by every grp.check()); "below" -- convergence -- is the real check there."""
     torch = sim.torch
-    nc, lo = sim.ncol, sim.col_lo
-    mv = sim.region("MV", torch.int16, (sim.n, sim.np_))
-    cols = torch.arange(nc, device=sim.device)
-    own = (mv[lo + cols, cols].to(torch.int32) & 0xFFFF)
+    nc = sim.ncol
+    own = sim.region("SELF_MV", torch.int32, (sim.np_,))[:nc]
     above = below = 0
     for r0 in range(0, sim.n, 16384):
-        blk = mv[r0:r0 + 16384, :nc].to(torch.int32) & 0xFFFF  # the inexact bit included: never set here
+        blk = sim.mv_words(slice(r0, r0 + 16384))[:, :nc]  # decoded words, the inexact bit included: never set here
         above += int((blk > own[None, :]).sum().item())
         if converged:
             below += int((blk < own[None, :]).sum().item())
@@ -58,7 +59,8 @@ def test_config4_262144_slice0_of_8():
                         quiet_from=settle + 1)
     boot = driver.boot_ops(n, K)
     sim = GossipSim(synthetic_node_ids(n), key_names(K), cfg, init="warm", tombstones=False, fd_ring=False,
-                    hist_cap=16, initial_ops=boot, held=False, shards=G, shard=0, hb8=True)  # bench.py's layout
+                    hist_cap=16, initial_ops=boot, held=False, shards=G, shard=0, hb8=True,
+                    mv8=True)  # bench.py's layout
     assert (sim.col_lo, sim.ncol) == (0, 32768)
     grp = ShardGroup([sim], SoloComm(G), cfg["mtu"])
     plans = driver.prepare(spec, settle + 1 + quiet, torch, sim.device)

@@ -1,10 +1,12 @@
-"""8-bit heartbeat views (GS_HB8, GPU only).
+"""8-bit heartbeat and max_version views (GS_HB8, GS_MV8; GPU only).
 
 GS_R_HB holds each view's heartbeat mod 2^8, decoded against the owner's own heartbeat (GS_R_SELF_HB):
 exact while no view lags its owner by 2^8 or more.  gs_begin_round sweeps the lags at least every 64
 round starts + phases and counts a lag >= 2^7 in err_hb_lag, so a run either decodes
-exactly or is reported inexact.  The headline and config 4 run with it (bench.py; its lag census,
-tools/hb_lag.py, peaks at 49 there).
+exactly or is reported inexact.  GS_MV8 does the same for max_version views (version mod 2^7 | the
+inexact flag, decoded against the owner's own max_version, GS_R_SELF_MV): a view only falls behind when its
+owner writes, gs_owner_writes sweeps at least every 64 calls and counts a lag >= 2^6.  The headline and
+config 4 run with both (bench.py; the heartbeat-lag census, tools/hb_lag.py, peaks at 49 there).
 """
 
 import numpy as np
@@ -22,13 +24,14 @@ SCHED = [[(0, 1), (2, 3), (4, 5), (6, 7)], [(1, 2), (3, 4), (5, 6), (7, 0)], [(0
          [(5, 0), (6, 1), (7, 2), (4, 3)]]
 
 
+@pytest.mark.parametrize("mv8", [False, True], ids=["hb8", "hb8mv8"])
 @pytest.mark.parametrize("name", ["sched16", "warm128"])
-def test_hb8_matches_reference_golden(name):
-    """The warm golden scenarios (MTU truncation, holes, churn) in the 8-bit layout: the reference's
+def test_hb8_matches_reference_golden(name, mv8):
+    """The warm golden scenarios (MTU truncation, holes, churn) in the 8-bit layouts: the reference's
     canonical state after every round."""
     scen = load_scenario(name)
     exp = scen["expect"]
-    sim = make_backend(GossipSim, scen, tombstones=False, hb8=True)
+    sim = make_backend(GossipSim, scen, tombstones=False, hb8=True, mv8=mv8)
     res = replay_and_compare(sim, scen, exp["states"], exp["hashes"])
     assert res is None, f"{name}: first mismatch at round {res[0]}: {res[1]}"
     assert sim.check()["err_hb_lag"] == 0
@@ -106,3 +109,85 @@ def test_hb8_refused_outside_the_record_phases():
         GossipSim(ids, key_names(2), dict(DEFAULT_CFG), "cold", None, tombstones=False, hb8=True)
     with pytest.raises(GsError):
         GossipSim(ids, key_names(20), dict(DEFAULT_CFG), "warm", None, tombstones=False, hb8=True)
+
+
+def test_mv8_versions_past_2_7_with_an_absence_match_oracle():
+    """Eight nodes each writing a key every round they are up, 170 rounds: every owner's max_version passes
+    2^7 (views wrap mod 2^7), node 7 is down for 20 rounds (its views fall 20 versions behind), and MTU
+    truncation leaves holes (the inexact flag in the byte); the device matches the C oracle array for array
+    and the automatic sweeps ran clean."""
+    import torch
+
+    n, rounds, down0, down1 = 8, 170, 100, 120
+    ids, keys = synthetic_node_ids(n), key_names(2)
+    init = {j: [(0, f"v{j}")] for j in range(n)}
+    cfg = dict(DEFAULT_CFG, mtu=400)
+    gpu = GossipSim(ids, keys, cfg, "warm", init, tombstones=False, fd_ring=True, hist_cap=100, hb8=True, mv8=True)
+    orc = OracleSim(ids, keys, cfg, "warm", init)
+    for r in range(rounds):
+        up = np.ones(n, np.uint8)
+        if down0 <= r < down1:
+            up[7] = 0
+        up_dev = torch.from_numpy(up).to(gpu.device)
+        t = round_tick(r)
+        for j in range(n):
+            if up[j]:
+                gpu.write(t, j, r % 2, 0, f"v{j}.{r}")
+                orc.write(t, j, r % 2, 0, f"v{j}.{r}")
+        gpu.begin_round(t, up_dev)
+        orc.begin_round(t, up)
+        for p in range(2):
+            pairs = [(a, b) for a, b in SCHED[(r + p) % len(SCHED)] if up[a] and up[b]]
+            gpu.run_phase(phase_tick(r, p), pairs)
+            orc.run_phase(phase_tick(r, p), pairs)
+        gpu.liveness(liveness_tick(r, 2), up_dev)
+        orc.liveness(liveness_tick(r, 2), up)
+        if r in (30, down1 - 1, down1 + 3, rounds - 1):
+            want = orc.export()
+            diff = compare_exports(gpu.export(), want)
+            assert diff is None, f"round {r}: {diff}"
+    assert np.asarray(want["mv"]).max() > 128, "max_versions must pass 2^7"
+    c = gpu.check()
+    assert c["err_hb_lag"] == 0 and c["truncated"] > 0
+
+
+def test_mv8_lag_sweep_flags_views_at_2_6():
+    """A max_version view lagging its owner by >= 2^6 versions (injected) trips err_hb_lag; 2^6 - 1 does
+    not, and decodes exactly (the inexact flag kept apart)."""
+    import torch
+
+    from aiocluster_amd._lib import GsError
+
+    n = 8
+    ids, keys = synthetic_node_ids(n), key_names(2)
+    init = {j: [(0, f"v{j}")] for j in range(n)}
+    gpu = GossipSim(ids, keys, dict(DEFAULT_CFG), "warm", init, tombstones=False, fd_ring=True, hist_cap=8,
+                    hb8=True, mv8=True)
+    up_dev = torch.ones(n, dtype=torch.uint8, device=gpu.device)
+    gpu.begin_round(round_tick(0), up_dev)
+    gpu.liveness(liveness_tick(0, 0), up_dev)
+    M = gpu.region("SELF_MV", torch.int32, (gpu.np_,))
+    mv = gpu.region("MV", torch.uint8, (n, gpu.np_))
+    M[3] = 1000
+    for o in range(n):
+        mv[o, 3] = (1000 - 5) & 0x7F
+    mv[3, 3] = 1000 & 0x7F
+    mv[5, 3] = ((1000 - 63) & 0x7F) | 0x80  # lag 2^6 - 1, with holes: exact, not flagged
+    gpu.check_heartbeat_lag()
+    assert gpu.check()["err_hb_lag"] == 0
+    w = int(gpu.mv_words(slice(5, 6))[0, 3].item())
+    assert w == (1000 - 63) | 0x8000
+    mv[6, 3] = (1000 - 64) & 0x7F  # lag 2^6
+    gpu.check_heartbeat_lag()
+    with pytest.raises(GsError, match="err_hb_lag"):
+        gpu.check()
+
+
+def test_mv8_refused_without_hb8_or_with_tombstones():
+    from aiocluster_amd._lib import GsError
+
+    ids = synthetic_node_ids(8)
+    with pytest.raises(GsError):
+        GossipSim(ids, key_names(2), dict(DEFAULT_CFG), "warm", None, tombstones=False, mv8=True)
+    with pytest.raises(GsError):
+        GossipSim(ids, key_names(2), dict(DEFAULT_CFG), "warm", None, tombstones=True, hb8=True, mv8=True)
