@@ -58,7 +58,7 @@ def fd_sum_bits(window: int) -> int:
 REGIONS = [
     "HB", "MV", "GC", "HELD", "FD", "FD_STATE", "TS", "RING", "POS", "ORD", "ROW",
     "LAST_W", "HIST", "HIST_VID", "NID_SIZE", "KEY_LEN", "STAMP", "COUNTERS", "SLICE_BITS", "PEND", "PEND_STAMP", "LATEST",
-    "SELF_HB", "CAND", "CAND_N", "FD_TOD", "FD_LAST", "SLOT_STAT", "RING_SLOT", "SELF_MV", "VLOG",
+    "SELF_HB", "CAND", "CAND_N", "FD_TOD", "FD_LAST", "SLOT_STAT", "RING_SLOT", "SELF_MV", "SELF_PK", "VLOG",
 ]
 REGION = {n: i for i, n in enumerate(REGIONS)}
 
@@ -82,7 +82,7 @@ EXPORTS = [
     "gs_latest_tick", "gs_flush_reports", "gs_set_ring_rows",
 ]
 
-API_VERSION = 13
+API_VERSION = 14
 MAX_PHASES = 64  # GS_MAX_PHASES
 
 

@@ -139,6 +139,10 @@ struct Dev {
     uint32_t hb8;   // GS_HB8: hb holds u8 views (mod 2^8), else u16 (mod 2^16)
     uint32_t mv8;   // GS_MV8: mv holds u8 views (version mod 2^7 | inexact << 7), else u16 words
     uint32_t *self_mv;  // [NP] each owner column's own max_version (GS_R_SELF_MV)
+    // GS_MV8: [NP] both owner values packed for pass 1 (self_pack): one 16-byte load per 4 columns decodes
+    // both 8-bit views -- the heartbeat needs only R mod 2^8 and whether R is 0 (R < 2^15 kept exactly),
+    // the max_version word only M (< 2^15)
+    uint32_t *self_pk;
     // event stream (gs_set_events): records {observer, owner, key | kind << 8, old version, new version,
     // tick, seq, 0}; kind 0 = on_key_change, 1 = node join, 2 = node leave; seq orders them (gossip_sim.h,
 // gs_set_events).  ev == nullptr: off
@@ -298,6 +302,15 @@ __device__ __forceinline__ uint32_t mv_dec8(uint32_t s, uint32_t M) {
     return (M - ((M - (s & 0x7Fu)) & 0x7Fu)) | ((s & 0x80u) << 8);
 }
 __device__ __forceinline__ uint32_t mv_enc8(uint32_t w) { return (w & 0x7Fu) | ((w >> 8) & 0x80u); }
+// GS_R_SELF_PK: Rx = R mod 2^15 | (R >= 2^15) << 15 is congruent to R mod 2^8 and is 0 iff R is, and
+// every 8-bit view decodes to Rx - lag (lag < 2^8 <= Rx unless Rx = R < 2^15): the same order and the same
+// zero test as the true heartbeats, and the same low byte
+__device__ __forceinline__ uint32_t self_pack(uint32_t R, uint32_t M) {
+    return (R & 0x7FFFu) | (R >= 0x8000u ? 0x8000u : 0u) | (M << 16);
+}
+__device__ __forceinline__ void self_repack(const Dev &d, uint32_t j) {
+    if (d.self_pk) d.self_pk[j] = self_pack(d.self_hb[j], d.self_mv[j]);
+}
 __device__ __forceinline__ uint32_t mv_word(const Dev &d, size_t p, uint32_t j) {  // j: local owner column
     return d.mv8 ? mv_dec8(reinterpret_cast<const uint8_t *>(d.mv)[p], d.self_mv[j]) : (uint32_t)d.mv[p];
 }
@@ -1027,7 +1040,7 @@ __device__ __forceinline__ uint32_t sched4(const Dev &d, size_t p, uint32_t t) {
 // this form while the current one computes, so nothing waits on the prefetch until it is decoded one
 // iteration later (and the packed form holds 12 VGPRs instead of 20).
 struct GrpRaw {
-    uint4 R, M;  // the owners' own heartbeats; with MV8 their own max_versions
+    uint4 R;  // the owners' own heartbeats (MV8: GS_R_SELF_PK, both values packed)
     uint2 hA, hB, mA, mB;
     uint4 pA, pB;
     uint32_t sA, sB;
@@ -1035,7 +1048,7 @@ struct GrpRaw {
 template <bool GENM, bool HB8 = false, bool MV8 = false>
 __device__ __forceinline__ void load_grp(const Dev &d, size_t ra, size_t rb, uint32_t c0, uint32_t t, bool schA,
                                          bool schB, GrpRaw &g) {
-    g.R = *reinterpret_cast<const uint4 *>(d.self_hb + c0);
+    g.R = *reinterpret_cast<const uint4 *>((MV8 ? d.self_pk : d.self_hb) + c0);
     if (HB8) {  // 4 bytes per lane (4 views)
         const uint8_t *h8 = reinterpret_cast<const uint8_t *>(d.hb);
         g.hA = make_uint2(*reinterpret_cast<const uint32_t *>(h8 + ra + c0), 0u);
@@ -1046,7 +1059,6 @@ __device__ __forceinline__ void load_grp(const Dev &d, size_t ra, size_t rb, uin
     }
     if (MV8) {  // 4 bytes per lane, decoded against the owners' own max_versions
         const uint8_t *m8 = reinterpret_cast<const uint8_t *>(d.mv);
-        g.M = *reinterpret_cast<const uint4 *>(d.self_mv + c0);
         g.mA = make_uint2(*reinterpret_cast<const uint32_t *>(m8 + ra + c0), 0u);
         g.mB = make_uint2(*reinterpret_cast<const uint32_t *>(m8 + rb + c0), 0u);
     } else {
@@ -1067,7 +1079,16 @@ __device__ __forceinline__ void load_grp(const Dev &d, size_t ra, size_t rb, uin
 template <bool HB8 = false, bool MV8 = false>
 __device__ __forceinline__ void dec_grp(const GrpRaw &r, Grp &g) {
     const uint32_t R[4] = {r.R.x, r.R.y, r.R.z, r.R.w};
-    if (HB8) {
+    if (MV8) {  // packed: Rx = the low 16 bits (self_pack), M = the high 16
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const uint32_t Rx = R[i] & 0xFFFFu, M = R[i] >> 16;
+            g.hA[i] = hb_dec8((r.hA.x >> (8 * i)) & 0xFFu, Rx);
+            g.hB[i] = hb_dec8((r.hB.x >> (8 * i)) & 0xFFu, Rx);
+            g.mA[i] = mv_dec8((r.mA.x >> (8 * i)) & 0xFFu, M);
+            g.mB[i] = mv_dec8((r.mB.x >> (8 * i)) & 0xFFu, M);
+        }
+    } else if (HB8) {
 #pragma unroll
         for (int i = 0; i < 4; i++) {
             g.hA[i] = hb_dec8((r.hA.x >> (8 * i)) & 0xFFu, R[i]);
@@ -1079,14 +1100,7 @@ __device__ __forceinline__ void dec_grp(const GrpRaw &r, Grp &g) {
 #pragma unroll
         for (int i = 0; i < 4; i++) { g.hA[i] = hb_dec(hA[i], R[i]); g.hB[i] = hb_dec(hB[i], R[i]); }
     }
-    if (MV8) {
-        const uint32_t M[4] = {r.M.x, r.M.y, r.M.z, r.M.w};
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            g.mA[i] = mv_dec8((r.mA.x >> (8 * i)) & 0xFFu, M[i]);
-            g.mB[i] = mv_dec8((r.mB.x >> (8 * i)) & 0xFFu, M[i]);
-        }
-    } else {
+    if (!MV8) {
         g.mA[0] = r.mA.x & 0xFFFFu; g.mA[1] = r.mA.x >> 16; g.mA[2] = r.mA.y & 0xFFFFu; g.mA[3] = r.mA.y >> 16;
         g.mB[0] = r.mB.x & 0xFFFFu; g.mB[1] = r.mB.x >> 16; g.mB[2] = r.mB.y & 0xFFFFu; g.mB[3] = r.mB.y >> 16;
     }
@@ -1348,6 +1362,15 @@ __device__ inline PackState chain_unpack(uint64_t v) {
 #ifndef P1_AHEAD
 #define P1_AHEAD 1  // pass-1 groups loaded ahead of the one being computed (1 or 2: 2 measured slower, r2o)
 #endif
+// 8-bit views (HB8 + MV8, GS_R_SELF_PK): a group's loads are a third of the 16-bit ones, so the pass is
+// bound by groups in flight, not bytes: two groups ahead at 5 waves per SIMD, 96 VGPRs, no spills
+// (r3j: 3.11 ms per phase vs 3.42 at one ahead / 4 waves; 6 waves spill, 4.43 ms)
+#ifndef P1N_AHEAD
+#define P1N_AHEAD 2
+#endif
+#ifndef P1N_WAVES
+#define P1N_WAVES 5
+#endif
 // FUSE: the same workgroup then packs and applies both directions from the records (wave 0: b -> a,
 // wave 1: a -> b) right after streaming the rows, while the receivers' max_version lines are still in L2
 // (the applies are one scattered 2-byte store per NodeDelta; tools/membench.hip prices those at 25 G/s
@@ -1359,7 +1382,7 @@ __device__ inline PackState chain_unpack(uint64_t v) {
 // Dev::spec); k_settle then only settles the deltas that do not fit and the candidates with holes.
 // HB8 (not with FUSE): GS_HB8's 8-bit heartbeat views.
 template <int KW, bool FUSE, bool SPEC = false, bool HB8 = false, bool MV8 = false>
-__global__ __launch_bounds__(XB, (KW == 4 ? (FUSE ? P1_WAVES : P1S_WAVES) : 1)) void k_pass1(Dev d, const int32_t *ini, const int32_t *res,
+__global__ __launch_bounds__(XB, (KW == 4 ? (FUSE ? P1_WAVES : MV8 ? P1N_WAVES : P1S_WAVES) : 1)) void k_pass1(Dev d, const int32_t *ini, const int32_t *res,
                                                                        uint32_t n, uint32_t t, uint32_t seq,
                                                                        uint32_t e0) {
     static_assert(!(FUSE && SPEC), "the fused packer applies every NodeDelta itself");
@@ -1401,19 +1424,24 @@ __global__ __launch_bounds__(XB, (KW == 4 ? (FUSE ? P1_WAVES : P1S_WAVES) : 1)) 
     // responder inc_heartbeat (server.py:524): the owner's own heartbeat R is raised once, here; the
     // view hb[b][b] is raised in the loop.  Other exchanges of the phase decode column b against R or
     // R + 1, and both bound every view of b in the rows they touch
-    if (tid == 0 && b - d.col_lo < d.ncol) d.self_hb[b - d.col_lo] += 1u;
+    if (tid == 0 && b - d.col_lo < d.ncol) {
+        const uint32_t jb = b - d.col_lo, R1 = d.self_hb[jb] + 1u;
+        d.self_hb[jb] = R1;
+        if (MV8) d.self_pk[jb] = self_pack(R1, d.self_mv[jb]);
+    }
     const uint32_t c0s = lo + (uint32_t)lane * 4u;
     auto loop = [&](auto sch) {
         constexpr bool SCH = decltype(sch)::value;
         uint32_t c0 = c0s;
-        // P1_AHEAD groups in flight ahead of the one being computed
+        // AHEAD groups in flight ahead of the one being computed
+        constexpr int AHEAD = MV8 ? P1N_AHEAD : P1_AHEAD;
         GrpRaw r0, r1, r2;
         constexpr uint32_t STEP = WAVE * 4u;
         if (c0 < hi) load_grp<false, HB8, MV8>(d, ra, rb, c0, t, SCH && schA, SCH && schB, r0);
-        if (P1_AHEAD > 1 && c0 + STEP < hi) load_grp<false, HB8, MV8>(d, ra, rb, c0 + STEP, t, SCH && schA, SCH && schB, r1);
+        if (AHEAD > 1 && c0 + STEP < hi) load_grp<false, HB8, MV8>(d, ra, rb, c0 + STEP, t, SCH && schA, SCH && schB, r1);
         while (c0 < hi) {
             const uint32_t c1 = c0 + STEP;
-            if (P1_AHEAD > 1) {
+            if (AHEAD > 1) {
                 if (c1 + STEP < hi) load_grp<false, HB8, MV8>(d, ra, rb, c1 + STEP, t, SCH && schA, SCH && schB, r2);
             } else if (c1 < hi) {
                 load_grp<false, HB8, MV8>(d, ra, rb, c1, t, SCH && schA, SCH && schB, r1);
@@ -1432,7 +1460,7 @@ __global__ __launch_bounds__(XB, (KW == 4 ? (FUSE ? P1_WAVES : P1S_WAVES) : 1)) 
             const uint32_t recAB = emit_dir(gAB, LAB, nABc, c0, nAB, mA, mB, alg);
             if (SPEC && ((P1_LINE & 2) || (recBA | recAB))) spec_merge<MV8>(d, ra, rb, c0, recBA, recAB, mA, mB, alg);
             r0 = r1;
-            if (P1_AHEAD > 1) r1 = r2;
+            if (AHEAD > 1) r1 = r2;
             c0 = c1;
         }
     };
@@ -2055,6 +2083,7 @@ __global__ __launch_bounds__(LB) void k_begin_round(Dev d, const uint8_t *up, ui
     if (threadIdx.x == 0 && o - d.col_lo < d.ncol) {
         const uint32_t R = d.self_hb[o - d.col_lo] + 1u;
         d.self_hb[o - d.col_lo] = R;
+        self_repack(d, o - d.col_lo);
         hb_put(d, pix(d, o, o - d.col_lo), R);
     }
     if (!(d.flags & GS_TOMBSTONES) || !d.row[o * 4 + 1]) return;
@@ -2551,6 +2580,7 @@ __global__ __launch_bounds__(LB) void k_owner_writes(Dev d, const gs_write *ops,
     *held = (uint8_t)nw;
     mv_put(d, pj, ver);
     d.self_mv[j] = ver;
+    self_repack(d, j);
     // Cluster.set / set_with_ttl emit on_key_change (server.py:193-215, 238-252); delete and
     // delete_after_ttl mutate the stored VersionedValue in place, so old and new are the same
     // object and nothing is emitted (server.py:199-203, 211-215)
@@ -2575,6 +2605,7 @@ __global__ __launch_bounds__(LB) void k_boot_self(Dev d) {
     const size_t p = pix(d, o, o - d.col_lo);
     hb_put(d, p, 1u);  // Cluster.__init__: inc_heartbeat (server.py:95-96)
     d.self_hb[o - d.col_lo] = 1u;
+    self_repack(d, o - d.col_lo);
     if (!(d.flags & GS_CANONICAL)) {
         d.pos[p] = 0u;
         d.ord[(size_t)o * d.NP] = o;
@@ -3236,6 +3267,7 @@ int check_bound(gs_handle *h) {
     d.ring_slot = (uint32_t *)h->reg[GS_R_RING_SLOT];
     d.vlog = (uint32_t *)h->reg[GS_R_VLOG];
     d.self_mv = (uint32_t *)h->reg[GS_R_SELF_MV];
+    d.self_pk = (uint32_t *)h->reg[GS_R_SELF_PK];
     return GS_OK;
 }
 
@@ -3451,6 +3483,7 @@ int gs_create(const gs_config *cfg, gs_handle **out) {
     b[GS_R_SELF_HB] = NP * 4;
     b[GS_R_MV] = pairs * ((c.flags & GS_MV8) ? 1 : 2);
     b[GS_R_SELF_MV] = NP * 4;
+    b[GS_R_SELF_PK] = (c.flags & GS_MV8) ? NP * 4 : 0;
     b[GS_R_GC] = (c.flags & GS_TOMBSTONES) ? pairs * 4 : 0;  // last_gc_version stays 0 without tombstone GC
     b[GS_R_HELD] = (c.flags & GS_NO_HELD) ? 0 : pairs * KP;
     b[GS_R_FD] = pairs * 4;
@@ -3563,7 +3596,7 @@ int gs_boot(gs_handle *h, const uint16_t *nid_size, const uint8_t *key_len) {
     const int zero[] = {GS_R_HB, GS_R_SELF_HB, GS_R_MV, GS_R_GC, GS_R_HELD, GS_R_FD, GS_R_FD_LAST, GS_R_FD_STATE, GS_R_FD_TOD,
                         GS_R_RING, GS_R_ROW, GS_R_LAST_W, GS_R_HIST, GS_R_HIST_VID,
                         GS_R_STAMP, GS_R_COUNTERS, GS_R_SLICE_BITS, GS_R_PEND, GS_R_PEND_STAMP, GS_R_LATEST,
-                        GS_R_SLOT_STAT, GS_R_VLOG, GS_R_SELF_MV};
+                        GS_R_SLOT_STAT, GS_R_VLOG, GS_R_SELF_MV, GS_R_SELF_PK};
     for (int r : zero)
         if (h->bytes[r]) HIPCHK(h, hipMemsetAsync(h->reg[r], 0, h->bytes[r], s));
     if (h->bytes[GS_R_TS]) HIPCHK(h, hipMemsetAsync(h->reg[GS_R_TS], 0xFF, h->bytes[GS_R_TS], s));

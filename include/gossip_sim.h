@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define GS_API_VERSION 13
+#define GS_API_VERSION 14
 #define GS_MAX_PHASES 64  /* gs_schedule_phases: phases per round */
 #define GS_TICK_US 15625u
 #define GS_NONE 0xFFFFFFFFu
@@ -162,6 +162,8 @@ enum gs_region {
                                         between gs_phase_count and gs_phase_pack */
     GS_R_RING_SLOT,   /* u32 [N]       sampled rings: each observer row's ring slot, GS_NONE = compact windows */
     GS_R_SELF_MV,     /* u32 [NP]      each owner column's own max_version (its latest write's version) */
+    GS_R_SELF_PK,     /* u32 [NP]      GS_MV8: both, packed for pass 1: own heartbeat mod 2^15 | (heartbeat >= 2^15)
+                                        << 15 | own max_version << 16 */
     GS_R_VLOG,        /* u32 [NC][VL]  each owner's writes by version (no GS_TOMBSTONES only: every write is version
                                         max_version + 1), VL = K * (hist_cap - 1) + 1 rounded up to 4: entry v =
                                         DeltaPb bytes of write v's KeyValueUpdatePb field | (version of the
