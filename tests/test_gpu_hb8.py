@@ -121,7 +121,7 @@ def test_mv8_versions_past_2_7_with_an_absence_match_oracle():
     n, rounds, down0, down1 = 8, 170, 100, 120
     ids, keys = synthetic_node_ids(n), key_names(2)
     init = {j: [(0, f"v{j}")] for j in range(n)}
-    cfg = dict(DEFAULT_CFG, mtu=150)
+    cfg = dict(DEFAULT_CFG, mtu=300)
     gpu = GossipSim(ids, keys, cfg, "warm", init, tombstones=False, fd_ring=True, hist_cap=100, hb8=True, mv8=True)
     orc = OracleSim(ids, keys, cfg, "warm", init)
     for r in range(rounds):
