@@ -412,11 +412,11 @@ int gs_emit_delta(gs_handle *h, const gs_wire *w, uint32_t sender, uint32_t rece
 
 /* Measurement (no handle; asynchronous on `stream`): a 16-B-per-lane streaming copy of `bytes`
  * (multiple of 16, 16-B aligned DEVICE buffers) -- the HBM ceiling bench.py reports -- and a
- * read-only stream of `bytes` at `width` = 8 or 16 B per lane (DEVICE u64 *sink keeps the loads), the
+ * read-only stream of `bytes` at `width` = 4, 8 or 16 B per lane (DEVICE u64 *sink keeps the loads), the
  * known byte count that calibrates rocprofv3's FETCH_SIZE for those access widths. */
 int gs_stream_copy(void *dst, const void *src, uint64_t bytes, void *stream);
 int gs_stream_read(const void *src, uint64_t bytes, uint32_t width, uint64_t *sink, void *stream);
-/* a write-only stream of `bytes` at `width` = 8 or 16 B per lane: the known byte count for WRITE_SIZE */
+/* a write-only stream of `bytes` at `width` = 4, 8 or 16 B per lane: the known byte count for WRITE_SIZE */
 int gs_stream_write(void *dst, uint64_t bytes, uint32_t width, void *stream);
 
 /* Per-kernel timing (measurement): with timing on, every launch of the kinds below is bracketed by HIP

@@ -2,8 +2,8 @@
 
 MI355X_MICROARCH.md (HBM section): FETCH_SIZE reports half the bytes of a 16-B-per-lane streaming read;
 other widths are uncalibrated.  This runs, on 1 GiB buffers (well past the 256 MiB Infinity Cache),
-one read-only stream at 8 and at 16 B per lane (gs_stream_read) and one write-only stream at 8 and 16
-B per lane (gs_stream_write), each launched once; tools/pmc_summary.py divides the known bytes by the
+one read-only stream at 4, 8 and 16 B per lane (gs_stream_read) and one write-only stream at 4, 8 and
+16 B per lane (gs_stream_write), each launched once; tools/pmc_summary.py divides the known bytes by the
 counters of these launches to get the factor for each access width.
 """
 
@@ -32,13 +32,13 @@ def main():
     sink = torch.zeros(1, dtype=torch.int64, device=dev)
     stream = torch.cuda.current_stream(dev)
     P = C.c_void_p
-    for w in (8, 16):
+    for w in (4, 8, 16):
         assert L.gs_stream_read(P(src.data_ptr()), CAL_BYTES, w, P(sink.data_ptr()), P(stream.cuda_stream)) == 0
         torch.cuda.synchronize(dev)
-    for w in (8, 16):
+    for w in (4, 8, 16):
         assert L.gs_stream_write(P(dst.data_ptr()), CAL_BYTES, w, P(stream.cuda_stream)) == 0
         torch.cuda.synchronize(dev)
-    print(json.dumps({"cal_bytes": CAL_BYTES, "launches": ["read8", "read16", "write8", "write16"]}))
+    print(json.dumps({"cal_bytes": CAL_BYTES, "launches": ["read4", "read8", "read16", "write4", "write8", "write16"]}))
 
 
 if __name__ == "__main__":

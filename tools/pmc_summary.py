@@ -8,7 +8,9 @@ under the same counters, and this script derives a factor per access width:
     factor = known bytes / (counter KiB x 1024)
 Each kernel's bytes are then (FETCH_SIZE x f_read(width) + WRITE_SIZE x f_write(width)) x 1024 with the
 width of the kernel's dominant streams:
-    k_pass1       8 B per lane (u16 heartbeat / max_version rows, 4 columns per lane; stores likewise)
+    k_pass1       4 B per lane (8-bit heartbeat / max_version rows, GS_HB8 + GS_MV8, 4 columns per lane;
+                  stores likewise; the 16-B owner-value loads are L2 hits)
+    k_lite        8 B (candidate records; the rest are gathers)
     k_pack_slice  8 B (candidate records; the rest are gathers, which no stream calibrates)
     k_settle      8 B (likewise: candidate records, owner-table gathers)
     k_liveness    16 B per lane (two 16-B window loads + one 16-B state load per 4 columns)
@@ -31,17 +33,17 @@ from collections import defaultdict
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
-KERNELS = ("k_pass1", "k_pack_slice", "k_settle", "k_liveness", "k_exchange", "k_count", "k_begin_round",
+KERNELS = ("k_pass1", "k_pack_slice", "k_settle", "k_lite", "k_liveness", "k_exchange", "k_count", "k_begin_round",
            "k_owner_writes", "k_reset_sched", "k_warm", "k_boot_self", "k_phi_row")
-WIDTH = {"k_pass1": 8, "k_pack_slice": 8, "k_settle": 8, "k_liveness": 16, "k_exchange": 8, "k_count": 8}
-KIND = {"k_pass1": "pass1", "k_pack_slice": "pack", "k_settle": "pack", "k_liveness": "liveness", "k_exchange": "pass1",
-        "k_count": "count"}
+WIDTH = {"k_pass1": 4, "k_pack_slice": 8, "k_settle": 8, "k_lite": 8, "k_liveness": 16, "k_exchange": 8, "k_count": 8}
+KIND = {"k_pass1": "pass1", "k_pack_slice": "pack", "k_settle": "count", "k_lite": "lite", "k_liveness": "liveness",
+        "k_exchange": "pass1", "k_count": "count"}
 CAL_BYTES = 1 << 30
 
 
 def short(name: str) -> str:
     if "k_read<" in name or "k_write<" in name:
-        w = 8 if "2u>" in name else 16
+        w = 8 if "2u>" in name else 16 if "4u>" in name else 4
         return ("read" if "k_read<" in name else "write") + str(w)
     for k in KERNELS:
         if k in name:
@@ -121,7 +123,7 @@ def calibration(root: str) -> dict:
     f, _ = counters(root, "cal_fetch", "FETCH_SIZE")
     w, _ = counters(root, "cal_write", "WRITE_SIZE")
     cal = {}
-    for width in (8, 16):
+    for width in (4, 8, 16):
         r, wr = f.get(f"read{width}"), w.get(f"write{width}")
         cal[f"read{width}"] = CAL_BYTES / (r * 1024) if r else None
         cal[f"write{width}"] = CAL_BYTES / (wr * 1024) if wr else None
