@@ -2498,21 +2498,30 @@ __global__ __launch_bounds__(LB) void k_hb_lag(Dev d, uint32_t chunks) {
     uint32_t bad = 0;
     if (j0 < d.ncol) {
         const size_t p0 = pix(d, o, j0);
-        const uint4 raw = d.hb8 ? *reinterpret_cast<const uint4 *>(reinterpret_cast<const uint8_t *>(d.hb) + p0)
-                                : *reinterpret_cast<const uint4 *>(d.hb + p0);
-        const uint32_t w[4] = {raw.x, raw.y, raw.z, raw.w};
-        for (uint32_t i = 0; i < per && j0 + i < d.ncol; i++) {
-            const uint32_t j = j0 + i;
-            if (genm && d.pos[p0 + i] == NONE) continue;
-            const uint32_t s = d.hb8 ? (w[i >> 2] >> (8 * (i & 3))) & 0xFFu : (w[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
-            const uint32_t lag = d.hb8 ? (d.self_hb[j] - s) & 0xFFu : (d.self_hb[j] - s) & 0xFFFFu;
-            if (lag >= (d.hb8 ? 0x80u : 0x8000u)) bad++;
-        }
-        if (d.mv8) {  // GS_MV8: max_version views lag their owner by < 2^6 at every sweep
-            const uint8_t *m8 = reinterpret_cast<const uint8_t *>(d.mv);
-            for (uint32_t i = 0; i < per && j0 + i < d.ncol; i++) {
-                const uint32_t s = m8[p0 + i];
-                if (((d.self_mv[j0 + i] - (s & 0x7Fu)) & 0x7Fu) >= 0x40u) bad++;
+        // one 16-byte load per region: the thread's heartbeat views (and GS_MV8 max_version views)
+        const uint4 hr = d.hb8 ? *reinterpret_cast<const uint4 *>(reinterpret_cast<const uint8_t *>(d.hb) + p0)
+                               : *reinterpret_cast<const uint4 *>(d.hb + p0);
+        const uint4 mr = d.mv8 ? *reinterpret_cast<const uint4 *>(reinterpret_cast<const uint8_t *>(d.mv) + p0)
+                               : make_uint4(0u, 0u, 0u, 0u);
+        const uint32_t hw[4] = {hr.x, hr.y, hr.z, hr.w}, mw[4] = {mr.x, mr.y, mr.z, mr.w};
+        for (uint32_t q = 0; q < per / 4u && j0 + 4u * q < d.ncol; q++) {
+            const uint32_t jq = j0 + 4u * q;
+            // the owners' own values, 4 columns per 16-byte load (L2): GS_MV8 packed (R mod 2^8 and M)
+            const uint4 ow = *reinterpret_cast<const uint4 *>((d.mv8 ? d.self_pk : d.self_hb) + jq);
+            const uint32_t own[4] = {ow.x, ow.y, ow.z, ow.w};
+            uint32_t ps[4] = {0u, 0u, 0u, 0u};
+            if (genm) ld4(d.pos + p0 + 4u * q, ps);
+#pragma unroll
+            for (uint32_t i = 0; i < 4; i++) {
+                if (jq + i >= d.ncol || (genm && ps[i] == NONE)) continue;
+                const uint32_t k = 4u * q + i;  // view index within the thread's loads
+                const uint32_t s = d.hb8 ? (hw[k >> 2] >> (8 * (k & 3))) & 0xFFu : (hw[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
+                const uint32_t lag = d.hb8 ? (own[i] - s) & 0xFFu : (own[i] - s) & 0xFFFFu;
+                if (lag >= (d.hb8 ? 0x80u : 0x8000u)) bad++;
+                if (d.mv8) {  // GS_MV8: max_version views lag their owner by < 2^6 at every sweep
+                    const uint32_t sm = (mw[k >> 2] >> (8 * (k & 3))) & 0x7Fu;
+                    if ((((own[i] >> 16) - sm) & 0x7Fu) >= 0x40u) bad++;
+                }
             }
         }
     }

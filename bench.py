@@ -487,6 +487,11 @@ def main():
                     help="version-only layout (GS_NO_HELD, config 4): needs an mtu no delta reaches")
     args = ap.parse_args()
 
+    if args.peer_select:
+        # every round scheduled by the reference's selection: ~16 phases per round and uneven responder
+        # load let heartbeat views lag their owners past the 8-bit bound (r3l: err_hb_lag), so such runs
+        # use the 16-bit views (the headline's permutation schedule peaks at a lag of 49: tools/hb_lag.py)
+        args.wide_views = True
     world = int(os.environ.get("WORLD_SIZE", "0"))
     if world == 0:
         if args.gpus > 1:  # plain `python bench.py --gpus N`: become the launcher of N ranks
@@ -600,6 +605,12 @@ def main():
     ps = None
     if ps_steps:
         ps = peer_select_rounds(sims, plans, R0 + args.steps + 1, ps_steps, args, n, dev)
+        # the state after the selected rounds: a lag sweep now, and every device check counter (8-bit views
+        # are exact only while every lag stays below the sweep bound: reported, not assumed)
+        sims[0].check_heartbeat_lag()
+        errs = {k: v for k, v in sims[0].counters().items() if k.startswith("err_") and v}
+        ps["device_errors"] = errs
+        ps["exact"] = not errs
     horizon = sims[0].horizon()
     c4 = None
     if args.config4_steps and (world == C4_GPUS or args.config4):

@@ -167,8 +167,11 @@ def test_mv8_lag_sweep_flags_views_at_2_6():
     gpu.begin_round(round_tick(0), up_dev)
     gpu.liveness(liveness_tick(0, 0), up_dev)
     M = gpu.region("SELF_MV", torch.int32, (gpu.np_,))
+    PK = gpu.region("SELF_PK", torch.int32, (gpu.np_,))  # pass 1's and the sweep's packed copy
+    R3 = int(gpu.region("SELF_HB", torch.int32, (gpu.np_,))[3].item())
     mv = gpu.region("MV", torch.uint8, (n, gpu.np_))
     M[3] = 1000
+    PK[3] = (R3 & 0x7FFF) | (1000 << 16)
     for o in range(n):
         mv[o, 3] = (1000 - 5) & 0x7F
     mv[3, 3] = 1000 & 0x7F
