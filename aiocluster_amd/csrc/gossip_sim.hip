@@ -2930,6 +2930,75 @@ __global__ __launch_bounds__(LB) void k_sel_count(Dev d, const uint8_t *up, uint
     }
 }
 
+// The seed probe (server.py:700-717) of row o and the resolved picks out: thread 0 of the resolve kernels.
+__device__ void sel_seed_probe(const Dev &d, uint32_t o, uint32_t L, uint32_t D, uint32_t F, uint64_t seed,
+                               uint32_t round, const int32_t *seeds, uint32_t n_seeds, const uint32_t *s_hit,
+                               int32_t *oo) {
+    bool has_seed = false;
+    uint32_t S = 0;
+    for (uint32_t q = 0; q < n_seeds; q++) {
+        if ((uint32_t)seeds[q] == o) continue;
+        S++;
+        for (uint32_t i = 0; i < F; i++) has_seed |= s_hit[i] == (uint32_t)seeds[q];
+    }
+    uint32_t pick = NONE;
+    if (S && (!has_seed || L < S)) {
+        uint32_t c[4];
+        sel_rand(seed, round, o, SEL_SEED, c);
+        const double ps = (L + D) == 0u ? 1.0 : (double)S / (double)(L + D);
+        if (L == 0u || unit53(c[0], c[1]) <= ps) {
+            uint32_t k = below(c[2], S);
+            for (uint32_t q = 0; q < n_seeds; q++) {
+                if ((uint32_t)seeds[q] == o) continue;
+                if (k-- == 0) { pick = (uint32_t)seeds[q]; break; }
+            }
+        }
+    }
+    for (uint32_t i = 0; i < F + 1; i++) oo[i] = s_hit[i] == NONE ? -1 : (int32_t)(d.col_lo + s_hit[i]);
+    oo[F + 1] = pick == NONE ? -1 : (int32_t)pick;
+}
+
+// Canonical layout (every observer knows every owner, no dict positions): the same counts from 16 state
+// bytes per thread and load -- live = membership 1, dead = membership 2 (bit 1), known = every column but
+// the observer's own (whose state stays unknown: liveness skips it).
+__device__ __forceinline__ uint32_t memb_live4(uint32_t w) {  // bytes whose membership bits are 01
+    const uint32_t m = w & 0x03030303u;
+    return m & ~(m >> 1) & 0x01010101u;
+}
+__device__ __forceinline__ uint32_t memb_dead4(uint32_t w) { return (w >> 1) & 0x01010101u; }
+__global__ __launch_bounds__(LB) void k_sel_count16(Dev d, const uint8_t *up, uint32_t *scnt) {
+    const uint32_t o = blockIdx.x;
+    if (!up[o]) return;
+    uint32_t L = 0, D = 0;
+    const uint8_t *row = d.fd_state + (size_t)o * d.NP;
+    for (uint32_t j0 = threadIdx.x * 16u; j0 < d.ncol; j0 += LB * 16u) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(row + j0);  // NP is a multiple of 64: in the row
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const uint32_t jq = j0 + 4u * q;
+            uint32_t keep = 0x01010101u;  // columns < ncol (the padding's state bytes are never written: 0)
+            if (jq + 4u > d.ncol) keep = jq >= d.ncol ? 0u : (0x01010101u >> (8u * (jq + 4u - d.ncol)));
+            const uint32_t js = o - d.col_lo - jq;  // the observer's own column is not a peer
+            if (js < 4u) keep &= ~(0x01u << (8u * js));
+            L += (uint32_t)__popc(memb_live4(w[q]) & keep);
+            D += (uint32_t)__popc(memb_dead4(w[q]) & keep);
+        }
+    }
+    __shared__ uint32_t s2[2][LB / WAVE];
+    const uint32_t wv = threadIdx.x >> 6;
+    const unsigned long long l = wave_sum(L), dd = wave_sum(D);
+    if ((threadIdx.x & 63) == 0) { s2[0][wv] = (uint32_t)l; s2[1][wv] = (uint32_t)dd; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t a = 0, b = 0;
+        for (int i = 0; i < LB / WAVE; i++) { a += s2[0][i]; b += s2[1][i]; }
+        scnt[o * 4 + 0] = a;
+        scnt[o * 4 + 1] = b;
+        scnt[o * 4 + 2] = d.ncol - (o - d.col_lo < d.ncol ? 1u : 0u);  // known: every column but o's own
+    }
+}
+
 // Floyd's sample of k distinct ranks of [0, n) and the dead probe, by rank; targets resolved next.
 // sel[o][0..F) = live (or peer) ranks, sel[o][F] = dead rank, NONE where absent.
 __global__ __launch_bounds__(LB) void k_sel_pick(Dev d, const uint8_t *up, const uint32_t *scnt, uint32_t F,
@@ -2955,6 +3024,79 @@ __global__ __launch_bounds__(LB) void k_sel_pick(Dev d, const uint8_t *up, const
         const double pd = (double)D / (double)(L + 1u);
         if (pd > unit53(c[0], c[1])) so[F] = below(c[2], D);
     }
+}
+
+// k-th set bit (k < popc(m)) of a 16-bit mask
+__device__ __forceinline__ uint32_t nth_bit16(uint32_t m, uint32_t k) {
+    for (uint32_t i = 0; i < k; i++) m &= m - 1u;
+    return (uint32_t)__builtin_ctz(m);
+}
+// Canonical layout: k_sel_resolve with 16 columns per thread and step (one 16-byte state load); the pool
+// (live, or every known node when none is live) and dead masks are ranked by a block scan of their
+// popcounts, so a row takes ncol / 4096 steps instead of ncol / 256.
+__global__ __launch_bounds__(LB) void k_sel_resolve16(Dev d, const uint8_t *up, const uint32_t *scnt, uint32_t F,
+                                                      uint64_t seed, uint32_t round, const int32_t *seeds,
+                                                      uint32_t n_seeds, const uint32_t *sel, int32_t *out) {
+    __shared__ uint32_t s_w[LB / WAVE][2];
+    __shared__ uint32_t s_rank[10], s_hit[10];
+    const uint32_t o = blockIdx.x;
+    int32_t *oo = out + (size_t)o * (F + 2);
+    if (!up[o]) {
+        for (uint32_t i = threadIdx.x; i < F + 2; i += LB) oo[i] = -1;
+        return;
+    }
+    const uint32_t L = scnt[o * 4 + 0];
+    const bool from_live = L != 0;
+    if (threadIdx.x < F + 1) {
+        s_rank[threadIdx.x] = sel[(size_t)o * (F + 2) + threadIdx.x];
+        s_hit[threadIdx.x] = NONE;
+    }
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    const uint8_t *row = d.fd_state + (size_t)o * d.NP;
+    uint32_t base_pool = 0, base_dead = 0;
+    for (uint32_t b0 = 0; b0 < d.ncol; b0 += LB * 16u) {
+        const uint32_t j0 = b0 + threadIdx.x * 16u;
+        uint32_t mp = 0, md = 0;  // bit i: column j0 + i is in the pool / dead
+        if (j0 < d.ncol) {
+            const uint4 v = *reinterpret_cast<const uint4 *>(row + j0);
+            const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+#pragma unroll
+                for (int b = 0; b < 4; b++) {
+                    const uint32_t j = j0 + 4u * q + b;
+                    const uint32_t st = (wd[q] >> (8 * b)) & FD_MEMB;
+                    const bool valid = j < d.ncol && d.col_lo + j != o;
+                    const bool live = valid && st == 1u, dead = valid && st >= 2u;
+                    mp |= (uint32_t)(from_live ? live : valid) << (4 * q + b);
+                    md |= (uint32_t)dead << (4 * q + b);
+                }
+            }
+        }
+        const uint32_t cp = (uint32_t)__popc(mp), cd = (uint32_t)__popc(md);
+        const uint32_t ip = wave_incl_scan(cp), id = wave_incl_scan(cd);
+        if (lane == 63) { s_w[w][0] = ip; s_w[w][1] = id; }
+        __syncthreads();
+        uint32_t op = base_pool + ip - cp, od = base_dead + id - cd, tp = 0, td = 0;
+        for (uint32_t i = 0; i < LB / WAVE; i++) {
+            if (i < w) { op += s_w[i][0]; od += s_w[i][1]; }
+            tp += s_w[i][0];
+            td += s_w[i][1];
+        }
+        for (uint32_t i = 0; i < F; i++) {
+            const uint32_t r = s_rank[i];
+            if (r != NONE && r >= op && r < op + cp) s_hit[i] = j0 + nth_bit16(mp, r - op);
+        }
+        {
+            const uint32_t r = s_rank[F];
+            if (r != NONE && r >= od && r < od + cd) s_hit[F] = j0 + nth_bit16(md, r - od);
+        }
+        base_pool += tp;
+        base_dead += td;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) sel_seed_probe(d, o, L, scnt[o * 4 + 1], F, seed, round, seeds, n_seeds, s_hit, oo);
 }
 
 // Resolve ranks to node ids in column order (one workgroup per row), then the seed probe.
@@ -3011,31 +3153,7 @@ __global__ __launch_bounds__(LB) void k_sel_resolve(Dev d, const uint8_t *up, co
         base_dead += td;
         __syncthreads();
     }
-    if (threadIdx.x == 0) {
-        bool has_seed = false;
-        uint32_t S = 0;
-        for (uint32_t q = 0; q < n_seeds; q++) {
-            if ((uint32_t)seeds[q] == o) continue;
-            S++;
-            for (uint32_t i = 0; i < F; i++) has_seed |= s_hit[i] == (uint32_t)seeds[q];
-        }
-        const uint32_t D = scnt[o * 4 + 1];
-        uint32_t pick = NONE;
-        if (S && (!has_seed || L < S)) {
-            uint32_t c[4];
-            sel_rand(seed, round, o, SEL_SEED, c);
-            const double ps = (L + D) == 0u ? 1.0 : (double)S / (double)(L + D);
-            if (L == 0u || unit53(c[0], c[1]) <= ps) {
-                uint32_t k = below(c[2], S);
-                for (uint32_t q = 0; q < n_seeds; q++) {
-                    if ((uint32_t)seeds[q] == o) continue;
-                    if (k-- == 0) { pick = (uint32_t)seeds[q]; break; }
-                }
-            }
-        }
-        for (uint32_t i = 0; i < F + 1; i++) oo[i] = s_hit[i] == NONE ? -1 : (int32_t)(d.col_lo + s_hit[i]);
-        oo[F + 1] = pick == NONE ? -1 : (int32_t)pick;
-    }
+    if (threadIdx.x == 0) sel_seed_probe(d, o, L, scnt[o * 4 + 1], F, seed, round, seeds, n_seeds, s_hit, oo);
 }
 
 // Conflict-free phases for the round's exchanges e = o * (F + 2) + slot (initiator o, responder
@@ -4254,11 +4372,14 @@ int gs_select_peers(gs_handle *h, const uint8_t *up, uint32_t fanout, const int3
     if (h->G > 1) return fail(h, GS_E_UNSUPPORTED, "gs_select_peers needs the whole matrix (one slice)");
     uint32_t *scnt = (uint32_t *)scratch;
     uint32_t *sel = scnt + (size_t)h->N * 4;
-    k_sel_count<<<h->N, LB, 0, h->stream>>>(h->d, up, scnt);
+    const bool canon = (h->cfg.flags & GS_CANONICAL) != 0;
+    if (canon) k_sel_count16<<<h->N, LB, 0, h->stream>>>(h->d, up, scnt);
+    else k_sel_count<<<h->N, LB, 0, h->stream>>>(h->d, up, scnt);
     HIPCHK(h, hipGetLastError());
     k_sel_pick<<<(h->N + LB - 1) / LB, LB, 0, h->stream>>>(h->d, up, scnt, fanout, seed, round, sel);
     HIPCHK(h, hipGetLastError());
-    k_sel_resolve<<<h->N, LB, 0, h->stream>>>(h->d, up, scnt, fanout, seed, round, seeds, n_seeds, sel, targets);
+    if (canon) k_sel_resolve16<<<h->N, LB, 0, h->stream>>>(h->d, up, scnt, fanout, seed, round, seeds, n_seeds, sel, targets);
+    else k_sel_resolve<<<h->N, LB, 0, h->stream>>>(h->d, up, scnt, fanout, seed, round, seeds, n_seeds, sel, targets);
     HIPCHK(h, hipGetLastError());
     return GS_OK;
 }
