@@ -87,6 +87,7 @@ struct Dev {
     uint32_t ablate;  // profiling only (env GS_ABLATE): 1 = skip packing, 2 = skip pass-1 stores; results invalid
     double phi_thr, prior5;
     double prior5t;  // prior5 in ticks (x 64): the liveness sweep's division-free phi test
+    float phi_thr_f, prior5t_f;  // the same in binary32: the sweep's first, full-rate test (2^-20 margin)
     uint16_t *hb;       // heartbeat mod 2^16 (hb_dec: exact while a view lags its owner by < 2^16)
     uint32_t *self_hb;  // [NP] each owner column's own heartbeat, full width
     uint32_t *gc;
@@ -2147,6 +2148,9 @@ template <int RING>
 // the per-workgroup plane staging, stamp check and counter atomics are paid once per `per` chunks).
 // decide = false: only replay the pending reports into the windows, for every row (a round with phases
 // more than 16 ticks after its plane base: the planes are emptied mid-round)
+#ifndef LIVE_F32
+#define LIVE_F32 1  // the phi decision's first test in binary32 (A/B: 0 = binary64 with a 2^-30 margin)
+#endif
 #ifndef LIVE_WAVES
 #define LIVE_WAVES 8  // waves per SIMD k_liveness is compiled for (<= 64 VGPRs)
 #endif
@@ -2250,16 +2254,26 @@ __global__ __launch_bounds__(LB, LIVE_WAVES) void k_liveness(Dev d, const uint8_
                 bool alive = false;
                 if (has && len) {
                     // phi <= threshold (failure_detector.py:43-53, 97-98) decided without the two binary64
-                    // divisions when it is clear by a margin (2^-30 relative, far above their rounding):
-                    // phi ~ elapsed (len + 5) / (sum + 5 prior) in ticks; the exact expression otherwise
+                    // divisions when it is clear by a margin: phi ~ elapsed (len + 5) / (sum + 5 prior) in
+                    // ticks.  First in binary32 (full rate: elapsed < 2^24 ticks, len + 5 and sum < 2^24 are
+                    // exact, the three roundings and the two constants' add < 2^-21 relative) with a 2^-20
+                    // margin, then in binary64 with 2^-30 (far above its rounding), the exact expression
+                    // otherwise
+#if LIVE_F32
+                    const float lf = (float)(t - f.last) * (float)(len + 5u);
+                    const float rf = d.phi_thr_f * ((float)f.sum + d.prior5t_f);
+                    if (lf < rf * (1.0f - 0x1p-20f)) {
+                        alive = true;
+                    } else if (!(lf > rf * (1.0f + 0x1p-20f))) {  // too close: the exact expression
+#else
                     const double lhs = (double)(t - f.last) * (double)(len + 5u);  // exact: < 2^43
                     const double rhs = d.phi_thr * ((double)f.sum + d.prior5t);
                     if (lhs < rhs * (1.0 - 0x1p-30)) {
                         alive = true;
                     } else if (!(lhs > rhs * (1.0 + 0x1p-30))) {
+#endif
                         const double mean = ((double)f.sum * TICK_S + d.prior5) / ((double)len + 5.0);
-                        const double phi = ((double)(t - f.last) * TICK_S) / mean;
-                        alive = phi <= d.phi_thr;
+                        alive = ((double)(t - f.last) * TICK_S) / mean <= d.phi_thr;
                     }
                 }
                 const uint32_t mb = st & FD_MEMB;
@@ -3681,6 +3695,8 @@ int gs_create(const gs_config *cfg, gs_handle **out) {
     d.phi_thr = c.phi_threshold;
     d.prior5 = c.prior_weighted;
     d.prior5t = c.prior_weighted * 64.0;
+    d.phi_thr_f = (float)c.phi_threshold;
+    d.prior5t_f = (float)d.prior5t;
     *out = h;
     return GS_OK;
 }

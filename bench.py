@@ -612,6 +612,7 @@ def main():
         ps["device_errors"] = errs
         ps["exact"] = not errs
     horizon = sims[0].horizon()
+    sliced = group is not None  # (the config-4 leg below releases the headline's handles first)
     c4 = None
     if args.config4_steps and (world == C4_GPUS or args.config4):
         for s_ in sims:
@@ -631,7 +632,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed_max / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "strong" if group is not None else "weak",
+            "scaling": "strong" if sliced else "weak",
             "vs_baseline": None,
             # the state is integer: heartbeat and max_version views stored as u8 (GS_HB8 + GS_MV8; exact
             # decode against the owners' own values, guarded: DESIGN.md §3), computed in u32; phi in binary64
@@ -646,7 +647,7 @@ def main():
                 "parallelism": (f"owner-column slices x{world} (RCCL all-gather of slice totals"
                                 + (", library-driven: gs_comm_init)" if args.native_comm else ")") if world > 1
                                 else f"slice 0 of {args.rehearse_slices} (rehearsal)" if args.rehearse_slices > 1
-                                else f"owner-column slices x{args.slices} in one process" if group is not None
+                                else f"owner-column slices x{args.slices} in one process" if sliced
                                 else "1 GPU"),
                 **({"unscheduled_exchanges": unscheduled} if sel is not None else {}),
             },
