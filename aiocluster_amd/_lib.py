@@ -82,7 +82,7 @@ EXPORTS = [
     "gs_latest_tick", "gs_flush_reports", "gs_set_ring_rows",
 ]
 
-API_VERSION = 14
+API_VERSION = 15
 MAX_PHASES = 64  # GS_MAX_PHASES
 
 
@@ -196,7 +196,7 @@ def load():
         "gs_reset_counters": (C.c_int, [P]),
         "gs_set_timing": (C.c_int, [P, C.c_int]),
         "gs_phase_overflow": (C.c_int, [P, u32, P, P, P, P, C.POINTER(u32)]),
-        "gs_phase_chain": (C.c_int, [P, P, P, u32, u32, u32, P, u32, P, P, P]),
+        "gs_phase_chain": (C.c_int, [P, P, P, u32, u32, u32, P, u32, P, P, P, P]),
         "gs_comm_id": (C.c_int, [P]),
         "gs_comm_init": (C.c_int, [P, P, u32, u32]),
         "gs_run_phase_group": (C.c_int, [P, u32, P, P, u32, u32]),

@@ -564,7 +564,21 @@ struct PackState {
     uint32_t S;  // DeltaPb bytes committed so far (wave-uniform)
     bool tail;   // the budget was exceeded once: first-fit continuation mode
     bool stop;   // the delta is complete (>= mtu, or less than the smallest NodeDelta left)
+    uint32_t m1 = NONE;  // count mode: the smallest single-kv NodeDelta (min1) among the candidates seen
 };
+__device__ inline uint32_t wave_min(uint32_t x) {
+#pragma unroll
+    for (int dd = 32; dd >= 1; dd >>= 1) {
+        const uint32_t y = __shfl_xor(x, dd, WAVE);
+        x = y < x ? y : x;
+    }
+    return x;
+}
+// a slice total (gs_phase_count): DeltaPb bytes | min1 << 40 (GS_TOT_MIN1_NONE: no candidate); the
+// chain steps skip a slice whose min1 cannot fit (k_chain_step)
+__device__ inline uint64_t tot_word(uint64_t bytes, uint32_t m1) {
+    return bytes | ((uint64_t)(m1 < GS_TOT_MIN1_NONE ? m1 : GS_TOT_MIN1_NONE) << 40);
+}
 
 // One group: lane i holds the i-th candidate of the group in sender order (cand = false: none).
 // COUNT: only sum the DeltaPb bytes of every candidate (owner-sharded runs: the slice total).
@@ -720,6 +734,7 @@ __device__ __forceinline__ void pack_dir(const Dev &d, uint32_t s, uint32_t r, c
     bool tail, stop;
     pack_begin(d, COUNT, pst, S, tail, stop);
     uint32_t nr = 0;    // REC: NodeDeltas recorded so far (wave-uniform)
+    uint32_t m1 = pst.m1;  // COUNT: the smallest min1 so far
     uint32_t pend = 0;  // wave-uniform: candidates carried from earlier windows (< 64), in rv
     uint32_t rv = 0;    // lane i < pend: the i-th carried candidate's position
     // canonical: the next window's bitmap word is loaded one window ahead (the bitmap is in HBM on the
@@ -789,6 +804,7 @@ __device__ __forceinline__ void pack_dir(const Dev &d, uint32_t s, uint32_t r, c
                 eval_cand<KW, GENM>(d, s, r, ds, j, t, c, ck, st.alg);
                 st.cand++;
             }
+            if (COUNT) m1 = min(m1, wave_min(cand && c.emsg ? c.min1 : NONE));
             pack_group<KW, COUNT, REC>(d, s, r, t, c, cand, S, tail, stop, st, tomb, rec, nr);
         }
         if (!last) {  // carry the rest (< 64): entry lim + i to lane i
@@ -803,6 +819,7 @@ __device__ __forceinline__ void pack_dir(const Dev &d, uint32_t s, uint32_t r, c
     pst.S = S;
     pst.tail = tail;
     pst.stop = stop;
+    pst.m1 = m1;
     if (REC) {
         if (lane == 0) *nrec = nr;
         return;
@@ -824,7 +841,7 @@ __device__ __forceinline__ void pack_list(const Dev &d, uint32_t s, uint32_t r, 
     bool tail, stop;
     pack_begin(d, COUNT, pst, S, tail, stop);
     const bool specd = !COUNT && d.spec;
-    uint32_t nr = 0;
+    uint32_t nr = 0, m1 = pst.m1;
     uint2 nxt = make_uint2(0u, 0u);
     if ((uint32_t)lane < n) nxt = L[lane];
     for (uint32_t c0 = 0; c0 < n && (specd || !stop); c0 += WAVE) {
@@ -851,11 +868,13 @@ __device__ __forceinline__ void pack_list(const Dev &d, uint32_t s, uint32_t r, 
             eval_cand<KW, false, true>(d, s, r, ds, cr.x, t, c, ck, st.alg, cr.y);
             st.cand++;
         }
+        if (COUNT) m1 = min(m1, wave_min(cand && c.emsg ? c.min1 : NONE));
         pack_group<KW, COUNT, false>(d, s, r, t, c, cand, S, tail, stop, st, tomb, nullptr, nr, specd);
     }
     pst.S = S;
     pst.tail = tail;
     pst.stop = stop;
+    pst.m1 = m1;
     if (!COUNT && lane == 0) shard_add(d, C_DBYTES, S - S0);
 }
 
@@ -876,13 +895,13 @@ constexpr int LITE_B = 4;
 constexpr uint32_t LITE_FULL = 1u, LITE_DONE = 2u;
 template <bool APPLY = true>
 __device__ __forceinline__ bool pack_lite(const Dev &d, uint32_t rcv, size_t slot, uint32_t S0, WStats &st,
-                                          uint32_t &Tout) {
+                                          uint32_t &Tout, uint32_t *m1out = nullptr) {
     const int lane = lane_id();
     const uint32_t n0 = d.cand_n[slot * 2], n1 = d.cand_n[slot * 2 + 1];
     if (n0 > GS_CAND_CAP || n1 > GS_CAND_CAP) return false;  // a half continues in its bitmap
     const uint2 *L0 = d.cand + slot * 2 * GS_CAND_CAP, *L1 = L0 + GS_CAND_CAP;
     const uint32_t nt = n0 + n1;
-    uint32_t sum = 0, kvs = 0, alg = 0;
+    uint32_t sum = 0, kvs = 0, alg = 0, m1 = NONE;
     bool bad = false;
     for (uint32_t c0 = 0; c0 < nt; c0 += WAVE * LITE_B) {
         uint2 rc[LITE_B];
@@ -907,12 +926,15 @@ __device__ __forceinline__ bool pack_lite(const Dev &d, uint32_t rcv, size_t slo
             if (rc[u].x == NONE || !ev[u]) continue;
             const uint32_t j = rc[u].x, ms = rc[u].y & 0xFFFFu, mr = rc[u].y >> 16;
             uint32_t kv = ev[u] & 0xFFFFu, nk = 1;  // write ms is the latest <= ms of its key
-            for (uint32_t v = mr + 1u; v < ms; v++) {  // lag > 1 (rare): the other writes of (mr, ms)
+            uint32_t kv1 = kv;  // the lowest version's kv (min1: the NodeDelta with only that kv)
+            for (uint32_t v = ms - 1u; v > mr; v--) {  // lag > 1 (rare): the other writes of (mr, ms)
                 const uint32_t e = d.vlog[(size_t)j * d.VL + v];
-                if ((e >> 16) > ms) { kv += e & 0xFFFFu; nk++; }
+                if ((e >> 16) > ms) { kv += e & 0xFFFFu; nk++; kv1 = e & 0xFFFFu; }
                 alg += 4;
             }
-            sum += msgf(msgf(ns[u]) + ufield(mr) + 1u + vlen(ms) + kv);
+            const uint32_t base = msgf(ns[u]) + ufield(mr) + 1u + vlen(ms);
+            sum += msgf(base + kv);
+            m1 = min(m1, msgf(base + kv1));
             kvs += nk;
             alg += 8 + 4 + 2;
         }
@@ -922,6 +944,7 @@ __device__ __forceinline__ bool pack_lite(const Dev &d, uint32_t rcv, size_t slo
     if (!APPLY) {
         st.alg += alg;
         Tout = T;
+        if (m1out) *m1out = wave_min(m1);
         return true;
     }
     if ((uint64_t)S0 + T > d.mtu) return false;
@@ -1595,7 +1618,7 @@ __global__ __launch_bounds__(XB, (KW == 4 ? XB_WAVES : 1)) void k_exchange(Dev d
         bool ctomb = false;
         PackState pst{0u, false, false};
         pack_dir<KW, false, true>(d, snd, rcv, ds, nullptr, d.ncol, w0 ? bBA : bAB, wbuf, t, cs, ctomb, pst);
-        if (lane == 0) io.tot[(size_t)e * 2 + wid] = pst.S;
+        if (lane == 0) io.tot[(size_t)e * 2 + wid] = tot_word(pst.S, pst.m1);
         const unsigned long long s_alg = wave_sum(alg), s_rep = wave_sum(reports), s_hbw = wave_sum(hbw);
         if (lane == 0) {
             shard_add(d, C_ALG, s_alg);
@@ -1697,7 +1720,7 @@ __global__ __launch_bounds__(XB, (KW == 4 ? PK_WAVES : 1)) void k_pack_slice(Dev
     PackState pst;
     if (io.step == 0) {
         uint64_t P = 0;
-        for (uint32_t g = 0; g < d.shard; g++) P += io.tot_all[(size_t)g * n * 2 + slot];
+        for (uint32_t g = 0; g < d.shard; g++) P += GS_TOT_BYTES(io.tot_all[(size_t)g * n * 2 + slot]);
         if (P > d.mtu) {
             if (lane == 0) io.chain[slot] = CHAIN_PENDING;
             return;
@@ -1749,7 +1772,7 @@ __global__ __launch_bounds__(OVB) void k_ov_count(const uint64_t *tot_all, uint3
     const uint32_t sl = blockIdx.x * OVB + threadIdx.x;
     uint64_t sum = 0;
     if (sl < slots)
-        for (uint32_t g = 0; g < G; g++) sum += tot_all[(size_t)g * slots + sl];
+        for (uint32_t g = 0; g < G; g++) sum += GS_TOT_BYTES(tot_all[(size_t)g * slots + sl]);
     const int c = __syncthreads_count(sl < slots && sum > mtu);
     if (threadIdx.x == 0) blkcnt[blockIdx.x] = (uint32_t)c;
 }
@@ -1771,7 +1794,7 @@ __global__ __launch_bounds__(OVB) void k_ov_write(const uint64_t *tot_all, uint3
     const uint32_t sl = blockIdx.x * OVB + threadIdx.x;
     uint64_t sum = 0;
     if (sl < slots)
-        for (uint32_t g = 0; g < G; g++) sum += tot_all[(size_t)g * slots + sl];
+        for (uint32_t g = 0; g < G; g++) sum += GS_TOT_BYTES(tot_all[(size_t)g * slots + sl]);
     const bool f = sl < slots && sum > mtu;
     const unsigned long long m = __ballot(f);
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
@@ -1783,6 +1806,33 @@ __global__ __launch_bounds__(OVB) void k_ov_write(const uint64_t *tot_all, uint3
         const uint32_t i = pre + (uint32_t)__popcll(m & ((1ull << l) - 1ull));
         list[i] = sl;
         chainc[i] = chain[sl];
+    }
+}
+
+// the pending counts of all G slices (entry count of each gathered chainc) summed into *out
+__global__ __launch_bounds__(WAVE) void k_sum_pending(const uint64_t *chain_all, uint32_t G, uint32_t count,
+                                                      uint64_t *out) {
+    unsigned long long s = 0;
+    for (uint32_t g = threadIdx.x; g < G; g += WAVE) s += chain_all[(size_t)g * (count + 1u) + count];
+    s = wave_sum(s);
+    if (threadIdx.x == 0) *out = s;
+}
+
+// chainc[count] = this slice's listed slots still pending (the count itself read from the list's tail when
+// cnt_dev is set: gs_phase_overflow's count is not known to the host without a read)
+__global__ __launch_bounds__(OVB) void k_pending(const uint32_t *list, const uint32_t *cnt_dev, uint32_t count,
+                                                 const uint64_t *chain, uint64_t *chainc) {
+    const uint32_t c = cnt_dev ? *cnt_dev : count;
+    uint32_t p = 0;
+    for (uint32_t i = threadIdx.x; i < c; i += OVB) p += chain[list[i]] == CHAIN_PENDING ? 1u : 0u;
+    __shared__ uint32_t s[OVB / WAVE];
+    const unsigned long long w = wave_sum(p);
+    if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = (uint32_t)w;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t a = 0;
+        for (uint32_t k = 0; k < OVB / WAVE; k++) a += s[k];
+        chainc[c] = a;
     }
 }
 
@@ -1804,17 +1854,31 @@ __global__ __launch_bounds__(LB) void k_gather_u64(GatherPtrs p, uint32_t G, uin
 // slot still pending on this slice continues from its predecessor's gathered state (chain_all =
 // [G][count] of every slice's chainc).  State goes to both chain (by slot) and chainc (by list index).
 template <int KW>
+// Resume point (gs_phase_chain): the nearest finished predecessor f; every slice between f and this one is
+// pending, and is skipped only if it cannot add a NodeDelta after f (f's delta is complete, or that slice's
+// smallest single-kv NodeDelta exceeds the budget f left: first-fit continuation tests each owner's
+// smallest prefix against it, state.py:392-413, and the budget only shrinks) -- its own resume then ends in
+// f's state too.  Slices before the first to overflow all finished at step 0, so f exists.
 __global__ __launch_bounds__(WAVE) void k_chain_step(Dev d, const int32_t *ini, const int32_t *res, uint32_t t,
                                                      const uint32_t *list, uint32_t count, const uint64_t *chain_all,
-                                                     uint64_t *chain, uint64_t *chainc) {
+                                                     uint64_t *chain, uint64_t *chainc, const uint64_t *tot_all,
+                                                     uint32_t n) {
     __shared__ __attribute__((aligned(16))) uint16_t s_wbuf[WIN];
     const int lane = lane_id();
+    const size_t stride = (size_t)count + 1u;  // chain_all[g][count + 1]: entry count = g's pending slots
     for (uint32_t i = blockIdx.x; i < count; i += gridDim.x) {
         const uint32_t slot = list[i];
         if (chain[slot] != CHAIN_PENDING) continue;
-        const uint64_t prev = chain_all[(size_t)(d.shard - 1) * count + i];
-        if (prev == CHAIN_PENDING) continue;
+        int f = (int)d.shard - 1;
+        while (f >= 0 && chain_all[(size_t)f * stride + i] == CHAIN_PENDING) f--;
+        if (f < 0) continue;
+        const uint64_t prev = chain_all[(size_t)f * stride + i];
         PackState pst = chain_unpack(prev);
+        bool ok = true;
+        for (uint32_t h = (uint32_t)f + 1u; h < d.shard && ok; h++)
+            ok = pst.stop || pst.S >= d.mtu ||
+                 (pst.tail && GS_TOT_MIN1(tot_all[(size_t)h * n * 2 + slot]) > d.mtu - pst.S);
+        if (!ok) continue;
         const uint32_t e = slot >> 1, wid = slot & 1u;
         const uint32_t a = (uint32_t)ini[e], b = (uint32_t)res[e];
         const bool w0 = wid == 0;
@@ -1935,13 +1999,13 @@ __global__ __launch_bounds__(XB, (KW == 4 ? PK_WAVES : 1)) void k_settle(Dev d, 
         if (d.spec) {
             const SlotSum s = settle_sum<KW>(d, snd, rcv, ds, slot, wbuf, t, salg);
             if (lane == 0) {
-                io.tot[slot] = s.T;
+                io.tot[slot] = tot_word(s.T, 0u);  // (speculative A/B path: no chain skipping)
                 d.slot_stat[slot] = make_uint4(s.nd, s.kvs, s.cand, s.clean ? 0u : 1u);
             }
         } else {
             if (d.lite && !(d.slot_stat[slot].w & LITE_FULL)) return;  // k_lite wrote the slice total
             pack_records<KW, true>(d, snd, rcv, ds, slot, wbuf, t, st, tomb, pst);
-            if (lane == 0) io.tot[slot] = pst.S;
+            if (lane == 0) io.tot[slot] = tot_word(pst.S, pst.m1);
             salg = st.alg;
         }
         const unsigned long long s_alg = wave_sum(salg);
@@ -1963,7 +2027,7 @@ __global__ __launch_bounds__(XB, (KW == 4 ? PK_WAVES : 1)) void k_settle(Dev d, 
         if (d.lite && (d.slot_stat[slot].w & LITE_DONE)) return;  // k_lite applied it and wrote its chain state
         unsigned long long P = 0, all = 0;
         for (uint32_t g = 0; g < d.shards; g++) {
-            const unsigned long long x = io.tot_all[(size_t)g * n * 2 + slot];
+            const unsigned long long x = GS_TOT_BYTES(io.tot_all[(size_t)g * n * 2 + slot]);
             if (g < d.shard) P += x;
             all += x;
         }
@@ -1980,8 +2044,9 @@ __global__ __launch_bounds__(XB, (KW == 4 ? PK_WAVES : 1)) void k_settle(Dev d, 
                 st.kvs = ss.y;
                 st.cand = ss.z;
                 if (lane == 0) {
-                    shard_add(d, C_DBYTES, io.tot_all[(size_t)d.shard * n * 2 + slot]);
-                    io.chain[slot] = (uint64_t)(P + io.tot_all[(size_t)d.shard * n * 2 + slot]);  // not listed
+                    const unsigned long long own = GS_TOT_BYTES(io.tot_all[(size_t)d.shard * n * 2 + slot]);
+                    shard_add(d, C_DBYTES, own);
+                    io.chain[slot] = (uint64_t)(P + own);  // not listed
                 }
             }
         }
@@ -2043,14 +2108,15 @@ __global__ __launch_bounds__(XB, LITE_WAVES) void k_lite(Dev d, const int32_t *i
             if (lane == 0) shard_add(d, C_DBYTES, T);
         }
     } else if (MODE == 1) {
-        if (!sched && pack_lite<false>(d, rcv, slot, 0u, st, T)) {
+        uint32_t m1 = NONE;
+        if (!sched && pack_lite<false>(d, rcv, slot, 0u, st, T, &m1)) {
             flag = 0u;
-            if (lane == 0) io.tot[slot] = T;
+            if (lane == 0) io.tot[slot] = tot_word(T, m1);
         }
     } else {
         unsigned long long P = 0;
-        for (uint32_t g = 0; g < d.shard; g++) P += io.tot_all[(size_t)g * n * 2 + slot];
-        const unsigned long long own = io.tot_all[(size_t)d.shard * n * 2 + slot];
+        for (uint32_t g = 0; g < d.shard; g++) P += GS_TOT_BYTES(io.tot_all[(size_t)g * n * 2 + slot]);
+        const unsigned long long own = GS_TOT_BYTES(io.tot_all[(size_t)d.shard * n * 2 + slot]);
         if (!sched && P + own <= d.mtu && pack_lite<true>(d, rcv, slot, (uint32_t)P, st, T)) {
             flag = LITE_DONE;
             const uint32_t S = (uint32_t)P + T;  // every NodeDelta whole: pack_group's state after the last one
@@ -3326,6 +3392,7 @@ struct gs_handle {
     ncclComm_t comm = nullptr;
     struct {
         uint64_t *tot = nullptr, *tot_all = nullptr, *chain = nullptr, *chainc = nullptr, *chain_all = nullptr;
+        uint64_t *pend = nullptr;  // device: the pending slots summed over the slices (sliced_phase's one read per step)
         uint32_t *list = nullptr;
         uint32_t cap = 0;  // exchanges the buffers hold
     } sc;
@@ -3707,7 +3774,7 @@ void gs_destroy(gs_handle *h) {
         for (auto &pr : v) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
     for (hipEvent_t e : h->evpool) (void)hipEventDestroy(e);
     for (void *p : {(void *)h->sc.tot, (void *)h->sc.tot_all, (void *)h->sc.chain, (void *)h->sc.chainc,
-                    (void *)h->sc.chain_all, (void *)h->sc.list})
+                    (void *)h->sc.chain_all, (void *)h->sc.list, (void *)h->sc.pend})
         if (p) (void)hipFree(p);
     if (h->comm) (void)ncclCommDestroy(h->comm);
     delete h;
@@ -3962,6 +4029,8 @@ int gs_phase_overflow(gs_handle *h, uint32_t n, const uint64_t *slice_bytes_all,
     HIPCHK(h, hipGetLastError());
     k_ov_write<<<nb, OVB, 0, h->stream>>>(slice_bytes_all, slots, h->G, h->cfg.mtu, chain, list, chainc);
     HIPCHK(h, hipGetLastError());
+    k_pending<<<1, OVB, 0, h->stream>>>(list, list + slots + nb, 0u, chain, chainc);  // chainc[count]
+    HIPCHK(h, hipGetLastError());
     if (count) {  // count = NULL: no read back (another slice in this process reads the same count)
         HIPCHK(h, hipMemcpyAsync(count, list + slots + nb, 4, hipMemcpyDeviceToHost, h->stream));
         HIPCHK(h, hipStreamSynchronize(h->stream));
@@ -3970,18 +4039,26 @@ int gs_phase_overflow(gs_handle *h, uint32_t n, const uint64_t *slice_bytes_all,
 }
 
 int gs_phase_chain(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t n, uint32_t tick, uint32_t step,
-                   const uint32_t *list, uint32_t count, const uint64_t *chain_all, uint64_t *chain, uint64_t *chainc) {
+                   const uint32_t *list, uint32_t count, const uint64_t *chain_all, uint64_t *chain, uint64_t *chainc,
+                   const uint64_t *slice_bytes_all) {
     if (h && (!n || !count)) return GS_OK;
     int rc = check_phase(h, ini, res, n, tick, true);
     if (rc) return rc;
     if (h->G < 2 || !h->d.cand) return fail(h, GS_E_UNSUPPORTED, "gs_phase_chain needs a sliced canonical handle");
-    if (!list || !chain_all || !chain || !chainc || step < 1 || step >= h->G || count > 2 * n) return GS_E_INVALID;
-    if (h->shard == 0) return GS_OK;  // slice 0 always finishes at step 0
+    if (!list || !chain_all || !chain || !chainc || !slice_bytes_all || step < 1 || step >= h->G || count > 2 * n)
+        return GS_E_INVALID;
+    if (h->shard == 0) return GS_OK;  // slice 0 always finishes at step 0 (its pending entry stays 0)
     hipEvent_t e0 = nullptr;
     if ((rc = time_begin(h, e0))) return rc;
     const uint32_t grid = std::min<uint32_t>(count, 2048u);
-    if (h->KP <= 16) k_chain_step<4><<<grid, WAVE, 0, h->stream>>>(h->d, ini, res, tick, list, count, chain_all, chain, chainc);
-    else k_chain_step<KWB><<<grid, WAVE, 0, h->stream>>>(h->d, ini, res, tick, list, count, chain_all, chain, chainc);
+    if (h->KP <= 16)
+        k_chain_step<4><<<grid, WAVE, 0, h->stream>>>(h->d, ini, res, tick, list, count, chain_all, chain, chainc,
+                                                       slice_bytes_all, n);
+    else
+        k_chain_step<KWB><<<grid, WAVE, 0, h->stream>>>(h->d, ini, res, tick, list, count, chain_all, chain, chainc,
+                                                         slice_bytes_all, n);
+    HIPCHK(h, hipGetLastError());
+    k_pending<<<1, OVB, 0, h->stream>>>(list, nullptr, count, chain, chainc);  // chainc[count]
     HIPCHK(h, hipGetLastError());
     return time_end(h, GS_KT_PACK, e0);
 }
@@ -3992,15 +4069,16 @@ namespace {
 int ensure_scratch(gs_handle *h, uint32_t n) {
     if (h->sc.cap >= n) return GS_OK;
     for (void *p : {(void *)h->sc.tot, (void *)h->sc.tot_all, (void *)h->sc.chain, (void *)h->sc.chainc,
-                    (void *)h->sc.chain_all, (void *)h->sc.list})
+                    (void *)h->sc.chain_all, (void *)h->sc.list, (void *)h->sc.pend})
         if (p) HIPCHK(h, hipFree(p));
     const uint32_t cap = std::max(n, 1024u);
     const size_t s2 = (size_t)2 * cap * 8, G = h->G;
     HIPCHK(h, hipMalloc(&h->sc.tot, s2));
     HIPCHK(h, hipMalloc(&h->sc.chain, s2));
-    HIPCHK(h, hipMalloc(&h->sc.chainc, s2));
+    HIPCHK(h, hipMalloc(&h->sc.chainc, s2 + 8));                 // [2 cap + 1]: the pending entry last
     HIPCHK(h, hipMalloc(&h->sc.tot_all, G * s2));
-    HIPCHK(h, hipMalloc(&h->sc.chain_all, G * s2));
+    HIPCHK(h, hipMalloc(&h->sc.chain_all, G * (s2 + 8)));      // [G][count + 1]
+    HIPCHK(h, hipMalloc(&h->sc.pend, 8));
     HIPCHK(h, hipMalloc(&h->sc.list, (size_t)GS_OVERFLOW_LIST_LEN(cap) * 4));
     h->sc.cap = cap;
     return GS_OK;
@@ -4056,12 +4134,21 @@ int sliced_phase(gs_handle *const *hs, uint32_t nh, const int32_t *ini, const in
     if (!count) return GS_OK;
     const uint32_t G = hs[0]->G;
     for (uint32_t step = 1; step < G; step++) {
+        // every slice's chain states and pending count (entry count); the same data on every slice, so each
+        // reads the same sum and all stop together
         if ((rc = gather_u64(hs, nh, [](gs_handle *h) { return h->sc.chainc; },
-                             [](gs_handle *h) { return h->sc.chain_all; }, count)))
+                             [](gs_handle *h) { return h->sc.chain_all; }, (size_t)count + 1)))
             return rc;
+        gs_handle *h0 = hs[0];
+        k_sum_pending<<<1, WAVE, 0, h0->stream>>>(h0->sc.chain_all, G, count, h0->sc.pend);
+        HIPCHK(h0, hipGetLastError());
+        uint64_t pend = 0;
+        HIPCHK(h0, hipMemcpyAsync(&pend, h0->sc.pend, 8, hipMemcpyDeviceToHost, h0->stream));
+        HIPCHK(h0, hipStreamSynchronize(h0->stream));
+        if (!pend) break;
         for (uint32_t i = 0; i < nh; i++)
             if ((rc = gs_phase_chain(hs[i], ini, res, n, tick, step, hs[i]->sc.list, count, hs[i]->sc.chain_all,
-                                     hs[i]->sc.chain, hs[i]->sc.chainc)))
+                                     hs[i]->sc.chain, hs[i]->sc.chainc, hs[i]->sc.tot_all)))
                 return rc;
     }
     return GS_OK;

@@ -13,12 +13,15 @@ order — and stops adding once the DeltaPb is full.  Per phase:
 2. all-gather of those totals (16 B per exchange per slice; RCCL over xGMI);
 3. ``gs_phase_pack(step 0)``: each slice packs and applies its owners starting
    at the byte count its predecessors reach when they all fit whole;
-4. only for the (exchange, direction) slots whose totals sum past the MTU: G-1
-   further steps, each an all-gather of those slots' chain states (8 bytes per
-   overflowing slot and slice) and a ``gs_phase_chain`` that lets the next slice
-   continue where its predecessor's packing stopped.  ``gs_phase_overflow`` lists
-   the slots on the device -- the same list on every slice -- and returns their
-   number, the one host read per phase.
+4. only for the (exchange, direction) slots whose totals sum past the MTU: chain
+   steps, each an all-gather of those slots' chain states (8 bytes per
+   overflowing slot and slice, plus each slice's pending count) and a
+   ``gs_phase_chain`` that lets a pending slice continue where its nearest
+   finished predecessor stopped, skipping slices that cannot add a NodeDelta
+   (their smallest one exceeds the budget left: each total carries it); the
+   steps stop once no slot is pending (usually after one).  ``gs_phase_overflow``
+   lists the slots on the device -- the same list on every slice -- and returns
+   their number: one host read per phase, and one per step.
 
 The result equals ``gs_run_phase`` on a single handle bit for bit (tested on one
 GPU with G in-process slices).  ``comm`` abstracts the gather: ``LocalComm``
@@ -33,6 +36,7 @@ import numpy as np
 from ._lib import COUNTER_FIELDS, GsError, overflow_list_len
 
 CHAIN_PENDING = -1  # u64 ~0 viewed as int64 (gossip_sim.hip CHAIN_PENDING)
+TOT_BYTES_MASK = (1 << 40) - 1  # a slice total's DeltaPb bytes (GS_TOT_BYTES); the smallest NodeDelta above
 
 
 class LocalComm:
@@ -134,7 +138,7 @@ def run_sliced_phase(slices, comm, mtu: int, t: int, ini, res) -> int:
         s.phase_pack(t, ini, res, 0, tot_all, None, ch)
     if not all(s.has_records for s in slices):
         # fused count pass (GS_FUSED=1): every slot's chain state travels; one host read decides
-        if not bool((tot_all.sum(0) > mtu).any()):
+        if not bool(((tot_all & TOT_BYTES_MASK).sum(0) > mtu).any()):
             return 1
         for step in range(1, comm.world):
             chain_all = comm.gather(chains)
@@ -143,17 +147,23 @@ def run_sliced_phase(slices, comm, mtu: int, t: int, ini, res) -> int:
         return comm.world
     dev = tots[0].device
     lists = [torch.empty(overflow_list_len(n), dtype=torch.int32, device=dev) for _ in slices]
-    chaincs = [torch.empty(2 * n, dtype=torch.int64, device=dev) for _ in slices]
+    chaincs = [torch.empty(2 * n + 1, dtype=torch.int64, device=dev) for _ in slices]
     # the same gathered totals give every slice the same list: one host read per process
     for i in range(len(slices) - 1, -1, -1):
         count = slices[i].phase_overflow(tot_all, chains[i], lists[i], chaincs[i], read=i == 0)
     if count == 0:
         return 1
+    steps = 1
     for step in range(1, comm.world):
-        chain_all = comm.gather([cc[:count] for cc in chaincs])
+        # every slice's chain states + pending count (entry count): the same on every rank, so all stop
+        # together once no slot is pending (a chain usually resolves in one step, gs_phase_chain)
+        chain_all = comm.gather([cc[: count + 1] for cc in chaincs])
+        if int(chain_all[:, count].sum().item()) == 0:
+            break
         for s, ch, lb, cc in zip(slices, chains, lists, chaincs):
-            s.phase_chain(t, ini, res, step, lb, count, chain_all, ch, cc)
-    return comm.world
+            s.phase_chain(t, ini, res, step, lb, count, chain_all, ch, cc, tot_all)
+        steps += 1
+    return steps
 
 
 class ShardGroup:

@@ -418,12 +418,14 @@ class GossipSim:
                                            C.byref(cnt) if read else None), "gs_phase_overflow")
         return int(cnt.value) if read else None
 
-    def phase_chain(self, t: int, ini, res, step: int, list_buf, count: int, chain_all, chain, chainc):
-        """gs_phase_chain step ``step`` over the ``count`` listed slots (chain_all = gathered [G, count])."""
+    def phase_chain(self, t: int, ini, res, step: int, list_buf, count: int, chain_all, chain, chainc, tot_all):
+        """gs_phase_chain step ``step`` over the ``count`` listed slots (chain_all = gathered [G, count + 1],
+        entry count = that slice's pending slots; tot_all = the phase's gathered slice totals)."""
         n = int(ini.numel())
         self._chk(self.L.gs_phase_chain(self.h, C.c_void_p(ini.data_ptr()), C.c_void_p(res.data_ptr()), n, t, step,
                                         C.c_void_p(list_buf.data_ptr()), count, C.c_void_p(chain_all.data_ptr()),
-                                        C.c_void_p(chain.data_ptr()), C.c_void_p(chainc.data_ptr())),
+                                        C.c_void_p(chain.data_ptr()), C.c_void_p(chainc.data_ptr()),
+                                        C.c_void_p(tot_all.data_ptr())),
                   "gs_phase_chain")
 
     def flush_reports(self, t: int):

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define GS_API_VERSION 14
+#define GS_API_VERSION 15
 #define GS_MAX_PHASES 64  /* gs_schedule_phases: phases per round */
 #define GS_TICK_US 15625u
 #define GS_NONE 0xFFFFFFFFu
@@ -272,7 +272,8 @@ int gs_run_phase(gs_handle *h, const int32_t *initiators, const int32_t *respond
  * cluster run, per phase, on the same initiators/responders:
  *   1. gs_phase_count: pass 1 of every exchange on this slice's columns (heartbeats, failure-detector
  *      reports, stale-owner bitmaps) and, per exchange and direction, the DeltaPb bytes of all this
- *      slice's stale owners: DEVICE u64 slice_bytes[n][2] (dir 0 = responder -> initiator).
+ *      slice's stale owners: DEVICE u64 slice_bytes[n][2] (dir 0 = responder -> initiator) =
+ *      bytes | (the smallest single-kv NodeDelta among them, GS_TOT_MIN1_NONE if none) << 40;
  *   2. the caller gathers every slice's slice_bytes into slice_bytes_all[G][n][2] (slice order), e.g.
  *      an RCCL all-gather;
  *   3. gs_phase_pack(step 0): packing + apply_delta of this slice's owners, resumed at the DeltaPb
@@ -286,19 +287,27 @@ int gs_phase_count(gs_handle *h, const int32_t *initiators, const int32_t *respo
                    uint64_t *slice_bytes);
 int gs_phase_pack(gs_handle *h, const int32_t *initiators, const int32_t *responders, uint32_t n, uint32_t tick,
                   uint32_t step, const uint64_t *slice_bytes_all, const uint64_t *chain_all, uint64_t *chain);
+#define GS_TOT_BYTES(x) ((x) & ((1ull << 40) - 1ull))
+#define GS_TOT_MIN1(x) ((uint32_t)((x) >> 40))
+#define GS_TOT_MIN1_NONE 0xFFFFFFu
 /* Compacted chain (replaces step 4 above on canonical handles built with candidate records):
  *   gs_phase_overflow (blocking: one 4-byte read): the slots (2e + dir) whose gathered slice totals sum
- *     past the mtu, in slot order, into DEVICE list[GS_OVERFLOW_LIST_LEN(n)] (the tail is scratch), this slice's chain
- *     state of each into DEVICE chainc[2n], and their number into *count (host; NULL: not read back);
- *   for step = 1 .. G-1: gather every slice's chainc[count] into chain_all[G][count], then
- *     gs_phase_chain(step) (one wave per listed slot; chain and chainc updated).
- * Every slice computes the same list from the same gathered totals, so only count x 8 bytes per slice
- * travel per step. */
+ *     past the mtu, in slot order, into DEVICE list[GS_OVERFLOW_LIST_LEN(n)] (the tail is scratch), this
+ *     slice's chain state of each into DEVICE chainc[2n + 1] and, at chainc[count], how many of them this
+ *     slice still has pending; their number into *count (host; NULL: not read back);
+ *   then, for step = 1 .. G-1: gather every slice's chainc[0 .. count] into chain_all[G][count + 1]; stop
+ *     once every slice's pending entry (chain_all[g][count]) is 0; else gs_phase_chain(step) (one wave per
+ *     listed slot; chain, chainc and the pending entry updated).
+ * A pending slice resumes from its nearest finished predecessor f when every slice between them is
+ * pending and cannot add a NodeDelta: f's delta is complete, or that slice's smallest single-kv
+ * NodeDelta (GS_TOT_MIN1 of its total) exceeds the budget f left (first-fit continuation would skip all
+ * of its owners) -- so a chain usually resolves in one step instead of G - 1.  Every slice computes the
+ * same list from the same gathered totals, so only (count + 1) x 8 bytes per slice travel per step. */
 int gs_phase_overflow(gs_handle *h, uint32_t n, const uint64_t *slice_bytes_all, const uint64_t *chain,
                       uint32_t *list, uint64_t *chainc, uint32_t *count);
 int gs_phase_chain(gs_handle *h, const int32_t *initiators, const int32_t *responders, uint32_t n, uint32_t tick,
                    uint32_t step, const uint32_t *list, uint32_t count, const uint64_t *chain_all, uint64_t *chain,
-                   uint64_t *chainc);
+                   uint64_t *chainc, const uint64_t *slice_bytes_all);
 
 /* ---- Multi-GPU: one handle per device, each holding one owner-column
  * slice; the library drives the sliced phase itself (count, all-gather of the slice totals, packing,

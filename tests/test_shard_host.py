@@ -13,7 +13,7 @@ import numpy as np
 import pytest
 import torch
 
-from aiocluster_amd.shard import CHAIN_PENDING, LocalComm, run_sliced_phase
+from aiocluster_amd.shard import CHAIN_PENDING, TOT_BYTES_MASK, LocalComm, run_sliced_phase
 
 MTU = 100
 
@@ -57,37 +57,53 @@ class ToySlice:
         self.has_records = has_records
 
     def phase_overflow(self, tot_all, chain, list_buf, chainc, read=True):
-        tot = tot_all.sum(0).reshape(-1)
+        tot = (tot_all & TOT_BYTES_MASK).sum(0).reshape(-1)
         idx = (tot > MTU).nonzero().flatten()
         list_buf[: len(idx)] = idx.to(list_buf.dtype)
         chainc[: len(idx)] = chain.reshape(-1)[idx]
+        chainc[len(idx)] = int((chain.reshape(-1)[idx] == CHAIN_PENDING).sum())  # pending entry
         return len(idx)
 
-    def phase_chain(self, t, ini, res, step, list_buf, count, chain_all, chain, chainc):
+    def phase_chain(self, t, ini, res, step, list_buf, count, chain_all, chain, chainc, tot_all):
+        """k_chain_step: resume from the nearest finished predecessor f, skipping the pending slices between
+        that cannot add a candidate (delta complete, or their smallest candidate above the budget left)."""
         flat = chain.view(-1)
         for i in range(count):
             slot = int(list_buf[i])
             e, d = slot // 2, slot % 2
             if self.g == 0 or int(flat[slot]) != CHAIN_PENDING:
                 continue
-            prev = int(chain_all[self.g - 1, i])
-            if prev == CHAIN_PENDING:
+            f = self.g - 1
+            while f >= 0 and int(chain_all[f, i]) == CHAIN_PENDING:
+                f -= 1
+            if f < 0:
                 continue
-            sent, S, tail, stop = seq_pack(self.cands[e][d], *dec(prev))
+            S, tail, stop = dec(int(chain_all[f, i]))
+            ok = all(stop or S >= MTU or (tail and ((int(tot_all[h, e, d]) & (1 << 64) - 1) >> 40) > MTU - S)
+                     for h in range(f + 1, self.g))
+            if not ok:
+                continue
+            sent, S, tail, stop = seq_pack(self.cands[e][d], S, tail, stop)
             self.sent[(e, d)] = sent
             flat[slot] = chainc[i] = enc(S, tail, stop)
+        chainc[count] = sum(int(flat[int(list_buf[i])]) == CHAIN_PENDING for i in range(count))
 
     def phase_count(self, t, ini, res):
+        """slice totals: bytes | the smallest candidate << 40 (0xFFFFFF: none), as gs_phase_count"""
         n = int(ini.numel())
-        return torch.tensor([[sum(s for _, s in self.cands[e][d]) for d in range(2)] for e in range(n)],
-                            dtype=torch.int64)
+
+        def word(c):  # u64 as the device writes it, viewed as int64
+            w = sum(s for _, s in c) | (min((s for _, s in c), default=0xFFFFFF) << 40)
+            return w - (1 << 64) if w >= 1 << 63 else w
+
+        return torch.tensor([[word(self.cands[e][d]) for d in range(2)] for e in range(n)], dtype=torch.int64)
 
     def phase_pack(self, t, ini, res, step, tot_all, chain_all, chain):
         n = int(ini.numel())
         for e in range(n):
             for d in range(2):
                 if step == 0:
-                    P = int(tot_all[: self.g, e, d].sum()) if self.g else 0
+                    P = int((tot_all[: self.g, e, d] & TOT_BYTES_MASK).sum()) if self.g else 0
                     if P > MTU:
                         chain[e, d] = CHAIN_PENDING
                         continue
@@ -127,7 +143,7 @@ def check(slices, cands, G, n):
             assert got == want, (e, d, got, want)
 
 
-@pytest.mark.parametrize("G,records", [(2, True), (3, True), (5, True), (3, False)])
+@pytest.mark.parametrize("G,records", [(2, True), (3, True), (5, True), (8, True), (3, False)])
 def test_chain_protocol_in_process(G, records):
     rng = np.random.default_rng(G)
     n = 40
@@ -135,7 +151,33 @@ def test_chain_protocol_in_process(G, records):
     slices = [ToySlice(g, cands[g], records) for g in range(G)]
     ini = torch.zeros(n, dtype=torch.int32)
     steps = run_sliced_phase(slices, LocalComm(G), MTU, 0, ini, ini)
-    assert steps == G  # these inputs overflow the MTU somewhere
+    # these inputs overflow the MTU somewhere; the compacted chain stops once nothing is pending
+    assert (2 <= steps <= G) if records else steps == G
+    check(slices, cands, G, n)
+
+
+@pytest.mark.parametrize("big", [45, 80])
+def test_chain_skips_slices_that_cannot_fit(big):
+    """Eight slices whose owners are all larger than any budget left after the MTU is crossed (big = 80:
+    every pending slice is skipped, one chain step), or a mix (big = 45 with small owners in some slices:
+    those cannot be skipped and the chain takes more steps) -- either way the union equals one sequential
+    pass."""
+    G, n = 8, 12
+    rng = np.random.default_rng(big)
+    cands = [[[[] for _ in range(2)] for _ in range(n)] for _ in range(G)]
+    for e in range(n):
+        for d in range(2):
+            cid = 0
+            for g in range(G):
+                for _ in range(3):
+                    small = big == 45 and g % 3 == 2 and rng.random() < 0.5
+                    cands[g][e][d].append((cid, int(rng.integers(2, 6)) if small else big))
+                    cid += 1
+    slices = [ToySlice(g, cands[g]) for g in range(G)]
+    ini = torch.zeros(n, dtype=torch.int32)
+    steps = run_sliced_phase(slices, LocalComm(G), MTU, 0, ini, ini)
+    if big == 80:
+        assert steps == 2, steps
     check(slices, cands, G, n)
 
 
