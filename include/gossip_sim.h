@@ -75,7 +75,7 @@ typedef struct gs_config {
     uint32_t n_keys;                /* K <= 64 keys per node */
     uint32_t hist_cap;              /* C <= 255: writes kept per (owner, key), ordinal 0 = absent */
     uint32_t mtu;                   /* Config.max_payload_size (entities.py:105) */
-    uint32_t flags;                 /* GS_CANONICAL | GS_TOMBSTONES | GS_FD_RING */
+    uint32_t flags;                 /* GS_CANONICAL | GS_TOMBSTONES | GS_FD_RING | GS_NO_HELD | GS_HB8 | GS_MV8 */
     uint32_t window;                /* FailureDetectorConfig.sampling_window_size (entities.py:88) */
     uint32_t max_interval_ticks;    /* FailureDetectorConfig.max_interval (entities.py:89) */
     uint32_t tombstone_grace_ticks; /* Config.marked_for_deletion_grace_period (entities.py:101) */
