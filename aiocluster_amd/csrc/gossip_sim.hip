@@ -272,6 +272,7 @@ struct Cand {
     uint32_t hs[KW], hr[KW];  // held write ordinals, 4 keys per word (sender / receiver)
     bool rx;                  // prefix views (no GS_TOMBSTONES): the receiver's view is S_j(mr)
     bool fast;                // ... and so is the sender's: hr was not loaded
+    bool light;               // evaluated from the version log (eval_light): hs not loaded either
 };
 // The sender's kvs of one candidate, per key: eval_cand's working set, not kept in Cand (32 VGPRs at
 // KW = 4): the packer re-reads a key's history entry (the sender's held ordinal hs) in the rare paths
@@ -457,6 +458,37 @@ __device__ __forceinline__ void eval_cand(const Dev &d, uint32_t s, uint32_t r, 
     c.nkv = nk;
     c.emsg = nk ? msgf(c.base + sum) : 0u;
     c.min1 = nk ? msgf(c.base + minkv) : 0u;
+    c.light = false;
+}
+
+// A prefix candidate (both views S_j(M), no tombstones: last_gc 0; j in the receiver's digest, so from = mr)
+// from the owner's version log alone, as pack_lite sizes it: NodeDelta j holds the writes v in (mr, ms]
+// that no write <= ms overwrote (VLOG next > ms).  No latest-write row, no history entry; the sender's held
+// ordinals (hs) are not derived (c.light): the rare paths that need them -- a truncated NodeDelta's kv
+// ranking, its apply -- derive them from the owner's tables.
+template <int KW>
+__device__ __forceinline__ void eval_light(const Dev &d, uint32_t j, uint32_t ms, uint32_t mr, Cand<KW> &c,
+                                           uint32_t &alg) {
+    const uint32_t *vl = d.vlog + (size_t)j * d.VL;
+    uint32_t kv = vl[ms] & 0xFFFFu, kv1 = kv, nk = 1;  // write ms is the latest <= ms of its key
+    alg += 4 + 2;
+    for (uint32_t v = ms - 1u; v > mr; v--) {  // lag > 1: the other writes of (mr, ms), lowest last
+        const uint32_t e = vl[v];
+        alg += 4;
+        if ((e >> 16) > ms) { kv += e & 0xFFFFu; nk++; kv1 = e & 0xFFFFu; }
+    }
+    c.j = j;
+    c.from = mr;
+    c.gs = c.gr = 0u;
+    c.ms = ms;
+    c.mr = mr;
+    c.rx = c.fast = c.light = true;
+    c.base = msgf(d.nid_size[j]) + ufield(mr) + 1u + vlen(ms);
+    c.nkv = nk;
+    c.emsg = msgf(c.base + kv);
+    c.min1 = msgf(c.base + kv1);
+#pragma unroll
+    for (int q = 0; q < KW; q++) c.hs[q] = c.hr[q] = 0u;
 }
 
 // NodeState.apply_delta (state.py:190-233) at receiver r of the NodeDelta {owner c.j, the
@@ -496,11 +528,18 @@ __device__ __forceinline__ void apply_cand(const Dev &d, uint32_t s, uint32_t r,
     uint32_t hr0[KW];
 #pragma unroll
     for (int q = 0; q < KW; q++) hr0[q] = hr[q];
+    uint32_t hs[KW];  // the sender's held ordinals: S_j(ms) for a candidate evaluated from the version log
+    if (c.light) {
+        derive_held<KW>(d, c.j, c.ms, hs, alg);
+    } else {
+#pragma unroll
+        for (int q = 0; q < KW; q++) hs[q] = c.hs[q];
+    }
 #pragma unroll
     for (int q = 0; q < 4 * KW; q++) {
         if ((uint32_t)q >= d.K) continue;
         uint32_t wr = byte_of(hr, q);
-        const uint32_t ws = byte_of(c.hs, q);
+        const uint32_t ws = byte_of(hs, q);
         if (jump && wr && (uint32_t)d.hist[hix(d, c.j, wr, q)] <= g) {
             wr = 0;
             if (tt) tsr[q] = NONE;
@@ -638,13 +677,21 @@ __device__ __forceinline__ void pack_group(const Dev &d, uint32_t s, uint32_t r,
             uint32_t v = 0, kvm = 0;
             {
                 const uint32_t jx = __shfl(c.j, x, WAVE);
-                uint32_t hsx[KW];
-#pragma unroll
-                for (int w = 0; w < KW; w++) hsx[w] = __shfl(c.hs[w], x, WAVE);
                 uint32_t wq = 0;
+                if (__shfl((int)c.light, x, WAVE)) {  // version-log candidate: key q's latest write <= ms
+                    const uint32_t msx = __shfl(c.ms, x, WAVE);
+                    if (lane < (int)d.K) {
+                        wq = d.last_w[(size_t)jx * d.KP + lane];
+                        while (wq && (uint32_t)d.hist[hix(d, jx, wq, (uint32_t)lane)] > msx) wq--;
+                    }
+                } else {
+                    uint32_t hsx[KW];
 #pragma unroll
-                for (int w = 0; w < KW; w++)
-                    if ((lane >> 2) == w) wq = (hsx[w] >> (8 * (lane & 3))) & 0xFFu;
+                    for (int w = 0; w < KW; w++) hsx[w] = __shfl(c.hs[w], x, WAVE);
+#pragma unroll
+                    for (int w = 0; w < KW; w++)
+                        if ((lane >> 2) == w) wq = (hsx[w] >> (8 * (lane & 3))) & 0xFFu;
+                }
                 if (lane < (int)d.K && wq) {
                     const uint64_t e = d.hist[hix(d, jx, wq, (uint32_t)lane)];
                     v = (uint32_t)e;
@@ -735,6 +782,8 @@ __device__ __forceinline__ void pack_dir(const Dev &d, uint32_t s, uint32_t r, c
     pack_begin(d, COUNT, pst, S, tail, stop);
     uint32_t nr = 0;    // REC: NodeDeltas recorded so far (wave-uniform)
     uint32_t m1 = pst.m1;  // COUNT: the smallest min1 so far
+    // canonical prefix candidates from the version log (eval_light; not for the wire emitter's records)
+    const bool lightok = !GENM && !REC && d.vlog && !d.ev && !ds.sched;
     uint32_t pend = 0;  // wave-uniform: candidates carried from earlier windows (< 64), in rv
     uint32_t rv = 0;    // lane i < pend: the i-th carried candidate's position
     // canonical: the next window's bitmap word is loaded one window ahead (the bitmap is in HBM on the
@@ -788,18 +837,25 @@ __device__ __forceinline__ void pack_dir(const Dev &d, uint32_t s, uint32_t r, c
             c.emsg = 0;
             c.min1 = 0;
             uint32_t j = 0;
+            bool light = false;
+            c.light = false;
             if (cand) {
                 const uint32_t p = ci < pend ? rv : win + wbuf[ci - pend];
                 j = GENM ? order[p] : p;
-                if (!GENM && !COUNT && tail && d.vlog) {  // tail mode: skip what cannot fit (min1_lb)
+                if (!GENM && d.vlog && (lightok || (!COUNT && tail))) {
                     const uint32_t msw = mv_word(d, pix(d, s, j), j), mrw = mv_word(d, pix(d, r, j), j);
                     st.alg += 4;
-                    if (!((msw | mrw) & MV_INEXACT) &&
-                        min1_lb(d, j, msw, ds.sched ? 0u : mrw) > d.mtu - S)
-                        cand = false;
+                    const bool fast = !((msw | mrw) & MV_INEXACT);
+                    // tail mode: skip what cannot fit (min1_lb)
+                    if (!COUNT && tail && fast && min1_lb(d, j, msw, ds.sched ? 0u : mrw) > d.mtu - S) cand = false;
+                    else if (lightok && fast) {
+                        eval_light<KW>(d, j, msw, mrw, c, st.alg);
+                        light = true;
+                        st.cand++;
+                    }
                 }
             }
-            if (cand) {
+            if (cand && !light) {
                 CandKeys<KW> ck;
                 eval_cand<KW, GENM>(d, s, r, ds, j, t, c, ck, st.alg);
                 st.cand++;
@@ -841,6 +897,9 @@ __device__ __forceinline__ void pack_list(const Dev &d, uint32_t s, uint32_t r, 
     bool tail, stop;
     pack_begin(d, COUNT, pst, S, tail, stop);
     const bool specd = !COUNT && d.spec;
+    // prefix candidates from the version log (eval_light): no hook events (their applies take the per-key
+    // path), no scheduled-for-deletion test due (a digest may leave owners out: from = 0), not speculative
+    const bool lightok = d.vlog && !d.ev && !ds.sched && !specd;
     uint32_t nr = 0, m1 = pst.m1;
     uint2 nxt = make_uint2(0u, 0u);
     if ((uint32_t)lane < n) nxt = L[lane];
@@ -863,9 +922,14 @@ __device__ __forceinline__ void pack_list(const Dev &d, uint32_t s, uint32_t r, 
         Cand<KW> c;
         c.emsg = 0;
         c.min1 = 0;
+        c.light = false;
         if (cand) {
-            CandKeys<KW> ck;
-            eval_cand<KW, false, true>(d, s, r, ds, cr.x, t, c, ck, st.alg, cr.y);
+            if (lightok && rec_fast(cr.y)) {
+                eval_light<KW>(d, cr.x, cr.y & 0xFFFFu, cr.y >> 16, c, st.alg);
+            } else {
+                CandKeys<KW> ck;
+                eval_cand<KW, false, true>(d, s, r, ds, cr.x, t, c, ck, st.alg, cr.y);
+            }
             st.cand++;
         }
         if (COUNT) m1 = min(m1, wave_min(cand && c.emsg ? c.min1 : NONE));
