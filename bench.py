@@ -14,9 +14,9 @@ runs every exchange on its columns, and the ranks exchange only 16 bytes per exc
 overflows the MTU).  ``value`` is the cluster's exchanges / the slowest rank's time.
 ``--slices G`` rehearses the same sliced path with G slices in one process on one GPU.
 
-Prints ONE JSON line (rank 0) with the roofline of the dominant kernel (k_pass1<fused>: each phase is
-one launch, pass 1 then packing + apply_delta in the same workgroup; every kernel HIP-event timed on the
-library's stream, gs_kernel_times), the CPU baseline (the C oracle on 16 host threads and on one, timed
+Prints ONE JSON line (rank 0) with the roofline of the dominant kernel (k_pass1; each phase is k_pass1,
+then k_lite -- whole deltas sized from the owners' version logs and applied -- then the exact packer for
+the rest; every kernel HIP-event timed on the library's stream, gs_kernel_times), the CPU baseline (the C oracle on 16 host threads and on one, timed
 on a bounded sample of exchanges whose rows are copied from the device state after the timed rounds,
 checked bit-exact against the device first) and 3 rounds scheduled by the device's own peer selection.
 """
