@@ -297,6 +297,10 @@ def roofline(sims, local_c, exch, kt, elapsed, torch, dev, rank, group, workload
         "achieved_frac_of_copy_ceiling": d["achieved"] / copy_gbs if copy_gbs and d.get("achieved") else None,
         "traffic_gbs": d.get("traffic_gbs"),
         "kernels": per,
+        "note": ("k_pass1 streams 8-bit heartbeat + max_version views (GS_HB8 + GS_MV8): ~0.43 MB of HBM per "
+                 "exchange (PMC), 1.07 MB with round 2's 16-bit views, so its frac fell while its time did too; "
+                 "at these bytes it is bound by loads in flight per wave (2 groups ahead at 5 waves/SIMD), "
+                 "not by HBM bandwidth (DESIGN.md §7b, §10)") if d["kernel"] == "k_pass1" else None,
         "survey_formula_bytes_per_phase": survey,
         "survey_formula_gbs_over_pass1": survey / (kt["pass1"][0] / launches / 1e3) / 1e9 if kt["pass1"][0] else None,
     }
