@@ -198,7 +198,7 @@ def _gloo_worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        rng = np.random.default_rng(7)
+        rng = np.random.default_rng(7 + world)
         n = 30
         cands = make_cands(rng, world, n)
         s = ToySlice(rank, cands[rank])
@@ -211,7 +211,10 @@ def _gloo_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_chain_protocol_gloo_world2():
+@pytest.mark.parametrize("world", [2, 4])
+def test_chain_protocol_gloo(world):
+    """The compacted, skipping chain over torch.distributed (gloo): every rank reads the same gathered
+    pending counts, so all stop at the same step, and the ranks' union equals one sequential pass."""
     import socket
 
     import torch.multiprocessing as mp
@@ -221,18 +224,20 @@ def test_chain_protocol_gloo_world2():
         port = sk.getsockname()[1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_gloo_worker, args=(r, 2, port, q)) for r in range(2)]
+    ps = [ctx.Process(target=_gloo_worker, args=(r, world, port, q)) for r in range(world)]
     for p in ps:
         p.start()
     res = sorted(q.get(timeout=120) for _ in ps)
     for p in ps:
         p.join(60)
         assert p.exitcode == 0
-    rng = np.random.default_rng(7)
+    rng = np.random.default_rng(7 + world)
     n = 30
-    cands = make_cands(rng, 2, n)
-    slices = [ToySlice(g, cands[g]) for g in range(2)]
+    cands = make_cands(rng, world, n)
+    slices = [ToySlice(g, cands[g]) for g in range(world)]
+    steps0 = res[0][1]
     for (rank, steps, sent, ex), s in zip(res, slices):
-        assert steps == 2 and ex == 3  # 1 + 2 summed over the ranks
+        assert steps == steps0 and 2 <= steps <= world  # the same stop on every rank
+        assert ex == world * (world + 1) // 2  # 1 + 2 + ... summed over the ranks
         s.sent = sent
-    check(slices, cands, 2, n)
+    check(slices, cands, world, n)
