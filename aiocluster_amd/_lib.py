@@ -26,6 +26,7 @@ GS_FD_RING = 4
 GS_NO_HELD = 8
 GS_HB8 = 16  # 8-bit heartbeat views (include/gossip_sim.h)
 GS_MV8 = 32  # 8-bit max_version views
+GS_SLICED = 64  # the sliced phase path with one slice (a world-1 run of the multi-GPU code)
 GS_NONE = 0xFFFFFFFF
 GS_E_INVALID = -1
 GS_MV_INEXACT = 0x8000
@@ -68,7 +69,7 @@ COUNTER_FIELDS = [
     "exchanges", "hb_reports", "node_deltas", "kvs_sent", "truncated", "delta_bytes", "alg_bytes", "hb_writes",
     "candidates", "live_pairs", "tomb_gc", "err_fd_overflow", "err_hist_full", "err_bad_index", "err_conflict",
     "err_fd_gc", "err_insert", "fd_gc", "q9", "pack_bytes", "err_holes", "err_hb_lag", "plane_flushes",
-    "fd_saturated", "lite_slots",
+    "fd_saturated", "lite_slots", "lag_sweeps", "lite_bytes",
 ]
 
 # Every symbol include/gossip_sim.h declares (checked by tests/test_abi.py).
@@ -82,7 +83,7 @@ EXPORTS = [
     "gs_latest_tick", "gs_flush_reports", "gs_set_ring_rows",
 ]
 
-API_VERSION = 15
+API_VERSION = 16
 MAX_PHASES = 64  # GS_MAX_PHASES
 
 

@@ -66,16 +66,18 @@ constexpr uint32_t NPL = GS_PLANES;  // report bit planes per observer row (phas
 static_assert(NPL == 16 || NPL == 32, "k_liveness stages 16 or 32 planes");
 constexpr double TICK_S = 1.0 / 64.0;
 constexpr uint32_t HB_LAG_CHECK_EVERY = 1u << 14;  // round starts + phases between heartbeat-lag sweeps
-constexpr uint32_t HB8_LAG_CHECK_EVERY = 1u << 6;  // ... with GS_HB8 (checked at round starts: < 2^7 apart)
+constexpr uint32_t HB8_LAG_CHECK_EVERY = 1u << 6;  // ... with GS_HB8 (checked before every round start and phase)
 
 enum Ctr {
     C_EXCH = 0, C_REPORTS, C_ND, C_KVS, C_TRUNC, C_DBYTES, C_ALG, C_HBW, C_CAND, C_LIVE, C_TOMBGC,
     C_E_FDOVF, C_E_HIST, C_E_IDX, C_E_CONFLICT, C_E_FDGC, C_E_INSERT, C_FDGC, C_Q9, C_PACKB, C_E_HOLES,
-    C_E_HBLAG, C_FLUSH /* host-side: plane_flushes */, C_FDSAT, C_LITE,
-    C_CEN0 = 26, C_NUM = C_CEN0 + 6  // gs_fd_census scratch slots (not part of gs_counters)
+    C_E_HBLAG, C_FLUSH /* host-side: plane_flushes */, C_FDSAT, C_LITE, C_SWEEPS /* host-side: lag_sweeps */,
+    C_LITEB,
+    C_CEN0 = 32, C_NUM = C_CEN0 + 6  // gs_fd_census scratch slots (not part of gs_counters)
 };
-static_assert(C_NUM <= 32, "counter region");
-static_assert(C_FDSAT < C_CEN0, "gs_counters fields before the census scratch");
+constexpr int CROW = 40;  // u64 slots per counter shard row (the 32 gs_counters fields, then the census scratch)
+static_assert(C_NUM <= CROW, "counter region");
+static_assert(C_LITEB < 32, "gs_counters fields");
 static_assert(sizeof(gs_counters) == 32 * 8, "gs_counters layout");
 
 struct Dev {
@@ -227,7 +229,7 @@ __device__ inline unsigned long long wave_sum(unsigned long long x) {
 }
 
 __device__ inline void shard_add(const Dev &d, int c, unsigned long long v) {
-    if (v) atomicAdd(&d.ctr[(blockIdx.x % NSHARD) * 32 + c], v);
+    if (v) atomicAdd(&d.ctr[(blockIdx.x % NSHARD) * CROW + c], v);
 }
 
 enum EvKind { EV_KEY = 0, EV_JOIN = 1, EV_LEAVE = 2 };
@@ -2200,6 +2202,7 @@ __global__ __launch_bounds__(XB, LITE_WAVES) void k_lite(Dev d, const int32_t *i
     if (lane == 0) {
         shard_add(d, C_ALG, s_alg);
         shard_add(d, C_PACKB, s_alg);
+        shard_add(d, C_LITEB, s_alg);  // k_lite's share of pack_bytes (its own roofline entry)
         shard_add(d, C_ND, s_nd);
         shard_add(d, C_KVS, s_kv);
         shard_add(d, C_CAND, s_cd);
@@ -2581,7 +2584,7 @@ __global__ __launch_bounds__(LB) void k_fd_census(Dev d, const uint8_t *up) {
 
 __global__ void k_zero_slots(Dev d, uint32_t lo, uint32_t n) {
     const uint32_t i = threadIdx.x;
-    if (i < NSHARD * n) d.ctr[(i / n) * 32 + lo + i % n] = 0ull;
+    if (i < NSHARD * n) d.ctr[(i / n) * CROW + lo + i % n] = 0ull;
 }
 
 // SamplingWindow.phi (failure_detector.py:43-53) of every target of observer o; NaN for None.
@@ -2629,7 +2632,8 @@ __global__ __launch_bounds__(LB) void k_fd_age(Dev d, uint32_t t) {
 // decoded lags are the true ones -- a view at >= 2^15 is counted in err_hb_lag (the run is reported
 // inexact) before any decode can go wrong.
 // GS_HB8 (views mod 2^8): the same argument with a sweep at least every 64 round starts + phases (checked
-// at gs_begin_round, so at most 64 + 63 increments apart) and lags >= 2^7 counted: < 2^7 + 2^7 < 2^8.
+// before every round start and every phase, so at most 64 increments apart) and lags >= 2^7 counted:
+// < 2^7 + 2^6 < 2^8.
 // GS_MV8 (max_version views mod 2^7): a view only falls behind when its owner writes (one version per
 // gs_owner_writes call at most), gs_owner_writes sweeps at least every 64 calls, and lags >= 2^6 are
 // counted: < 2^6 + 2^6 = 2^7 between sweeps.
@@ -3426,10 +3430,12 @@ struct gs_handle {
     Dev d;
     uint32_t N, NP, K, KP, C, W;
     uint32_t G, shard, col_lo, ncol;  // owner-column slice
+    bool sliced;                      // phases take the sliced path (G > 1, or GS_SLICED with one slice)
     bool reports_pending;             // phases ran since the last gs_liveness
     bool round_open;                  // gs_begin_round ran and gs_liveness has not closed the round yet
     uint32_t last_phase_tick;
     uint64_t plane_flushes;           // mid-round report replays (rounds with phases > 16 ticks after the base)
+    uint64_t lag_sweeps = 0;          // k_hb_lag sweeps run (gs_counters.lag_sweeps)
     uint32_t hb_incs;                 // rounds + phases since the last heartbeat-lag check (gs_check_heartbeat_lag)
     uint32_t mv_incs = 0;             // GS_MV8: gs_owner_writes calls since the last lag check
     uint32_t age_tick = 0;            // tick of the last window-age sweep (k_fd_age)
@@ -3439,6 +3445,7 @@ struct gs_handle {
     hipStream_t stream;
     uint32_t seq;
     bool booted;
+    bool started = false;             // a round has begun (gs_set_ring_rows refuses from then on)
     // canonical unsliced handles run a phase on candidate records (k_pass1 + k_settle); env GS_FUSED=1
     // selects the single fused k_exchange (and, on sliced handles, the fused count pass) for A/B runs
     bool split;
@@ -3634,6 +3641,10 @@ int check_phase(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t n
     if (n > h->N / 2) return fail(h, GS_E_INVALID, "a phase has at most n_nodes/2 exchanges (got %u)", n);
     if (exchange_lds(h) > 160 * 1024)
         return fail(h, GS_E_UNSUPPORTED, "slice too wide for the LDS bitmaps (%zu B)", exchange_lds(h));
+    // 8-bit heartbeat views: the lag sweep also runs mid-round, so however many phases a round has, no two
+    // sweeps are more than HB8_LAG_CHECK_EVERY owner increments apart (the sweep only reads: safe between
+    // phases, and gs_phase_pack continues the phase its gs_phase_count started)
+    if (!pack && h->d.hb8 && h->hb_incs >= HB8_LAG_CHECK_EVERY) return gs_check_heartbeat_lag(h);
     return GS_OK;
 }
 
@@ -3738,6 +3749,7 @@ int gs_create(const gs_config *cfg, gs_handle **out) {
     h->cfg = c;
     h->N = c.n_nodes;
     h->G = G;
+    h->sliced = G > 1 || (c.flags & GS_SLICED);
     h->shard = c.shard;
     h->col_lo = G > 1 ? (uint32_t)col_lo : 0u;
     h->ncol = ncol;
@@ -3779,10 +3791,14 @@ int gs_create(const gs_config *cfg, gs_handle **out) {
     b[GS_R_NID_SIZE] = NP * 2;
     b[GS_R_KEY_LEN] = KP;
     b[GS_R_STAMP] = NR * 4;
-    b[GS_R_COUNTERS] = (uint64_t)NSHARD * 32 * 8;
+    b[GS_R_COUNTERS] = (uint64_t)NSHARD * CROW * 8;
     const bool fused = getenv("GS_FUSED") && atoi(getenv("GS_FUSED"));
-    h->split = G == 1 && (c.flags & GS_CANONICAL) && !fused;
-    b[GS_R_SLICE_BITS] = (G > 1 || h->split) ? (N / 2) * 2 * (NP / 32) * 4 : 0;
+    if ((c.flags & GS_SLICED) && !(c.flags & GS_CANONICAL)) {
+        delete h;
+        return GS_E_INVALID;  // sliced phases walk owners in column order
+    }
+    h->split = !h->sliced && (c.flags & GS_CANONICAL) && !fused;
+    b[GS_R_SLICE_BITS] = (h->sliced || h->split) ? (N / 2) * 2 * (NP / 32) * 4 : 0;
     // candidate records: canonical handles (one slice: k_pass1 fused with packing; sliced: k_pass1 + k_count,
     // gather, k_pack_slice)
     const bool recs = (c.flags & GS_CANONICAL) && !fused;
@@ -3909,6 +3925,8 @@ int gs_set_ring_rows(gs_handle *h, const uint32_t *rows, uint32_t n) {
     if (!h || !h->booted || (n && !rows)) return GS_E_INVALID;
     if (n > h->cfg.ring_rows)
         return fail(h, GS_E_INVALID, "gs_set_ring_rows: %u rows for %u ring slots (gs_config.ring_rows)", n, h->cfg.ring_rows);
+    // a row switched between a compact window and a ring slot later would read a stale or empty ring
+    if (h->started) return fail(h, GS_E_INVALID, "gs_set_ring_rows: after gs_boot, before the first round only");
     std::vector<uint32_t> slot(h->N, NONE);
     for (uint32_t i = 0; i < n; i++) {
         if (rows[i] >= h->N || slot[rows[i]] != NONE)
@@ -3967,6 +3985,7 @@ int gs_begin_round(gs_handle *h, const uint8_t *up, uint32_t tick) {
     k_begin_round<<<h->N, LB, 0, h->stream>>>(h->d, up, tick);
     HIPCHK(h, hipGetLastError());
     h->round_open = true;
+    h->started = true;
     h->hb_incs++;
     return GS_OK;
 }
@@ -3976,6 +3995,7 @@ int gs_check_heartbeat_lag(gs_handle *h) {
     const uint32_t per = h->d.hb8 ? 16u : 8u, chunks = (h->ncol + LB * per - 1) / (LB * per);
     k_hb_lag<<<h->N * chunks, LB, 0, h->stream>>>(h->d, chunks);
     HIPCHK(h, hipGetLastError());
+    h->lag_sweeps++;
     h->hb_incs = 0;
     h->mv_incs = 0;
     return GS_OK;
@@ -3990,7 +4010,7 @@ int sliced_phase(gs_handle *const *hs, uint32_t nh, const int32_t *ini, const in
 int gs_run_phase(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t n, uint32_t tick) {
     int rc = check_phase(h, ini, res, n, tick);
     if (rc) return rc;
-    if (h->G > 1) {
+    if (h->sliced) {
         if (!h->comm)
             return fail(h, GS_E_UNSUPPORTED, "sliced handle without gs_comm_init: use gs_run_phase_group or gs_phase_*");
         return n ? sliced_phase(&h, 1, ini, res, n, tick) : GS_OK;
@@ -4027,7 +4047,7 @@ int gs_phase_count(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_
                    uint64_t *slice_bytes) {
     int rc = check_phase(h, ini, res, n, tick);
     if (rc) return rc;
-    if (h->G < 2) return fail(h, GS_E_UNSUPPORTED, "gs_phase_count needs a sliced handle (n_shards > 1)");
+    if (!h->sliced) return fail(h, GS_E_UNSUPPORTED, "gs_phase_count needs a sliced handle (n_shards > 1 or GS_SLICED)");
     if (!n) return GS_OK;
     if (!slice_bytes) return GS_E_INVALID;
     if ((rc = fd_age(h, tick)) || (rc = advance_planes(h, tick))) return rc;
@@ -4060,7 +4080,7 @@ int gs_phase_pack(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t
     if (h && !n) return GS_OK;
     int rc = check_phase(h, ini, res, n, tick, true);
     if (rc) return rc;
-    if (h->G < 2) return fail(h, GS_E_UNSUPPORTED, "gs_phase_pack needs a sliced handle (n_shards > 1)");
+    if (!h->sliced) return fail(h, GS_E_UNSUPPORTED, "gs_phase_pack needs a sliced handle (n_shards > 1 or GS_SLICED)");
     if (!n) return GS_OK;
     if (!slice_bytes_all || !chain || step >= h->G || (step && !chain_all)) return GS_E_INVALID;
     SliceIO io{};
@@ -4086,7 +4106,7 @@ int gs_phase_overflow(gs_handle *h, uint32_t n, const uint64_t *slice_bytes_all,
     if (!h || !h->booted) return GS_E_INVALID;
     if (count) *count = 0;
     if (!n) return GS_OK;
-    if (h->G < 2 || !h->d.cand) return fail(h, GS_E_UNSUPPORTED, "gs_phase_overflow needs a sliced canonical handle");
+    if (!h->sliced || !h->d.cand) return fail(h, GS_E_UNSUPPORTED, "gs_phase_overflow needs a sliced canonical handle");
     if (!slice_bytes_all || !chain || !list || !chainc) return GS_E_INVALID;
     const uint32_t slots = 2 * n, nb = (slots + OVB - 1) / OVB;
     k_ov_count<<<nb, OVB, 0, h->stream>>>(slice_bytes_all, slots, h->G, h->cfg.mtu, list + slots);
@@ -4108,7 +4128,7 @@ int gs_phase_chain(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_
     if (h && (!n || !count)) return GS_OK;
     int rc = check_phase(h, ini, res, n, tick, true);
     if (rc) return rc;
-    if (h->G < 2 || !h->d.cand) return fail(h, GS_E_UNSUPPORTED, "gs_phase_chain needs a sliced canonical handle");
+    if (!h->sliced || !h->d.cand) return fail(h, GS_E_UNSUPPORTED, "gs_phase_chain needs a sliced canonical handle");
     if (!list || !chain_all || !chain || !chainc || !slice_bytes_all || step < 1 || step >= h->G || count > 2 * n)
         return GS_E_INVALID;
     if (h->shard == 0) return GS_OK;  // slice 0 always finishes at step 0 (its pending entry stays 0)
@@ -4156,6 +4176,10 @@ int gather_u64(gs_handle *const *hs, uint32_t nh, uint64_t *(*src)(gs_handle *),
     if (!count) return GS_OK;
     if (nh == 1) {
         gs_handle *h = hs[0];
+        if (!h->comm) {  // GS_SLICED, one slice held alone (gs_run_phase_group): the gather is a copy
+            HIPCHK(h, hipMemcpyAsync(dst(h), src(h), count * 8, hipMemcpyDeviceToDevice, h->stream));
+            return GS_OK;
+        }
         const ncclResult_t r = ncclAllGather(src(h), dst(h), count, ncclUint64, h->comm, h->stream);
         if (r != ncclSuccess) return fail(h, GS_E_HIP, "ncclAllGather: %s", ncclGetErrorString(r));
         return GS_OK;
@@ -4253,7 +4277,7 @@ int gs_run_phase_group(gs_handle *const *hs, uint32_t n_handles, const int32_t *
         if (!hs[i] || hs[i]->shard != i || hs[i]->G != h0->G || hs[i]->N != h0->N || hs[i]->stream != h0->stream)
             return fail(h0, GS_E_INVALID, "gs_run_phase_group: handle %u is not slice %u of this cluster on one stream", i, i);
     }
-    if (h0->G == 1) return gs_run_phase(h0, ini, res, n, tick);
+    if (!h0->sliced) return gs_run_phase(h0, ini, res, n, tick);
     if (!n) return check_phase(h0, ini, res, n, tick);
     return sliced_phase(hs, n_handles, ini, res, n, tick);
 }
@@ -4480,14 +4504,14 @@ int gs_emit_delta(gs_handle *h, const gs_wire *w, uint32_t sender, uint32_t rece
 
 int gs_read_counters(gs_handle *h, gs_counters *out) {
     if (!h || !out || !h->reg[GS_R_COUNTERS]) return GS_E_INVALID;
-    std::vector<unsigned long long> buf((size_t)NSHARD * 32);
+    std::vector<unsigned long long> buf((size_t)NSHARD * CROW);
     HIPCHK(h, hipMemcpyAsync(buf.data(), h->reg[GS_R_COUNTERS], buf.size() * 8, hipMemcpyDeviceToHost, h->stream));
     HIPCHK(h, hipStreamSynchronize(h->stream));
-    uint64_t acc[32] = {0};
+    uint64_t acc[32] = {0};  // the gs_counters fields (the census scratch follows them in each row)
     for (int s = 0; s < NSHARD; s++)
-        for (int c = 0; c < 32; c++) acc[c] += buf[(size_t)s * 32 + c];
+        for (int c = 0; c < 32; c++) acc[c] += buf[(size_t)s * CROW + c];
     acc[C_FLUSH] = h->plane_flushes;
-    for (int c = C_CEN0; c < C_NUM; c++) acc[c] = 0;  // census scratch, not counters
+    acc[C_SWEEPS] = h->lag_sweeps;
     memcpy(out, acc, sizeof acc);
     return GS_OK;
 }
@@ -4520,6 +4544,7 @@ int gs_reset_counters(gs_handle *h) {
     if (!h || !h->reg[GS_R_COUNTERS]) return GS_E_INVALID;
     HIPCHK(h, hipMemsetAsync(h->reg[GS_R_COUNTERS], 0, h->bytes[GS_R_COUNTERS], h->stream));
     h->plane_flushes = 0;
+    h->lag_sweeps = 0;
     return GS_OK;
 }
 
@@ -4615,12 +4640,12 @@ int gs_fd_census(gs_handle *h, const uint8_t *up, gs_census *out) {
     dim3 grid((h->ncol + LB - 1) / LB, h->N);
     k_fd_census<<<grid, LB, 0, h->stream>>>(h->d, up);
     HIPCHK(h, hipGetLastError());
-    std::vector<unsigned long long> buf((size_t)NSHARD * 32);
+    std::vector<unsigned long long> buf((size_t)NSHARD * CROW);
     HIPCHK(h, hipMemcpyAsync(buf.data(), h->reg[GS_R_COUNTERS], buf.size() * 8, hipMemcpyDeviceToHost, h->stream));
     HIPCHK(h, hipStreamSynchronize(h->stream));
     uint64_t acc[5] = {0, 0, 0, 0, 0};
     for (int sh = 0; sh < NSHARD; sh++)
-        for (int i = 0; i < 5; i++) acc[i] += buf[(size_t)sh * 32 + C_CEN0 + i];
+        for (int i = 0; i < 5; i++) acc[i] += buf[(size_t)sh * CROW + C_CEN0 + i];
     out->up_pairs = acc[0];
     out->up_dead = acc[1];
     out->up_live = acc[2];

@@ -34,7 +34,8 @@ from datetime import timedelta
 import numpy as np
 
 from . import _lib
-from ._lib import GS_CANONICAL, GS_FD_RING, GS_HB8, GS_MV8, GS_NO_HELD, GS_NONE, GS_TOMBSTONES, REGION, TICK_US, GsError
+from ._lib import (GS_CANONICAL, GS_FD_RING, GS_HB8, GS_MV8, GS_NO_HELD, GS_NONE, GS_SLICED, GS_TOMBSTONES, REGION,
+                   TICK_US, GsError)
 from .entities import ClusterSnapshot, NodeId, NodeState, VersionedValue, VersionStatusEnum
 from .pbsize import nodeid_size
 
@@ -171,7 +172,7 @@ class GossipSim:
                  tombstones: bool = True, fd_ring: bool | None = None, hist_cap: int = 64,
                  nid_sizes: list[int] | None = None, initial_ops: list[np.ndarray] | None = None,
                  canonical: bool | None = None, shards: int = 1, shard: int = 0, held: bool = True,
-                 ring_rows=None, hb8: bool = False, mv8: bool = False):
+                 ring_rows=None, hb8: bool = False, mv8: bool = False, sliced: bool = False):
         import torch
 
         if not torch.cuda.is_available():
@@ -213,6 +214,11 @@ class GossipSim:
         self.mv8 = bool(mv8)
         if mv8:
             flags |= GS_MV8
+        # GS_SLICED: the sliced phase path (count, gather, pack) even with one slice -- the multi-GPU code on
+        # one GPU (a world-1 RCCL communicator or process group); phases then go through ShardGroup
+        self.sliced = shards > 1 or bool(sliced)
+        if sliced:
+            flags |= GS_SLICED
         W = int(cfg["window"])
         # sampled rings: these observer rows keep interval rings (exact eviction), the others compact windows
         self.ring_rows = sorted(set(int(x) for x in ring_rows)) if ring_rows else []
@@ -373,7 +379,7 @@ class GossipSim:
         return ini, res
 
     def run_phase_arrays(self, t: int, initiators, responders):
-        if self.shards > 1:
+        if self.sliced:
             raise GsError("a column slice runs phases through ShardGroup (gs_phase_count / gs_phase_pack)")
         ini, res = self._pairs_dev(initiators, responders)
         n = int(ini.numel())
@@ -461,10 +467,15 @@ class GossipSim:
         self._chk(self.L.gs_kernel_times(self.h, C.byref(kt)), "gs_kernel_times")
         return {k: (kt.ms[i], int(kt.launches[i])) for i, k in enumerate(_lib.KT_KINDS)}
 
-    def check(self) -> dict:
-        """Raise if any device-side check failed; return the counters."""
+    def check(self, accept_saturated: bool = False) -> dict:
+        """Raise if any device-side check failed; return the counters.  With sampled rings (``ring_rows``) a
+        compact row's window that would need an eviction is counted in fd_saturated: the ring rows stay exact,
+        the compact rows do not (BoundedArrayStats, failure_detector.py:131-162), so that raises too unless the
+        caller accepts the sampled-ring contract (``accept_saturated``)."""
         c = self.counters()
         errs = {k: v for k, v in c.items() if k.startswith("err_") and v}
+        if c["fd_saturated"] and not accept_saturated:
+            errs["fd_saturated"] = c["fd_saturated"]
         if errs.get("err_fd_gc"):
             raise GsError(f"FailureDetector.garbage_collect is due in a canonical (warm, index-order) state; "
                           f"removing nodes needs the general layout (init='cold' or canonical=False): {errs}")
@@ -532,11 +543,12 @@ class GossipSim:
         hi = self.n if row_hi is None else row_hi
         self._chk(self.L.gs_materialize_held(self.h, row_lo, hi), "gs_materialize_held")
 
-    def horizon(self) -> dict:
+    def horizon(self, rounds: int | None = None) -> dict:
         """Headroom to the two bounds of the exact compact layout: the most intervals any
         sampling window holds since its last reset (compact windows: err_fd_overflow at W; the ring
         evicts exactly), and the most writes of any (owner, key) of this slice (err_hist_full at
-        hist_cap - 1)."""
+        hist_cap - 1).  With ``rounds`` (rounds run so far) each bound is also projected linearly: the rounds
+        left until the fastest-growing window / (owner, key) reaches it at the rate seen so far."""
         torch = self.torch
         sb = _lib.fd_sum_bits(int(self.cfg["window"]))
         fd = self.region("FD", torch.int32, (self.n, self.np_))
@@ -545,9 +557,21 @@ class GossipSim:
             blk = fd[r0:r0 + 8192, : self.ncol]
             mx = max(mx, int(((blk >> sb) & ((1 << (32 - sb)) - 1)).max().item()))
         lw = self.region("LAST_W", torch.uint8, (self.ncol, self.kp))[:, : self.k]
-        return {"max_window_count": mx, "window": int(self.cfg["window"]),
-                "fd_ring": "all rows" if self.flags & GS_FD_RING else f"{len(self.ring_rows)} sampled rows",
-                "max_writes_per_owner_key": int(lw.max().item()), "hist_cap_writes": self.hist_cap - 1}
+        mw = int(lw.max().item())
+        c = self.counters()
+        out = {"max_window_count": mx, "window": int(self.cfg["window"]),
+               "fd_ring": "all rows" if self.flags & GS_FD_RING else f"{len(self.ring_rows)} sampled rows",
+               "max_writes_per_owner_key": mw, "hist_cap_writes": self.hist_cap - 1,
+               "fd_saturated": c["fd_saturated"], "err_fd_overflow": c["err_fd_overflow"],
+               "err_hist_full": c["err_hist_full"], "err_hb_lag": c["err_hb_lag"]}
+        if rounds:
+            W = int(self.cfg["window"])
+            out["rounds_run"] = int(rounds)
+            # compact windows: appends since the last reset grow by at most one per report; ring windows evict
+            out["projected_rounds_to_window"] = (None if self.flags & GS_FD_RING else
+                                                 int((W - mx) * rounds / max(mx, 1)))
+            out["projected_rounds_to_hist_cap"] = int((self.hist_cap - 1 - mw) * rounds / max(mw, 1))
+        return out
 
     def inexact_views(self) -> int:
         """Views with holes (GS_MV_INEXACT set): those whose HELD row the exchange kernel keeps."""

@@ -102,22 +102,35 @@ def cpu_baseline(sim, cfg, rd, sample: int, min_seconds: float = 10.0, threads: 
         for a, b in mine[i]:
             L.orc_exchange(hs[i], a, b, t * rowcheck.TICK_US)
 
+    # host cores: thread i pinned to the i-th CPU this process may use (the main thread to the next one)
+    cpus = sorted(os.sched_getaffinity(0))
+    pin = cpus[: T + 1] if len(cpus) > T else None
+
+    def pin_to(k):
+        if pin is not None:
+            os.sched_setaffinity(0, {pin[k]})  # Linux: pid 0 = the calling thread
+
+    load0 = os.getloadavg()[0]
     # one thread: every handle's pairs in turn, on restored rows, until ~min_seconds/3 are timed
-    dt1, reps1 = 0.0, 0
-    while dt1 < min_seconds / 3 or reps1 == 0:
+    dt1, reps1, rate1 = 0.0, 0, []
+    pin_to(T)
+    while dt1 < min_seconds / 3 or reps1 < 3:
         for i in range(T):
             restore(i)
         t0 = time.perf_counter()
         for i in range(T):
             run(i)
-        dt1 += time.perf_counter() - t0
+        dt = time.perf_counter() - t0
+        dt1 += dt
         reps1 += 1
+        rate1.append(len(pairs) / dt)
     # T threads (ctypes drops the GIL during each oracle call), a barrier around every timed pass
     import threading
     bar = threading.Barrier(T + 1)
     stop = [False]
 
     def worker(i):
+        pin_to(i)
         while True:
             bar.wait()  # restore
             if stop[0]:
@@ -130,26 +143,44 @@ def cpu_baseline(sim, cfg, rd, sample: int, min_seconds: float = 10.0, threads: 
     ths = [threading.Thread(target=worker, args=(i,), daemon=True) for i in range(T)]
     for th in ths:
         th.start()
-    dtT, repsT = 0.0, 0
-    while dtT < min_seconds or repsT == 0:
+    dtT, repsT, rateT = 0.0, 0, []
+    while dtT < min_seconds or repsT < 3:
         bar.wait()
         bar.wait()
         t0 = time.perf_counter()
         bar.wait()
-        dtT += time.perf_counter() - t0
+        dt = time.perf_counter() - t0
+        dtT += dt
         repsT += 1
+        rateT.append(len(pairs) / dt)
     stop[0] = True
     bar.wait()
     for th in ths:
         th.join()
+    if pin is not None:
+        os.sched_setaffinity(0, set(cpus))
     ro.close()
     n, K = sim.n, sim.k
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), model)
+    except OSError:
+        pass
+    q = lambda xs, f: float(np.percentile(np.asarray(xs), f))  # noqa: E731
     return {
-        "value": len(pairs) * repsT / dtT,
+        "value": q(rateT, 50),
         "unit": "exchanges/s",
         "cores": T,
         "kind": "port",
-        "single_core_value": len(pairs) * reps1 / dt1,
+        "statistic": f"median of {repsT} timed passes (p10 {q(rateT, 10):.0f}, p90 {q(rateT, 90):.0f}; mean "
+                     f"{len(pairs) * repsT / dtT:.0f})",
+        "single_core_value": q(rate1, 50),
+        "single_core_statistic": f"median of {reps1} passes (p10 {q(rate1, 10):.0f}, p90 {q(rate1, 90):.0f})",
+        "host": {"cpu_model": model, "cpus_allowed": len(cpus),
+                 "pinning": (f"thread i on CPU {pin[0]}+i, single-thread runs on CPU {pin[T]}" if pin is not None
+                             else "unpinned (fewer allowed CPUs than threads)"),
+                 "loadavg_1min_before": load0},
         "sample": f"{len(pairs)} exchanges (disjoint pairs of the first phase of the round after the timed ones) "
                   f"at N={n}, K={K}, on oracle rows copied from the device state after that round's "
                   f"gs_begin_round, dealt to {T} host threads (one oracle handle each) and run {repsT}x on "
@@ -250,6 +281,7 @@ def roofline(sims, local_c, exch, kt, elapsed, torch, dev, rank, group, workload
     region without tombstones, so that formula overstates the bytes."""
     alg = sum(x["alg_bytes"] for x in local_c)
     packb = sum(x["pack_bytes"] for x in local_c)
+    liteb = sum(x["lite_bytes"] for x in local_c)  # k_lite's part of pack_bytes
     ncols = sum(s_.ncol for s_ in sims)
     fused = kt["pack"][1] == 0
     per = {}
@@ -261,7 +293,9 @@ def roofline(sims, local_c, exch, kt, elapsed, torch, dev, rank, group, workload
         if kind == "pass1":
             b = (alg if fused else alg - packb) / launches
         elif kind == "pack":
-            b = packb / launches
+            b = (packb - liteb) / launches
+        elif kind == "lite":
+            b = liteb / launches
         ent = {"kernel": ("k_pass1<fused>: pass 1, then packing + apply_delta in the same workgroup"
                           if (fused and kind == "pass1") else KERNEL_OF[kind]),
                "avg_launch_ms": avg_s * 1e3, "launches": launches, "share_of_step": ms / 1e3 / elapsed}
@@ -365,7 +399,7 @@ def config4_leg(args, world: int, rank: int, dist, dev) -> dict:
     exch = sum(plans[r]["exchanges"] for r in range(S + W, S + W + T))
     assert c["exchanges"] == exch, (c["exchanges"], exch)
     _, el_max = aggregate(0.0, el, dist, dev)
-    hz = sim.horizon()
+    hz = sim.horizon(rounds=S + W + T)
     sim.close()
     del sim, grp
     torch.cuda.empty_cache()
@@ -615,7 +649,8 @@ def main():
         errs = {k: v for k, v in sims[0].counters().items() if k.startswith("err_") and v}
         ps["device_errors"] = errs
         ps["exact"] = not errs
-    horizon = sims[0].horizon()
+    rounds_run = R0 + args.steps + (1 if cpu is not None else 0) + (ps_steps + 1 if ps is not None else 0)
+    horizon = sims[0].horizon(rounds=rounds_run)
     sliced = group is not None  # (the config-4 leg below releases the headline's handles first)
     c4 = None
     if args.config4_steps and (world == C4_GPUS or args.config4):
@@ -661,7 +696,8 @@ def main():
             **({"ABLATION_RESULTS_INVALID": os.environ["GS_ABLATE"]} if os.environ.get("GS_ABLATE") else {}),
             "counters": {**{k: v for k, v in c.items() if not k.startswith("err_")}, "inexact_views": inexact},
             # headroom to the exact layout's two bounds: err_fd_overflow at a window count of W (compact
-            # windows), err_hist_full at hist_cap - 1 writes of one (owner, key)
+            # windows), err_hist_full at hist_cap - 1 writes of one (owner, key); each projected in rounds at
+            # the growth rate of this run; fd_saturated (sampled rings' inexact compact rows) raises in check()
             "exactness": horizon,
             "config4": c4,
         }

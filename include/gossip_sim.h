@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define GS_API_VERSION 15
+#define GS_API_VERSION 16
 #define GS_MAX_PHASES 64  /* gs_schedule_phases: phases per round */
 #define GS_TICK_US 15625u
 #define GS_NONE 0xFFFFFFFFu
@@ -55,14 +55,17 @@ extern "C" {
                              get holes is counted in err_holes.  16 B less per pair at K = 16 (config 4) */
 #define GS_HB8 16u        /* 8-bit heartbeat views: GS_R_HB is u8 [N][NP] (mod 2^8, decoded against the owner's
                              own heartbeat like the 16-bit store), exact while every view lags its owner by < 2^8;
-                             gs_begin_round sweeps the lags at least every 64 round starts + phases and counts
-                             a lag >= 128 in err_hb_lag.  Needs GS_CANONICAL, n_keys <= 16 and the record phases
+                             gs_begin_round and the phases sweep the lags at least every 64 round starts + phases
+                             and count a lag >= 128 in err_hb_lag.  Needs GS_CANONICAL, n_keys <= 16 and the record phases
                              (not env GS_FUSED / GS_PACK=fused): half the heartbeat bytes of every exchange */
 #define GS_MV8 32u        /* 8-bit max_version views (needs GS_HB8 and !GS_TOMBSTONES): GS_R_MV is u8 [N][NP] =
                              version mod 2^7 | GS_MV_INEXACT >> 8, decoded against the owner's own max_version
                              (GS_R_SELF_MV); exact while every view lags its owner by < 2^7 versions:
                              gs_owner_writes sweeps the lags at least every 64 calls and counts a lag >= 2^6
                              in err_hb_lag */
+#define GS_SLICED 64u     /* phases take the sliced path (gs_phase_count / gather / gs_phase_pack, or gs_run_phase
+                             over a gs_comm_init communicator) even with one slice (n_shards <= 1): a one-GPU
+                             world-1 run of the multi-GPU code (needs GS_CANONICAL) */
 
 /* owner write ops (NodeState.set/delete/set_with_ttl/delete_after_ttl, state.py:137-180) */
 #define GS_OP_SET 0u
@@ -75,7 +78,7 @@ typedef struct gs_config {
     uint32_t n_keys;                /* K <= 64 keys per node */
     uint32_t hist_cap;              /* C <= 255: writes kept per (owner, key), ordinal 0 = absent */
     uint32_t mtu;                   /* Config.max_payload_size (entities.py:105) */
-    uint32_t flags;                 /* GS_CANONICAL | GS_TOMBSTONES | GS_FD_RING | GS_NO_HELD | GS_HB8 | GS_MV8 */
+    uint32_t flags;                 /* GS_CANONICAL | GS_TOMBSTONES | GS_FD_RING | GS_NO_HELD | GS_HB8 | GS_MV8 | GS_SLICED */
     uint32_t window;                /* FailureDetectorConfig.sampling_window_size (entities.py:88) */
     uint32_t max_interval_ticks;    /* FailureDetectorConfig.max_interval (entities.py:89) */
     uint32_t tombstone_grace_ticks; /* Config.marked_for_deletion_grace_period (entities.py:101) */
@@ -132,7 +135,7 @@ enum gs_region {
     GS_R_NID_SIZE,    /* u16 [NP]      NodeIdPb size per owner column (entities.py:62-72) */
     GS_R_KEY_LEN,     /* u8  [KP]      UTF-8 key length per key index */
     GS_R_STAMP,       /* u32 [N rounded to 64] per-node phase stamp (conflict check) */
-    GS_R_COUNTERS,    /* u64 [64][32]  sharded gs_counters (summed by gs_read_counters) */
+    GS_R_COUNTERS,    /* u64 [64][40]  sharded gs_counters (summed by gs_read_counters) and census scratch */
     GS_R_SLICE_BITS,  /* u32 [N/2][2][NP/32] stale-owner bitmaps per exchange and direction: between
                                         gs_phase_count and gs_phase_pack (n_shards > 1), and between the two
                                         kernels of a canonical one-slice gs_run_phase */
@@ -209,7 +212,11 @@ typedef struct gs_counters {
                                   windows are exact only up to W intervals; the ring rows are exact) */
     uint64_t lite_slots;       /* (exchange, direction) slots whose whole delta k_lite sized and applied (the exact
                                   packer skipped them) */
-    uint64_t reserved[7];
+    uint64_t lag_sweeps;       /* host count: heartbeat / max_version lag sweeps run (gs_check_heartbeat_lag, by
+                                  itself or from gs_begin_round / the phases / gs_owner_writes) */
+    uint64_t lite_bytes;       /* the part of pack_bytes moved by k_lite (records read, version-log entries, NodeId
+                                  sizes, the receivers' max_version stores) */
+    uint64_t reserved[5];
 } gs_counters;
 
 /* Failure-detector membership census (gs_fd_census): (observer, target) pairs with the observer up and

@@ -33,12 +33,32 @@ def _run(sim, plans, rounds):
     sim.check()
 
 
-@pytest.mark.parametrize("hb8", [True, False], ids=["hb8", "hb16"])
-def test_config3_65536_every_phase_of_two_rounds_matches_oracle(hb8):
+def _write_burst(sim, torch, tick, calls=70, per_call=2048, seed=7):
+    """``calls`` owner-write batches at ``tick`` (distinct owners per batch, any key): more than the 64
+    gs_owner_writes calls between GS_MV8 lag sweeps, so the sweep inside gs_owner_writes runs, while no
+    owner writes often enough (a few versions each) for a view to reach the 2^6 sweep bound."""
+    rng = np.random.default_rng(seed)
+    vid = 1 << 25
+    for _ in range(calls):
+        ops = np.zeros((per_call, 5), dtype=np.int32)
+        ops[:, 0] = rng.permutation(sim.n)[:per_call]
+        ops[:, 1] = rng.integers(0, sim.k, per_call)
+        ops[:, 3] = vid + np.arange(per_call)
+        ops[:, 4] = 12
+        vid += per_call
+        sim.owner_writes(ops.view(np.uint32), tick)
+
+
+@pytest.mark.parametrize("layout", ["hb16", "hb8", "hb8mv8"])
+def test_config3_65536_every_phase_of_two_rounds_matches_oracle(layout):
     """BASELINE config 3 (the bench workload): 65,536 nodes x 16 keys, fanout 3, warm, 5 % writes + 5 %
-    up/down churn, window 1000, mtu 65,507, prefix-view layout, 8-bit (the bench's) or 16-bit heartbeat
-    views; 20 settle rounds, the owner tables vs the write stream, then every phase of rounds 20 and 21 on
-    16 random exchanges each."""
+    up/down churn, window 1000, mtu 65,507, prefix-view layout with HELD rows for views with holes, in
+    three view widths: 16-bit heartbeat + max_version views, 8-bit heartbeats (GS_HB8), and the bench's
+    own layout, 8-bit heartbeats + 8-bit max_versions (GS_HB8 + GS_MV8, ``bench.py`` default); 20 settle
+    rounds, the owner tables vs the write stream, then every phase of rounds 20 and 21 on 16 random
+    exchanges each.  In the bench's layout round 21 starts with a burst of 70 owner-write batches, so the
+    max_version lag sweep of gs_owner_writes runs (every 64 calls) and the phases then spread the new
+    versions, checked against the oracle; no view may reach the sweep bound (err_hb_lag = 0)."""
     import torch
 
     n, K = 65536, 16
@@ -46,13 +66,18 @@ def test_config3_65536_every_phase_of_two_rounds_matches_oracle(hb8):
     spec = WorkloadSpec(n=n, k=K, fanout=3, seed=0, init="warm", write_frac=0.05, down_frac=0.05, down_rounds=3)
     boot = driver.boot_ops(n, K)
     sim = GossipSim(synthetic_node_ids(n), key_names(K), cfg, init="warm", tombstones=False, fd_ring=False,
-                    hist_cap=16, initial_ops=boot, hb8=hb8)
+                    hist_cap=16, initial_ops=boot, hb8=layout != "hb16", mv8=layout == "hb8mv8")
     dev = sim.device
     plans = driver.prepare(spec, 22, torch, dev)
     _run(sim, plans, 20)
     assert check_owner_tables(sim, plan_batches(K, n, plans[:20], boot)) is None
     for r in (20, 21):
         rd = plans[r]
+        if r == 21 and layout == "hb8mv8":
+            sweeps = sim.check()["lag_sweeps"]
+            _write_burst(sim, torch, rd["t"])
+            c = sim.check()  # err_hb_lag = 0: the sweeps found every max_version lag < 2^6
+            assert c["lag_sweeps"] > sweeps, (sweeps, c["lag_sweeps"])
         driver.begin([sim], rd)
         diff, info = check_round_rows(sim, cfg, rd, sample=16, seed=r)
         assert diff is None, f"round {r}: {diff}"
@@ -60,6 +85,7 @@ def test_config3_65536_every_phase_of_two_rounds_matches_oracle(hb8):
         assert info["phases"] >= 8 and info["node_deltas"] > 0 and info["hb_reports"] > 0, info
     c = sim.check()
     assert c["exchanges"] > 0
+    assert (c["lag_sweeps"] > 0) == (layout != "hb16")  # 8-bit views: swept every <= 64 round starts + phases
     sim.close()
 
 

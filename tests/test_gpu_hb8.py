@@ -194,3 +194,59 @@ def test_mv8_refused_without_hb8_or_with_tombstones():
         GossipSim(ids, key_names(2), dict(DEFAULT_CFG), "warm", None, tombstones=False, mv8=True)
     with pytest.raises(GsError):
         GossipSim(ids, key_names(2), dict(DEFAULT_CFG), "warm", None, tombstones=True, hb8=True, mv8=True)
+
+
+def _long_round(gpu, orc, phases, t0):
+    """One round of ``phases`` phases at ticks t0 + 1 .. t0 + phases: node 1 answers in every phase (its
+    own heartbeat rises by one per phase), nodes 6 and 7 are up but take part in none (their views of 1
+    fall behind by one per phase)."""
+    import torch
+
+    n = gpu.n
+    up = np.ones(n, np.uint8)
+    up_dev = torch.from_numpy(up).to(gpu.device)
+    gpu.begin_round(t0, up_dev)
+    if orc is not None:
+        orc.begin_round(t0, up)
+    for p in range(phases):
+        pairs = [(0, 1), (2, 3), (4, 5)] if p % 2 == 0 else [(2, 1), (4, 3), (0, 5)]
+        gpu.run_phase(t0 + 1 + p, pairs)
+        if orc is not None:
+            orc.run_phase(t0 + 1 + p, pairs)
+    gpu.liveness(t0 + 1 + phases, up_dev)
+    if orc is not None:
+        orc.liveness(t0 + 1 + phases, up)
+
+
+def test_hb8_round_of_100_phases_matches_oracle():
+    """A round may hold more phases than the 64 round starts + phases between lag sweeps: the
+    phases sweep too, so the views of an idle node, lagging ~100 behind by the round's end, stay exact;
+    the device matches the C oracle array for array and the mid-round sweeps ran clean."""
+    n = 8
+    ids, keys = synthetic_node_ids(n), key_names(2)
+    init = {j: [(0, f"v{j}")] for j in range(n)}
+    gpu = GossipSim(ids, keys, dict(DEFAULT_CFG), "warm", init, tombstones=False, fd_ring=True, hist_cap=8,
+                    hb8=True, mv8=True)
+    orc = OracleSim(ids, keys, dict(DEFAULT_CFG), "warm", init)
+    _long_round(gpu, orc, 100, round_tick(0))
+    want = orc.export()
+    assert np.asarray(want["hb"])[1, 1] - np.asarray(want["hb"])[7, 1] >= 100  # the idle view's lag
+    diff = compare_exports(gpu.export(), want)
+    assert diff is None, diff
+    c = gpu.check()
+    assert c["err_hb_lag"] == 0 and c["lag_sweeps"] >= 1 and c["plane_flushes"] >= 1
+
+
+def test_hb8_round_of_300_phases_is_reported_not_silently_wrong():
+    """300 phases in one round: the idle nodes' views of node 1 would fall 2^8 behind and decode wrongly.
+    A mid-round sweep counts them in err_hb_lag (at 2^7) before that happens, so the run raises."""
+    from aiocluster_amd._lib import GsError
+
+    n = 8
+    ids, keys = synthetic_node_ids(n), key_names(2)
+    init = {j: [(0, f"v{j}")] for j in range(n)}
+    gpu = GossipSim(ids, keys, dict(DEFAULT_CFG), "warm", init, tombstones=False, fd_ring=True, hist_cap=8,
+                    hb8=True)
+    _long_round(gpu, None, 300, round_tick(0))
+    with pytest.raises(GsError, match="err_hb_lag"):
+        gpu.check()

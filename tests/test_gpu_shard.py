@@ -68,6 +68,31 @@ def test_native_group_matches_single_handle(n, G, mtu):
     assert c1["truncated"] > 0
 
 
+@pytest.mark.parametrize("mv8", [False, True], ids=["hb16", "hb8mv8"])
+def test_eight_slices_skip_chain_steps_and_match_single_handle(mv8):
+    """G = 8 in-process slices (LocalComm) with a binding mtu: deltas cut across slice boundaries, and the
+    skipping chain (a pending slice resumes from its nearest finished predecessor when the slices between
+    cannot add a NodeDelta) must give exactly one handle's state, while some chained phase resolves in
+    fewer than G pack steps."""
+    n, G = 512, 8
+    spec = WorkloadSpec(n=n, k=8, fanout=3, seed=88, init="warm", write_frac=0.3, down_frac=0.05, down_rounds=3)
+    scen = make_scenario("skip512x8", spec, 10, {"mtu": 900})
+    kw = dict(tombstones=False, fd_ring=False, hb8=mv8, mv8=mv8)
+    one = make_backend(GossipSim, scen, **kw)
+    grp = sharded(scen, G, **kw)
+    for r in range(len(scen["rounds"])):
+        replay_round(one, scen, r)
+        replay_round(grp, scen, r)
+        diff = compare_exports(grp.export(), one.export())
+        assert diff is None, f"round {r}: {diff}"
+    c1, cg = one.check(), grp.check()
+    for k in ("exchanges", "hb_reports", "node_deltas", "kvs_sent", "truncated", "delta_bytes", "hb_writes"):
+        assert cg[k] == c1[k], (k, cg[k], c1[k])
+    chained = [s for s in grp.phase_steps if s > 1]
+    assert c1["truncated"] > 0 and chained, grp.phase_steps
+    assert min(chained) < G, f"no chained phase skipped a step: {sorted(set(chained))}"
+
+
 def test_read_rows_copies_out_regions():
     """gs_read_rows (blocking copy-out of observer rows) returns the bytes of the bound regions, and
     complete HELD rows for prefix views (materialized first)."""
