@@ -67,6 +67,7 @@ static_assert(NPL == 16 || NPL == 32, "k_liveness stages 16 or 32 planes");
 constexpr double TICK_S = 1.0 / 64.0;
 constexpr uint32_t HB_LAG_CHECK_EVERY = 1u << 14;  // round starts + phases between heartbeat-lag sweeps
 constexpr uint32_t HB8_LAG_CHECK_EVERY = 1u << 6;  // ... with GS_HB8 (checked before every round start and phase)
+constexpr uint32_t MV8_LAG_CHECK_EVERY = 1u << 5;  // GS_MV8: gs_owner_writes calls between max_version lag sweeps
 
 enum Ctr {
     C_EXCH = 0, C_REPORTS, C_ND, C_KVS, C_TRUNC, C_DBYTES, C_ALG, C_HBW, C_CAND, C_LIVE, C_TOMBGC,
@@ -146,6 +147,11 @@ struct Dev {
     // both 8-bit views -- the heartbeat needs only R mod 2^8 and whether R is 0 (R < 2^15 kept exactly),
     // the max_version word only M (< 2^15)
     uint32_t *self_pk;
+    // GS_MV8 (pass 1 of the record phases, k_pass1v): per 16-owner group, bits 0-15 = "owner j's own heartbeat
+    // is < 2^8" (an 8-bit view of it stored as 0 is then the heartbeat 0), bits 16-31 = "owner j is hot": at the
+    // last lag sweep some view of j lagged by >= HOT_HB heartbeats or HOT_MV versions (GS_R_P1FLAGS)
+    uint32_t *p1flags;
+    uint32_t pl16;  // report planes in the 16-column layout of k_pass1v (plane16_bit), else the ballot layout
     // event stream (gs_set_events): records {observer, owner, key | kind << 8, old version, new version,
     // tick, seq, 0}; kind 0 = on_key_change, 1 = node join, 2 = node leave; seq orders them (gossip_sim.h,
 // gs_set_events).  ev == nullptr: off
@@ -209,6 +215,12 @@ __device__ inline uint32_t fd_st(uint32_t st, const Fd &f) {
 }
 
 __device__ inline int lane_id() { return (int)__lane_id(); }
+// pass 1's row halves (one wave each; candidate lists per half): columns [0, H) and [H, ncol), H a multiple of
+// the pass's step -- 256 columns (k_pass1: 4 per lane) or 1024 (k_pass1v: 16 per lane)
+__device__ inline uint32_t half_cols(const Dev &d) {
+    const uint32_t m = d.pl16 ? 1023u : 255u;
+    return ((d.ncol + 1u) / 2u + m) & ~m;
+}
 
 __device__ inline bool bit(const uint32_t *bm, uint32_t j) { return (bm[j >> 5] >> (j & 31u)) & 1u; }
 
@@ -312,8 +324,15 @@ __device__ __forceinline__ uint32_t mv_enc8(uint32_t w) { return (w & 0x7Fu) | (
 __device__ __forceinline__ uint32_t self_pack(uint32_t R, uint32_t M) {
     return (R & 0x7FFFu) | (R >= 0x8000u ? 0x8000u : 0u) | (M << 16);
 }
+__device__ __forceinline__ void set_small(const Dev &d, uint32_t j, uint32_t R) {
+    if (!d.p1flags) return;
+    const uint32_t b = 1u << (j & 15u), w = d.p1flags[j >> 4];
+    if (R < 256u && !(w & b)) atomicOr(&d.p1flags[j >> 4], b);
+    else if (R >= 256u && (w & b)) atomicAnd(&d.p1flags[j >> 4], ~b);
+}
 __device__ __forceinline__ void self_repack(const Dev &d, uint32_t j) {
     if (d.self_pk) d.self_pk[j] = self_pack(d.self_hb[j], d.self_mv[j]);
+    set_small(d, j, d.self_hb[j]);
 }
 __device__ __forceinline__ uint32_t mv_word(const Dev &d, size_t p, uint32_t j) {  // j: local owner column
     return d.mv8 ? mv_dec8(reinterpret_cast<const uint8_t *>(d.mv)[p], d.self_mv[j]) : (uint32_t)d.mv[p];
@@ -1044,7 +1063,7 @@ template <int KW, bool COUNT>
 __device__ __forceinline__ void pack_records(const Dev &d, uint32_t snd, uint32_t rcv, const DigestSide &ds,
                                              size_t slot, uint16_t *wbuf, uint32_t t, WStats &st, bool &tomb,
                                              PackState &pst) {
-    const uint32_t H = ((d.ncol + 1u) / 2u + 255u) & ~255u;
+    const uint32_t H = half_cols(d);
     const uint32_t words = d.NP / 32;
     for (uint32_t hf = 0; hf < 2 && (COUNT || d.spec || !pst.stop); hf++) {
         const uint32_t nh = d.cand_n[slot * 2 + hf];
@@ -1497,7 +1516,7 @@ __global__ __launch_bounds__(XB, (KW == 4 ? (FUSE ? P1_WAVES : MV8 ? P1N_WAVES :
     uint32_t *gBA = d.sbits + (size_t)e * 2 * words, *gAB = gBA + words;
     // wave w streams row half w (columns [w*H, min((w+1)*H, ncol)), H a multiple of 256), so its candidate
     // lists hold that half in column order and the packer reads half 0's list, then half 1's
-    const uint32_t H = ((d.ncol + 1u) / 2u + 255u) & ~255u;
+    const uint32_t H = half_cols(d);
     const uint32_t lo = (uint32_t)wid * H, hi = min(lo + H, d.ncol);
     uint2 *LBA = d.cand + ((size_t)e * 4 + 0 * 2 + wid) * GS_CAND_CAP;
     uint2 *LAB = d.cand + ((size_t)e * 4 + 1 * 2 + wid) * GS_CAND_CAP;
@@ -1593,6 +1612,312 @@ __global__ __launch_bounds__(XB, (KW == 4 ? (FUSE ? P1_WAVES : MV8 ? P1N_WAVES :
             shard_add(d, C_CAND, p_cd);
         }
     }
+}
+
+// ---------------------------------------------------------------- k_pass1v (GS_HB8 + GS_MV8, round 4)
+// Pass 1 of a canonical record phase on 8-bit views, byte-parallel: each lane takes 16 consecutive owner
+// columns per step (one 16-byte load per row and region), and the per-column rules of pass1_grp run on four
+// views per 32-bit word.  Two views of one owner compare without the owner's own value: at the last lag sweep
+// no view of a column or row that is not hot lagged by HOT_HB heartbeats / HOT_MV versions or more, and since
+// then it fell behind by at most 64 / 32 more (k_hb_lag), so two such heartbeat views differ by less than 2^7
+// and two max_version views by less than 2^6: the sign of their difference mod 2^8 (mod 2^7) orders them.  A
+// stored heartbeat byte 0 is the heartbeat 0 exactly when the owner's own heartbeat is < 2^8 (GS_R_P1FLAGS
+// small bits).  Everything else -- the exchange's own columns a and b (the responder's +1), a row that may hold
+// targets scheduled for deletion, hot rows and columns, the partial last group -- takes pass1_grp's per-column
+// path on the same loads (decoded against the owners' own values: exact for lags < 2^8).
+// Report planes: 16-column layout (d.pl16, plane16_bit): one u16 per lane and step, zeros included.
+#ifndef P1V_AHEAD
+#define P1V_AHEAD 1  // groups of 16 columns loaded ahead of the one being computed
+#endif
+#ifndef P1V_WAVES
+#define P1V_WAVES 6  // waves per SIMD k_pass1v is compiled for
+#endif
+constexpr uint32_t B7 = 0x80808080u, L7 = 0x7F7F7F7Fu;
+// the 16-column plane layout: plane u16 g holds columns 16 g .. 16 g + 15, column 16 g + 4 q + i at bit 4 i + q
+__device__ __forceinline__ uint32_t plane16_bit(uint32_t c) { return 4u * (c & 3u) + ((c >> 2) & 3u); }
+// bit 7 of byte i of w[q] -> bit 4 i + q (the plane layout of one lane's 16 columns)
+__device__ __forceinline__ uint32_t pack16(const uint32_t (&w)[4]) {
+    const uint32_t x = (w[0] >> 7) | (w[1] >> 6) | (w[2] >> 5) | (w[3] >> 4);  // byte i: bit q
+    const uint32_t y = (x | (x >> 4)) & 0x00FF00FFu;
+    return (y & 0xFFu) | (y >> 8);
+}
+// bit 7 of byte i of w -> bit i
+__device__ __forceinline__ uint32_t nib7(uint32_t w) {
+    const uint32_t x = (w >> 7) & 0x01010101u;
+    return (x | (x >> 7) | (x >> 14) | (x >> 21)) & 0xFu;
+}
+// bit i of a nibble -> bit 7 of byte i
+__device__ __forceinline__ uint32_t spread7(uint32_t n) { return ((n * 0x204081u) & 0x01010101u) << 7; }
+// bit i of a nibble -> bit 4 i
+__device__ __forceinline__ uint32_t spread4(uint32_t n) {
+    return (n & 1u) | ((n & 2u) << 3) | ((n & 4u) << 6) | ((n & 8u) << 9);
+}
+// per-byte (x - y) mod 2^8
+__device__ __forceinline__ uint32_t bsub(uint32_t x, uint32_t y) { return ((x | B7) - (y & L7)) ^ (~(x ^ y) & B7); }
+// wave-wide inclusive prefix sum (DPP: row shifts, then the row broadcasts)
+__device__ __forceinline__ uint32_t wave_scan_dpp(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);  // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false);  // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false);  // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false);  // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);  // row_bcast:15
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);  // row_bcast:31
+    return x;
+}
+
+// One direction's stale owners of one step (nm[q]: bit 7 of byte i = column c + 4 q + i) go out as records
+// {column, sender max_version word | receiver max_version word << 16} appended in column order (lane order,
+// then column) to the wave's list L (the first GS_CAND_CAP; cnt counts all), and -- from the step whose owners
+// overflow the list on -- as natural-order bitmap bits, 16 per lane (the packers walk the bitmap past the
+// last record).  Every lane of the wave calls this (act = false: no columns).
+__device__ __forceinline__ void emit_v(const Dev &d, uint16_t *gw16, uint2 *L, uint32_t &cnt, uint32_t c, bool act,
+                                       const uint32_t (&nm)[4], const uint4 &sS, const uint4 &sR, uint32_t &alg) {
+    const uint32_t my = act ? (uint32_t)(__popc(nm[0]) + __popc(nm[1]) + __popc(nm[2]) + __popc(nm[3])) : 0u;
+    const uint32_t incl = wave_scan_dpp(my);
+    const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    if (act && cnt + tot > GS_CAND_CAP) {
+        gw16[c >> 4] = (uint16_t)(nib7(nm[0]) | (nib7(nm[1]) << 4) | (nib7(nm[2]) << 8) | (nib7(nm[3]) << 12));
+        alg += 2;
+    }
+    if (tot == 0u) return;
+    if (my) {
+        uint32_t off = cnt + incl - my;
+        const uint32_t s4[4] = {sS.x, sS.y, sS.z, sS.w}, r4[4] = {sR.x, sR.y, sR.z, sR.w};
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            for (uint32_t m = nm[q]; m; m &= m - 1u) {
+                if (off < GS_CAND_CAP) {
+                    const uint32_t i = (uint32_t)__builtin_ctz(m) >> 3, j = c + 4u * q + i;
+                    const uint32_t M = d.self_mv[j];
+                    const uint32_t ms = mv_dec8((s4[q] >> (8 * i)) & 0xFFu, M), mr = mv_dec8((r4[q] >> (8 * i)) & 0xFFu, M);
+                    L[off] = make_uint2(j, ms | (mr << 16));
+                    alg += 8;
+                }
+                off++;
+            }
+        }
+    }
+    cnt += tot;
+}
+
+// k_pass1v's per-column path for one lane's 16 columns (out of line: it runs for a few lanes per exchange, and
+// inlined its registers would cost the byte-parallel loop its occupancy): pass1_grp's rules on decoded values
+// (exact for lags < 2^8) -- the responder's +1, columns a and b, targets scheduled for deletion, the last
+// partial group.  Outputs in k_pass1v's word forms.
+struct P1vSlow {
+    uint32_t nwA[4], nwB[4], nba[4], nab[4];
+    uint32_t pA, pB, upA, upB, hbw, reports;
+};
+__device__ __noinline__ P1vSlow pass1v_slow(const uint32_t *self_pk, const uint8_t *fd_state, const uint32_t *tod,
+                                            uint32_t delay, uint32_t col_lo, uint32_t ncol, size_t ra, size_t rb,
+                                            uint32_t c, uint32_t a, uint32_t b, uint32_t t, bool schA, bool schB,
+                                            uint4 hA4, uint4 hB4, uint4 mA4, uint4 mB4) {
+    P1vSlow o{};
+    const uint32_t x4[4] = {hA4.x, hA4.y, hA4.z, hA4.w}, y4[4] = {hB4.x, hB4.y, hB4.z, hB4.w};
+    const uint32_t ma4[4] = {mA4.x, mA4.y, mA4.z, mA4.w}, mb4[4] = {mB4.x, mB4.y, mB4.z, mB4.w};
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const uint32_t c0 = c + 4u * q;
+        const uint4 pk = *reinterpret_cast<const uint4 *>(self_pk + c0);
+        const uint32_t pk4[4] = {pk.x, pk.y, pk.z, pk.w};
+        uint32_t oA = 0u, oB = 0u, rA = 0u, rB = 0u, bA = 0u, bB = 0u;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const uint32_t j = c0 + i, jg = col_lo + j;
+            const bool valid = j < ncol;
+            // scheduled for deletion (only in rows whose earliest scheduled tick has passed): not in the digest
+            const bool sa = schA && valid && (fd_state[ra + j] & FD_MEMB) == FD_DEAD && is_sched(tod[ra + j], t, delay);
+            const bool sb = schB && valid && (fd_state[rb + j] & FD_MEMB) == FD_DEAD && is_sched(tod[rb + j], t, delay);
+            const uint32_t Rx = pk4[i] & 0xFFFFu, M = pk4[i] >> 16;
+            uint32_t hA = hb_dec8((x4[q] >> (8 * i)) & 0xFFu, Rx), hB = hb_dec8((y4[q] >> (8 * i)) & 0xFFu, Rx);
+            const uint32_t mA = mv_dec8((ma4[q] >> (8 * i)) & 0xFFu, M) & MV_MASK;
+            const uint32_t mB = mv_dec8((mb4[q] >> (8 * i)) & 0xFFu, M) & MV_MASK;
+            const bool isb = valid && jg == b;
+            hB += isb ? 1u : 0u;  // responder inc_heartbeat (server.py:524)
+            const bool upB = valid && !sa && jg != b && hA > hB;  // b merges a's digest (server.py:336-337)
+            const bool repB = upB && hB != 0u;                   // state.py:280-287
+            hB = upB ? hA : hB;
+            const bool upA = valid && !sb && jg != a && hB > hA;  // then a merges b's (server.py:340, 356-357)
+            const bool repA = upA && hA != 0u;
+            hA = upA ? hB : hA;
+            oA |= (hA & 0xFFu) << (8 * i);
+            oB |= (hB & 0xFFu) << (8 * i);
+            o.upA |= (uint32_t)upA;
+            o.upB |= (uint32_t)(upB || isb);
+            o.hbw += (uint32_t)upA + (uint32_t)upB + (uint32_t)isb;
+            rA |= (uint32_t)repA << i;
+            rB |= (uint32_t)repB << i;
+            o.reports += (uint32_t)repA + (uint32_t)repB;
+            // stale owners (state.py:347-357) against each side's digest
+            bA |= (uint32_t)(valid && !sb && mB > (sa ? 0u : mA)) << (8 * i + 7);  // b -> a
+            bB |= (uint32_t)(valid && !sa && mA > (sb ? 0u : mB)) << (8 * i + 7);  // a -> b
+        }
+        o.nwA[q] = oA;
+        o.nwB[q] = oB;
+        o.nba[q] = bA;
+        o.nab[q] = bB;
+        o.pA |= spread4(rA) << q;
+        o.pB |= spread4(rB) << q;
+    }
+    return o;
+}
+
+struct V16 {
+    uint4 hA, hB, mA, mB;
+    uint32_t fl;  // GS_R_P1FLAGS word of the group: small bits | hot bits << 16
+};
+
+template <int AHEAD>
+__global__ __launch_bounds__(XB, P1V_WAVES) void k_pass1v(Dev d, const int32_t *ini, const int32_t *res, uint32_t n,
+                                                          uint32_t t, uint32_t seq) {
+    const uint32_t e = blockIdx.x;
+    if (e >= n) return;
+    const int tid = threadIdx.x, lane = tid & (WAVE - 1), wid = tid >> 6;
+    const int32_t ai = ini[e], bi = res[e];
+    if (ai < 0 || bi < 0 || (uint32_t)ai >= d.N || (uint32_t)bi >= d.N || ai == bi) {
+        if (tid == 0) shard_add(d, C_E_IDX, 1);
+        return;
+    }
+    const uint32_t a = (uint32_t)ai, b = (uint32_t)bi;
+    if (tid == 0) {
+        const uint32_t oa = atomicMax(&d.stamp[a], seq), ob = atomicMax(&d.stamp[b], seq);
+        if (oa == seq || ob == seq) shard_add(d, C_E_CONFLICT, 1);
+    }
+    const uint4 rowA = *reinterpret_cast<const uint4 *>(d.row + (size_t)a * 4);
+    const uint4 rowB = *reinterpret_cast<const uint4 *>(d.row + (size_t)b * 4);
+    const bool schA = t >= rowA.z, schB = t >= rowB.z;
+    // the whole exchange on the per-column path: a row that may hold a target scheduled for deletion, or a hot row
+    const bool rslow = schA || schB || ((rowA.w | rowB.w) & 4u);
+    const size_t ra = (size_t)a * d.NP, rb = (size_t)b * d.NP;
+    const uint32_t words = d.NP / 32;
+    uint16_t *gBA = reinterpret_cast<uint16_t *>(d.sbits + (size_t)e * 2 * words), *gAB = gBA + 2 * words;
+    // wave w streams row half w (columns [w H, min((w + 1) H, ncol)), H a multiple of 1024): its candidate lists
+    // hold that half in column order, and the packer reads half 0's list, then half 1's
+    const uint32_t H = half_cols(d);
+    const uint32_t lo = (uint32_t)wid * H, hi = min(lo + H, d.ncol);
+    uint2 *LBA = d.cand + ((size_t)e * 4 + 0 * 2 + wid) * GS_CAND_CAP;
+    uint2 *LAB = d.cand + ((size_t)e * 4 + 1 * 2 + wid) * GS_CAND_CAP;
+    uint32_t nBAc = 0, nABc = 0, alg = 0, reports = 0, hbw = 0;
+    const uint32_t ph = t - d.t_round - 1u;
+    uint16_t *planeA = reinterpret_cast<uint16_t *>(d.pend + ((size_t)a * NPL + ph) * d.PW);
+    uint16_t *planeB = reinterpret_cast<uint16_t *>(d.pend + ((size_t)b * NPL + ph) * d.PW);
+    if (tid == 0) {
+        d.pstamp[a * NPL + ph] = t;
+        d.pstamp[b * NPL + ph] = t;
+    }
+    const uint32_t ja = a - d.col_lo, jb = b - d.col_lo;  // this slice's columns of a and b (>= ncol: not here)
+    // responder inc_heartbeat (server.py:524): the owner's own heartbeat is raised here (the per-column path
+    // decodes against it, R or R + 1 alike); the view hb[b][b] in the loop; the small bit after the phase
+    if (tid == 0 && jb < d.ncol) {
+        const uint32_t R1 = d.self_hb[jb] + 1u;
+        d.self_hb[jb] = R1;
+        d.self_pk[jb] = self_pack(R1, d.self_mv[jb]);
+    }
+    const uint8_t *h8 = reinterpret_cast<const uint8_t *>(d.hb), *m8 = reinterpret_cast<const uint8_t *>(d.mv);
+    auto load = [&](uint32_t c, V16 &v) {
+        v.hA = *reinterpret_cast<const uint4 *>(h8 + ra + c);
+        v.hB = *reinterpret_cast<const uint4 *>(h8 + rb + c);
+        v.mA = *reinterpret_cast<const uint4 *>(m8 + ra + c);
+        v.mB = *reinterpret_cast<const uint4 *>(m8 + rb + c);
+        v.fl = d.p1flags[c >> 4];
+    };
+    constexpr uint32_t STEP = WAVE * 16u;
+    V16 buf[AHEAD + 1];
+#pragma unroll
+    for (int k = 0; k < AHEAD; k++)
+        if (lo + lane * 16u + k * STEP < hi) load(lo + lane * 16u + k * STEP, buf[k]);
+    for (uint32_t s0 = lo; s0 < hi; s0 += STEP) {  // wave-uniform trip count (the scans need every lane)
+        const uint32_t c = s0 + (uint32_t)lane * 16u;
+        const bool act = c < hi;
+        if (c + AHEAD * STEP < hi) load(c + AHEAD * STEP, buf[AHEAD]);
+        if (!AHEAD && act) load(c, buf[0]);
+        const V16 &v = buf[0];
+        const uint32_t x4[4] = {v.hA.x, v.hA.y, v.hA.z, v.hA.w}, y4[4] = {v.hB.x, v.hB.y, v.hB.z, v.hB.w};
+        const uint32_t ma4[4] = {v.mA.x, v.mA.y, v.mA.z, v.mA.w}, mb4[4] = {v.mB.x, v.mB.y, v.mB.z, v.mB.w};
+        uint32_t repA[4] = {0u, 0u, 0u, 0u}, repB[4] = {0u, 0u, 0u, 0u};
+        uint32_t nba[4] = {0u, 0u, 0u, 0u}, nab[4] = {0u, 0u, 0u, 0u};
+        uint32_t pA = 0u, pB = 0u;  // the lane's plane u16s
+        const bool slow = act && (rslow || (v.fl >> 16) || c + 16u > d.ncol || ja - c < 16u || jb - c < 16u);
+        if (act && !slow) {
+            uint32_t nw[4], upAll = 0u, upBll = 0u;
+            const uint32_t sm = v.fl & 0xFFFFu;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const uint32_t x = x4[q], y = y4[q];
+                const uint32_t dd = bsub(x, y);  // (hA - hB) mod 2^8, |hA - hB| < 2^7
+                const uint32_t upA = dd & B7;    // hB > hA: a takes b's heartbeat
+                const uint32_t upB = ((((dd & L7) + L7) | dd) & ~dd) & B7;  // hA > hB: b takes a's
+                const uint32_t mA_ = (upA << 1) - (upA >> 7);
+                nw[q] = (y & mA_) | (x & ~mA_);  // both rows end with the larger heartbeat
+                // _report_heartbeat reports unless the old heartbeat was 0 (state.py:280-287)
+                const uint32_t s7 = sm ? spread7((sm >> (4 * q)) & 0xFu) : 0u;
+                const uint32_t zA = ~(((x & L7) + L7) | x) & B7, zB = ~(((y & L7) + L7) | y) & B7;
+                repA[q] = upA & ~(zA & s7);
+                repB[q] = upB & ~(zB & s7);
+                upAll |= upA;
+                upBll |= upB;
+                hbw += (uint32_t)__popc(upA | upB);
+                // stale owners (state.py:347-357): mB > mA -> b -> a, mA > mB -> a -> b; |mA - mB| < 2^6
+                const uint32_t ev = (((mb4[q] & L7) | B7) - (ma4[q] & L7)) & L7;  // (mB - mA) mod 2^7
+                const uint32_t e6 = (ev << 1) & B7;
+                nba[q] = (ev + L7) & B7 & ~e6;
+                nab[q] = e6;
+            }
+            if (!(d.ablate & 2u)) {
+                if (upAll) *reinterpret_cast<uint4 *>(reinterpret_cast<uint8_t *>(d.hb) + ra + c) = make_uint4(nw[0], nw[1], nw[2], nw[3]);
+                if (upBll) *reinterpret_cast<uint4 *>(reinterpret_cast<uint8_t *>(d.hb) + rb + c) = make_uint4(nw[0], nw[1], nw[2], nw[3]);
+            }
+            alg += 64u + (upAll ? 16u : 0u) + (upBll ? 16u : 0u);
+            pA = pack16(repA);
+            pB = pack16(repB);
+            reports += (uint32_t)(__popc(pA) + __popc(pB));
+        } else if (slow) {
+            const P1vSlow o = pass1v_slow(d.self_pk, d.fd_state, d.tod, d.sched_delay, d.col_lo, d.ncol, ra, rb, c, a, b,
+                                          t, schA, schB, v.hA, v.hB, v.mA, v.mB);
+            if (!(d.ablate & 2u)) {
+                if (o.upA) *reinterpret_cast<uint4 *>(reinterpret_cast<uint8_t *>(d.hb) + ra + c) = make_uint4(o.nwA[0], o.nwA[1], o.nwA[2], o.nwA[3]);
+                if (o.upB) *reinterpret_cast<uint4 *>(reinterpret_cast<uint8_t *>(d.hb) + rb + c) = make_uint4(o.nwB[0], o.nwB[1], o.nwB[2], o.nwB[3]);
+            }
+            alg += 64u + (o.upA ? 16u : 0u) + (o.upB ? 16u : 0u);
+            hbw += o.hbw;
+            reports += o.reports;
+            pA = o.pA;
+            pB = o.pB;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                nba[q] = o.nba[q];
+                nab[q] = o.nab[q];
+            }
+        }
+        if (act) {
+            planeA[c >> 4] = (uint16_t)pA;
+            planeB[c >> 4] = (uint16_t)pB;
+            alg += 4;
+        }
+        emit_v(d, gBA, LBA, nBAc, c, act, nba, v.mB, v.mA, alg);  // b -> a: sender b, receiver a
+        emit_v(d, gAB, LAB, nABc, c, act, nab, v.mA, v.mB, alg);
+#pragma unroll
+        for (int k = 0; k < AHEAD; k++) buf[k] = buf[k + 1];
+    }
+    if (lane == 0) {
+        d.cand_n[(size_t)e * 4 + 0 * 2 + wid] = nBAc;
+        d.cand_n[(size_t)e * 4 + 1 * 2 + wid] = nABc;
+    }
+    const unsigned long long s_alg = wave_sum(alg), s_rep = wave_sum(reports), s_hbw = wave_sum(hbw);
+    if (lane == 0) {
+        shard_add(d, C_ALG, s_alg);
+        shard_add(d, C_REPORTS, s_rep);
+        shard_add(d, C_HBW, s_hbw);
+        if (wid == 0 && d.shard == 0) shard_add(d, C_EXCH, 1);  // slices: every slice runs every exchange
+    }
+}
+// After a k_pass1v phase: the responders' small bits (their own heartbeat rose by one in the phase; pass 1
+// read the bits as they were before it, consistently for every exchange of the phase)
+__global__ __launch_bounds__(LB) void k_p1v_fix(Dev d, const int32_t *res, uint32_t n) {
+    const uint32_t e = blockIdx.x * LB + threadIdx.x;
+    if (e >= n) return;
+    const uint32_t jb = (uint32_t)res[e] - d.col_lo;
+    if ((uint32_t)res[e] < d.N && jb < d.ncol) set_small(d, jb, d.self_hb[jb]);
 }
 
 // MODE 0: the whole exchange (one slice).  MODE 1: sharded count pass (pass 1, then the slice totals).
@@ -2007,7 +2332,7 @@ __device__ __forceinline__ SlotSum settle_sum(const Dev &d, uint32_t snd, uint32
             }
         }
         if (nh > GS_CAND_CAP) {  // the bitmap tail: its owners are not merged, the pack walks them
-            const uint32_t H = ((d.ncol + 1u) / 2u + 255u) & ~255u, words = d.NP / 32;
+            const uint32_t H = half_cols(d), words = d.NP / 32;
             const uint32_t pmin = L[GS_CAND_CAP - 1].x + 1u;
             WStats cs{0, 0, 0, 0, 0};
             bool ctomb = false;
@@ -2353,11 +2678,21 @@ __global__ __launch_bounds__(LB, LIVE_WAVES) void k_liveness(Dev d, const uint8_
         const size_t p = pix(d, o, c0);
         // this thread's four columns: bit ph of q[i] = a report in phase ph
         uint32_t q[4] = {0u, 0u, 0u, 0u};
-        const uint32_t lb = plane_bit(c0);
-        for (uint32_t m = vm; m; m &= m - 1u) {
-            const uint32_t ph = (uint32_t)__builtin_ctz(m);
+        if (d.pl16) {  // k_pass1v's layout: column 16 g + 4 q + i at bit 4 i + q of u16 g
+            const uint32_t ui = (c0 & 255u) >> 4, qs = (c0 >> 2) & 3u;
+            for (uint32_t m = vm; m; m &= m - 1u) {
+                const uint32_t ph = (uint32_t)__builtin_ctz(m);
+                const uint32_t u = (uint32_t)reinterpret_cast<const uint16_t *>(s_pl[wv][ph])[ui] >> qs;
 #pragma unroll
-            for (int i = 0; i < 4; i++) q[i] |= (uint32_t)((s_pl[wv][ph][i] >> lb) & 1ull) << ph;
+                for (int i = 0; i < 4; i++) q[i] |= ((u >> (4 * i)) & 1u) << ph;
+            }
+        } else {
+            const uint32_t lb = plane_bit(c0);
+            for (uint32_t m = vm; m; m &= m - 1u) {
+                const uint32_t ph = (uint32_t)__builtin_ctz(m);
+#pragma unroll
+                for (int i = 0; i < 4; i++) q[i] |= (uint32_t)((s_pl[wv][ph][i] >> lb) & 1ull) << ph;
+            }
         }
         uint32_t sc[4] = {sc4.x, sc4.y, sc4.z, sc4.w};
         uint32_t lt[4] = {l4.x & 0xFFFFu, l4.x >> 16, l4.y & 0xFFFFu, l4.y >> 16};
@@ -2635,15 +2970,27 @@ __global__ __launch_bounds__(LB) void k_fd_age(Dev d, uint32_t t) {
 // before every round start and every phase, so at most 64 increments apart) and lags >= 2^7 counted:
 // < 2^7 + 2^6 < 2^8.
 // GS_MV8 (max_version views mod 2^7): a view only falls behind when its owner writes (one version per
-// gs_owner_writes call at most), gs_owner_writes sweeps at least every 64 calls, and lags >= 2^6 are
-// counted: < 2^6 + 2^6 = 2^7 between sweeps.
+// gs_owner_writes call at most), gs_owner_writes sweeps at least every 32 calls, and lags >= 2^6 are
+// counted: < 2^6 + 2^5 < 2^7 between sweeps.
+// The same sweep marks the views k_pass1v's byte-parallel path may not take (GS_R_P1FLAGS, ROW word 3 bit 2):
+// a view lagging by >= HOT_HB heartbeats or HOT_MV versions makes its owner column "hot", or, when a chunk
+// of the row holds HOT_ROW_MIN such views (a node back from a long absence), its observer row.  Between two
+// sweeps a view falls behind by at most 64 heartbeats (HB8_LAG_CHECK_EVERY) and 32 versions
+// (MV8_LAG_CHECK_EVERY), so every view of a row and column that are not hot lags by < 128 heartbeats and
+// < 64 versions: the bounds under which pass 1 compares two 8-bit views without their owner's value.
 // One workgroup per (row, chunk of LB x 16 columns); each thread reads 16 views (u8) or 8 (u16).
+constexpr uint32_t HOT_HB = 64, HOT_MV = 32, HOT_ROW_MIN = 16;
 __global__ __launch_bounds__(LB) void k_hb_lag(Dev d, uint32_t chunks) {
+    __shared__ uint32_t s_hot;
     const bool genm = !(d.flags & GS_CANONICAL);
     const uint32_t o = blockIdx.x / chunks, cb = blockIdx.x % chunks;
     const uint32_t per = d.hb8 ? 16u : 8u;
     const uint32_t j0 = (cb * LB + threadIdx.x) * per;
-    uint32_t bad = 0;
+    uint32_t bad = 0, hot = 0;  // hot: bit k = view k of this thread's (at most 16)
+    if (d.p1flags) {
+        if (threadIdx.x == 0) s_hot = 0u;
+        __syncthreads();
+    }
     if (j0 < d.ncol) {
         const size_t p0 = pix(d, o, j0);
         // one 16-byte load per region: the thread's heartbeat views (and GS_MV8 max_version views)
@@ -2654,9 +3001,10 @@ __global__ __launch_bounds__(LB) void k_hb_lag(Dev d, uint32_t chunks) {
         const uint32_t hw[4] = {hr.x, hr.y, hr.z, hr.w}, mw[4] = {mr.x, mr.y, mr.z, mr.w};
         for (uint32_t q = 0; q < per / 4u && j0 + 4u * q < d.ncol; q++) {
             const uint32_t jq = j0 + 4u * q;
-            // the owners' own values, 4 columns per 16-byte load (L2): GS_MV8 packed (R mod 2^8 and M)
-            const uint4 ow = *reinterpret_cast<const uint4 *>((d.mv8 ? d.self_pk : d.self_hb) + jq);
-            const uint32_t own[4] = {ow.x, ow.y, ow.z, ow.w};
+            // the owners' own values, 4 columns per 16-byte load (L2)
+            const uint4 ow = *reinterpret_cast<const uint4 *>(d.self_hb + jq);
+            const uint4 om = d.mv8 ? *reinterpret_cast<const uint4 *>(d.self_mv + jq) : make_uint4(0u, 0u, 0u, 0u);
+            const uint32_t own[4] = {ow.x, ow.y, ow.z, ow.w}, owm[4] = {om.x, om.y, om.z, om.w};
             uint32_t ps[4] = {0u, 0u, 0u, 0u};
             if (genm) ld4(d.pos + p0 + 4u * q, ps);
 #pragma unroll
@@ -2666,15 +3014,36 @@ __global__ __launch_bounds__(LB) void k_hb_lag(Dev d, uint32_t chunks) {
                 const uint32_t s = d.hb8 ? (hw[k >> 2] >> (8 * (k & 3))) & 0xFFu : (hw[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
                 const uint32_t lag = d.hb8 ? (own[i] - s) & 0xFFu : (own[i] - s) & 0xFFFFu;
                 if (lag >= (d.hb8 ? 0x80u : 0x8000u)) bad++;
+                bool h = d.hb8 && lag >= HOT_HB;
                 if (d.mv8) {  // GS_MV8: max_version views lag their owner by < 2^6 at every sweep
                     const uint32_t sm = (mw[k >> 2] >> (8 * (k & 3))) & 0x7Fu;
-                    if ((((own[i] >> 16) - sm) & 0x7Fu) >= 0x40u) bad++;
+                    const uint32_t ml = (owm[i] - sm) & 0x7Fu;
+                    if (ml >= 0x40u) bad++;
+                    h = h || ml >= HOT_MV;
                 }
+                hot |= (uint32_t)h << k;
             }
+        }
+    }
+    if (d.p1flags) {  // k_pass1v's hot rows and columns (cleared by k_hot_clear before the sweep)
+        const uint32_t nh = (uint32_t)__popc(hot);
+        const unsigned long long wn = wave_sum(nh);
+        if ((threadIdx.x & 63) == 0 && wn) atomicAdd(&s_hot, (uint32_t)wn);
+        __syncthreads();
+        if (s_hot >= HOT_ROW_MIN) {
+            if (threadIdx.x == 0) atomicOr(&d.row[o * 4 + 3], 4u);
+        } else if (hot) {  // 16 views per thread: one 16-column group (per = 16 with GS_HB8)
+            atomicOr(&d.p1flags[j0 >> 4], hot << 16);
         }
     }
     const unsigned long long sb = wave_sum(bad);
     if ((threadIdx.x & 63) == 0) shard_add(d, C_E_HBLAG, sb);
+}
+// k_hb_lag's hot marks start from nothing at every sweep
+__global__ __launch_bounds__(LB) void k_hot_clear(Dev d) {
+    const uint32_t i = blockIdx.x * LB + threadIdx.x;
+    if (i < d.N) d.row[i * 4 + 3] &= ~4u;
+    if (i < d.NP / 16u) d.p1flags[i] &= 0xFFFFu;
 }
 
 // ------------------------------------------------------------------ owner writes
@@ -3550,6 +3919,7 @@ int check_bound(gs_handle *h) {
     d.vlog = (uint32_t *)h->reg[GS_R_VLOG];
     d.self_mv = (uint32_t *)h->reg[GS_R_SELF_MV];
     d.self_pk = (uint32_t *)h->reg[GS_R_SELF_PK];
+    d.p1flags = (uint32_t *)h->reg[GS_R_P1FLAGS];
     return GS_OK;
 }
 
@@ -3653,6 +4023,15 @@ int launch_pass1(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t 
     hipEvent_t e0 = nullptr;
     int rc = time_begin(h, e0);
     if (rc) return rc;
+    if (h->d.pl16) {  // GS_MV8 record phases: the byte-parallel pass 1
+        k_pass1v<P1V_AHEAD><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, h->seq);
+        HIPCHK(h, hipGetLastError());
+        rc = time_end(h, GS_KT_PASS1, e0);
+        if (rc) return rc;
+        k_p1v_fix<<<(n + LB - 1) / LB, LB, 0, h->stream>>>(h->d, res, n);
+        HIPCHK(h, hipGetLastError());
+        return GS_OK;
+    }
     if (h->d.mv8) {  // GS_MV8 implies GS_HB8
         if (h->d.spec) k_pass1<4, false, true, true, true><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, h->seq, 0u);
         else k_pass1<4, false, false, true, true><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, h->seq, 0u);
@@ -3771,6 +4150,7 @@ int gs_create(const gs_config *cfg, gs_handle **out) {
     b[GS_R_MV] = pairs * ((c.flags & GS_MV8) ? 1 : 2);
     b[GS_R_SELF_MV] = NP * 4;
     b[GS_R_SELF_PK] = (c.flags & GS_MV8) ? NP * 4 : 0;
+    b[GS_R_P1FLAGS] = (c.flags & GS_MV8) ? NP / 16 * 4 : 0;  // k_pass1v's small / hot bits
     b[GS_R_GC] = (c.flags & GS_TOMBSTONES) ? pairs * 4 : 0;  // last_gc_version stays 0 without tombstone GC
     b[GS_R_HELD] = (c.flags & GS_NO_HELD) ? 0 : pairs * KP;
     b[GS_R_FD] = pairs * 4;
@@ -3838,6 +4218,12 @@ int gs_create(const gs_config *cfg, gs_handle **out) {
     d.VL = VL;
     d.hb8 = (c.flags & GS_HB8) ? 1u : 0u;
     d.mv8 = (c.flags & GS_MV8) ? 1u : 0u;
+    // GS_MV8 record phases run k_pass1v (its 16-column report planes) unless env GS_P1=old (round 3's k_pass1, A/B
+    // runs) or the speculative-merge mode asks for k_pass1's merge
+    {
+        const char *p1 = getenv("GS_P1");
+        d.pl16 = d.mv8 && h->pack_mode == 2 && !(p1 && !strcmp(p1, "old")) ? 1u : 0u;
+    }
     if (const char *ab = getenv("GS_ABLATE")) d.ablate = (uint32_t)atoi(ab);
     d.phi_thr = c.phi_threshold;
     d.prior5 = c.prior_weighted;
@@ -3889,7 +4275,7 @@ int gs_boot(gs_handle *h, const uint16_t *nid_size, const uint8_t *key_len) {
     const int zero[] = {GS_R_HB, GS_R_SELF_HB, GS_R_MV, GS_R_GC, GS_R_HELD, GS_R_FD, GS_R_FD_LAST, GS_R_FD_STATE, GS_R_FD_TOD,
                         GS_R_RING, GS_R_ROW, GS_R_LAST_W, GS_R_HIST, GS_R_HIST_VID,
                         GS_R_STAMP, GS_R_COUNTERS, GS_R_SLICE_BITS, GS_R_PEND, GS_R_PEND_STAMP, GS_R_LATEST,
-                        GS_R_SLOT_STAT, GS_R_VLOG, GS_R_SELF_MV, GS_R_SELF_PK};
+                        GS_R_SLOT_STAT, GS_R_VLOG, GS_R_SELF_MV, GS_R_SELF_PK, GS_R_P1FLAGS};
     for (int r : zero)
         if (h->bytes[r]) HIPCHK(h, hipMemsetAsync(h->reg[r], 0, h->bytes[r], s));
     if (h->bytes[GS_R_TS]) HIPCHK(h, hipMemsetAsync(h->reg[GS_R_TS], 0xFF, h->bytes[GS_R_TS], s));
@@ -3960,7 +4346,7 @@ int gs_materialize_held(gs_handle *h, uint32_t row_lo, uint32_t row_hi) {
 int gs_owner_writes(gs_handle *h, const gs_write *ops, uint32_t n, uint32_t tick) {
     if (!h || !h->booted) return GS_E_INVALID;
     if (!n) return GS_OK;
-    if (h->d.mv8 && h->mv_incs >= 64) {  // 8-bit max_version views: at most 64 owner versions between sweeps
+    if (h->d.mv8 && h->mv_incs >= MV8_LAG_CHECK_EVERY) {  // 8-bit max_version views: <= 32 owner versions between sweeps
         int rc = gs_check_heartbeat_lag(h);
         if (rc) return rc;
     }
@@ -3993,6 +4379,10 @@ int gs_begin_round(gs_handle *h, const uint8_t *up, uint32_t tick) {
 int gs_check_heartbeat_lag(gs_handle *h) {
     if (!h || !h->booted) return GS_E_INVALID;
     const uint32_t per = h->d.hb8 ? 16u : 8u, chunks = (h->ncol + LB * per - 1) / (LB * per);
+    if (h->d.p1flags) {
+        k_hot_clear<<<(std::max(h->N, h->NP / 16u) + LB - 1) / LB, LB, 0, h->stream>>>(h->d);
+        HIPCHK(h, hipGetLastError());
+    }
     k_hb_lag<<<h->N * chunks, LB, 0, h->stream>>>(h->d, chunks);
     HIPCHK(h, hipGetLastError());
     h->lag_sweeps++;

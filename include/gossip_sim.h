@@ -171,6 +171,9 @@ enum gs_region {
                                         max_version + 1), VL = K * (hist_cap - 1) + 1 rounded up to 4: entry v =
                                         DeltaPb bytes of write v's KeyValueUpdatePb field | (version of the
                                         next write of the same key, 0xFFFF = none) << 16 */
+    GS_R_P1FLAGS,     /* u32 [NP/16]   GS_MV8: per 16-owner group, bit i = owner 16 g + i's own heartbeat is < 2^8, bit
+                                        16 + i = that owner is "hot" (some view of it lagged by >= 64 heartbeats or >= 32
+                                        versions at the last lag sweep): pass 1's byte-parallel path skips hot owners */
     GS_NUM_REGIONS
 };
 

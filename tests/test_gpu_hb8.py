@@ -37,16 +37,20 @@ def test_hb8_matches_reference_golden(name, mv8):
     assert sim.check()["err_hb_lag"] == 0
 
 
-def test_hb8_heartbeats_past_2_8_with_a_long_absence_match_oracle():
+@pytest.mark.parametrize("mv8", [False, True], ids=["hb8", "hb8mv8"])
+def test_hb8_heartbeats_past_2_8_with_a_long_absence_match_oracle(mv8):
     """Eight nodes, 400 rounds: every heartbeat wraps mod 2^8 several times, and node 7 is down for 25
     rounds (its views of the others fall ~75 behind, its windows go silent), then returns; the device
-    matches the C oracle (unbounded heartbeats) array for array, and the automatic lag sweeps ran clean."""
+    matches the C oracle (unbounded heartbeats) array for array, and the automatic lag sweeps ran clean.
+    With GS_MV8 pass 1 is k_pass1v: the lagging views make their row hot (per-column path) until a sweep
+    finds them caught up."""
     import torch
 
     n, rounds, down0, down1 = 8, 400, 150, 175
     ids, keys = synthetic_node_ids(n), key_names(2)
     init = {j: [(0, f"v{j}")] for j in range(n)}
-    gpu = GossipSim(ids, keys, dict(DEFAULT_CFG), "warm", init, tombstones=False, fd_ring=True, hist_cap=8, hb8=True)
+    gpu = GossipSim(ids, keys, dict(DEFAULT_CFG), "warm", init, tombstones=False, fd_ring=True, hist_cap=8, hb8=True,
+                    mv8=mv8)
     orc = OracleSim(ids, keys, dict(DEFAULT_CFG), "warm", init)
     for r in range(rounds):
         up = np.ones(n, np.uint8)

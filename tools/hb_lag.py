@@ -1,8 +1,9 @@
 """Heartbeat-lag census of the headline workload (GPU): after each round, the largest lag R_j - hb[o][j]
-of any view behind its owner's own heartbeat, and the count of views at or above 64 / 128.  Sizes the
-8-bit heartbeat layout (GS_HB8: exact while every lag < 128, guarded by k_hb_lag).
+of any view behind its owner's own heartbeat, the count of views at or above 64 / 128, and how they
+concentrate: observer rows / owner columns holding any view at or above 64, and the up state of those rows.
+Sizes the 8-bit heartbeat layout (GS_HB8) and its escape path.
 
-    python tools/hb_lag.py [--nodes 65536] [--rounds 40] [--down-rounds 3]
+    python tools/hb_lag.py [--nodes 65536] [--rounds 40] [--down-rounds 3] [--peer-select]
 """
 
 import argparse
@@ -27,6 +28,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=40)
     ap.add_argument("--down-rounds", type=int, default=3)
     ap.add_argument("--partition", type=int, nargs=2, default=None, help="rounds [a, b) split into halves")
+    ap.add_argument("--peer-select", action="store_true", help="rounds scheduled by the device's select_nodes_for_gossip")
+    ap.add_argument("--every", type=int, default=1, help="census every this many rounds")
     a = ap.parse_args()
     n, K = a.nodes, 16
     cfg = dict(DEFAULT_CFG)
@@ -38,19 +41,35 @@ def main():
     sim = GossipSim(synthetic_node_ids(n), key_names(K), cfg, init="warm", tombstones=False, fd_ring=False,
                     hist_cap=16, initial_ops=driver.boot_ops(n, K))
     plans = driver.prepare(spec, a.rounds, torch, sim.device)
+    sel = None
+    if a.peer_select:
+        from aiocluster_amd.peers import PeerSelector
+
+        sel = PeerSelector(sim, fanout=3, seeds=list(range(0, n, max(1, n // 8))), seed=0)
     hb = sim.region("HB", torch.int16, (n, sim.np_))
     out = []
     for r in range(a.rounds):
-        driver.run_round([sim], plans[r], group=None)
+        driver.run_round([sim], plans[r], group=None, sel=sel)
+        if (r + 1) % a.every:
+            continue
         R = sim.region("SELF_HB", torch.int32, (sim.np_,))[:n].to(torch.int64)
         mx, c64, c128 = 0, 0, 0
+        rows64 = torch.zeros(n, dtype=torch.bool, device=sim.device)
+        cols64 = torch.zeros(n, dtype=torch.bool, device=sim.device)
         for o0 in range(0, n, 4096):
             s = hb[o0:o0 + 4096, :n].to(torch.int64) & 0xFFFF
             lag = (R.unsqueeze(0) - s) & 0xFFFF
             mx = max(mx, int(lag.max().item()))
-            c64 += int((lag >= 64).sum().item())
+            big = lag >= 64
+            c64 += int(big.sum().item())
             c128 += int((lag >= 128).sum().item())
-        rec = {"round": r, "max_lag": mx, "views_ge_64": c64, "views_ge_128": c128}
+            rows64[o0:o0 + 4096] = big.any(1)
+            cols64 |= big.any(0)
+        up = plans[r]["up"].to(torch.bool)
+        rec = {"round": r, "max_lag": mx, "views_ge_64": c64, "views_ge_128": c128,
+               "rows_with_ge_64": int(rows64.sum().item()), "of_them_down": int((rows64 & ~up).sum().item()),
+               "cols_with_ge_64": int(cols64.sum().item()), "max_R": int(R.max().item()),
+               "phases": len(plans[r]["phases"]) if sel is None else None}
         out.append(rec)
         print(json.dumps(rec), flush=True)
     sim.check()
