@@ -70,7 +70,7 @@ COUNTER_FIELDS = [
     "exchanges", "hb_reports", "node_deltas", "kvs_sent", "truncated", "delta_bytes", "alg_bytes", "hb_writes",
     "candidates", "live_pairs", "tomb_gc", "err_fd_overflow", "err_hist_full", "err_bad_index", "err_conflict",
     "err_fd_gc", "err_insert", "fd_gc", "q9", "pack_bytes", "err_holes", "err_hb_lag", "plane_flushes",
-    "fd_saturated", "lite_slots", "lag_sweeps", "lite_bytes",
+    "fd_saturated", "lite_slots", "lag_sweeps", "lite_bytes", "live_bytes",
 ]
 
 # Every symbol include/gossip_sim.h declares (checked by tests/test_abi.py).

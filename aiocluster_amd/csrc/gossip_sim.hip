@@ -54,6 +54,9 @@ constexpr int LB = 256;  // liveness / elementwise workgroups
 #define LIVE_PER 8  // 1024-column chunks per k_liveness workgroup
 #endif
 constexpr int NSHARD = 64;
+// native vectors: the nontemporal load / store builtins take them (not HIP's uint4 struct)
+typedef unsigned int v4u_t __attribute__((ext_vector_type(4)));
+typedef unsigned int v2u_t __attribute__((ext_vector_type(2)));
 constexpr uint32_t WIN = 16 * 64;  // positions per packer window (16 per lane)
 // KW of the kernels for K > 16 keys (up to 64).  Those instantiations take most of the build time; a
 // development build with -DGS_KW4_ONLY (tools/build_dev.sh) leaves them out and refuses K > 16.
@@ -73,12 +76,12 @@ enum Ctr {
     C_EXCH = 0, C_REPORTS, C_ND, C_KVS, C_TRUNC, C_DBYTES, C_ALG, C_HBW, C_CAND, C_LIVE, C_TOMBGC,
     C_E_FDOVF, C_E_HIST, C_E_IDX, C_E_CONFLICT, C_E_FDGC, C_E_INSERT, C_FDGC, C_Q9, C_PACKB, C_E_HOLES,
     C_E_HBLAG, C_FLUSH /* host-side: plane_flushes */, C_FDSAT, C_LITE, C_SWEEPS /* host-side: lag_sweeps */,
-    C_LITEB,
+    C_LITEB, C_LIVEB,
     C_CEN0 = 32, C_NUM = C_CEN0 + 6  // gs_fd_census scratch slots (not part of gs_counters)
 };
 constexpr int CROW = 40;  // u64 slots per counter shard row (the 32 gs_counters fields, then the census scratch)
 static_assert(C_NUM <= CROW, "counter region");
-static_assert(C_LITEB < 32, "gs_counters fields");
+static_assert(C_LIVEB < 32, "gs_counters fields");
 static_assert(sizeof(gs_counters) == 32 * 8, "gs_counters layout");
 
 struct Dev {
@@ -973,8 +976,31 @@ __device__ __forceinline__ void pack_list(const Dev &d, uint32_t s, uint32_t r, 
 // store.  Returns false with nothing stored otherwise; the caller runs the exact packer (pack_records).
 // Lane l takes candidates l, l + 64, ... of the two halves' lists in order (sums only: order-free); B
 // groups per step, so their record loads, then their log loads, are in flight together.
-// APPLY = false: only the delta's DeltaPb total (a sliced count pass: every candidate, whatever the mtu).
 constexpr int LITE_B = 4;
+// The applies of a whole delta of prefix candidates (pack_lite): each receiver view becomes S_j(ms), one
+// max_version store per recorded owner (apply_cand's fast path); lanes take records l, l + 64, ...
+__device__ __forceinline__ void lite_apply(const Dev &d, uint32_t rcv, size_t slot, WStats &st) {
+    const int lane = lane_id();
+    const uint32_t n0 = d.cand_n[slot * 2], n1 = d.cand_n[slot * 2 + 1], nt = n0 + n1;
+    const uint2 *L0 = d.cand + slot * 2 * GS_CAND_CAP, *L1 = L0 + GS_CAND_CAP;
+    for (uint32_t c0 = 0; c0 < nt; c0 += WAVE * LITE_B) {
+        uint2 rc[LITE_B];
+#pragma unroll
+        for (int u = 0; u < LITE_B; u++) {
+            const uint32_t i = c0 + (uint32_t)(u * WAVE + lane);
+            rc[u] = i < nt ? (i < n0 ? L0[i] : L1[i - n0]) : make_uint2(NONE, 0u);
+        }
+#pragma unroll
+        for (int u = 0; u < LITE_B; u++) {
+            if (rc[u].x == NONE) continue;
+            mv_put(d, pix(d, rcv, rc[u].x), rc[u].y & 0xFFFFu);  // max(ms, mr) = ms
+            st.alg += 8 + 4;
+            st.nd++;
+            st.cand++;
+        }
+    }
+}
+// APPLY = false: only the delta's DeltaPb total (a sliced count pass: every candidate, whatever the mtu).
 // k_lite's per-slot flags (Dev::slot_stat[slot].w): LITE_FULL = the exact packer must size / pack the slot,
 // LITE_DONE = k_lite completed it
 constexpr uint32_t LITE_FULL = 1u, LITE_DONE = 2u;
@@ -1028,28 +1054,13 @@ __device__ __forceinline__ bool pack_lite(const Dev &d, uint32_t rcv, size_t slo
     if (__ballot(bad) != 0ull) return false;
     if (!APPLY) {
         st.alg += alg;
+        st.kvs += kvs;  // (per lane: the caller reduces it)
         Tout = T;
         if (m1out) *m1out = wave_min(m1);
         return true;
     }
     if ((uint64_t)S0 + T > d.mtu) return false;
-    // apply: every NodeDelta whole (the records are L2-hot from the pass above)
-    for (uint32_t c0 = 0; c0 < nt; c0 += WAVE * LITE_B) {
-        uint2 rc[LITE_B];
-#pragma unroll
-        for (int u = 0; u < LITE_B; u++) {
-            const uint32_t i = c0 + (uint32_t)(u * WAVE + lane);
-            rc[u] = i < nt ? (i < n0 ? L0[i] : L1[i - n0]) : make_uint2(NONE, 0u);
-        }
-#pragma unroll
-        for (int u = 0; u < LITE_B; u++) {
-            if (rc[u].x == NONE) continue;
-            mv_put(d, pix(d, rcv, rc[u].x), rc[u].y & 0xFFFFu);  // max(ms, mr) = ms
-            alg += 4;
-            st.nd++;
-            st.cand++;
-        }
-    }
+    lite_apply(d, rcv, slot, st);  // the records are L2-hot from the pass above
     st.kvs += kvs;
     st.alg += alg;
     Tout = T;
@@ -1229,12 +1240,12 @@ __device__ __forceinline__ Fd fd_report_val(const Dev &d, uint16_t *rg, uint32_t
         if (iv <= d.max_iv) {
             if (rg) {
                 const uint32_t slot = f.cnt % d.W;
-                if (f.cnt >= d.W) f.sum -= rg[slot];  // subtract-then-add (failure_detector.py:140-143)
+                if (f.cnt >= d.W) { f.sum -= rg[slot]; alg += 2; }  // subtract-then-add (failure_detector.py:140-143)
                 rg[slot] = (uint16_t)iv;
                 f.sum += iv;
                 f.cnt += 1;
                 if (f.cnt >= 2u * d.W) f.cnt -= d.W;
-                alg += 4;
+                alg += 2;
             } else if (f.cnt >= d.W) {
                 ovf += 1;  // eviction needs the ring: flagged, the run is reported inexact
             } else {
@@ -1244,7 +1255,6 @@ __device__ __forceinline__ Fd fd_report_val(const Dev &d, uint16_t *rg, uint32_t
         }
     }
     f.last = t;
-    alg += 16;
     return f;
 }
 
@@ -2502,13 +2512,25 @@ __global__ __launch_bounds__(XB, LITE_WAVES) void k_lite(Dev d, const int32_t *i
         uint32_t m1 = NONE;
         if (!sched && pack_lite<false>(d, rcv, slot, 0u, st, T, &m1)) {
             flag = 0u;
-            if (lane == 0) io.tot[slot] = tot_word(T, m1);
+            const uint32_t kv = (uint32_t)wave_sum(st.kvs);  // for step 0 (MODE 2): it applies without re-sizing
+            if (lane == 0) {
+                io.tot[slot] = tot_word(T, m1);
+                d.slot_stat[slot].y = kv;
+            }
+            st.kvs = 0u;  // counted when sent (MODE 2 or the exact packer)
         }
     } else {
         unsigned long long P = 0;
         for (uint32_t g = 0; g < d.shard; g++) P += GS_TOT_BYTES(io.tot_all[(size_t)g * n * 2 + slot]);
         const unsigned long long own = GS_TOT_BYTES(io.tot_all[(size_t)d.shard * n * 2 + slot]);
-        if (!sched && P + own <= d.mtu && pack_lite<true>(d, rcv, slot, (uint32_t)P, st, T)) {
+        // the count pass (MODE 1) sized this slot from the version log (slot_stat flag 0): apply only
+        const uint4 ss = d.slot_stat[slot];
+        if (!sched && P + own <= d.mtu && ss.w == 0u) {
+            lite_apply(d, rcv, slot, st);
+            if (lane == 0) st.kvs = ss.y;
+            T = (uint32_t)own;
+        }
+        if (!sched && P + own <= d.mtu && (ss.w == 0u || pack_lite<true>(d, rcv, slot, (uint32_t)P, st, T))) {
             flag = LITE_DONE;
             const uint32_t S = (uint32_t)P + T;  // every NodeDelta whole: pack_group's state after the last one
             const bool stop = S >= d.mtu || d.mtu - S < d.lb_min;
@@ -2612,6 +2634,9 @@ template <int RING>
 #ifndef LIVE_WAVES
 #define LIVE_WAVES 8  // waves per SIMD k_liveness is compiled for (<= 64 VGPRs)
 #endif
+#ifndef LIVE_NT
+#define LIVE_NT 0  // A/B: non-temporal loads / stores of the windows and state bytes
+#endif
 __global__ __launch_bounds__(LB, LIVE_WAVES) void k_liveness(Dev d, const uint8_t *up, uint32_t t, uint32_t chunks,
                                                  uint32_t per, bool replay, bool decide) {
     // [wave][phase][the wave's 4 plane words of this chunk]: each wave stages and reads only its own
@@ -2653,9 +2678,17 @@ __global__ __launch_bounds__(LB, LIVE_WAVES) void k_liveness(Dev d, const uint8_
     if (c0 < d.ncol) {
         const size_t p = pix(d, o, c0);
         if (upo || vm) {
-            sc4 = *reinterpret_cast<const uint4 *>(d.fd + p);
-            l4 = *reinterpret_cast<const uint2 *>(d.fd_last + p);
-            s4 = *reinterpret_cast<const uint32_t *>(d.fd_state + p);
+            if (LIVE_NT) {  // streamed once per round: non-temporal
+                const v4u_t x = __builtin_nontemporal_load(reinterpret_cast<const v4u_t *>(d.fd + p));
+                const v2u_t y = __builtin_nontemporal_load(reinterpret_cast<const v2u_t *>(d.fd_last + p));
+                sc4 = make_uint4(x.x, x.y, x.z, x.w);
+                l4 = make_uint2(y.x, y.y);
+                s4 = __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(d.fd_state + p));
+            } else {
+                sc4 = *reinterpret_cast<const uint4 *>(d.fd + p);
+                l4 = *reinterpret_cast<const uint2 *>(d.fd_last + p);
+                s4 = *reinterpret_cast<const uint32_t *>(d.fd_state + p);
+            }
         }
         if (upo && genm) ld4(d.pos + p, ps);
     }
@@ -2698,7 +2731,7 @@ __global__ __launch_bounds__(LB, LIVE_WAVES) void k_liveness(Dev d, const uint8_
         uint32_t lt[4] = {l4.x & 0xFFFFu, l4.x >> 16, l4.y & 0xFFFFu, l4.y >> 16};
         bool dw = false;
         uint32_t td[4] = {NONE, NONE, NONE, NONE};
-        if (exact && (s4 & 0x02020202u)) ld4(d.tod + p, td);
+        if (exact && (s4 & 0x02020202u)) { ld4(d.tod + p, td); alg += 16; }
         uint32_t s4n = s4;
 #pragma unroll
         for (int i = 0; i < 4; i++) {
@@ -2706,11 +2739,34 @@ __global__ __launch_bounds__(LB, LIVE_WAVES) void k_liveness(Dev d, const uint8_
             Fd f = fd_get(d, st, lt[i], sc[i], t);  // t is at or after every report tick of this round
             uint32_t m = q[i];  // only if vm != 0: then the window was loaded
             if (m) {
-                while (m) {
-                    const uint32_t bb = (uint32_t)__builtin_ctz(m);
-                    m &= m - 1u;
-                    f = fd_report_val(d, RING && rrow ? rrow + (size_t)(c0 + i) * d.W : nullptr, d.t_round + 1u + bb,
-                                      f, alg, ovf);
+                // report_heartbeat at ticks t_round + 1 + p for the phases p of m (failure_detector.py:32-38):
+                // intervals between reports of one round are < NPL ticks, so with max_interval >= NPL - 1 all
+                // but the first are appended and they telescope: (k - 1) intervals summing to p_last - p_first,
+                // plus the first one if it is <= max_interval; a compact window that would fill up, and the
+                // rings (their intervals one by one), replay report by report
+                bool loop = (RING && rrow) || d.max_iv < NPL - 1u;
+                if (!loop) {
+                    const uint32_t p1 = (uint32_t)__builtin_ctz(m), pk = 31u - (uint32_t)__builtin_clz(m);
+                    uint32_t app = (uint32_t)__popc(m) - 1u, add = pk - p1;
+                    if (f.last != NONE) {
+                        const uint32_t iv = d.t_round + 1u + p1 - f.last;
+                        if (iv <= d.max_iv) { app++; add += iv; }
+                    }
+                    if (f.cnt + app <= d.W) {
+                        f.cnt += app;
+                        f.sum += add;
+                        f.last = d.t_round + 1u + pk;
+                    } else {
+                        loop = true;
+                    }
+                }
+                if (loop) {
+                    while (m) {
+                        const uint32_t bb = (uint32_t)__builtin_ctz(m);
+                        m &= m - 1u;
+                        f = fd_report_val(d, RING && rrow ? rrow + (size_t)(c0 + i) * d.W : nullptr, d.t_round + 1u + bb,
+                                          f, alg, ovf);
+                    }
                 }
                 dw = true;
             }
@@ -2752,7 +2808,7 @@ __global__ __launch_bounds__(LB, LIVE_WAVES) void k_liveness(Dev d, const uint8_
                 if (!alive) {
                     sn = FD_DEAD;
                     uint32_t tod = td[i];  // loaded for the dead pairs of a row being recomputed
-                    if (mb != FD_DEAD) { tod = t; d.tod[p + i] = t; }  // time_of_death recorded once
+                    if (mb != FD_DEAD) { tod = t; d.tod[p + i] = t; alg += 4; }  // time_of_death recorded once
                     if (has && (f.sum | f.cnt)) { f.sum = f.cnt = 0u; dw = true; }  // reset
                     if (mb != FD_DEAD || exact) {
                         const uint32_t sat = tod + d.sched_delay;
@@ -2770,10 +2826,22 @@ __global__ __launch_bounds__(LB, LIVE_WAVES) void k_liveness(Dev d, const uint8_
             s4n = (s4n & ~(0xFFu << (8 * i))) | (st << (8 * i));
         }
         if (dw) {
-            *reinterpret_cast<uint4 *>(d.fd + p) = make_uint4(sc[0], sc[1], sc[2], sc[3]);
-            *reinterpret_cast<uint2 *>(d.fd_last + p) = make_uint2(lt[0] | (lt[1] << 16), lt[2] | (lt[3] << 16));
+            if (LIVE_NT) {
+                __builtin_nontemporal_store(v4u_t{sc[0], sc[1], sc[2], sc[3]}, reinterpret_cast<v4u_t *>(d.fd + p));
+                __builtin_nontemporal_store(v2u_t{lt[0] | (lt[1] << 16), lt[2] | (lt[3] << 16)},
+                                            reinterpret_cast<v2u_t *>(d.fd_last + p));
+            } else {
+                *reinterpret_cast<uint4 *>(d.fd + p) = make_uint4(sc[0], sc[1], sc[2], sc[3]);
+                *reinterpret_cast<uint2 *>(d.fd_last + p) = make_uint2(lt[0] | (lt[1] << 16), lt[2] | (lt[3] << 16));
+            }
+            alg += 24;
         }
-        if (s4n != s4) *reinterpret_cast<uint32_t *>(d.fd_state + p) = s4n;
+        if (s4n != s4) {
+            if (LIVE_NT) __builtin_nontemporal_store(s4n, reinterpret_cast<uint32_t *>(d.fd_state + p));
+            else *reinterpret_cast<uint32_t *>(d.fd_state + p) = s4n;
+            alg += 4;
+        }
+        if (upo || vm) alg += 28;  // the four windows (sum | cnt, last tick) and state bytes read
     }
     }
     // earliest scheduled-for-deletion tick of this row
@@ -2781,10 +2849,14 @@ __global__ __launch_bounds__(LB, LIVE_WAVES) void k_liveness(Dev d, const uint8_
         const uint32_t y = __shfl_xor(minS, dd, WAVE);
         if (y < minS) minS = y;
     }
-    const unsigned long long sl = wave_sum(live), sg = wave_sum(gcdue), so = wave_sum(ovf);
+    // in-kernel algorithmic bytes (C_LIVEB): windows, states, times of death and ring entries read and
+    // written (fd_report_val's per-report 16 B estimate is replaced by these element counts), and the
+    // report planes staged (32 B per valid phase per wave and chunk)
+    const unsigned long long sl = wave_sum(live), sg = wave_sum(gcdue), so = wave_sum(ovf), sa = wave_sum(alg);
     if ((threadIdx.x & 63) == 0) {
         if (minS != NONE) atomicMin(&d.row[o * 4 + 2], minS);
         if (sl) shard_add(d, C_LIVE, sl);
+        shard_add(d, C_LIVEB, sa + (unsigned long long)__popc(vm) * 32u * (cb1 - cb0));
         // a full compact window that needed an eviction: an error, except with sampled rings, where the
         // compact rows are documented as exact only up to W intervals (fd_saturated)
         if (so) shard_add(d, d.ring_slot ? C_FDSAT : C_E_FDOVF, so);
@@ -3751,22 +3823,26 @@ __global__ __launch_bounds__(LB) void k_luby_scatter(const int32_t *out, const u
 }
 
 // ------------------------------------------------------------------ measurement kernels
-// Streaming copy at 16 B per lane (4 loads in flight per lane, then 4 stores): the measured HBM
-// ceiling bench.py prices k_exchange against.  And a read-only stream at 8 or 16 B per lane whose
-// known byte count calibrates rocprofv3's FETCH_SIZE for the widths the exchange kernel uses.
-// measurement kernels (gs_stream_copy / _read / _write): grid-stride, 8 loads in flight per lane,
-// launched with 32,768 blocks -- the fastest of the copy shapes tools/membench.hip compares
-__global__ __launch_bounds__(256) void k_copy16(uint4 *__restrict__ dst, const uint4 *__restrict__ src, uint64_t n16) {
-    const uint64_t stride = (uint64_t)gridDim.x * 256u;
-    uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
-    for (; i + 7 * stride < n16; i += 8 * stride) {
-        uint4 v[8];
+// Streaming copy: the measured HBM ceiling bench.py reports beside the 8 TB/s peak.  And read-only / write-only
+// streams at 4, 8 or 16 B per lane whose known byte counts calibrate rocprofv3's FETCH_SIZE / WRITE_SIZE.
+// measurement kernels (gs_stream_copy / _read / _write).  The copy: each wave moves contiguous 16 KiB chunks
+// (64 lanes x 16 B x 16 loads in flight per lane, non-temporal loads and stores), chunks dealt grid-stride
+// over 65,536 workgroups -- the fastest copy shape of tools/membench8.hip on the box (5.99 TB/s vs 5.30 for
+// round 3's grid-stride 8-deep copy, r4b)
+__global__ __launch_bounds__(256) void k_copy16(v4u_t *__restrict__ dst, const v4u_t *__restrict__ src, uint64_t n16) {
+    const uint64_t waves = (uint64_t)gridDim.x * 4u, wid = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t chunks = n16 / 1024u;
+    for (uint64_t c = wid; c < chunks; c += waves) {
+        const uint64_t b = c * 1024u + lane;
+        v4u_t v[16];
 #pragma unroll
-        for (int u = 0; u < 8; u++) v[u] = src[i + u * stride];
+        for (int u = 0; u < 16; u++) v[u] = __builtin_nontemporal_load(src + b + u * 64);
 #pragma unroll
-        for (int u = 0; u < 8; u++) dst[i + u * stride] = v[u];
+        for (int u = 0; u < 16; u++) __builtin_nontemporal_store(v[u], dst + b + u * 64);
     }
-    for (; i < n16; i += stride) dst[i] = src[i];
+    // the tail (< 16 KiB): grid-stride
+    for (uint64_t i = chunks * 1024u + (uint64_t)blockIdx.x * 256u + threadIdx.x; i < n16; i += waves * 64u) dst[i] = src[i];
 }
 template <typename V>
 __global__ __launch_bounds__(256) void k_write(V *__restrict__ dst, uint64_t n) {
@@ -5046,7 +5122,7 @@ int gs_fd_census(gs_handle *h, const uint8_t *up, gs_census *out) {
 
 int gs_stream_copy(void *dst, const void *src, uint64_t bytes, void *stream) {
     if (!dst || !src || (bytes & 15u) || ((uintptr_t)dst & 15u) || ((uintptr_t)src & 15u)) return GS_E_INVALID;
-    k_copy16<<<32768, 256, 0, (hipStream_t)stream>>>((uint4 *)dst, (const uint4 *)src, bytes / 16);
+    k_copy16<<<65536, 256, 0, (hipStream_t)stream>>>((v4u_t *)dst, (const v4u_t *)src, bytes / 16);
     return hipGetLastError() == hipSuccess ? GS_OK : GS_E_HIP;
 }
 

@@ -269,7 +269,15 @@ def load_traffic(workload: str, kernel: str, units_per_launch: float):
 KERNEL_OF = {"pass1": "k_pass1", "pack": "k_pack_slice", "liveness": "k_liveness", "count": "k_settle", "lite": "k_lite"}
 
 
-def roofline(sims, local_c, exch, kt, elapsed, torch, dev, rank, group, workload) -> dict:
+def pass1_kernel(wide_views: bool) -> str:
+    """The pass-1 kernel the library launches (gs_create: GS_MV8 record phases run k_pass1v unless env GS_P1=old or
+    GS_PACK asks for another packing mode)."""
+    if wide_views or os.environ.get("GS_P1") == "old" or os.environ.get("GS_PACK", "split") != "split":
+        return "k_pass1"
+    return "k_pass1v"
+
+
+def roofline(sims, local_c, exch, kt, elapsed, torch, dev, rank, group, workload, p1name="k_pass1") -> dict:
     """Roofline of the dominant kernel (by summed time; HBM-bound integer/byte work, no MFMA) plus the
     same figures for the other kernels of the round.
 
@@ -282,6 +290,7 @@ def roofline(sims, local_c, exch, kt, elapsed, torch, dev, rank, group, workload
     alg = sum(x["alg_bytes"] for x in local_c)
     packb = sum(x["pack_bytes"] for x in local_c)
     liteb = sum(x["lite_bytes"] for x in local_c)  # k_lite's part of pack_bytes
+    liveb = sum(x["live_bytes"] for x in local_c)  # k_liveness's element bytes
     ncols = sum(s_.ncol for s_ in sims)
     fused = kt["pack"][1] == 0
     per = {}
@@ -296,14 +305,17 @@ def roofline(sims, local_c, exch, kt, elapsed, torch, dev, rank, group, workload
             b = (packb - liteb) / launches
         elif kind == "lite":
             b = liteb / launches
+        elif kind == "liveness":
+            b = liveb / launches
+        kname = p1name if kind == "pass1" else KERNEL_OF[kind]
         ent = {"kernel": ("k_pass1<fused>: pass 1, then packing + apply_delta in the same workgroup"
-                          if (fused and kind == "pass1") else KERNEL_OF[kind]),
+                          if (fused and kind == "pass1") else kname),
                "avg_launch_ms": avg_s * 1e3, "launches": launches, "share_of_step": ms / 1e3 / elapsed}
         if b is not None:
             ent.update(alg_bytes_per_launch=b, achieved=b / avg_s / 1e9, frac=b / avg_s / 1e9 / HBM_PEAK_GBPS)
         units = exch / launches if kind != "liveness" else 1.0
         if group is None:
-            tr, note = load_traffic(workload, KERNEL_OF[kind], units)
+            tr, note = load_traffic(workload, kname, units)
             ent.update(traffic=tr, traffic_source=note, traffic_gbs=tr / avg_s / 1e9 if tr else None)
         per[kind] = ent
     dom = max(per, key=lambda k: kt[k][0])
@@ -321,9 +333,12 @@ def roofline(sims, local_c, exch, kt, elapsed, torch, dev, rank, group, workload
         "traffic": d.get("traffic"),
         "traffic_source": d.get("traffic_source", "sliced run: not profiled"),
         "alg_bytes_per_launch": d.get("alg_bytes_per_launch"),
-        "alg_bytes_basis": "in-kernel element bytes of HBM-resident regions (C_ALG): both rows' u16 heartbeats + "
-                           "max versions read, changed heartbeat groups written, report bit planes, stale-owner "
-                           "bitmaps and candidate records written (pass 1); packing + apply (C_PACKB)",
+        "alg_bytes_basis": "in-kernel element bytes of HBM-resident regions: pass 1 (C_ALG - C_PACKB): both rows' "
+                           "heartbeat + max_version views read (1 B each with GS_HB8 + GS_MV8), changed 16-column "
+                           "heartbeat groups written, report bit planes, candidate records and overflow bitmap words "
+                           "written; k_lite / packer (C_LITEB / C_PACKB - C_LITEB): records, version-log entries, "
+                           "NodeId sizes, history rows, max_version stores; k_liveness (C_LIVEB): windows, state bytes, "
+                           "times of death read and written, report planes replayed",
         "avg_launch_ms": d["avg_launch_ms"],
         "launches": d["launches"],
         "kernel_share_of_step": d["share_of_step"],
@@ -331,10 +346,9 @@ def roofline(sims, local_c, exch, kt, elapsed, torch, dev, rank, group, workload
         "achieved_frac_of_copy_ceiling": d["achieved"] / copy_gbs if copy_gbs and d.get("achieved") else None,
         "traffic_gbs": d.get("traffic_gbs"),
         "kernels": per,
-        "note": ("k_pass1 streams 8-bit heartbeat + max_version views (GS_HB8 + GS_MV8): ~0.43 MB of HBM per "
-                 "exchange (PMC), 1.07 MB with round 2's 16-bit views, so its frac fell while its time did too; "
-                 "at these bytes it is bound by loads in flight per wave (2 groups ahead at 5 waves/SIMD), "
-                 "not by HBM bandwidth (DESIGN.md §7b, §10)") if d["kernel"] == "k_pass1" else None,
+        "note": ("k_pass1v streams 8-bit heartbeat + max_version views (GS_HB8 + GS_MV8), 16 columns per lane, and "
+                 "runs pass 1's per-column rules on 4 views per 32-bit word (DESIGN.md §4)") if d["kernel"] == "k_pass1v"
+                else None,
         "survey_formula_bytes_per_phase": survey,
         "survey_formula_gbs_over_pass1": survey / (kt["pass1"][0] / launches / 1e3) / 1e9 if kt["pass1"][0] else None,
     }
@@ -634,7 +648,8 @@ def main():
         s_.set_timing(False)
     # a sliced cluster: every rank runs the same exchanges on its columns -> count them once
     exch_total, elapsed_max = aggregate(exch if (group is None or rank == 0) else 0, elapsed, dist, dev)
-    roof = roofline(sims[:1], local_c[:1], exch, kt, elapsed, torch, dev, rank, group, workload)
+    roof = roofline(sims[:1], local_c[:1], exch, kt, elapsed, torch, dev, rank, group, workload,
+                    pass1_kernel(args.wide_views))
     cpu = None
     if rank == 0 and group is None and not args.no_cpu_baseline:
         rd = plans[R0 + args.steps]

@@ -219,7 +219,9 @@ typedef struct gs_counters {
                                   itself or from gs_begin_round / the phases / gs_owner_writes) */
     uint64_t lite_bytes;       /* the part of pack_bytes moved by k_lite (records read, version-log entries, NodeId
                                   sizes, the receivers' max_version stores) */
-    uint64_t reserved[5];
+    uint64_t live_bytes;       /* element bytes the liveness sweeps (k_liveness) loaded and stored: windows, state
+                                  bytes, times of death, ring entries, the report planes they replayed */
+    uint64_t reserved[4];
 } gs_counters;
 
 /* Failure-detector membership census (gs_fd_census): (observer, target) pairs with the observer up and

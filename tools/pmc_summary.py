@@ -8,8 +8,9 @@ under the same counters, and this script derives a factor per access width:
     factor = known bytes / (counter KiB x 1024)
 Each kernel's bytes are then (FETCH_SIZE x f_read(width) + WRITE_SIZE x f_write(width)) x 1024 with the
 width of the kernel's dominant streams:
-    k_pass1       4 B per lane (8-bit heartbeat / max_version rows, GS_HB8 + GS_MV8, 4 columns per lane;
-                  stores likewise; the 16-B owner-value loads are L2 hits)
+    k_pass1v      16 B per lane (8-bit heartbeat / max_version rows, GS_HB8 + GS_MV8, 16 columns per lane;
+                  stores likewise; the 4-B flag words are L2 hits)
+    k_pass1       4 B per lane (round 3's pass 1, env GS_P1=old; 4 columns per lane)
     k_lite        8 B (candidate records; the rest are gathers)
     k_pack_slice  8 B (candidate records; the rest are gathers, which no stream calibrates)
     k_settle      8 B (likewise: candidate records, owner-table gathers)
@@ -33,10 +34,10 @@ from collections import defaultdict
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
-KERNELS = ("k_pass1", "k_pack_slice", "k_settle", "k_lite", "k_liveness", "k_exchange", "k_count", "k_begin_round",
+KERNELS = ("k_pass1v", "k_pass1", "k_pack_slice", "k_settle", "k_lite", "k_liveness", "k_exchange", "k_count", "k_begin_round",
            "k_owner_writes", "k_reset_sched", "k_warm", "k_boot_self", "k_phi_row")
-WIDTH = {"k_pass1": 4, "k_pack_slice": 8, "k_settle": 8, "k_lite": 8, "k_liveness": 16, "k_exchange": 8, "k_count": 8}
-KIND = {"k_pass1": "pass1", "k_pack_slice": "pack", "k_settle": "count", "k_lite": "lite", "k_liveness": "liveness",
+WIDTH = {"k_pass1v": 16, "k_pass1": 4, "k_pack_slice": 8, "k_settle": 8, "k_lite": 8, "k_liveness": 16, "k_exchange": 8, "k_count": 8}
+KIND = {"k_pass1v": "pass1", "k_pass1": "pass1", "k_pack_slice": "pack", "k_settle": "count", "k_lite": "lite", "k_liveness": "liveness",
         "k_exchange": "pass1", "k_count": "count"}
 CAL_BYTES = 1 << 30
 
