@@ -60,7 +60,7 @@ REGIONS = [
     "HB", "MV", "GC", "HELD", "FD", "FD_STATE", "TS", "RING", "POS", "ORD", "ROW",
     "LAST_W", "HIST", "HIST_VID", "NID_SIZE", "KEY_LEN", "STAMP", "COUNTERS", "SLICE_BITS", "PEND", "PEND_STAMP", "LATEST",
     "SELF_HB", "CAND", "CAND_N", "FD_TOD", "FD_LAST", "SLOT_STAT", "RING_SLOT", "SELF_MV", "SELF_PK", "VLOG",
-    "P1FLAGS",
+    "P1FLAGS", "ESC16", "ESC_SLOT", "ESC_OWNER", "ESC_REQ",
 ]
 REGION = {n: i for i, n in enumerate(REGIONS)}
 
@@ -70,7 +70,7 @@ COUNTER_FIELDS = [
     "exchanges", "hb_reports", "node_deltas", "kvs_sent", "truncated", "delta_bytes", "alg_bytes", "hb_writes",
     "candidates", "live_pairs", "tomb_gc", "err_fd_overflow", "err_hist_full", "err_bad_index", "err_conflict",
     "err_fd_gc", "err_insert", "fd_gc", "q9", "pack_bytes", "err_holes", "err_hb_lag", "plane_flushes",
-    "fd_saturated", "lite_slots", "lag_sweeps", "lite_bytes", "live_bytes",
+    "fd_saturated", "lite_slots", "lag_sweeps", "lite_bytes", "live_bytes", "hb_escapes", "hb_releases",
 ]
 
 # Every symbol include/gossip_sim.h declares (checked by tests/test_abi.py).
@@ -84,7 +84,7 @@ EXPORTS = [
     "gs_latest_tick", "gs_flush_reports", "gs_set_ring_rows",
 ]
 
-API_VERSION = 16
+API_VERSION = 17
 MAX_PHASES = 64  # GS_MAX_PHASES
 
 
@@ -105,6 +105,7 @@ class GsConfig(C.Structure):
         ("n_shards", C.c_uint32),
         ("shard", C.c_uint32),
         ("ring_rows", C.c_uint32),
+        ("esc_cols", C.c_uint32),
     ]
 
 

@@ -76,12 +76,12 @@ enum Ctr {
     C_EXCH = 0, C_REPORTS, C_ND, C_KVS, C_TRUNC, C_DBYTES, C_ALG, C_HBW, C_CAND, C_LIVE, C_TOMBGC,
     C_E_FDOVF, C_E_HIST, C_E_IDX, C_E_CONFLICT, C_E_FDGC, C_E_INSERT, C_FDGC, C_Q9, C_PACKB, C_E_HOLES,
     C_E_HBLAG, C_FLUSH /* host-side: plane_flushes */, C_FDSAT, C_LITE, C_SWEEPS /* host-side: lag_sweeps */,
-    C_LITEB, C_LIVEB,
+    C_LITEB, C_LIVEB, C_ESC, C_ESCREL,
     C_CEN0 = 32, C_NUM = C_CEN0 + 6  // gs_fd_census scratch slots (not part of gs_counters)
 };
 constexpr int CROW = 40;  // u64 slots per counter shard row (the 32 gs_counters fields, then the census scratch)
 static_assert(C_NUM <= CROW, "counter region");
-static_assert(C_LIVEB < 32, "gs_counters fields");
+static_assert(C_ESCREL < 32, "gs_counters fields");
 static_assert(sizeof(gs_counters) == 32 * 8, "gs_counters layout");
 
 struct Dev {
@@ -155,6 +155,12 @@ struct Dev {
     // last lag sweep some view of j lagged by >= HOT_HB heartbeats or HOT_MV versions (GS_R_P1FLAGS)
     uint32_t *p1flags;
     uint32_t pl16;  // report planes in the 16-column layout of k_pass1v (plane16_bit), else the ballot layout
+    // escaped owner columns (gs_config.esc_cols, k_pass1v handles): EC slots of 16-bit views [N][EC]; esc_slot[j] =
+    // the slot of column j or NONE; esc_owner[s] = the column of slot s or NONE; esc_req = the sweep's scratch
+    // (columns to escape, bitmap [NP/32], then the move count and list)
+    uint16_t *esc16;
+    uint32_t *esc_slot, *esc_owner, *esc_req;
+    uint32_t EC;
     // event stream (gs_set_events): records {observer, owner, key | kind << 8, old version, new version,
     // tick, seq, 0}; kind 0 = on_key_change, 1 = node join, 2 = node leave; seq orders them (gossip_sim.h,
 // gs_set_events).  ev == nullptr: off
@@ -1115,11 +1121,17 @@ __device__ __forceinline__ uint32_t hb_dec8(uint32_t s, uint32_t R) { return R -
 __device__ __forceinline__ uint32_t hb_raw(const Dev &d, size_t p) {
     return d.hb8 ? (uint32_t) reinterpret_cast<const uint8_t *>(d.hb)[p] : (uint32_t)d.hb[p];
 }
+// an escaped owner column (gs_config.esc_cols) keeps its views in 16-bit slots: the slot index of view p, or NONE
+__device__ __forceinline__ uint32_t esc_of(const Dev &d, size_t p) { return d.EC ? d.esc_slot[p % d.NP] : NONE; }
 __device__ __forceinline__ void hb_put(const Dev &d, size_t p, uint32_t v) {
-    if (d.hb8) reinterpret_cast<uint8_t *>(d.hb)[p] = (uint8_t)v;
+    const uint32_t es = esc_of(d, p);
+    if (es != NONE) d.esc16[(p / d.NP) * d.EC + es] = (uint16_t)v;
+    else if (d.hb8) reinterpret_cast<uint8_t *>(d.hb)[p] = (uint8_t)v;
     else d.hb[p] = (uint16_t)v;
 }
 __device__ __forceinline__ uint32_t hb_view(const Dev &d, size_t p, uint32_t R) {
+    const uint32_t es = esc_of(d, p);
+    if (es != NONE) return hb_dec(d.esc16[(p / d.NP) * d.EC + es], R);
     return d.hb8 ? hb_dec8(hb_raw(d, p), R) : hb_dec(hb_raw(d, p), R);
 }
 __device__ __forceinline__ void st4b(uint8_t *p, const uint32_t (&v)[4]) {
@@ -1721,7 +1733,8 @@ struct P1vSlow {
 __device__ __noinline__ P1vSlow pass1v_slow(const uint32_t *self_pk, const uint8_t *fd_state, const uint32_t *tod,
                                             uint32_t delay, uint32_t col_lo, uint32_t ncol, size_t ra, size_t rb,
                                             uint32_t c, uint32_t a, uint32_t b, uint32_t t, bool schA, bool schB,
-                                            uint4 hA4, uint4 hB4, uint4 mA4, uint4 mB4) {
+                                            uint4 hA4, uint4 hB4, uint4 mA4, uint4 mB4, const uint32_t *esc_slot,
+                                            uint16_t *esc16, uint32_t EC, const uint32_t *self_hb) {
     P1vSlow o{};
     const uint32_t x4[4] = {hA4.x, hA4.y, hA4.z, hA4.w}, y4[4] = {hB4.x, hB4.y, hB4.z, hB4.w};
     const uint32_t ma4[4] = {mA4.x, mA4.y, mA4.z, mA4.w}, mb4[4] = {mB4.x, mB4.y, mB4.z, mB4.w};
@@ -1730,6 +1743,11 @@ __device__ __noinline__ P1vSlow pass1v_slow(const uint32_t *self_pk, const uint8
         const uint32_t c0 = c + 4u * q;
         const uint4 pk = *reinterpret_cast<const uint4 *>(self_pk + c0);
         const uint32_t pk4[4] = {pk.x, pk.y, pk.z, pk.w};
+        uint32_t es4[4] = {NONE, NONE, NONE, NONE};  // escaped columns: 16-bit views in their slots
+        if (EC) {
+            const uint4 e = *reinterpret_cast<const uint4 *>(esc_slot + c0);
+            es4[0] = e.x; es4[1] = e.y; es4[2] = e.z; es4[3] = e.w;
+        }
         uint32_t oA = 0u, oB = 0u, rA = 0u, rB = 0u, bA = 0u, bB = 0u;
 #pragma unroll
         for (int i = 0; i < 4; i++) {
@@ -1739,7 +1757,17 @@ __device__ __noinline__ P1vSlow pass1v_slow(const uint32_t *self_pk, const uint8
             const bool sa = schA && valid && (fd_state[ra + j] & FD_MEMB) == FD_DEAD && is_sched(tod[ra + j], t, delay);
             const bool sb = schB && valid && (fd_state[rb + j] & FD_MEMB) == FD_DEAD && is_sched(tod[rb + j], t, delay);
             const uint32_t Rx = pk4[i] & 0xFFFFu, M = pk4[i] >> 16;
-            uint32_t hA = hb_dec8((x4[q] >> (8 * i)) & 0xFFu, Rx), hB = hb_dec8((y4[q] >> (8 * i)) & 0xFFu, Rx);
+            const uint32_t es = es4[i];
+            const size_t eA = (size_t)a * EC + es, eB = (size_t)b * EC + es;
+            uint32_t hA, hB;
+            if (es != NONE) {  // decoded against the full own heartbeat: the stores below keep its low 16 bits
+                const uint32_t R = self_hb[j];
+                hA = hb_dec(esc16[eA], R);
+                hB = hb_dec(esc16[eB], R);
+            } else {
+                hA = hb_dec8((x4[q] >> (8 * i)) & 0xFFu, Rx);
+                hB = hb_dec8((y4[q] >> (8 * i)) & 0xFFu, Rx);
+            }
             const uint32_t mA = mv_dec8((ma4[q] >> (8 * i)) & 0xFFu, M) & MV_MASK;
             const uint32_t mB = mv_dec8((mb4[q] >> (8 * i)) & 0xFFu, M) & MV_MASK;
             const bool isb = valid && jg == b;
@@ -1750,6 +1778,10 @@ __device__ __noinline__ P1vSlow pass1v_slow(const uint32_t *self_pk, const uint8
             const bool upA = valid && !sb && jg != a && hB > hA;  // then a merges b's (server.py:340, 356-357)
             const bool repA = upA && hA != 0u;
             hA = upA ? hB : hA;
+            if (es != NONE) {
+                if (upA) esc16[eA] = (uint16_t)hA;
+                if (upB || isb) esc16[eB] = (uint16_t)hB;
+            }
             oA |= (hA & 0xFFu) << (8 * i);
             oB |= (hB & 0xFFu) << (8 * i);
             o.upA |= (uint32_t)upA;
@@ -1883,7 +1915,7 @@ __global__ __launch_bounds__(XB, P1V_WAVES) void k_pass1v(Dev d, const int32_t *
             reports += (uint32_t)(__popc(pA) + __popc(pB));
         } else if (slow) {
             const P1vSlow o = pass1v_slow(d.self_pk, d.fd_state, d.tod, d.sched_delay, d.col_lo, d.ncol, ra, rb, c, a, b,
-                                          t, schA, schB, v.hA, v.hB, v.mA, v.mB);
+                                          t, schA, schB, v.hA, v.hB, v.mA, v.mB, d.esc_slot, d.esc16, d.EC, d.self_hb);
             if (!(d.ablate & 2u)) {
                 if (o.upA) *reinterpret_cast<uint4 *>(reinterpret_cast<uint8_t *>(d.hb) + ra + c) = make_uint4(o.nwA[0], o.nwA[1], o.nwA[2], o.nwA[3]);
                 if (o.upB) *reinterpret_cast<uint4 *>(reinterpret_cast<uint8_t *>(d.hb) + rb + c) = make_uint4(o.nwB[0], o.nwB[1], o.nwB[2], o.nwB[3]);
@@ -2635,7 +2667,7 @@ template <int RING>
 #define LIVE_WAVES 8  // waves per SIMD k_liveness is compiled for (<= 64 VGPRs)
 #endif
 #ifndef LIVE_NT
-#define LIVE_NT 0  // A/B: non-temporal loads / stores of the windows and state bytes
+#define LIVE_NT 1  // non-temporal loads / stores of the windows and state bytes (streamed once per round; r4c: 11.86 vs 12.21 ms)
 #endif
 __global__ __launch_bounds__(LB, LIVE_WAVES) void k_liveness(Dev d, const uint8_t *up, uint32_t t, uint32_t chunks,
                                                  uint32_t per, bool replay, bool decide) {
@@ -3059,6 +3091,7 @@ __global__ __launch_bounds__(LB) void k_hb_lag(Dev d, uint32_t chunks) {
     const uint32_t per = d.hb8 ? 16u : 8u;
     const uint32_t j0 = (cb * LB + threadIdx.x) * per;
     uint32_t bad = 0, hot = 0;  // hot: bit k = view k of this thread's (at most 16)
+    uint32_t hotc = 0;           // ... of an escaped column: always marks the column (k_esc_plan's release test)
     if (d.p1flags) {
         if (threadIdx.x == 0) s_hot = 0u;
         __syncthreads();
@@ -3079,14 +3112,29 @@ __global__ __launch_bounds__(LB) void k_hb_lag(Dev d, uint32_t chunks) {
             const uint32_t own[4] = {ow.x, ow.y, ow.z, ow.w}, owm[4] = {om.x, om.y, om.z, om.w};
             uint32_t ps[4] = {0u, 0u, 0u, 0u};
             if (genm) ld4(d.pos + p0 + 4u * q, ps);
+            uint32_t es[4] = {NONE, NONE, NONE, NONE};  // escape slots (gs_config.esc_cols)
+            if (d.EC) ld4(d.esc_slot + jq, es);
 #pragma unroll
             for (uint32_t i = 0; i < 4; i++) {
                 if (jq + i >= d.ncol || (genm && ps[i] == NONE)) continue;
                 const uint32_t k = 4u * q + i;  // view index within the thread's loads
-                const uint32_t s = d.hb8 ? (hw[k >> 2] >> (8 * (k & 3))) & 0xFFu : (hw[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
-                const uint32_t lag = d.hb8 ? (own[i] - s) & 0xFFu : (own[i] - s) & 0xFFFFu;
-                if (lag >= (d.hb8 ? 0x80u : 0x8000u)) bad++;
-                bool h = d.hb8 && lag >= HOT_HB;
+                bool h;
+                if (es[i] != NONE) {  // an escaped column: 16-bit views, exact while they lag by < 2^15
+                    const uint32_t lag = (own[i] - d.esc16[(size_t)o * d.EC + es[i]]) & 0xFFFFu;
+                    if (lag >= 0x8000u) bad++;
+                    hotc |= (uint32_t)(lag >= HOT_HB) << k;  // no view hot at this sweep: k_esc_plan moves it back
+                    h = false;
+                } else {
+                    const uint32_t s = d.hb8 ? (hw[k >> 2] >> (8 * (k & 3))) & 0xFFu : (hw[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
+                    const uint32_t lag = d.hb8 ? (own[i] - s) & 0xFFu : (own[i] - s) & 0xFFFFu;
+                    if (lag >= (d.hb8 ? 0x80u : 0x8000u)) {
+                        // 8-bit views: escape the column (k_esc_plan; its views lag by < 2^7 + 2^6 now, exact), or,
+                        // without escape slots, count the view
+                        if (d.EC) atomicOr(&d.esc_req[(jq + i) >> 5], 1u << ((jq + i) & 31u));
+                        else bad++;
+                    }
+                    h = d.hb8 && lag >= HOT_HB;
+                }
                 if (d.mv8) {  // GS_MV8: max_version views lag their owner by < 2^6 at every sweep
                     const uint32_t sm = (mw[k >> 2] >> (8 * (k & 3))) & 0x7Fu;
                     const uint32_t ml = (owm[i] - sm) & 0x7Fu;
@@ -3104,9 +3152,9 @@ __global__ __launch_bounds__(LB) void k_hb_lag(Dev d, uint32_t chunks) {
         __syncthreads();
         if (s_hot >= HOT_ROW_MIN) {
             if (threadIdx.x == 0) atomicOr(&d.row[o * 4 + 3], 4u);
-        } else if (hot) {  // 16 views per thread: one 16-column group (per = 16 with GS_HB8)
-            atomicOr(&d.p1flags[j0 >> 4], hot << 16);
+            hot = 0u;
         }
+        if (hot | hotc) atomicOr(&d.p1flags[j0 >> 4], (hot | hotc) << 16);  // 16 views: one 16-column group
     }
     const unsigned long long sb = wave_sum(bad);
     if ((threadIdx.x & 63) == 0) shard_add(d, C_E_HBLAG, sb);
@@ -3116,6 +3164,85 @@ __global__ __launch_bounds__(LB) void k_hot_clear(Dev d) {
     const uint32_t i = blockIdx.x * LB + threadIdx.x;
     if (i < d.N) d.row[i * 4 + 3] &= ~4u;
     if (i < d.NP / 16u) d.p1flags[i] &= 0xFFFFu;
+}
+
+// Escaped owner columns (gs_config.esc_cols), after a lag sweep: one workgroup decides the moves -- an escaped
+// column none of whose views is hot any more (every lag < HOT_HB) goes back to 8-bit views, a column the sweep
+// flagged (a view lagging by >= 2^7) takes a free slot (none free: counted in err_hb_lag) -- and marks every
+// escaped column hot (pass 1 takes them on its per-column path); k_esc_move then copies the columns.  A slot
+// released here is not reused before the next sweep (the copy out reads it).
+constexpr uint32_t ESC_MAX = 4096;
+__device__ inline uint32_t *esc_moves(const Dev &d) { return d.esc_req + d.NP / 32; }  // [0] count, then pairs
+__global__ __launch_bounds__(1024) void k_esc_plan(Dev d) {
+    __shared__ uint32_t s_free[ESC_MAX];
+    __shared__ uint32_t s_nfree, s_next, s_nmove, s_esc, s_rel, s_err;
+    const uint32_t tid = threadIdx.x;
+    if (tid == 0) { s_nfree = 0; s_next = 0; s_nmove = 0; s_esc = 0; s_rel = 0; s_err = 0; }
+    __syncthreads();
+    uint32_t *mv = esc_moves(d);
+    // releases, and the slots free before this sweep
+    for (uint32_t sl = tid; sl < d.EC; sl += 1024) {
+        const uint32_t j = d.esc_owner[sl];
+        if (j == NONE) {
+            s_free[atomicAdd(&s_nfree, 1u)] = sl;
+        } else if (!((d.p1flags[j >> 4] >> (16u + (j & 15u))) & 1u)) {
+            const uint32_t m = atomicAdd(&s_nmove, 1u);
+            mv[1 + 2 * m] = j | 0x80000000u;  // out
+            mv[2 + 2 * m] = sl;
+            d.esc_slot[j] = NONE;
+            d.esc_owner[sl] = NONE;
+            atomicAdd(&s_rel, 1u);
+        }
+    }
+    __syncthreads();
+    // escapes
+    for (uint32_t w = tid; w < d.NP / 32; w += 1024) {
+        uint32_t bits = d.esc_req[w];
+        if (!bits) continue;
+        d.esc_req[w] = 0u;
+        for (; bits; bits &= bits - 1u) {
+            const uint32_t j = w * 32u + (uint32_t)__builtin_ctz(bits);
+            if (d.esc_slot[j] != NONE) continue;  // (already escaped: the sweep flags bytes only)
+            const uint32_t k = atomicAdd(&s_next, 1u);
+            if (k >= s_nfree) { atomicAdd(&s_err, 1u); continue; }
+            const uint32_t sl = s_free[k];
+            d.esc_owner[sl] = j;
+            d.esc_slot[j] = sl;
+            const uint32_t m = atomicAdd(&s_nmove, 1u);
+            mv[1 + 2 * m] = j;  // in
+            mv[2 + 2 * m] = sl;
+            atomicAdd(&s_esc, 1u);
+        }
+    }
+    __syncthreads();
+    // every escaped column is hot until it is moved back
+    for (uint32_t sl = tid; sl < d.EC; sl += 1024) {
+        const uint32_t j = d.esc_owner[sl];
+        if (j != NONE) atomicOr(&d.p1flags[j >> 4], 1u << (16u + (j & 15u)));
+    }
+    if (tid == 0) {
+        mv[0] = s_nmove;
+        shard_add(d, C_ESC, s_esc);
+        shard_add(d, C_ESCREL, s_rel);
+        shard_add(d, C_E_HBLAG, s_err);  // no free slot: the column stays in bytes, the run is reported inexact
+    }
+}
+// The moves of k_esc_plan for every observer row (one thread per row): in = the 8-bit view decoded against the
+// owner's own heartbeat (its lag < 2^7 + 2^6: exact) into the slot, out = the slot's view back to its byte (lag
+// < HOT_HB: exact)
+__global__ __launch_bounds__(LB) void k_esc_move(Dev d) {
+    const uint32_t o = blockIdx.x * LB + threadIdx.x;
+    if (o >= d.N) return;
+    const uint32_t *mv = esc_moves(d);
+    const uint32_t nm = mv[0];
+    uint8_t *h8 = reinterpret_cast<uint8_t *>(d.hb);
+    for (uint32_t m = 0; m < nm; m++) {
+        const uint32_t jw = mv[1 + 2 * m], sl = mv[2 + 2 * m], j = jw & 0x7FFFFFFFu;
+        const uint32_t R = d.self_hb[j];
+        const size_t p = pix(d, o, j), e = (size_t)o * d.EC + sl;
+        if (jw & 0x80000000u) h8[p] = (uint8_t)hb_dec(d.esc16[e], R);
+        else d.esc16[e] = (uint16_t)hb_dec8(h8[p], R);
+    }
 }
 
 // ------------------------------------------------------------------ owner writes
@@ -3996,6 +4123,10 @@ int check_bound(gs_handle *h) {
     d.self_mv = (uint32_t *)h->reg[GS_R_SELF_MV];
     d.self_pk = (uint32_t *)h->reg[GS_R_SELF_PK];
     d.p1flags = (uint32_t *)h->reg[GS_R_P1FLAGS];
+    d.esc16 = (uint16_t *)h->reg[GS_R_ESC16];
+    d.esc_slot = (uint32_t *)h->reg[GS_R_ESC_SLOT];
+    d.esc_owner = (uint32_t *)h->reg[GS_R_ESC_OWNER];
+    d.esc_req = (uint32_t *)h->reg[GS_R_ESC_REQ];
     return GS_OK;
 }
 
@@ -4227,6 +4358,16 @@ int gs_create(const gs_config *cfg, gs_handle **out) {
     b[GS_R_SELF_MV] = NP * 4;
     b[GS_R_SELF_PK] = (c.flags & GS_MV8) ? NP * 4 : 0;
     b[GS_R_P1FLAGS] = (c.flags & GS_MV8) ? NP / 16 * 4 : 0;  // k_pass1v's small / hot bits
+    if (c.esc_cols > ESC_MAX || (c.esc_cols && !(c.flags & GS_MV8))) {
+        delete h;
+        return GS_E_INVALID;
+    }
+    // escape slots only where k_pass1v runs (its per-column path reads them): set below with d.pl16
+    const uint64_t EC = c.esc_cols;
+    b[GS_R_ESC16] = N * EC * 2;
+    b[GS_R_ESC_SLOT] = EC ? NP * 4 : 0;
+    b[GS_R_ESC_OWNER] = EC * 4;
+    b[GS_R_ESC_REQ] = EC ? (NP / 32 + 1 + 4 * EC) * 4 : 0;
     b[GS_R_GC] = (c.flags & GS_TOMBSTONES) ? pairs * 4 : 0;  // last_gc_version stays 0 without tombstone GC
     b[GS_R_HELD] = (c.flags & GS_NO_HELD) ? 0 : pairs * KP;
     b[GS_R_FD] = pairs * 4;
@@ -4300,6 +4441,9 @@ int gs_create(const gs_config *cfg, gs_handle **out) {
         const char *p1 = getenv("GS_P1");
         d.pl16 = d.mv8 && h->pack_mode == 2 && !(p1 && !strcmp(p1, "old")) ? 1u : 0u;
     }
+    if (!d.pl16)
+        for (int r : {GS_R_ESC16, GS_R_ESC_SLOT, GS_R_ESC_OWNER, GS_R_ESC_REQ}) b[r] = 0;
+    d.EC = d.pl16 ? c.esc_cols : 0u;
     if (const char *ab = getenv("GS_ABLATE")) d.ablate = (uint32_t)atoi(ab);
     d.phi_thr = c.phi_threshold;
     d.prior5 = c.prior_weighted;
@@ -4351,13 +4495,15 @@ int gs_boot(gs_handle *h, const uint16_t *nid_size, const uint8_t *key_len) {
     const int zero[] = {GS_R_HB, GS_R_SELF_HB, GS_R_MV, GS_R_GC, GS_R_HELD, GS_R_FD, GS_R_FD_LAST, GS_R_FD_STATE, GS_R_FD_TOD,
                         GS_R_RING, GS_R_ROW, GS_R_LAST_W, GS_R_HIST, GS_R_HIST_VID,
                         GS_R_STAMP, GS_R_COUNTERS, GS_R_SLICE_BITS, GS_R_PEND, GS_R_PEND_STAMP, GS_R_LATEST,
-                        GS_R_SLOT_STAT, GS_R_VLOG, GS_R_SELF_MV, GS_R_SELF_PK, GS_R_P1FLAGS};
+                        GS_R_SLOT_STAT, GS_R_VLOG, GS_R_SELF_MV, GS_R_SELF_PK, GS_R_P1FLAGS, GS_R_ESC16, GS_R_ESC_REQ};
     for (int r : zero)
         if (h->bytes[r]) HIPCHK(h, hipMemsetAsync(h->reg[r], 0, h->bytes[r], s));
     if (h->bytes[GS_R_TS]) HIPCHK(h, hipMemsetAsync(h->reg[GS_R_TS], 0xFF, h->bytes[GS_R_TS], s));
     if (h->bytes[GS_R_POS]) HIPCHK(h, hipMemsetAsync(h->reg[GS_R_POS], 0xFF, h->bytes[GS_R_POS], s));
     if (h->bytes[GS_R_ORD]) HIPCHK(h, hipMemsetAsync(h->reg[GS_R_ORD], 0xFF, h->bytes[GS_R_ORD], s));
     if (h->bytes[GS_R_RING_SLOT]) HIPCHK(h, hipMemsetAsync(h->reg[GS_R_RING_SLOT], 0xFF, h->bytes[GS_R_RING_SLOT], s));
+    for (int r : {GS_R_ESC_SLOT, GS_R_ESC_OWNER})  // no escaped columns
+        if (h->bytes[r]) HIPCHK(h, hipMemsetAsync(h->reg[r], 0xFF, h->bytes[r], s));
     // tables
     // nid_size covers all n_nodes (the packer's stop bound must hold across slices); keep this slice's
     std::vector<uint16_t> ns(h->NP, 0);
@@ -4461,6 +4607,12 @@ int gs_check_heartbeat_lag(gs_handle *h) {
     }
     k_hb_lag<<<h->N * chunks, LB, 0, h->stream>>>(h->d, chunks);
     HIPCHK(h, hipGetLastError());
+    if (h->d.EC) {  // escaped owner columns: moves decided, then copied (one pass over the rows)
+        k_esc_plan<<<1, 1024, 0, h->stream>>>(h->d);
+        HIPCHK(h, hipGetLastError());
+        k_esc_move<<<(h->N + LB - 1) / LB, LB, 0, h->stream>>>(h->d);
+        HIPCHK(h, hipGetLastError());
+    }
     h->lag_sweeps++;
     h->hb_incs = 0;
     h->mv_incs = 0;
@@ -4819,7 +4971,7 @@ int gs_flush_reports(gs_handle *h, uint32_t tick) {
 
 int gs_read_rows(gs_handle *h, int region, uint32_t row_lo, uint32_t row_hi, void *out, uint64_t cap, uint64_t *len) {
     static const int rows_major[] = {GS_R_HB, GS_R_MV, GS_R_GC, GS_R_HELD, GS_R_FD, GS_R_FD_LAST, GS_R_FD_STATE,
-                                     GS_R_FD_TOD, GS_R_TS, GS_R_RING, GS_R_POS, GS_R_ORD, GS_R_ROW};
+                                     GS_R_FD_TOD, GS_R_TS, GS_R_RING, GS_R_POS, GS_R_ORD, GS_R_ROW, GS_R_ESC16};
     if (!h || !h->booted || !out || !len || row_lo > row_hi || row_hi > h->N) return GS_E_INVALID;
     if (std::find(std::begin(rows_major), std::end(rows_major), region) == std::end(rows_major))
         return fail(h, GS_E_INVALID, "gs_read_rows: region %d is not indexed by observer row", region);

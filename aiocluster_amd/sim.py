@@ -172,7 +172,7 @@ class GossipSim:
                  tombstones: bool = True, fd_ring: bool | None = None, hist_cap: int = 64,
                  nid_sizes: list[int] | None = None, initial_ops: list[np.ndarray] | None = None,
                  canonical: bool | None = None, shards: int = 1, shard: int = 0, held: bool = True,
-                 ring_rows=None, hb8: bool = False, mv8: bool = False, sliced: bool = False):
+                 ring_rows=None, hb8: bool = False, mv8: bool = False, sliced: bool = False, esc_cols: int | None = None):
         import torch
 
         if not torch.cuda.is_available():
@@ -229,6 +229,9 @@ class GossipSim:
         self.flags = flags
         self.canonical = bool(flags & GS_CANONICAL)
         c = make_config(n, k, cfg, flags, hist_cap, shards, shard, len(self.ring_rows))
+        # escape slots for owner columns whose 8-bit views fall >= 2^7 behind (GS_MV8): 256 by default
+        c.esc_cols = (256 if esc_cols is None else int(esc_cols)) if mv8 else 0
+        self.c_esc_cols = c.esc_cols
         h = C.c_void_p()
         rc = self.L.gs_create(C.byref(c), C.byref(h))
         if rc:
@@ -597,16 +600,32 @@ class GossipSim:
         """GS_R_HB as a device tensor [N, NP]: int16 views (mod 2^16), or uint8 with GS_HB8 (mod 2^8)."""
         return self.region("HB", self.torch.uint8 if self.hb8 else self.torch.int16, (self.n, self.np_))
 
-    def decode_heartbeats(self, hb: np.ndarray) -> np.ndarray:
-        """NodeState.heartbeat of host rows of GS_R_HB (u16, or u8 with GS_HB8; any leading shape [..., NP]):
+    def decode_heartbeats(self, hb: np.ndarray, rows=None) -> np.ndarray:
+        """NodeState.heartbeat of host rows of GS_R_HB (u16, or u8 with GS_HB8; shape [rows, NP] or [NP]):
         the stored value is the heartbeat mod 2^16 (2^8), decoded against the owner's own heartbeat R
-        (GS_R_SELF_HB)."""
+        (GS_R_SELF_HB).  ``rows``: the observer rows of ``hb`` (default: all rows, or the single row of a 1-D
+        ``hb``); escaped owner columns (gs_config.esc_cols) are read from their 16-bit slots (GS_R_ESC16)."""
         R = self.region("SELF_HB", self.torch.int32, (self.np_,)).cpu().numpy().view(np.uint32)
         if self.hb8:
             s = np.asarray(hb).view(np.uint8).astype(np.uint32)
-            return (R - ((R - s) & np.uint32(0xFF))).astype(np.uint32)
-        s = np.asarray(hb).view(np.uint16).astype(np.uint32)
-        return (R - ((R - s) & np.uint32(0xFFFF))).astype(np.uint32)
+            out = (R - ((R - s) & np.uint32(0xFF))).astype(np.uint32)
+        else:
+            s = np.asarray(hb).view(np.uint16).astype(np.uint32)
+            out = (R - ((R - s) & np.uint32(0xFFFF))).astype(np.uint32)
+        if "ESC_SLOT" in self.regions:
+            slot = self.region("ESC_SLOT", self.torch.int32, (self.np_,)).cpu().numpy().view(np.uint32)
+            cols = np.nonzero(slot != GS_NONE)[0]
+            if len(cols):
+                ec = int(self.c_esc_cols)
+                esc = self.region("ESC16", self.torch.int16, (self.n, ec)).cpu().numpy().view(np.uint16)
+                o = np.arange(self.n) if rows is None else np.asarray(rows, dtype=np.int64)
+                e = esc[o][:, slot[cols].astype(np.int64)].astype(np.uint32)  # [rows, escaped columns]
+                v = (R[cols] - ((R[cols] - e) & np.uint32(0xFFFF))).astype(np.uint32)
+                if out.ndim == 1:
+                    out[cols] = v[0]
+                else:
+                    out[:, cols] = v
+        return out
 
     def max_versions(self):
         """Device int32 [N, NP] NodeState.max_version of every view (GS_R_MV words: version | GS_MV_INEXACT)."""
@@ -632,7 +651,8 @@ class GossipSim:
             return (t if rows is None else t.index_select(0, sel)).cpu().numpy()
 
         g = {"rows": np.arange(n) if rows is None else rows}
-        g["HB"] = self.decode_heartbeats(rd("HB", torch.uint8 if self.hb8 else torch.int16, (n, NP)))
+        g["HB"] = self.decode_heartbeats(rd("HB", torch.uint8 if self.hb8 else torch.int16, (n, NP)),
+                                         None if rows is None else rows)
         for name in ("GC", "POS"):
             if name in self.regions:
                 g[name] = rd(name, torch.int32, (n, NP)).view(np.uint32)
@@ -803,10 +823,7 @@ class GossipSim:
                 return None
         self.materialize_held(o, o + 1)
         self.sync()
-        R = int(self.region("SELF_HB", torch.int32, (self.np_,))[j].item()) & 0xFFFFFFFF
-        s = int(self.hb_region()[o, j].item()) & 0xFFFF
-        m = 0xFF if self.hb8 else 0xFFFF
-        hb = (R - ((R - s) & m)) & 0xFFFFFFFF
+        hb = int(self.decode_heartbeats(self.hb_region()[o].cpu().numpy(), [o])[j])
         mv = int(self.mv_words(slice(o, o + 1))[0, j].item()) & 0x7FFF
         gc = int(self.region("GC", torch.int32, (n, self.np_))[o, j].item()) & 0xFFFFFFFF \
             if "GC" in self.regions else 0
@@ -845,7 +862,7 @@ class GossipSim:
         def row(name, dt=torch.int32):
             return self.region(name, dt, (n, self.np_))[o, :n].cpu().numpy()
 
-        hb = self.decode_heartbeats(self.hb_region()[o].cpu().numpy())[:n]
+        hb = self.decode_heartbeats(self.hb_region()[o].cpu().numpy(), [o])[:n]
         mv = self.mv_words(slice(o, o + 1))[0, :n].cpu().numpy().astype(np.uint32) & np.uint32(0x7FFF)
         gc = row("GC").view(np.uint32) if "GC" in self.regions else np.zeros(n, np.uint32)
         st = fd_state_word(row("FD_STATE", torch.uint8), row("FD_TOD"))

@@ -539,11 +539,9 @@ def main():
                     help="version-only layout (GS_NO_HELD, config 4): needs an mtu no delta reaches")
     args = ap.parse_args()
 
-    if args.peer_select:
-        # every round scheduled by the reference's selection: ~16 phases per round and uneven responder
-        # load let heartbeat views lag their owners past the 8-bit bound (r3l: err_hb_lag), so such runs
-        # use the 16-bit views (the headline's permutation schedule peaks at a lag of 49: tools/hb_lag.py)
-        args.wide_views = True
+    # --peer-select keeps the 8-bit views: the reference's selection routes the first rounds' seed picks to 8 hub
+    # columns whose views fall up to ~280 heartbeats behind (r4b census, tools/hb_lag.py); the lag sweeps move
+    # such columns to 16-bit escape slots (gs_config.esc_cols) and back, so the run stays exact
     world = int(os.environ.get("WORLD_SIZE", "0"))
     if world == 0:
         if args.gpus > 1:  # plain `python bench.py --gpus N`: become the launcher of N ranks

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define GS_API_VERSION 16
+#define GS_API_VERSION 17
 #define GS_MAX_PHASES 64  /* gs_schedule_phases: phases per round */
 #define GS_TICK_US 15625u
 #define GS_NONE 0xFFFFFFFFu
@@ -96,6 +96,13 @@ typedef struct gs_config {
                                        past W intervals, BoundedArrayStats); the other rows keep compact
                                        windows, exact up to W intervals, and a compact window that would need
                                        an eviction is counted in fd_saturated (not an error) */
+    uint32_t esc_cols;              /* GS_MV8 record phases: escape slots for owner columns whose views fall far behind
+                                       (<= 4096; 0 = none).  A lag sweep that finds a heartbeat view lagging its owner
+                                       by >= 2^7 moves every view of that owner column into a 16-bit slot (GS_R_ESC16,
+                                       exact while lags stay < 2^15) instead of counting err_hb_lag, and moves it back
+                                       once every view of it lags by < 2^6: the hub columns of the
+                                       reference's peer selection (seeds answering every phase) stay exact.  A sweep
+                                       that finds no free slot counts the column in err_hb_lag */
 } gs_config;
 
 /* device regions (all caller-allocated).  [N][NP] regions hold every observer row o and this
@@ -174,6 +181,12 @@ enum gs_region {
     GS_R_P1FLAGS,     /* u32 [NP/16]   GS_MV8: per 16-owner group, bit i = owner 16 g + i's own heartbeat is < 2^8, bit
                                         16 + i = that owner is "hot" (some view of it lagged by >= 64 heartbeats or >= 32
                                         versions at the last lag sweep): pass 1's byte-parallel path skips hot owners */
+    GS_R_ESC16,       /* u16 [N][esc_cols] the escaped owner columns' heartbeat views mod 2^16 (observer o, slot s),
+                                        decoded against the owner's own heartbeat; GS_R_HB's bytes of those columns
+                                        are not used while they are escaped */
+    GS_R_ESC_SLOT,    /* u32 [NP]      escape slot of each owner column, GS_NONE = its views are the bytes of GS_R_HB */
+    GS_R_ESC_OWNER,   /* u32 [esc_cols] the owner column of each slot, GS_NONE = free */
+    GS_R_ESC_REQ,     /* u32 [NP/32 + 16] sweep scratch: columns to escape (bitmap), then the sweep's move list */
     GS_NUM_REGIONS
 };
 
@@ -221,7 +234,9 @@ typedef struct gs_counters {
                                   sizes, the receivers' max_version stores) */
     uint64_t live_bytes;       /* element bytes the liveness sweeps (k_liveness) loaded and stored: windows, state
                                   bytes, times of death, ring entries, the report planes they replayed */
-    uint64_t reserved[4];
+    uint64_t hb_escapes;       /* owner columns moved to 16-bit escape slots by lag sweeps (gs_config.esc_cols) */
+    uint64_t hb_releases;      /* escaped owner columns moved back to 8-bit views */
+    uint64_t reserved[2];
 } gs_counters;
 
 /* Failure-detector membership census (gs_fd_census): (observer, target) pairs with the observer up and

@@ -16,7 +16,7 @@ from oracle import OracleSim
 
 from aiocluster_amd.scenario import DEFAULT_CFG
 from aiocluster_amd.sim import GossipSim
-from aiocluster_amd.workload import key_names, liveness_tick, phase_tick, round_tick, synthetic_node_ids
+from aiocluster_amd.workload import WorkloadSpec, key_names, liveness_tick, phase_tick, round_tick, synthetic_node_ids
 
 pytestmark = pytest.mark.gpu
 
@@ -254,3 +254,88 @@ def test_hb8_round_of_300_phases_is_reported_not_silently_wrong():
     _long_round(gpu, None, 300, round_tick(0))
     with pytest.raises(GsError, match="err_hb_lag"):
         gpu.check()
+
+
+def test_hb8mv8_round_of_300_phases_escapes_and_matches_oracle():
+    """The same 300-phase round with GS_MV8 (k_pass1v and escape slots, gs_config.esc_cols): the lag sweep that
+    finds the idle nodes' views of node 1 at >= 2^7 moves column 1 to 16-bit views, so the round stays exact;
+    the device matches the C oracle array for array, and the column goes back to bytes once caught up."""
+    import torch
+
+    n = 8
+    ids, keys = synthetic_node_ids(n), key_names(2)
+    init = {j: [(0, f"v{j}")] for j in range(n)}
+    gpu = GossipSim(ids, keys, dict(DEFAULT_CFG), "warm", init, tombstones=False, fd_ring=True, hist_cap=8,
+                    hb8=True, mv8=True)
+    orc = OracleSim(ids, keys, dict(DEFAULT_CFG), "warm", init)
+    _long_round(gpu, orc, 300, round_tick(0))
+    want = orc.export()
+    assert np.asarray(want["hb"])[1, 1] - np.asarray(want["hb"])[7, 1] >= 256  # beyond what a byte holds
+    diff = compare_exports(gpu.export(), want)
+    assert diff is None, diff
+    c = gpu.check()
+    assert c["err_hb_lag"] == 0 and c["hb_escapes"] >= 1, c
+    # a normal round lets the idle nodes catch up: the next sweeps move the column back
+    up = np.ones(n, np.uint8)
+    up_dev = torch.from_numpy(up).to(gpu.device)
+    for r in range(6, 30):
+        t = round_tick(r)
+        gpu.begin_round(t, up_dev)
+        orc.begin_round(t, up)
+        for p in range(2):
+            pairs = SCHED[(r + p) % len(SCHED)]
+            gpu.run_phase(phase_tick(r, p), pairs)
+            orc.run_phase(phase_tick(r, p), pairs)
+        gpu.liveness(liveness_tick(r, 2), up_dev)
+        orc.liveness(liveness_tick(r, 2), up)
+    gpu.check_heartbeat_lag()
+    diff = compare_exports(gpu.export(), orc.export())
+    assert diff is None, diff
+    c = gpu.check()
+    assert c["hb_releases"] >= 1 and c["err_hb_lag"] == 0, c
+
+
+def test_hb8mv8_100_selected_rounds_at_16384_match_oracle():
+    """the reference's own peer selection (select_nodes_for_gossip, 8 seeds; the first rounds
+    after a warm start route every node's seed pick to 8 hub columns, whose views then lag by up to ~280
+    heartbeats) drives 101 rounds of a 16,384-node cluster in the 8-bit layout (GS_HB8 + GS_MV8 with escape
+    slots).  Every phase of round 6 (hub columns escaped) and of round 100 is checked on sampled rows against
+    the C oracle, and no device check fires."""
+    import torch
+    from rowcheck import check_round_rows
+
+    from aiocluster_amd import driver
+    from aiocluster_amd.peers import PeerSelector
+    from aiocluster_amd.workload import TICKS_PER_ROUND, phase_tick as ptick
+
+    n, K = 16384, 16
+    cfg = dict(DEFAULT_CFG)
+    spec = WorkloadSpec(n=n, k=K, fanout=3, seed=4, init="warm", write_frac=0.05, down_frac=0.05, down_rounds=3)
+    sim = GossipSim(synthetic_node_ids(n), key_names(K), cfg, init="warm", tombstones=False, fd_ring=False,
+                    hist_cap=16, initial_ops=driver.boot_ops(n, K), hb8=True, mv8=True)
+    plans = driver.prepare(spec, 101, torch, sim.device)
+    sel = PeerSelector(sim, fanout=3, seeds=list(range(0, n, n // 8)), seed=4)
+    escaped_seen = 0
+    for r in range(101):
+        rd = plans[r]
+        if r in (6, 100):
+            driver.begin([sim], rd)
+            sel.select(rd["up"], rd["r"])
+            ph, offs, left = sel.schedule(rd["up"], rd["r"])
+            assert left == 0
+            rd["phases"] = [(a, b, m, ptick(rd["r"], p)) for p, (a, b, m) in enumerate(ph)]
+            rd["t_live"] = rd["t"] + 1 + len(ph)
+            assert rd["t_live"] < rd["t"] + TICKS_PER_ROUND
+            if r == 6:
+                slot = sim.region("ESC_SLOT", torch.int32, (sim.np_,))
+                escaped_seen = int((slot != -1).sum().item())
+            diff, info = check_round_rows(sim, cfg, rd, sample=16, seed=r)
+            assert diff is None, f"round {r}: {diff}"
+            assert info["phases"] >= 8 and info["hb_reports"] > 0, info
+        else:
+            driver.run_round([sim], rd, sel=sel)
+    sim.check_heartbeat_lag()
+    c = sim.check()
+    assert escaped_seen > 0 and c["hb_escapes"] > 0, (escaped_seen, c["hb_escapes"])
+    assert c["err_hb_lag"] == 0
+    sim.close()
