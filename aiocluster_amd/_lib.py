@@ -44,6 +44,10 @@ def slice_columns(n: int, shards: int, shard: int) -> tuple[int, int]:
     return lo, min(blk, n - lo)
 
 
+GS_CHAIN_DEVICE = 0xFFFFFFFF  # gs_phase_chain: the count stays on the device
+GS_CHAIN_CAP = 1024  # ... for at most this many overflowing slots
+
+
 def overflow_list_len(n: int) -> int:
     """u32 words of gs_phase_overflow's list for a phase of ``n`` exchanges (GS_OVERFLOW_LIST_LEN)."""
     return 2 * n + (2 * n + 1023) // 1024 + 1

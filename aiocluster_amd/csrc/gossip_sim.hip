@@ -2242,13 +2242,17 @@ __global__ __launch_bounds__(OVB) void k_ov_write(const uint64_t *tot_all, uint3
     }
 }
 
-// the pending counts of all G slices (entry count of each gathered chainc) summed into *out
+// the pending counts of all G slices (entry count of each gathered chainc) summed into *out.  cnt_dev: the count
+// is read on the device (GS_CHAIN_DEVICE: gathered rows of GS_CHAIN_CAP + 1 entries); a count above the cap gives
+// ~0 (the device step did not run: the host takes over)
 __global__ __launch_bounds__(WAVE) void k_sum_pending(const uint64_t *chain_all, uint32_t G, uint32_t count,
-                                                      uint64_t *out) {
+                                                      const uint32_t *cnt_dev, uint64_t *out) {
+    const uint32_t c = cnt_dev ? *cnt_dev : count;
+    const size_t stride = cnt_dev ? GS_CHAIN_CAP + 1u : (size_t)count + 1u;
     unsigned long long s = 0;
-    for (uint32_t g = threadIdx.x; g < G; g += WAVE) s += chain_all[(size_t)g * (count + 1u) + count];
+    for (uint32_t g = threadIdx.x; g < G; g += WAVE) s += chain_all[(size_t)g * stride + c];
     s = wave_sum(s);
-    if (threadIdx.x == 0) *out = s;
+    if (threadIdx.x == 0) *out = cnt_dev && c > GS_CHAIN_CAP ? ~0ull : s;
 }
 
 // chainc[count] = this slice's listed slots still pending (the count itself read from the list's tail when
@@ -2295,10 +2299,16 @@ template <int KW>
 __global__ __launch_bounds__(WAVE) void k_chain_step(Dev d, const int32_t *ini, const int32_t *res, uint32_t t,
                                                      const uint32_t *list, uint32_t count, const uint64_t *chain_all,
                                                      uint64_t *chain, uint64_t *chainc, const uint64_t *tot_all,
-                                                     uint32_t n) {
+                                                     uint32_t n, const uint32_t *cnt_dev) {
     __shared__ __attribute__((aligned(16))) uint16_t s_wbuf[WIN];
     const int lane = lane_id();
-    const size_t stride = (size_t)count + 1u;  // chain_all[g][count + 1]: entry count = g's pending slots
+    // chain_all[g][count + 1]: entry count = g's pending slots; GS_CHAIN_DEVICE (cnt_dev): the count from the
+    // device, rows of GS_CHAIN_CAP + 1 entries, nothing done above the cap (every slice sees the same count)
+    if (cnt_dev) {
+        count = *cnt_dev;
+        if (count > GS_CHAIN_CAP) return;
+    }
+    const size_t stride = cnt_dev ? GS_CHAIN_CAP + 1u : (size_t)count + 1u;
     for (uint32_t i = blockIdx.x; i < count; i += gridDim.x) {
         const uint32_t slot = list[i];
         if (chain[slot] != CHAIN_PENDING) continue;
@@ -4743,24 +4753,27 @@ int gs_phase_overflow(gs_handle *h, uint32_t n, const uint64_t *slice_bytes_all,
 int gs_phase_chain(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t n, uint32_t tick, uint32_t step,
                    const uint32_t *list, uint32_t count, const uint64_t *chain_all, uint64_t *chain, uint64_t *chainc,
                    const uint64_t *slice_bytes_all) {
+    const bool dev = count == GS_CHAIN_DEVICE;  // the count stays on the device (gs_phase_overflow's list tail)
     if (h && (!n || !count)) return GS_OK;
     int rc = check_phase(h, ini, res, n, tick, true);
     if (rc) return rc;
     if (!h->sliced || !h->d.cand) return fail(h, GS_E_UNSUPPORTED, "gs_phase_chain needs a sliced canonical handle");
-    if (!list || !chain_all || !chain || !chainc || !slice_bytes_all || step < 1 || step >= h->G || count > 2 * n)
+    if (!list || !chain_all || !chain || !chainc || !slice_bytes_all || step < 1 || step >= h->G ||
+        (!dev && count > 2 * n))
         return GS_E_INVALID;
     if (h->shard == 0) return GS_OK;  // slice 0 always finishes at step 0 (its pending entry stays 0)
     hipEvent_t e0 = nullptr;
     if ((rc = time_begin(h, e0))) return rc;
-    const uint32_t grid = std::min<uint32_t>(count, 2048u);
+    const uint32_t *cnt_dev = dev ? list + 2u * n + (2u * n + OVB - 1u) / OVB : nullptr;
+    const uint32_t grid = std::min<uint32_t>(dev ? GS_CHAIN_CAP : count, 2048u), c = dev ? 0u : count;
     if (h->KP <= 16)
-        k_chain_step<4><<<grid, WAVE, 0, h->stream>>>(h->d, ini, res, tick, list, count, chain_all, chain, chainc,
-                                                       slice_bytes_all, n);
+        k_chain_step<4><<<grid, WAVE, 0, h->stream>>>(h->d, ini, res, tick, list, c, chain_all, chain, chainc,
+                                                       slice_bytes_all, n, cnt_dev);
     else
-        k_chain_step<KWB><<<grid, WAVE, 0, h->stream>>>(h->d, ini, res, tick, list, count, chain_all, chain, chainc,
-                                                         slice_bytes_all, n);
+        k_chain_step<KWB><<<grid, WAVE, 0, h->stream>>>(h->d, ini, res, tick, list, c, chain_all, chain, chainc,
+                                                         slice_bytes_all, n, cnt_dev);
     HIPCHK(h, hipGetLastError());
-    k_pending<<<1, OVB, 0, h->stream>>>(list, nullptr, count, chain, chainc);  // chainc[count]
+    k_pending<<<1, OVB, 0, h->stream>>>(list, cnt_dev, c, chain, chainc);  // chainc[count]
     HIPCHK(h, hipGetLastError());
     return time_end(h, GS_KT_PACK, e0);
 }
@@ -4832,25 +4845,42 @@ int sliced_phase(gs_handle *const *hs, uint32_t nh, const int32_t *ini, const in
         return rc;
     for (uint32_t i = 0; i < nh; i++)
         if ((rc = gs_phase_pack(hs[i], ini, res, n, tick, 0, hs[i]->sc.tot_all, nullptr, hs[i]->sc.chain))) return rc;
-    uint32_t count = 0;
-    for (uint32_t i = nh; i-- > 0;)  // the same gathered totals give every slice the same list: read it once
+    for (uint32_t i = 0; i < nh; i++)  // the overflowing slots, listed on the device (the same list on every slice)
         if ((rc = gs_phase_overflow(hs[i], n, hs[i]->sc.tot_all, hs[i]->sc.chain, hs[i]->sc.list, hs[i]->sc.chainc,
-                                    i == 0 ? &count : nullptr)))
+                                    nullptr)))
             return rc;
-    if (!count) return GS_OK;
     const uint32_t G = hs[0]->G;
-    for (uint32_t step = 1; step < G; step++) {
-        // every slice's chain states and pending count (entry count); the same data on every slice, so each
-        // reads the same sum and all stop together
-        if ((rc = gather_u64(hs, nh, [](gs_handle *h) { return h->sc.chainc; },
-                             [](gs_handle *h) { return h->sc.chain_all; }, (size_t)count + 1)))
-            return rc;
-        gs_handle *h0 = hs[0];
-        k_sum_pending<<<1, WAVE, 0, h0->stream>>>(h0->sc.chain_all, G, count, h0->sc.pend);
+    if (G < 2) return GS_OK;  // one slice: step 0 finished every slot
+    gs_handle *h0 = hs[0];
+    const uint32_t *cnt0 = h0->sc.list + 2u * n + (2u * n + OVB - 1u) / OVB;  // gs_phase_overflow's count entry
+    auto gather_chain = [&](size_t entries) {
+        return gather_u64(hs, nh, [](gs_handle *h) { return h->sc.chainc; }, [](gs_handle *h) { return h->sc.chain_all; },
+                          entries);
+    };
+    auto pending = [&](uint32_t count, const uint32_t *cnt_dev, uint64_t &pend) {
+        k_sum_pending<<<1, WAVE, 0, h0->stream>>>(h0->sc.chain_all, G, count, cnt_dev, h0->sc.pend);
         HIPCHK(h0, hipGetLastError());
-        uint64_t pend = 0;
         HIPCHK(h0, hipMemcpyAsync(&pend, h0->sc.pend, 8, hipMemcpyDeviceToHost, h0->stream));
         HIPCHK(h0, hipStreamSynchronize(h0->stream));
+        return GS_OK;
+    };
+    // step 1 before any host read, on the device count (a chain usually resolves in it: one read ends the phase)
+    uint64_t pend = 0;
+    if ((rc = gather_chain(GS_CHAIN_CAP + 1u))) return rc;
+    for (uint32_t i = 0; i < nh; i++)
+        if ((rc = gs_phase_chain(hs[i], ini, res, n, tick, 1, hs[i]->sc.list, GS_CHAIN_DEVICE, hs[i]->sc.chain_all,
+                                 hs[i]->sc.chain, hs[i]->sc.chainc, hs[i]->sc.tot_all)))
+            return rc;
+    if ((rc = gather_chain(GS_CHAIN_CAP + 1u)) || (rc = pending(0u, cnt0, pend))) return rc;
+    if (!pend) return GS_OK;
+    // still pending (or more slots than the device step takes): the count to the host, the remaining steps
+    uint32_t count = 0;
+    HIPCHK(h0, hipMemcpyAsync(&count, cnt0, 4, hipMemcpyDeviceToHost, h0->stream));
+    HIPCHK(h0, hipStreamSynchronize(h0->stream));
+    for (uint32_t step = count > GS_CHAIN_CAP ? 1u : 2u; step < G; step++) {
+        // every slice's chain states and pending count (entry count); the same data on every slice, so each
+        // reads the same sum and all stop together
+        if ((rc = gather_chain((size_t)count + 1)) || (rc = pending(count, nullptr, pend))) return rc;
         if (!pend) break;
         for (uint32_t i = 0; i < nh; i++)
             if ((rc = gs_phase_chain(hs[i], ini, res, n, tick, step, hs[i]->sc.list, count, hs[i]->sc.chain_all,

@@ -33,7 +33,7 @@ from __future__ import annotations
 
 import numpy as np
 
-from ._lib import COUNTER_FIELDS, GsError, overflow_list_len
+from ._lib import COUNTER_FIELDS, GS_CHAIN_CAP, GS_CHAIN_DEVICE, GsError, overflow_list_len
 
 CHAIN_PENDING = -1  # u64 ~0 viewed as int64 (gossip_sim.hip CHAIN_PENDING)
 TOT_BYTES_MASK = (1 << 40) - 1  # a slice total's DeltaPb bytes (GS_TOT_BYTES); the smallest NodeDelta above
@@ -147,16 +147,31 @@ def run_sliced_phase(slices, comm, mtu: int, t: int, ini, res) -> int:
         return comm.world
     dev = tots[0].device
     lists = [torch.empty(overflow_list_len(n), dtype=torch.int32, device=dev) for _ in slices]
-    chaincs = [torch.empty(2 * n + 1, dtype=torch.int64, device=dev) for _ in slices]
-    # the same gathered totals give every slice the same list: one host read per process
+    # [2n + 1] (the listed slots' states, then the pending entry), at least GS_CHAIN_CAP + 1: the device step's rows
+    chaincs = [torch.empty(max(2 * n, GS_CHAIN_CAP) + 1, dtype=torch.int64, device=dev) for _ in slices]
+    # the overflowing slots, listed on the device (the same list on every slice); no count read
     for i in range(len(slices) - 1, -1, -1):
-        count = slices[i].phase_overflow(tot_all, chains[i], lists[i], chaincs[i], read=i == 0)
-    if count == 0:
+        slices[i].phase_overflow(tot_all, chains[i], lists[i], chaincs[i], read=False)
+    if comm.world < 2:
         return 1
-    steps = 1
-    for step in range(1, comm.world):
+    # step 1 on the device count (GS_CHAIN_DEVICE): a chain usually resolves in it, so one read -- the gathered
+    # pending entries -- ends the phase; more slots than GS_CHAIN_CAP, or a chain still pending, go on from the host
+    cap = GS_CHAIN_CAP
+    chain_all = comm.gather([cc[: cap + 1] for cc in chaincs])
+    for s, ch, lb, cc in zip(slices, chains, lists, chaincs):
+        s.phase_chain(t, ini, res, 1, lb, GS_CHAIN_DEVICE, chain_all, ch, cc, tot_all)
+    chain_all = comm.gather([cc[: cap + 1] for cc in chaincs])
+    ci = overflow_list_len(n) - 1  # gs_phase_overflow's count entry
+    cnt = lists[0][ci:ci + 1].to(torch.int64)
+    pend = torch.where(cnt > cap, torch.full_like(cnt, -1),
+                       chain_all.to(cnt.device).index_select(1, cnt.clamp(max=cap)).sum().reshape(1))
+    p_, count = (int(x) for x in torch.cat([pend, cnt]).tolist())  # the phase's one host read
+    if p_ == 0:
+        return 2 if count else 1
+    steps = 1 if count > cap else 2
+    for step in range(steps, comm.world):
         # every slice's chain states + pending count (entry count): the same on every rank, so all stop
-        # together once no slot is pending (a chain usually resolves in one step, gs_phase_chain)
+        # together once no slot is pending
         chain_all = comm.gather([cc[: count + 1] for cc in chaincs])
         if int(chain_all[:, count].sum().item()) == 0:
             break

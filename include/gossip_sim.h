@@ -335,6 +335,13 @@ int gs_phase_overflow(gs_handle *h, uint32_t n, const uint64_t *slice_bytes_all,
 int gs_phase_chain(gs_handle *h, const int32_t *initiators, const int32_t *responders, uint32_t n, uint32_t tick,
                    uint32_t step, const uint32_t *list, uint32_t count, const uint64_t *chain_all, uint64_t *chain,
                    uint64_t *chainc, const uint64_t *slice_bytes_all);
+/* count = GS_CHAIN_DEVICE: the count is not read back -- the kernels take it from `list` (gs_phase_overflow's count
+ * entry), every slice gathered GS_CHAIN_CAP + 1 entries of its chainc into chain_all[G][GS_CHAIN_CAP + 1], and a
+ * phase whose count exceeds GS_CHAIN_CAP is left to the host path (the step does nothing on any slice).  Lets a
+ * driver run step 1 before any host read: a chain usually resolves in that step, so one read of the gathered
+ * pending entries (k_sum_pending in the library driver) ends the phase. */
+#define GS_CHAIN_DEVICE 0xFFFFFFFFu
+#define GS_CHAIN_CAP 1024u
 
 /* ---- Multi-GPU: one handle per device, each holding one owner-column
  * slice; the library drives the sliced phase itself (count, all-gather of the slice totals, packing,

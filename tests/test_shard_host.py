@@ -13,6 +13,7 @@ import numpy as np
 import pytest
 import torch
 
+from aiocluster_amd._lib import GS_CHAIN_CAP, GS_CHAIN_DEVICE
 from aiocluster_amd.shard import CHAIN_PENDING, TOT_BYTES_MASK, LocalComm, run_sliced_phase
 
 MTU = 100
@@ -62,12 +63,17 @@ class ToySlice:
         list_buf[: len(idx)] = idx.to(list_buf.dtype)
         chainc[: len(idx)] = chain.reshape(-1)[idx]
         chainc[len(idx)] = int((chain.reshape(-1)[idx] == CHAIN_PENDING).sum())  # pending entry
+        list_buf[-1] = len(idx)  # the count entry (GS_OVERFLOW_LIST_LEN's last word)
         return len(idx)
 
     def phase_chain(self, t, ini, res, step, list_buf, count, chain_all, chain, chainc, tot_all):
         """k_chain_step: resume from the nearest finished predecessor f, skipping the pending slices between
         that cannot add a candidate (delta complete, or their smallest candidate above the budget left)."""
         flat = chain.view(-1)
+        if count == GS_CHAIN_DEVICE:  # the count from the list (gs_phase_overflow's entry); nothing above the cap
+            count = int(list_buf[-1])
+            if count > GS_CHAIN_CAP:
+                return
         for i in range(count):
             slot = int(list_buf[i])
             e, d = slot // 2, slot % 2

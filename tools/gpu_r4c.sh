@@ -18,6 +18,12 @@ if [ -n "$SLICES" ]; then
     tail -1 $O/bench_s$g.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; print('slices $g value', round(d['value']), 'ms/step', round(d['ms_per_step'],2), {k:(round(v['avg_launch_ms'],3), v['launches']) for k,v in r['kernels'].items()})"
   done
 fi
+if [ -n "$NATIVE_SLICES" ]; then  # the library driver (gs_run_phase_group): no Python per slice and launch
+  for g in 2 8; do
+    timeout -k 10 300 python -u bench.py --no-cpu-baseline --peer-select-steps 0 --slices $g --native-comm > $O/bench_n$g.log 2>&1 || { tail -20 $O/bench_n$g.log; exit 1; }
+    tail -1 $O/bench_n$g.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; print('native slices $g value', round(d['value']), 'ms/step', round(d['ms_per_step'],2), {k:(round(v['avg_launch_ms'],3), v['launches']) for k,v in r['kernels'].items()})"
+  done
+fi
 if [ -n "$PS" ]; then
   timeout -k 10 400 python -u bench.py --peer-select --settle 190 --steps 10 --warmup 2 --no-cpu-baseline > $O/bench_ps.log 2>&1 || { tail -20 $O/bench_ps.log; exit 1; }
   tail -1 $O/bench_ps.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('peer-select value', round(d['value']), 'ms/step', round(d['ms_per_step'],2), 'counters', {k: d['counters'][k] for k in ('lag_sweeps','hb_escapes','hb_releases')}, 'exactness', d['exactness'])"
