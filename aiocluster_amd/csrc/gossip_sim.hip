@@ -90,7 +90,8 @@ struct Dev {
     // (NP = ncol rounded to 64 is the row stride); shards = 1: the whole matrix
     uint32_t col_lo, ncol, shards, shard;
     uint32_t max_iv, tomb_grace, dead_grace, sched_delay, lb_min, sum_bits;
-    uint32_t ablate;  // profiling only (env GS_ABLATE): 1 = skip packing, 2 = skip pass-1 stores; results invalid
+    uint32_t ablate;  // profiling only (env GS_ABLATE): 1 = skip packing, 2 = skip pass-1 stores (results invalid);
+                      // A/B, results valid: 8 = k_pass1v without its slow-group slots, 16 = k_pass1v records decoded at emit
     double phi_thr, prior5;
     double prior5t;  // prior5 in ticks (x 64): the liveness sweep's division-free phi test
     float phi_thr_f, prior5t_f;  // the same in binary32: the sweep's first, full-rate test (2^-20 margin)
@@ -986,6 +987,11 @@ constexpr int LITE_B = 4;
 // The applies of a whole delta of prefix candidates (pack_lite): each receiver view becomes S_j(ms), one
 // max_version store per recorded owner (apply_cand's fast path); lanes take records l, l + 64, ...
 __device__ __forceinline__ void lite_apply(const Dev &d, uint32_t rcv, size_t slot, WStats &st) {
+    if (d.spec) {  // k_pass1v merged every recorded prefix candidate (Dev::spec): only the counts
+        const uint32_t nt = d.cand_n[slot * 2] + d.cand_n[slot * 2 + 1];
+        if (lane_id() == 0) { st.nd += nt; st.cand += nt; }
+        return;
+    }
     const int lane = lane_id();
     const uint32_t n0 = d.cand_n[slot * 2], n1 = d.cand_n[slot * 2 + 1], nt = n0 + n1;
     const uint2 *L0 = d.cand + slot * 2 * GS_CAND_CAP, *L1 = L0 + GS_CAND_CAP;
@@ -1688,12 +1694,15 @@ __device__ __forceinline__ uint32_t wave_scan_dpp(uint32_t x) {
 }
 
 // One direction's stale owners of one step (nm[q]: bit 7 of byte i = column c + 4 q + i) go out as records
-// {column, sender max_version word | receiver max_version word << 16} appended in column order (lane order,
+// {column, sender max_version byte | receiver max_version byte << 16} appended in column order (lane order,
 // then column) to the wave's list L (the first GS_CAND_CAP; cnt counts all), and -- from the step whose owners
 // overflow the list on -- as natural-order bitmap bits, 16 per lane (the packers walk the bitmap past the
-// last record).  Every lane of the wave calls this (act = false: no columns).
-__device__ __forceinline__ void emit_v(const Dev &d, uint16_t *gw16, uint2 *L, uint32_t &cnt, uint32_t c, bool act,
-                                       const uint32_t (&nm)[4], const uint4 &sS, const uint4 &sR, uint32_t &alg) {
+// last record).  Every lane of the wave calls this (act = false: no columns).  The bytes are decoded into
+// the record's word form after the loop (p1v_decode_records): a load of the owner's own max_version here
+// would make the wave wait for the loads in flight for the next step.
+__device__ __forceinline__ void emit_v(uint16_t *gw16, uint2 *L, uint32_t &cnt, uint32_t c, bool act,
+                                       const uint32_t (&nm)[4], const uint4 &sS, const uint4 &sR, uint32_t &alg,
+                                       uint32_t (&rec)[4], bool dec = false, const uint32_t *self_mv = nullptr) {
     const uint32_t my = act ? (uint32_t)(__popc(nm[0]) + __popc(nm[1]) + __popc(nm[2]) + __popc(nm[3])) : 0u;
     const uint32_t incl = wave_scan_dpp(my);
     const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
@@ -1705,17 +1714,25 @@ __device__ __forceinline__ void emit_v(const Dev &d, uint16_t *gw16, uint2 *L, u
     if (my) {
         uint32_t off = cnt + incl - my;
         const uint32_t s4[4] = {sS.x, sS.y, sS.z, sS.w}, r4[4] = {sR.x, sR.y, sR.z, sR.w};
+        // straight-line (at most 16 records): a loop with stores would make the compiler wait for every load
+        // in flight before entering it (the loaded views it reads were loaded outside it)
 #pragma unroll
         for (int q = 0; q < 4; q++) {
-            for (uint32_t m = nm[q]; m; m &= m - 1u) {
-                if (off < GS_CAND_CAP) {
-                    const uint32_t i = (uint32_t)__builtin_ctz(m) >> 3, j = c + 4u * q + i;
-                    const uint32_t M = d.self_mv[j];
-                    const uint32_t ms = mv_dec8((s4[q] >> (8 * i)) & 0xFFu, M), mr = mv_dec8((r4[q] >> (8 * i)) & 0xFFu, M);
-                    L[off] = make_uint2(j, ms | (mr << 16));
-                    alg += 8;
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                if ((nm[q] >> (8 * i + 7)) & 1u) {
+                    if (off < GS_CAND_CAP) {
+                        uint32_t w = ((s4[q] >> (8 * i)) & 0xFFu) | (((r4[q] >> (8 * i)) & 0xFFu) << 16);
+                        if (dec) {  // (A/B: decoded here)
+                            const uint32_t M = self_mv[c + 4u * q + i];
+                            w = mv_dec8(w & 0xFFu, M) | (mv_dec8(w >> 16, M) << 16);
+                        }
+                        L[off] = make_uint2(c + 4u * q + i, w);
+                        rec[q] |= 0x80u << (8 * i);
+                        alg += 8;
+                    }
+                    off++;
                 }
-                off++;
             }
         }
     }
@@ -1728,6 +1745,7 @@ __device__ __forceinline__ void emit_v(const Dev &d, uint16_t *gw16, uint2 *L, u
 // partial group.  Outputs in k_pass1v's word forms.
 struct P1vSlow {
     uint32_t nwA[4], nwB[4], nba[4], nab[4];
+    uint32_t gba[4], gab[4];  // bit 7 of byte i: the sender's max_version is the larger (b -> a: mB > mA; a -> b)
     uint32_t pA, pB, upA, upB, hbw, reports;
 };
 __device__ __noinline__ P1vSlow pass1v_slow(const uint32_t *self_pk, const uint8_t *fd_state, const uint32_t *tod,
@@ -1748,7 +1766,7 @@ __device__ __noinline__ P1vSlow pass1v_slow(const uint32_t *self_pk, const uint8
             const uint4 e = *reinterpret_cast<const uint4 *>(esc_slot + c0);
             es4[0] = e.x; es4[1] = e.y; es4[2] = e.z; es4[3] = e.w;
         }
-        uint32_t oA = 0u, oB = 0u, rA = 0u, rB = 0u, bA = 0u, bB = 0u;
+        uint32_t oA = 0u, oB = 0u, rA = 0u, rB = 0u, bA = 0u, bB = 0u, gA = 0u, gB = 0u;
 #pragma unroll
         for (int i = 0; i < 4; i++) {
             const uint32_t j = c0 + i, jg = col_lo + j;
@@ -1793,7 +1811,11 @@ __device__ __noinline__ P1vSlow pass1v_slow(const uint32_t *self_pk, const uint8
             // stale owners (state.py:347-357) against each side's digest
             bA |= (uint32_t)(valid && !sb && mB > (sa ? 0u : mA)) << (8 * i + 7);  // b -> a
             bB |= (uint32_t)(valid && !sa && mA > (sb ? 0u : mB)) << (8 * i + 7);  // a -> b
+            gA |= (uint32_t)(mB > mA) << (8 * i + 7);
+            gB |= (uint32_t)(mA > mB) << (8 * i + 7);
         }
+        o.gba[q] = gA;
+        o.gab[q] = gB;
         o.nwA[q] = oA;
         o.nwB[q] = oB;
         o.nba[q] = bA;
@@ -1809,12 +1831,44 @@ struct V16 {
     uint32_t fl;  // GS_R_P1FLAGS word of the group: small bits | hot bits << 16
 };
 
+// Slow groups taken ahead of the loop (one per lane): the loop itself then holds no call.  A call in the loop
+// makes the wave spill and reload around it, and the waits for those reloads where the two paths join drain
+// the loads in flight for the next step on every step, slow or not.
+constexpr uint32_t P1V_K = WAVE;
+constexpr uint32_t P1V_SLOT = 17;  // words per slow group: planes (pA | pB << 16), nba[4], nab[4], gba[4], gab[4]
+constexpr uint32_t P1V_SCAN = 128; // flag words per lane the scan takes (4 mask words): up to 8192 groups a wave
+
+// The records' max_version bytes -> the word form every consumer reads (emit_v stores the bytes)
+__device__ __forceinline__ void p1v_decode_records(const Dev &d, uint2 *L, uint32_t cnt, int lane) {
+    const uint32_t m = min(cnt, GS_CAND_CAP);
+    for (uint32_t i0 = 0; i0 < m; i0 += 4u * WAVE) {
+        uint2 r[4];
+        uint32_t M[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint32_t i = i0 + (uint32_t)(u * WAVE + lane);
+            r[u] = i < m ? L[i] : make_uint2(0u, 0u);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) M[u] = i0 + (uint32_t)(u * WAVE + lane) < m ? d.self_mv[r[u].x] : 0u;
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint32_t i = i0 + (uint32_t)(u * WAVE + lane);
+            if (i < m) L[i].y = mv_dec8(r[u].y & 0xFFu, M[u]) | (mv_dec8((r[u].y >> 16) & 0xFFu, M[u]) << 16);
+        }
+    }
+}
+
 template <int AHEAD>
 __global__ __launch_bounds__(XB, P1V_WAVES) void k_pass1v(Dev d, const int32_t *ini, const int32_t *res, uint32_t n,
                                                           uint32_t t, uint32_t seq) {
+    static_assert(AHEAD == 1 || AHEAD == 2, "k_pass1v keeps one or two groups in flight ahead");
+    __shared__ uint32_t s_col[XB / WAVE][P1V_K];
+    __shared__ uint32_t s_out[XB / WAVE][P1V_K * P1V_SLOT];
     const uint32_t e = blockIdx.x;
     if (e >= n) return;
-    const int tid = threadIdx.x, lane = tid & (WAVE - 1), wid = tid >> 6;
+    // wid through readfirstlane: the half bounds, list and plane pointers derived from it stay scalar
+    const int tid = threadIdx.x, lane = tid & (WAVE - 1), wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int32_t ai = ini[e], bi = res[e];
     if (ai < 0 || bi < 0 || (uint32_t)ai >= d.N || (uint32_t)bi >= d.N || ai == bi) {
         if (tid == 0) shard_add(d, C_E_IDX, 1);
@@ -1856,6 +1910,8 @@ __global__ __launch_bounds__(XB, P1V_WAVES) void k_pass1v(Dev d, const int32_t *
         d.self_pk[jb] = self_pack(R1, d.self_mv[jb]);
     }
     const uint8_t *h8 = reinterpret_cast<const uint8_t *>(d.hb), *m8 = reinterpret_cast<const uint8_t *>(d.mv);
+    uint8_t *hw8 = reinterpret_cast<uint8_t *>(d.hb), *mw8 = reinterpret_cast<uint8_t *>(d.mv);
+    const bool hbst = !(d.ablate & 2u), spec = d.spec != 0u, decv = (d.ablate & 16u) != 0u;
     auto load = [&](uint32_t c, V16 &v) {
         v.hA = *reinterpret_cast<const uint4 *>(h8 + ra + c);
         v.hB = *reinterpret_cast<const uint4 *>(h8 + rb + c);
@@ -1863,83 +1919,235 @@ __global__ __launch_bounds__(XB, P1V_WAVES) void k_pass1v(Dev d, const int32_t *
         v.mB = *reinterpret_cast<const uint4 *>(m8 + rb + c);
         v.fl = d.p1flags[c >> 4];
     };
+    // the per-column path's predicate for the group at column c (c < hi)
+    auto slow_at = [&](uint32_t c, uint32_t fl) {
+        return rslow || (fl >> 16) || c + 16u > d.ncol || ja - c < 16u || jb - c < 16u;
+    };
+    auto slow_group = [&](uint32_t c, const V16 &v) {
+        const P1vSlow o = pass1v_slow(d.self_pk, d.fd_state, d.tod, d.sched_delay, d.col_lo, d.ncol, ra, rb, c, a, b,
+                                      t, schA, schB, v.hA, v.hB, v.mA, v.mB, d.esc_slot, d.esc16, d.EC, d.self_hb);
+        if (hbst) {
+            if (o.upA) *reinterpret_cast<uint4 *>(hw8 + ra + c) = make_uint4(o.nwA[0], o.nwA[1], o.nwA[2], o.nwA[3]);
+            if (o.upB) *reinterpret_cast<uint4 *>(hw8 + rb + c) = make_uint4(o.nwB[0], o.nwB[1], o.nwB[2], o.nwB[3]);
+        }
+        alg += 64u + (o.upA ? 16u : 0u) + (o.upB ? 16u : 0u);
+        hbw += o.hbw;
+        reports += o.reports;
+        return o;
+    };
+
+    // Slow-group scan (not for a whole-slow exchange): lane l reads the flag words of the wave's groups
+    // [l CH, (l + 1) CH) (column order = lane order, then group), the slow groups are ranked by a wave scan
+    // and, if at most P1V_K, run now, one per lane, their outputs kept in LDS in column order
+    const uint32_t G = hi > lo ? (hi - lo + 15u) / 16u : 0u;
+    const uint32_t CH = ((G + WAVE - 1u) / WAVE + 3u) & ~3u;
+    bool table = false;
+    if (!rslow) {
+        table = CH <= P1V_SCAN && !(d.ablate & 8u);
+        uint32_t msk[P1V_SCAN / 32] = {0u, 0u, 0u, 0u}, cnt = 0u;
+        const uint32_t g0 = (uint32_t)lane * CH;
+        if (table) {
+            // branch-free: the hot groups from the flag words, then the groups of columns a and b and the
+            // partial last group by index; bits past the lane's chunk or the half are cleared
+            const uint32_t gmax4 = (G - 1u) & ~3u;  // loads past the lane's groups stay inside the wave's words
+            const uint32_t nv = G > g0 ? min(CH, G - g0) : 0u;  // the lane's groups
+            const uint32_t sp[3] = {ja - lo, jb - lo, (d.ncol & 15u) ? (d.ncol & ~15u) - lo : NONE};
+#pragma unroll
+            for (int w = 0; w < (int)(P1V_SCAN / 32); w++) {
+                if (32u * w >= CH) break;  // wave-uniform
+                uint4 f[8];
+#pragma unroll
+                for (int j = 0; j < 8; j++)
+                    f[j] = *reinterpret_cast<const uint4 *>(d.p1flags + (lo >> 4) + min(g0 + 32u * w + 4u * j, gmax4));
+                uint32_t m = 0u;
+#pragma unroll
+                for (int j = 0; j < 8; j++) {
+                    m |= (uint32_t)(f[j].x > 0xFFFFu) << (4 * j);
+                    m |= (uint32_t)(f[j].y > 0xFFFFu) << (4 * j + 1);
+                    m |= (uint32_t)(f[j].z > 0xFFFFu) << (4 * j + 2);
+                    m |= (uint32_t)(f[j].w > 0xFFFFu) << (4 * j + 3);
+                }
+#pragma unroll
+                for (int u = 0; u < 3; u++) {  // column offsets from lo -> group index within this block
+                    const uint32_t k = (sp[u] >> 4) - g0 - 32u * w;
+                    if (sp[u] < hi - lo && k < 32u) m |= 1u << k;
+                }
+                const uint32_t r = nv > 32u * w ? nv - 32u * w : 0u;
+                m &= r >= 32u ? ~0u : (1u << r) - 1u;
+                msk[w] = m;
+                cnt += (uint32_t)__popc(m);
+            }
+        }
+        const uint32_t incl = wave_scan_dpp(cnt);
+        const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        table = table && tot <= P1V_K;
+        if (table) {
+            uint32_t off = incl - cnt;
+#pragma unroll
+            for (int w = 0; w < (int)(P1V_SCAN / 32); w++)
+                for (uint32_t m = msk[w]; m; m &= m - 1u) s_col[wid][off++] = lo + 16u * (g0 + 32u * w + (uint32_t)__builtin_ctz(m));
+        }
+        __syncthreads();
+        if (table && (uint32_t)lane < tot) {
+            const uint32_t c = s_col[wid][lane];
+            V16 v;
+            load(c, v);
+            const P1vSlow o = slow_group(c, v);
+            uint32_t *so = &s_out[wid][lane * P1V_SLOT];
+            so[0] = o.pA | (o.pB << 16);
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                so[1 + q] = o.nba[q];
+                so[5 + q] = o.nab[q];
+                so[9 + q] = o.gba[q];
+                so[13 + q] = o.gab[q];
+            }
+        }
+        __syncthreads();
+    }
+
+    // The stream: two buffers, the next group's loads issued before the current group is computed.  TABLE:
+    // slow groups read their outputs from the scan's slots (no call in the loop); else they run the per-column
+    // path here (a whole-slow exchange, or more slow groups than slots).
     constexpr uint32_t STEP = WAVE * 16u;
-    V16 buf[AHEAD + 1];
+    const uint32_t clast = (max(hi, 1u) - 1u) & ~15u;  // the wave's last group (a valid one for an empty half)
+    // (with AHEAD = 2 the prologue's second load may also fall past the end: clamped the same way)
+    auto stream = [&](auto tag) {
+        constexpr bool TABLE = decltype(tag)::value;
+        uint32_t sbase = 0u;  // slow groups of the wave before this step (TABLE)
+        auto step = [&](uint32_t s0, const V16 &v, V16 &nx) __attribute__((always_inline)) {
+            const uint32_t c = s0 + (uint32_t)lane * 16u;
+            const bool act = c < hi;
+            // unconditional (a lane past the end reloads the last group): a load under a branch would make
+            // the wait for the current group's loads count as if the next group's were not in flight
+            load(c + AHEAD * STEP < hi ? c + AHEAD * STEP : clast, nx);
+            const uint32_t x4[4] = {v.hA.x, v.hA.y, v.hA.z, v.hA.w}, y4[4] = {v.hB.x, v.hB.y, v.hB.z, v.hB.w};
+            const uint32_t ma4[4] = {v.mA.x, v.mA.y, v.mA.z, v.mA.w}, mb4[4] = {v.mB.x, v.mB.y, v.mB.z, v.mB.w};
+            uint32_t nba[4] = {0u, 0u, 0u, 0u}, nab[4] = {0u, 0u, 0u, 0u};
+            uint32_t gba[4], gab[4];    // the sender's view is the larger (Dev::spec; the fast path's stale masks)
+            uint32_t pA = 0u, pB = 0u;  // the lane's plane u16s
+            const bool slow = act && slow_at(c, v.fl);
+            if (act && !slow) {
+                uint32_t repA[4], repB[4], nw[4], upAll = 0u, upBll = 0u;
+                const uint32_t sm = v.fl & 0xFFFFu;
 #pragma unroll
-    for (int k = 0; k < AHEAD; k++)
-        if (lo + lane * 16u + k * STEP < hi) load(lo + lane * 16u + k * STEP, buf[k]);
-    for (uint32_t s0 = lo; s0 < hi; s0 += STEP) {  // wave-uniform trip count (the scans need every lane)
-        const uint32_t c = s0 + (uint32_t)lane * 16u;
-        const bool act = c < hi;
-        if (c + AHEAD * STEP < hi) load(c + AHEAD * STEP, buf[AHEAD]);
-        if (!AHEAD && act) load(c, buf[0]);
-        const V16 &v = buf[0];
-        const uint32_t x4[4] = {v.hA.x, v.hA.y, v.hA.z, v.hA.w}, y4[4] = {v.hB.x, v.hB.y, v.hB.z, v.hB.w};
-        const uint32_t ma4[4] = {v.mA.x, v.mA.y, v.mA.z, v.mA.w}, mb4[4] = {v.mB.x, v.mB.y, v.mB.z, v.mB.w};
-        uint32_t repA[4] = {0u, 0u, 0u, 0u}, repB[4] = {0u, 0u, 0u, 0u};
-        uint32_t nba[4] = {0u, 0u, 0u, 0u}, nab[4] = {0u, 0u, 0u, 0u};
-        uint32_t pA = 0u, pB = 0u;  // the lane's plane u16s
-        const bool slow = act && (rslow || (v.fl >> 16) || c + 16u > d.ncol || ja - c < 16u || jb - c < 16u);
-        if (act && !slow) {
-            uint32_t nw[4], upAll = 0u, upBll = 0u;
-            const uint32_t sm = v.fl & 0xFFFFu;
+                for (int q = 0; q < 4; q++) {
+                    const uint32_t x = x4[q], y = y4[q];
+                    const uint32_t dd = bsub(x, y);  // (hA - hB) mod 2^8, |hA - hB| < 2^7
+                    const uint32_t upA = dd & B7;    // hB > hA: a takes b's heartbeat
+                    const uint32_t upB = ((((dd & L7) + L7) | dd) & ~dd) & B7;  // hA > hB: b takes a's
+                    const uint32_t mA_ = (upA << 1) - (upA >> 7);
+                    nw[q] = (y & mA_) | (x & ~mA_);  // both rows end with the larger heartbeat
+                    // _report_heartbeat reports unless the old heartbeat was 0 (state.py:280-287)
+                    const uint32_t s7 = sm ? spread7((sm >> (4 * q)) & 0xFu) : 0u;
+                    const uint32_t zA = ~(((x & L7) + L7) | x) & B7, zB = ~(((y & L7) + L7) | y) & B7;
+                    repA[q] = upA & ~(zA & s7);
+                    repB[q] = upB & ~(zB & s7);
+                    upAll |= upA;
+                    upBll |= upB;
+                    hbw += (uint32_t)__popc(upA | upB);
+                    // stale owners (state.py:347-357): mB > mA -> b -> a, mA > mB -> a -> b; |mA - mB| < 2^6
+                    const uint32_t ev = (((mb4[q] & L7) | B7) - (ma4[q] & L7)) & L7;  // (mB - mA) mod 2^7
+                    const uint32_t e6 = (ev << 1) & B7;
+                    nba[q] = (ev + L7) & B7 & ~e6;
+                    nab[q] = e6;
+                }
+                if (hbst) {
+                    if (upAll) *reinterpret_cast<uint4 *>(hw8 + ra + c) = make_uint4(nw[0], nw[1], nw[2], nw[3]);
+                    if (upBll) *reinterpret_cast<uint4 *>(hw8 + rb + c) = make_uint4(nw[0], nw[1], nw[2], nw[3]);
+                }
+                alg += 64u + (upAll ? 16u : 0u) + (upBll ? 16u : 0u);
+                pA = pack16(repA);
+                pB = pack16(repB);
+                reports += (uint32_t)(__popc(pA) + __popc(pB));
+            }
+            if constexpr (TABLE) {
+                const uint64_t sm = __ballot(slow);
+                if (slow) {
+                    const uint32_t slot = sbase + __builtin_amdgcn_mbcnt_hi((uint32_t)(sm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)sm, 0u));
+                    const uint32_t *so = &s_out[wid][slot * P1V_SLOT];
+                    pA = so[0] & 0xFFFFu;
+                    pB = so[0] >> 16;
 #pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const uint32_t x = x4[q], y = y4[q];
-                const uint32_t dd = bsub(x, y);  // (hA - hB) mod 2^8, |hA - hB| < 2^7
-                const uint32_t upA = dd & B7;    // hB > hA: a takes b's heartbeat
-                const uint32_t upB = ((((dd & L7) + L7) | dd) & ~dd) & B7;  // hA > hB: b takes a's
-                const uint32_t mA_ = (upA << 1) - (upA >> 7);
-                nw[q] = (y & mA_) | (x & ~mA_);  // both rows end with the larger heartbeat
-                // _report_heartbeat reports unless the old heartbeat was 0 (state.py:280-287)
-                const uint32_t s7 = sm ? spread7((sm >> (4 * q)) & 0xFu) : 0u;
-                const uint32_t zA = ~(((x & L7) + L7) | x) & B7, zB = ~(((y & L7) + L7) | y) & B7;
-                repA[q] = upA & ~(zA & s7);
-                repB[q] = upB & ~(zB & s7);
-                upAll |= upA;
-                upBll |= upB;
-                hbw += (uint32_t)__popc(upA | upB);
-                // stale owners (state.py:347-357): mB > mA -> b -> a, mA > mB -> a -> b; |mA - mB| < 2^6
-                const uint32_t ev = (((mb4[q] & L7) | B7) - (ma4[q] & L7)) & L7;  // (mB - mA) mod 2^7
-                const uint32_t e6 = (ev << 1) & B7;
-                nba[q] = (ev + L7) & B7 & ~e6;
-                nab[q] = e6;
-            }
-            if (!(d.ablate & 2u)) {
-                if (upAll) *reinterpret_cast<uint4 *>(reinterpret_cast<uint8_t *>(d.hb) + ra + c) = make_uint4(nw[0], nw[1], nw[2], nw[3]);
-                if (upBll) *reinterpret_cast<uint4 *>(reinterpret_cast<uint8_t *>(d.hb) + rb + c) = make_uint4(nw[0], nw[1], nw[2], nw[3]);
-            }
-            alg += 64u + (upAll ? 16u : 0u) + (upBll ? 16u : 0u);
-            pA = pack16(repA);
-            pB = pack16(repB);
-            reports += (uint32_t)(__popc(pA) + __popc(pB));
-        } else if (slow) {
-            const P1vSlow o = pass1v_slow(d.self_pk, d.fd_state, d.tod, d.sched_delay, d.col_lo, d.ncol, ra, rb, c, a, b,
-                                          t, schA, schB, v.hA, v.hB, v.mA, v.mB, d.esc_slot, d.esc16, d.EC, d.self_hb);
-            if (!(d.ablate & 2u)) {
-                if (o.upA) *reinterpret_cast<uint4 *>(reinterpret_cast<uint8_t *>(d.hb) + ra + c) = make_uint4(o.nwA[0], o.nwA[1], o.nwA[2], o.nwA[3]);
-                if (o.upB) *reinterpret_cast<uint4 *>(reinterpret_cast<uint8_t *>(d.hb) + rb + c) = make_uint4(o.nwB[0], o.nwB[1], o.nwB[2], o.nwB[3]);
-            }
-            alg += 64u + (o.upA ? 16u : 0u) + (o.upB ? 16u : 0u);
-            hbw += o.hbw;
-            reports += o.reports;
-            pA = o.pA;
-            pB = o.pB;
+                    for (int q = 0; q < 4; q++) {
+                        nba[q] = so[1 + q];
+                        nab[q] = so[5 + q];
+                        gba[q] = so[9 + q];
+                        gab[q] = so[13 + q];
+                    }
+                } else {
 #pragma unroll
-            for (int q = 0; q < 4; q++) {
-                nba[q] = o.nba[q];
-                nab[q] = o.nab[q];
+                    for (int q = 0; q < 4; q++) {
+                        gba[q] = nba[q];
+                        gab[q] = nab[q];
+                    }
+                }
+                sbase += (uint32_t)__popcll(sm);
+            } else if (slow) {
+                const P1vSlow o = slow_group(c, v);
+                pA = o.pA;
+                pB = o.pB;
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    nba[q] = o.nba[q];
+                    nab[q] = o.nab[q];
+                    gba[q] = o.gba[q];
+                    gab[q] = o.gab[q];
+                }
+            } else {
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    gba[q] = nba[q];
+                    gab[q] = nab[q];
+                }
             }
+            if (act) {
+                planeA[c >> 4] = (uint16_t)pA;
+                planeB[c >> 4] = (uint16_t)pB;
+                alg += 4;
+            }
+            uint32_t rBA[4] = {0u, 0u, 0u, 0u}, rAB[4] = {0u, 0u, 0u, 0u};  // recorded stale owners
+            emit_v(gBA, LBA, nBAc, c, act, nba, v.mB, v.mA, alg, rBA, decv, d.self_mv);  // b -> a: sender b, receiver a
+            emit_v(gAB, LAB, nABc, c, act, nab, v.mA, v.mB, alg, rAB, decv, d.self_mv);
+            if (spec && act) {
+                // speculative merge (Dev::spec): each recorded stale owner whose two views are prefix views
+                // (GS_MV_INEXACT clear: bit 7 of both bytes) gets the sender's view now, in the 16 bytes this
+                // step loaded -- a delta that fits sends every such NodeDelta whole, which is exactly that
+                // (apply_cand's fast path); the packer restores the receiver byte of the others (pack_list)
+                uint32_t nA[4], nB[4], wA = 0u, wB = 0u;
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const uint32_t fm = ~(ma4[q] | mb4[q]) & B7;
+                    const uint32_t ba = rBA[q] & fm & gba[q], ab = rAB[q] & fm & gab[q];  // max(ms, mr)
+                    const uint32_t sA = (ba << 1) - (ba >> 7), sB = (ab << 1) - (ab >> 7);  // byte masks
+                    nA[q] = (mb4[q] & sA) | (ma4[q] & ~sA);
+                    nB[q] = (ma4[q] & sB) | (mb4[q] & ~sB);
+                    wA |= ba;
+                    wB |= ab;
+                }
+                if (wA) { *reinterpret_cast<uint4 *>(mw8 + ra + c) = make_uint4(nA[0], nA[1], nA[2], nA[3]); alg += 16; }
+                if (wB) { *reinterpret_cast<uint4 *>(mw8 + rb + c) = make_uint4(nB[0], nB[1], nB[2], nB[3]); alg += 16; }
+            }
+        };
+        // AHEAD + 1 buffers in rotation (the loop unrolled by that many steps: no register moves)
+        V16 bf[AHEAD + 1];
+#pragma unroll
+        for (int k = 0; k < AHEAD; k++) load(min(lo + (uint32_t)lane * 16u + k * STEP, clast), bf[k]);
+        for (uint32_t s0 = lo; s0 < hi; s0 += (AHEAD + 1) * STEP) {  // wave-uniform trip count (the scans need every lane)
+#pragma unroll
+            for (int k = 0; k <= AHEAD; k++)
+                if (k == 0 || s0 + k * STEP < hi) step(s0 + k * STEP, bf[k], bf[(k + AHEAD) % (AHEAD + 1)]);
         }
-        if (act) {
-            planeA[c >> 4] = (uint16_t)pA;
-            planeB[c >> 4] = (uint16_t)pB;
-            alg += 4;
-        }
-        emit_v(d, gBA, LBA, nBAc, c, act, nba, v.mB, v.mA, alg);  // b -> a: sender b, receiver a
-        emit_v(d, gAB, LAB, nABc, c, act, nab, v.mA, v.mB, alg);
-#pragma unroll
-        for (int k = 0; k < AHEAD; k++) buf[k] = buf[k + 1];
+    };
+    if (table)
+        stream(std::true_type{});
+    else
+        stream(std::false_type{});
+    // this wave's records: bytes -> words (its own stores: visible to the wave after the fence)
+    if (!decv) {
+        __threadfence_block();
+        p1v_decode_records(d, LBA, nBAc, lane);
+        p1v_decode_records(d, LAB, nABc, lane);
     }
     if (lane == 0) {
         d.cand_n[(size_t)e * 4 + 0 * 2 + wid] = nBAc;
@@ -2418,7 +2626,73 @@ __device__ __forceinline__ SlotSum settle_sum(const Dev &d, uint32_t snd, uint32
 //          speculative slot whose whole delta fits over every slice and is clean here is complete.
 // Sequential semantics over the slices in column (= canonical dict) order, so the result is the
 // single-slice result bit for bit.
-template <int KW, int MODE>
+// k_lite's work for one (exchange, direction) slot (also run at the head of k_settle<LITE = true>, the sliced
+// phases' fused kernels); returns the slot's flag (slot_stat[slot].w, written here too)
+template <int MODE>
+__device__ __forceinline__ uint32_t lite_slot(const Dev &d, int32_t ai, int32_t bi, uint32_t n, uint32_t t,
+                                              const SliceIO &io, size_t slot, int wid, int lane) {
+    const uint32_t rcv = wid == 0 ? (uint32_t)ai : (uint32_t)bi;
+    const bool sched = t >= d.row[rcv * 4 + 2];  // the receiver's digest may leave owners out: exact packer
+    WStats st{0, 0, 0, 0, 0};
+    uint32_t T = 0, flag = LITE_FULL;
+    if (MODE == 0) {
+        if (!sched && pack_lite<true>(d, rcv, slot, 0u, st, T)) {
+            flag = LITE_DONE;
+            if (lane == 0) shard_add(d, C_DBYTES, T);
+        }
+    } else if (MODE == 1) {
+        uint32_t m1 = NONE;
+        if (!sched && pack_lite<false>(d, rcv, slot, 0u, st, T, &m1)) {
+            flag = 0u;
+            const uint32_t kv = (uint32_t)wave_sum(st.kvs);  // for step 0 (MODE 2): it applies without re-sizing
+            if (lane == 0) {
+                io.tot[slot] = tot_word(T, m1);
+                d.slot_stat[slot].y = kv;
+            }
+            st.kvs = 0u;  // counted when sent (MODE 2 or the exact packer)
+        }
+    } else {
+        unsigned long long P = 0;
+        for (uint32_t g = 0; g < d.shard; g++) P += GS_TOT_BYTES(io.tot_all[(size_t)g * n * 2 + slot]);
+        const unsigned long long own = GS_TOT_BYTES(io.tot_all[(size_t)d.shard * n * 2 + slot]);
+        // the count pass (MODE 1) sized this slot from the version log (slot_stat flag 0): apply only
+        const uint4 ss = d.slot_stat[slot];
+        if (!sched && P + own <= d.mtu && ss.w == 0u) {
+            lite_apply(d, rcv, slot, st);
+            if (lane == 0) st.kvs = ss.y;
+            T = (uint32_t)own;
+        }
+        if (!sched && P + own <= d.mtu && (ss.w == 0u || pack_lite<true>(d, rcv, slot, (uint32_t)P, st, T))) {
+            flag = LITE_DONE;
+            const uint32_t S = (uint32_t)P + T;  // every NodeDelta whole: pack_group's state after the last one
+            const bool stop = S >= d.mtu || d.mtu - S < d.lb_min;
+            if (lane == 0) {
+                shard_add(d, C_DBYTES, T);
+                io.chain[slot] = (uint64_t)S | ((uint64_t)stop << 33);
+            }
+        }
+    }
+    if (lane == 0) {
+        d.slot_stat[slot].w = flag;
+        if (flag == LITE_DONE) shard_add(d, C_LITE, 1);
+    }
+    const unsigned long long s_alg = wave_sum(st.alg), s_nd = wave_sum(st.nd), s_kv = wave_sum(st.kvs);
+    const unsigned long long s_cd = wave_sum(st.cand);
+    if (lane == 0) {
+        shard_add(d, C_ALG, s_alg);
+        shard_add(d, C_PACKB, s_alg);
+        shard_add(d, C_LITEB, s_alg);  // k_lite's share of pack_bytes (its own roofline entry)
+        shard_add(d, C_ND, s_nd);
+        shard_add(d, C_KVS, s_kv);
+        shard_add(d, C_CAND, s_cd);
+    }
+    return flag;
+}
+
+// LITE (sliced phases with Dev::lite, MODE 1 and 2): k_lite's slot work first, in the same wave, and the exact
+// count / pack only for the slots it leaves (one launch per step instead of two: a slice's kernels are short,
+// and their fixed cost per launch is what a sliced phase pays over one handle)
+template <int KW, int MODE, bool LITE = false>
 __global__ __launch_bounds__(XB, (KW == 4 ? PK_WAVES : 1)) void k_settle(Dev d, const int32_t *ini, const int32_t *res,
                                                                         uint32_t n, uint32_t t, SliceIO io) {
     __shared__ __attribute__((aligned(16))) uint16_t s_wbuf[2 * WIN];
@@ -2426,9 +2700,18 @@ __global__ __launch_bounds__(XB, (KW == 4 ? PK_WAVES : 1)) void k_settle(Dev d, 
     if (e >= n) return;
     const int tid = threadIdx.x, lane = tid & (WAVE - 1), wid = tid >> 6;
     const int32_t ai = ini[e], bi = res[e];
-    if (ai < 0 || bi < 0 || (uint32_t)ai >= d.N || (uint32_t)bi >= d.N || ai == bi) return;  // counted already
-    const uint32_t a = (uint32_t)ai, b = (uint32_t)bi;
     const size_t slot = (size_t)e * 2 + wid;
+    if (ai < 0 || bi < 0 || (uint32_t)ai >= d.N || (uint32_t)bi >= d.N || ai == bi) {  // counted already
+        if (LITE && lane == 0) d.slot_stat[slot].w = LITE_DONE;
+        return;
+    }
+    uint32_t lflag = 0u;  // LITE: the slot's flag from lite_slot
+    if (LITE) {
+        static_assert(!LITE || MODE == 1 || MODE == 2, "k_settle<LITE> runs the sliced steps");
+        lflag = lite_slot<MODE>(d, ai, bi, n, t, io, slot, wid, lane);
+        if (MODE == 1 ? !(lflag & LITE_FULL) : (lflag & LITE_DONE) != 0u) return;
+    }
+    const uint32_t a = (uint32_t)ai, b = (uint32_t)bi;
     const bool w0 = wid == 0;
     const uint32_t snd = w0 ? b : a, rcv = w0 ? a : b;
     const DigestSide ds{rcv, d.ncol, t >= d.row[rcv * 4 + 2]};
@@ -2446,7 +2729,7 @@ __global__ __launch_bounds__(XB, (KW == 4 ? PK_WAVES : 1)) void k_settle(Dev d, 
                 d.slot_stat[slot] = make_uint4(s.nd, s.kvs, s.cand, s.clean ? 0u : 1u);
             }
         } else {
-            if (d.lite && !(d.slot_stat[slot].w & LITE_FULL)) return;  // k_lite wrote the slice total
+            if (!LITE && d.lite && !(d.slot_stat[slot].w & LITE_FULL)) return;  // k_lite wrote the slice total
             pack_records<KW, true>(d, snd, rcv, ds, slot, wbuf, t, st, tomb, pst);
             if (lane == 0) io.tot[slot] = tot_word(pst.S, pst.m1);
             salg = st.alg;
@@ -2467,7 +2750,7 @@ __global__ __launch_bounds__(XB, (KW == 4 ? PK_WAVES : 1)) void k_settle(Dev d, 
             }
         }
     } else {  // MODE 2
-        if (d.lite && (d.slot_stat[slot].w & LITE_DONE)) return;  // k_lite applied it and wrote its chain state
+        if (!LITE && d.lite && (d.slot_stat[slot].w & LITE_DONE)) return;  // k_lite applied it and wrote its chain state
         unsigned long long P = 0, all = 0;
         for (uint32_t g = 0; g < d.shards; g++) {
             const unsigned long long x = GS_TOT_BYTES(io.tot_all[(size_t)g * n * 2 + slot]);
@@ -2541,61 +2824,7 @@ __global__ __launch_bounds__(XB, LITE_WAVES) void k_lite(Dev d, const int32_t *i
         if (lane == 0) d.slot_stat[slot].w = LITE_DONE;
         return;
     }
-    const uint32_t rcv = wid == 0 ? (uint32_t)ai : (uint32_t)bi;
-    const bool sched = t >= d.row[rcv * 4 + 2];  // the receiver's digest may leave owners out: exact packer
-    WStats st{0, 0, 0, 0, 0};
-    uint32_t T = 0, flag = LITE_FULL;
-    if (MODE == 0) {
-        if (!sched && pack_lite<true>(d, rcv, slot, 0u, st, T)) {
-            flag = LITE_DONE;
-            if (lane == 0) shard_add(d, C_DBYTES, T);
-        }
-    } else if (MODE == 1) {
-        uint32_t m1 = NONE;
-        if (!sched && pack_lite<false>(d, rcv, slot, 0u, st, T, &m1)) {
-            flag = 0u;
-            const uint32_t kv = (uint32_t)wave_sum(st.kvs);  // for step 0 (MODE 2): it applies without re-sizing
-            if (lane == 0) {
-                io.tot[slot] = tot_word(T, m1);
-                d.slot_stat[slot].y = kv;
-            }
-            st.kvs = 0u;  // counted when sent (MODE 2 or the exact packer)
-        }
-    } else {
-        unsigned long long P = 0;
-        for (uint32_t g = 0; g < d.shard; g++) P += GS_TOT_BYTES(io.tot_all[(size_t)g * n * 2 + slot]);
-        const unsigned long long own = GS_TOT_BYTES(io.tot_all[(size_t)d.shard * n * 2 + slot]);
-        // the count pass (MODE 1) sized this slot from the version log (slot_stat flag 0): apply only
-        const uint4 ss = d.slot_stat[slot];
-        if (!sched && P + own <= d.mtu && ss.w == 0u) {
-            lite_apply(d, rcv, slot, st);
-            if (lane == 0) st.kvs = ss.y;
-            T = (uint32_t)own;
-        }
-        if (!sched && P + own <= d.mtu && (ss.w == 0u || pack_lite<true>(d, rcv, slot, (uint32_t)P, st, T))) {
-            flag = LITE_DONE;
-            const uint32_t S = (uint32_t)P + T;  // every NodeDelta whole: pack_group's state after the last one
-            const bool stop = S >= d.mtu || d.mtu - S < d.lb_min;
-            if (lane == 0) {
-                shard_add(d, C_DBYTES, T);
-                io.chain[slot] = (uint64_t)S | ((uint64_t)stop << 33);
-            }
-        }
-    }
-    if (lane == 0) {
-        d.slot_stat[slot].w = flag;
-        if (flag == LITE_DONE) shard_add(d, C_LITE, 1);
-    }
-    const unsigned long long s_alg = wave_sum(st.alg), s_nd = wave_sum(st.nd), s_kv = wave_sum(st.kvs);
-    const unsigned long long s_cd = wave_sum(st.cand);
-    if (lane == 0) {
-        shard_add(d, C_ALG, s_alg);
-        shard_add(d, C_PACKB, s_alg);
-        shard_add(d, C_LITEB, s_alg);  // k_lite's share of pack_bytes (its own roofline entry)
-        shard_add(d, C_ND, s_nd);
-        shard_add(d, C_KVS, s_kv);
-        shard_add(d, C_CAND, s_cd);
-    }
+    lite_slot<MODE>(d, ai, bi, n, t, io, slot, wid, lane);
 }
 
 // ------------------------------------------------------------------ round start
@@ -2674,7 +2903,7 @@ template <int RING>
 #define LIVE_F32 1  // the phi decision's first test in binary32 (A/B: 0 = binary64 with a 2^-30 margin)
 #endif
 #ifndef LIVE_WAVES
-#define LIVE_WAVES 8  // waves per SIMD k_liveness is compiled for (<= 64 VGPRs)
+#define LIVE_WAVES 6  // waves per SIMD k_liveness is compiled for (<= 80 VGPRs: two chunks in flight)
 #endif
 #ifndef LIVE_NT
 #define LIVE_NT 1  // non-temporal loads / stores of the windows and state bytes (streamed once per round; r4c: 11.86 vs 12.21 ms)
@@ -2709,182 +2938,204 @@ __global__ __launch_bounds__(LB, LIVE_WAVES) void k_liveness(Dev d, const uint8_
     __syncthreads();
     const uint32_t vm = s_vm;
     const uint32_t cb1 = min(chunks, cb0 + per);
-    for (uint32_t cb = cb0; cb < cb1; cb++) {
-    // this chunk's windows and states are loaded before the plane staging (they do not depend on
-    // it), so the two global round trips of a chunk overlap; a down row has no valid planes (its
-    // node was in no exchange), so it loads windows only for up observers
-    const uint32_t c0 = (cb * LB + threadIdx.x) * 4u;
-    uint4 sc4 = make_uint4(0u, 0u, 0u, 0u);  // the four windows' sum | cnt words
-    uint2 l4 = make_uint2(0u, 0u);           // ... and their last-report ticks, u16 pairs
-    uint32_t s4 = 0u, ps[4] = {0u, 0u, 0u, 0u};  // s4: the four pairs' state bytes
-    if (c0 < d.ncol) {
-        const size_t p = pix(d, o, c0);
-        if (upo || vm) {
+    const uint32_t wv = threadIdx.x >> 6, ln = threadIdx.x & 63u;
+    // A down row without valid planes (its node was in no exchange) has nothing to replay or decide.  The
+    // chunks stream double-buffered: the next chunk's windows, states and plane words are loaded (always, at
+    // a clamped or shared address past the end, so that no wait counts them as absent) before the current
+    // chunk is computed, and the waits for the current chunk leave them in flight.
+    if (upo || vm) {
+        struct LW {
+            uint4 sc;      // the four windows' sum | cnt words
+            uint2 l;       // ... and their last-report ticks, u16 pairs
+            uint32_t s;    // the four pairs' state bytes
+            ulonglong2 pw; // this lane's 16 B of the chunk's report planes (lane l: phase l / 2, words 2 (l % 2) + {0, 1})
+        };
+        const uint32_t cmax = (d.ncol - 1u) & ~3u;
+        const uint32_t ph = ln >> 1;
+        const bool phv = ph < NPL && ((vm >> ph) & 1u);  // NPL = 16: lanes 0-31 only
+        const uint64_t *prow = d.pend + ((size_t)o * NPL + (phv ? ph : 0u)) * d.PW;
+        auto ldw = [&](uint32_t cb, bool real, LW &w) {
+            const uint32_t c0 = real ? min((cb * LB + threadIdx.x) * 4u, cmax) : 0u;
+            const size_t p = pix(d, o, c0);
             if (LIVE_NT) {  // streamed once per round: non-temporal
                 const v4u_t x = __builtin_nontemporal_load(reinterpret_cast<const v4u_t *>(d.fd + p));
                 const v2u_t y = __builtin_nontemporal_load(reinterpret_cast<const v2u_t *>(d.fd_last + p));
-                sc4 = make_uint4(x.x, x.y, x.z, x.w);
-                l4 = make_uint2(y.x, y.y);
-                s4 = __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(d.fd_state + p));
+                w.sc = make_uint4(x.x, x.y, x.z, x.w);
+                w.l = make_uint2(y.x, y.y);
+                w.s = __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(d.fd_state + p));
             } else {
-                sc4 = *reinterpret_cast<const uint4 *>(d.fd + p);
-                l4 = *reinterpret_cast<const uint2 *>(d.fd_last + p);
-                s4 = *reinterpret_cast<const uint32_t *>(d.fd_state + p);
+                w.sc = *reinterpret_cast<const uint4 *>(d.fd + p);
+                w.l = *reinterpret_cast<const uint2 *>(d.fd_last + p);
+                w.s = *reinterpret_cast<const uint32_t *>(d.fd_state + p);
             }
-        }
-        if (upo && genm) ld4(d.pos + p, ps);
-    }
-    const uint32_t wv = threadIdx.x >> 6, ln = threadIdx.x & 63u;
-    if (vm) {
-        __builtin_amdgcn_wave_barrier();  // this wave is done with the previous chunk's words
-        // 16 B per lane: NPL = 32 (lane l: phase l / 2, words 2 (l % 2) and 2 (l % 2) + 1), or NPL = 16
-        // (lanes 0-31 only); PW is a multiple of 4 and each wave's 4 words start on a multiple of 4
-        const uint32_t wi = cb * 16u + wv * 4u + (ln & 1u) * 2u;
-        const uint32_t ph = ln >> 1;
-        if (ph < NPL && ((vm >> ph) & 1u)) {
-            ulonglong2 w2 = make_ulonglong2(0ull, 0ull);
-            if (wi < d.PW) w2 = *reinterpret_cast<const ulonglong2 *>(d.pend + ((size_t)o * NPL + ph) * d.PW + wi);
-            *reinterpret_cast<ulonglong2 *>(&s_pl[wv][ph][(ln & 1u) * 2u]) = w2;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-    }
-    if (c0 < d.ncol) {
-        const size_t p = pix(d, o, c0);
-        // this thread's four columns: bit ph of q[i] = a report in phase ph
-        uint32_t q[4] = {0u, 0u, 0u, 0u};
-        if (d.pl16) {  // k_pass1v's layout: column 16 g + 4 q + i at bit 4 i + q of u16 g
-            const uint32_t ui = (c0 & 255u) >> 4, qs = (c0 >> 2) & 3u;
-            for (uint32_t m = vm; m; m &= m - 1u) {
-                const uint32_t ph = (uint32_t)__builtin_ctz(m);
-                const uint32_t u = (uint32_t)reinterpret_cast<const uint16_t *>(s_pl[wv][ph])[ui] >> qs;
-#pragma unroll
-                for (int i = 0; i < 4; i++) q[i] |= ((u >> (4 * i)) & 1u) << ph;
+            // PW is a multiple of 4 and each wave's 4 words start on a multiple of 4
+            const uint32_t wi = cb * 16u + wv * 4u + (ln & 1u) * 2u;
+            w.pw = *reinterpret_cast<const ulonglong2 *>(prow + (real && phv && wi < d.PW ? wi : 0u));
+        };
+        auto chunk = [&](uint32_t cb, const LW &cur, LW &nxt) __attribute__((always_inline)) {
+            const uint32_t c0 = (cb * LB + threadIdx.x) * 4u;
+            // the general layout's dict positions: loaded before the prefetch (and always, from a shared word
+            // of this row otherwise) so that their wait leaves the prefetch in flight
+            uint32_t ps[4];
+            {
+                const bool pl = upo && genm && c0 < d.ncol;
+                const uint4 pv = *reinterpret_cast<const uint4 *>(pl ? d.pos + pix(d, o, c0) : d.fd + pix(d, o, 0u));
+                ps[0] = pv.x; ps[1] = pv.y; ps[2] = pv.z; ps[3] = pv.w;
             }
-        } else {
-            const uint32_t lb = plane_bit(c0);
-            for (uint32_t m = vm; m; m &= m - 1u) {
-                const uint32_t ph = (uint32_t)__builtin_ctz(m);
-#pragma unroll
-                for (int i = 0; i < 4; i++) q[i] |= (uint32_t)((s_pl[wv][ph][i] >> lb) & 1ull) << ph;
+            ldw(cb + 1u, cb + 1u < cb1, nxt);
+            const uint4 sc4 = cur.sc;
+            const uint2 l4 = cur.l;
+            const uint32_t s4 = cur.s;
+            if (vm) {
+                __builtin_amdgcn_wave_barrier();  // this wave is done with the previous chunk's words
+                const uint32_t wi = cb * 16u + wv * 4u + (ln & 1u) * 2u;
+                if (phv) *reinterpret_cast<ulonglong2 *>(&s_pl[wv][ph][(ln & 1u) * 2u]) = wi < d.PW ? cur.pw : make_ulonglong2(0ull, 0ull);
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                __builtin_amdgcn_wave_barrier();
             }
-        }
-        uint32_t sc[4] = {sc4.x, sc4.y, sc4.z, sc4.w};
-        uint32_t lt[4] = {l4.x & 0xFFFFu, l4.x >> 16, l4.y & 0xFFFFu, l4.y >> 16};
-        bool dw = false;
-        uint32_t td[4] = {NONE, NONE, NONE, NONE};
-        if (exact && (s4 & 0x02020202u)) { ld4(d.tod + p, td); alg += 16; }
-        uint32_t s4n = s4;
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            uint32_t st = (s4 >> (8 * i)) & 0xFFu;
-            Fd f = fd_get(d, st, lt[i], sc[i], t);  // t is at or after every report tick of this round
-            uint32_t m = q[i];  // only if vm != 0: then the window was loaded
-            if (m) {
-                // report_heartbeat at ticks t_round + 1 + p for the phases p of m (failure_detector.py:32-38):
-                // intervals between reports of one round are < NPL ticks, so with max_interval >= NPL - 1 all
-                // but the first are appended and they telescope: (k - 1) intervals summing to p_last - p_first,
-                // plus the first one if it is <= max_interval; a compact window that would fill up, and the
-                // rings (their intervals one by one), replay report by report
-                bool loop = (RING && rrow) || d.max_iv < NPL - 1u;
-                if (!loop) {
-                    const uint32_t p1 = (uint32_t)__builtin_ctz(m), pk = 31u - (uint32_t)__builtin_clz(m);
-                    uint32_t app = (uint32_t)__popc(m) - 1u, add = pk - p1;
-                    if (f.last != NONE) {
-                        const uint32_t iv = d.t_round + 1u + p1 - f.last;
-                        if (iv <= d.max_iv) { app++; add += iv; }
+            if (c0 < d.ncol) {
+                const size_t p = pix(d, o, c0);
+                // this thread's four columns: bit ph of q[i] = a report in phase ph
+                uint32_t q[4] = {0u, 0u, 0u, 0u};
+                if (d.pl16) {  // k_pass1v's layout: column 16 g + 4 q + i at bit 4 i + q of u16 g
+                    const uint32_t ui = (c0 & 255u) >> 4, qs = (c0 >> 2) & 3u;
+                    for (uint32_t m = vm; m; m &= m - 1u) {
+                        const uint32_t ph = (uint32_t)__builtin_ctz(m);
+                        const uint32_t u = (uint32_t)reinterpret_cast<const uint16_t *>(s_pl[wv][ph])[ui] >> qs;
+        #pragma unroll
+                        for (int i = 0; i < 4; i++) q[i] |= ((u >> (4 * i)) & 1u) << ph;
                     }
-                    if (f.cnt + app <= d.W) {
-                        f.cnt += app;
-                        f.sum += add;
-                        f.last = d.t_round + 1u + pk;
+                } else {
+                    const uint32_t lb = plane_bit(c0);
+                    for (uint32_t m = vm; m; m &= m - 1u) {
+                        const uint32_t ph = (uint32_t)__builtin_ctz(m);
+        #pragma unroll
+                        for (int i = 0; i < 4; i++) q[i] |= (uint32_t)((s_pl[wv][ph][i] >> lb) & 1ull) << ph;
+                    }
+                }
+                uint32_t sc[4] = {sc4.x, sc4.y, sc4.z, sc4.w};
+                uint32_t lt[4] = {l4.x & 0xFFFFu, l4.x >> 16, l4.y & 0xFFFFu, l4.y >> 16};
+                bool dw = false;
+                uint32_t td[4] = {NONE, NONE, NONE, NONE};
+                if (exact && (s4 & 0x02020202u)) { ld4(d.tod + p, td); alg += 16; }
+                uint32_t s4n = s4;
+        #pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    uint32_t st = (s4 >> (8 * i)) & 0xFFu;
+                    Fd f = fd_get(d, st, lt[i], sc[i], t);  // t is at or after every report tick of this round
+                    uint32_t m = q[i];  // only if vm != 0: then the window was loaded
+                    if (m) {
+                        // report_heartbeat at ticks t_round + 1 + p for the phases p of m (failure_detector.py:32-38):
+                        // intervals between reports of one round are < NPL ticks, so with max_interval >= NPL - 1 all
+                        // but the first are appended and they telescope: (k - 1) intervals summing to p_last - p_first,
+                        // plus the first one if it is <= max_interval; a compact window that would fill up, and the
+                        // rings (their intervals one by one), replay report by report
+                        bool loop = (RING && rrow) || d.max_iv < NPL - 1u;
+                        if (!loop) {
+                            const uint32_t p1 = (uint32_t)__builtin_ctz(m), pk = 31u - (uint32_t)__builtin_clz(m);
+                            uint32_t app = (uint32_t)__popc(m) - 1u, add = pk - p1;
+                            if (f.last != NONE) {
+                                const uint32_t iv = d.t_round + 1u + p1 - f.last;
+                                if (iv <= d.max_iv) { app++; add += iv; }
+                            }
+                            if (f.cnt + app <= d.W) {
+                                f.cnt += app;
+                                f.sum += add;
+                                f.last = d.t_round + 1u + pk;
+                            } else {
+                                loop = true;
+                            }
+                        }
+                        if (loop) {
+                            while (m) {
+                                const uint32_t bb = (uint32_t)__builtin_ctz(m);
+                                m &= m - 1u;
+                                f = fd_report_val(d, RING && rrow ? rrow + (size_t)(c0 + i) * d.W : nullptr, d.t_round + 1u + bb,
+                                                  f, alg, ovf);
+                            }
+                        }
+                        dw = true;
+                    }
+                    const uint32_t j = c0 + i;
+                    if (upo && j < d.ncol && d.col_lo + j != o && !(genm && ps[i] == NONE)) {
+                        live++;
+                        const bool has = f.last != NONE;
+                        const uint32_t len = RING && rrow ? (f.cnt < d.W ? f.cnt : d.W) : f.cnt;
+                        bool alive = false;
+                        if (has && len) {
+                            // phi <= threshold (failure_detector.py:43-53, 97-98) decided without the two binary64
+                            // divisions when it is clear by a margin: phi ~ elapsed (len + 5) / (sum + 5 prior) in
+                            // ticks.  First in binary32 (full rate: elapsed < 2^24 ticks, len + 5 and sum < 2^24 are
+                            // exact, the three roundings and the two constants' add < 2^-21 relative) with a 2^-20
+                            // margin, then in binary64 with 2^-30 (far above its rounding), the exact expression
+                            // otherwise
+        #if LIVE_F32
+                            const float lf = (float)(t - f.last) * (float)(len + 5u);
+                            const float rf = d.phi_thr_f * ((float)f.sum + d.prior5t_f);
+                            if (lf < rf * (1.0f - 0x1p-20f)) {
+                                alive = true;
+                            } else if (!(lf > rf * (1.0f + 0x1p-20f))) {  // too close: the exact expression
+        #else
+                            const double lhs = (double)(t - f.last) * (double)(len + 5u);  // exact: < 2^43
+                            const double rhs = d.phi_thr * ((double)f.sum + d.prior5t);
+                            if (lhs < rhs * (1.0 - 0x1p-30)) {
+                                alive = true;
+                            } else if (!(lhs > rhs * (1.0 + 0x1p-30))) {
+        #endif
+                                const double mean = ((double)f.sum * TICK_S + d.prior5) / ((double)len + 5.0);
+                                alive = ((double)(t - f.last) * TICK_S) / mean <= d.phi_thr;
+                            }
+                        }
+                        const uint32_t mb = st & FD_MEMB;
+                        // node join / leave: the live set against the previous call's (server.py:611-616)
+                        if (d.ev && alive != (mb == FD_LIVE))
+                            emit_event(d, o, d.col_lo + j, (alive ? EV_JOIN : EV_LEAVE) << 8, 0u, 0u, t, 0u);
+                        uint32_t sn = FD_LIVE;
+                        if (!alive) {
+                            sn = FD_DEAD;
+                            uint32_t tod = td[i];  // loaded for the dead pairs of a row being recomputed
+                            if (mb != FD_DEAD) { tod = t; d.tod[p + i] = t; alg += 4; }  // time_of_death recorded once
+                            if (has && (f.sum | f.cnt)) { f.sum = f.cnt = 0u; dw = true; }  // reset
+                            if (mb != FD_DEAD || exact) {
+                                const uint32_t sat = tod + d.sched_delay;
+                                if (sat < minS) minS = sat;
+                            }
+                            if (exact && (uint64_t)t >= (uint64_t)tod + d.dead_grace) gcdue++;
+                        }
+                        st = (st & ~(uint32_t)FD_MEMB) | sn;
+                    }
+                    // a window whose last report is >= FD_OLD_AGE old keeps only that fact (fd_get)
+                    if ((st & (FD_WIN | FD_OLD)) == FD_WIN && t - f.last >= FD_OLD_AGE) st |= FD_OLD;
+                    if (q[i]) st = fd_st(st, f);
+                    sc[i] = fd_sc(d, f);
+                    lt[i] = f.last & 0xFFFFu;
+                    s4n = (s4n & ~(0xFFu << (8 * i))) | (st << (8 * i));
+                }
+                if (dw) {
+                    if (LIVE_NT) {
+                        __builtin_nontemporal_store(v4u_t{sc[0], sc[1], sc[2], sc[3]}, reinterpret_cast<v4u_t *>(d.fd + p));
+                        __builtin_nontemporal_store(v2u_t{lt[0] | (lt[1] << 16), lt[2] | (lt[3] << 16)},
+                                                    reinterpret_cast<v2u_t *>(d.fd_last + p));
                     } else {
-                        loop = true;
+                        *reinterpret_cast<uint4 *>(d.fd + p) = make_uint4(sc[0], sc[1], sc[2], sc[3]);
+                        *reinterpret_cast<uint2 *>(d.fd_last + p) = make_uint2(lt[0] | (lt[1] << 16), lt[2] | (lt[3] << 16));
                     }
+                    alg += 24;
                 }
-                if (loop) {
-                    while (m) {
-                        const uint32_t bb = (uint32_t)__builtin_ctz(m);
-                        m &= m - 1u;
-                        f = fd_report_val(d, RING && rrow ? rrow + (size_t)(c0 + i) * d.W : nullptr, d.t_round + 1u + bb,
-                                          f, alg, ovf);
-                    }
+                if (s4n != s4) {
+                    if (LIVE_NT) __builtin_nontemporal_store(s4n, reinterpret_cast<uint32_t *>(d.fd_state + p));
+                    else *reinterpret_cast<uint32_t *>(d.fd_state + p) = s4n;
+                    alg += 4;
                 }
-                dw = true;
+                if (upo || vm) alg += 28;  // the four windows (sum | cnt, last tick) and state bytes read
             }
-            const uint32_t j = c0 + i;
-            if (upo && j < d.ncol && d.col_lo + j != o && !(genm && ps[i] == NONE)) {
-                live++;
-                const bool has = f.last != NONE;
-                const uint32_t len = RING && rrow ? (f.cnt < d.W ? f.cnt : d.W) : f.cnt;
-                bool alive = false;
-                if (has && len) {
-                    // phi <= threshold (failure_detector.py:43-53, 97-98) decided without the two binary64
-                    // divisions when it is clear by a margin: phi ~ elapsed (len + 5) / (sum + 5 prior) in
-                    // ticks.  First in binary32 (full rate: elapsed < 2^24 ticks, len + 5 and sum < 2^24 are
-                    // exact, the three roundings and the two constants' add < 2^-21 relative) with a 2^-20
-                    // margin, then in binary64 with 2^-30 (far above its rounding), the exact expression
-                    // otherwise
-#if LIVE_F32
-                    const float lf = (float)(t - f.last) * (float)(len + 5u);
-                    const float rf = d.phi_thr_f * ((float)f.sum + d.prior5t_f);
-                    if (lf < rf * (1.0f - 0x1p-20f)) {
-                        alive = true;
-                    } else if (!(lf > rf * (1.0f + 0x1p-20f))) {  // too close: the exact expression
-#else
-                    const double lhs = (double)(t - f.last) * (double)(len + 5u);  // exact: < 2^43
-                    const double rhs = d.phi_thr * ((double)f.sum + d.prior5t);
-                    if (lhs < rhs * (1.0 - 0x1p-30)) {
-                        alive = true;
-                    } else if (!(lhs > rhs * (1.0 + 0x1p-30))) {
-#endif
-                        const double mean = ((double)f.sum * TICK_S + d.prior5) / ((double)len + 5.0);
-                        alive = ((double)(t - f.last) * TICK_S) / mean <= d.phi_thr;
-                    }
-                }
-                const uint32_t mb = st & FD_MEMB;
-                // node join / leave: the live set against the previous call's (server.py:611-616)
-                if (d.ev && alive != (mb == FD_LIVE))
-                    emit_event(d, o, d.col_lo + j, (alive ? EV_JOIN : EV_LEAVE) << 8, 0u, 0u, t, 0u);
-                uint32_t sn = FD_LIVE;
-                if (!alive) {
-                    sn = FD_DEAD;
-                    uint32_t tod = td[i];  // loaded for the dead pairs of a row being recomputed
-                    if (mb != FD_DEAD) { tod = t; d.tod[p + i] = t; alg += 4; }  // time_of_death recorded once
-                    if (has && (f.sum | f.cnt)) { f.sum = f.cnt = 0u; dw = true; }  // reset
-                    if (mb != FD_DEAD || exact) {
-                        const uint32_t sat = tod + d.sched_delay;
-                        if (sat < minS) minS = sat;
-                    }
-                    if (exact && (uint64_t)t >= (uint64_t)tod + d.dead_grace) gcdue++;
-                }
-                st = (st & ~(uint32_t)FD_MEMB) | sn;
-            }
-            // a window whose last report is >= FD_OLD_AGE old keeps only that fact (fd_get)
-            if ((st & (FD_WIN | FD_OLD)) == FD_WIN && t - f.last >= FD_OLD_AGE) st |= FD_OLD;
-            if (q[i]) st = fd_st(st, f);
-            sc[i] = fd_sc(d, f);
-            lt[i] = f.last & 0xFFFFu;
-            s4n = (s4n & ~(0xFFu << (8 * i))) | (st << (8 * i));
+        };
+        LW w0, w1;
+        ldw(cb0, true, w0);
+        for (uint32_t cb = cb0; cb < cb1; cb += 2u) {
+            chunk(cb, w0, w1);
+            if (cb + 1u < cb1) chunk(cb + 1u, w1, w0);
         }
-        if (dw) {
-            if (LIVE_NT) {
-                __builtin_nontemporal_store(v4u_t{sc[0], sc[1], sc[2], sc[3]}, reinterpret_cast<v4u_t *>(d.fd + p));
-                __builtin_nontemporal_store(v2u_t{lt[0] | (lt[1] << 16), lt[2] | (lt[3] << 16)},
-                                            reinterpret_cast<v2u_t *>(d.fd_last + p));
-            } else {
-                *reinterpret_cast<uint4 *>(d.fd + p) = make_uint4(sc[0], sc[1], sc[2], sc[3]);
-                *reinterpret_cast<uint2 *>(d.fd_last + p) = make_uint2(lt[0] | (lt[1] << 16), lt[2] | (lt[3] << 16));
-            }
-            alg += 24;
-        }
-        if (s4n != s4) {
-            if (LIVE_NT) __builtin_nontemporal_store(s4n, reinterpret_cast<uint32_t *>(d.fd_state + p));
-            else *reinterpret_cast<uint32_t *>(d.fd_state + p) = s4n;
-            alg += 4;
-        }
-        if (upo || vm) alg += 28;  // the four windows (sum | cnt, last tick) and state bytes read
-    }
     }
     // earliest scheduled-for-deletion tick of this row
     for (int dd = 32; dd >= 1; dd >>= 1) {
@@ -4153,6 +4404,15 @@ bool lite_ok(const gs_handle *h) {
     return h->pack_mode == 2 && (h->cfg.flags & GS_CANONICAL) && !(h->cfg.flags & GS_TOMBSTONES) && h->d.cand &&
            h->d.vlog && h->d.slot_stat && !h->d.ev && !(h->d.ablate & 1u);
 }
+// The same speculative merge in k_pass1v (GS_MV8 record phases, before k_lite): k_lite then only sizes the
+// deltas, and the exact packer restores what it does not send (env GS_P1SPEC=0: off, A/B)
+bool spec_v_ok(const gs_handle *h) {
+    static const bool on = [] {
+        const char *e = getenv("GS_P1SPEC");
+        return !(e && e[0] == '0');
+    }();
+    return on && h->d.pl16 && !h->sliced && lite_ok(h);
+}
 template <int MODE>
 int launch_lite(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t n, uint32_t tick, const SliceIO &io) {
     hipEvent_t e0 = nullptr;
@@ -4262,16 +4522,24 @@ int launch_pass1(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t 
     HIPCHK(h, hipGetLastError());
     return time_end(h, GS_KT_PASS1, e0);
 }
-template <int MODE>
+template <int MODE, bool LITE = false>
 int launch_settle(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t n, uint32_t tick, const SliceIO &io,
                   int kind) {
     hipEvent_t e0 = nullptr;
     int rc = time_begin(h, e0);
     if (rc) return rc;
-    if (h->KP <= 16) k_settle<4, MODE><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, io);
-    else k_settle<KWB, MODE><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, io);
+    if (h->KP <= 16) k_settle<4, MODE, LITE><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, io);
+    else k_settle<KWB, MODE, LITE><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, io);
     HIPCHK(h, hipGetLastError());
     return time_end(h, kind, e0);
+}
+// the sliced steps' lite + settle as one kernel (k_settle<LITE>); env GS_LITE_FUSE=0: two launches (A/B)
+bool lite_fuse() {
+    static const bool on = [] {
+        const char *e = getenv("GS_LITE_FUSE");
+        return !(e && e[0] == '0');
+    }();
+    return on;
 }
 
 // One canonical one-slice phase on the caller's stream (GS_PACK, A/B runs): default k_pass1 with the
@@ -4280,7 +4548,7 @@ int launch_settle(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t
 int run_split_phase(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t n, uint32_t tick) {
     hipEvent_t e0 = nullptr;
     int rc;
-    h->d.spec = spec_ok(h) ? 1u : 0u;
+    h->d.spec = spec_ok(h) || spec_v_ok(h) ? 1u : 0u;
     h->d.lite = lite_ok(h) ? 1u : 0u;
     if (h->pack_mode == 1) {
         if ((rc = time_begin(h, e0))) return rc;
@@ -4699,6 +4967,7 @@ int gs_phase_count(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_
     h->d.spec = spec_ok(h) ? 1u : 0u;
     h->d.lite = lite_ok(h) ? 1u : 0u;
     if ((rc = launch_pass1(h, ini, res, n, tick))) return rc;
+    if (h->d.lite && lite_fuse()) return launch_settle<1, true>(h, ini, res, n, tick, io, GS_KT_COUNT);
     if (h->d.lite && (rc = launch_lite<1>(h, ini, res, n, tick, io))) return rc;
     return launch_settle<1>(h, ini, res, n, tick, io, GS_KT_COUNT);
 }
@@ -4718,6 +4987,7 @@ int gs_phase_pack(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t
     io.step = step;
     if (step && h->shard == 0) return GS_OK;  // slice 0 always finishes at step 0
     if (step == 0 && h->d.cand) {
+        if (h->d.lite && lite_fuse()) return launch_settle<2, true>(h, ini, res, n, tick, io, GS_KT_PACK);
         if (h->d.lite && (rc = launch_lite<2>(h, ini, res, n, tick, io))) return rc;
         return launch_settle<2>(h, ini, res, n, tick, io, GS_KT_PACK);
     }

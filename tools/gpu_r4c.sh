@@ -28,6 +28,12 @@ if [ -n "$PS" ]; then
   timeout -k 10 400 python -u bench.py --peer-select --settle 190 --steps 10 --warmup 2 --no-cpu-baseline > $O/bench_ps.log 2>&1 || { tail -20 $O/bench_ps.log; exit 1; }
   tail -1 $O/bench_ps.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('peer-select value', round(d['value']), 'ms/step', round(d['ms_per_step'],2), 'counters', {k: d['counters'][k] for k in ('lag_sweeps','hb_escapes','hb_releases')}, 'exactness', d['exactness'])"
 fi
+if [ -n "$SLICETRACE" ]; then  # kernel trace of a sliced rehearsal (gaps between launches: tools/gaps.py)
+  for g in $SLICETRACE; do
+    (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace -d $GRAFT_REPO_ROOT/$O/st$g -o st --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --slices $g --steps 3 --warmup 1 --no-cpu-baseline --peer-select-steps 0 > $GRAFT_REPO_ROOT/$O/st$g.log 2>&1) || { tail -20 $O/st$g.log; exit 1; }
+  done
+  echo slicetrace
+fi
 if [ -n "$PROFILE" ]; then
   SQ=1 timeout -k 10 1100 bash tools/profile.sh $TAG > $O/profile.log 2>&1 || { tail -20 $O/profile.log; exit 1; }
   echo profiled
