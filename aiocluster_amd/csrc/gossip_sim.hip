@@ -51,7 +51,7 @@ constexpr int XB = 128;  // exchange workgroup: 2 waves
 #endif
 constexpr int LB = 256;  // liveness / elementwise workgroups
 #ifndef LIVE_PER
-#define LIVE_PER 8  // 1024-column chunks per k_liveness workgroup
+#define LIVE_PER 32  // 1024-column chunks per k_liveness workgroup (r4g/r4h at 65,536: 32 -> 10.85 ms, 16 -> 11.0-11.1, 8 -> 11.9, 4 -> 13.6)
 #endif
 constexpr int NSHARD = 64;
 // native vectors: the nontemporal load / store builtins take them (not HIP's uint4 struct)
@@ -91,7 +91,7 @@ struct Dev {
     uint32_t col_lo, ncol, shards, shard;
     uint32_t max_iv, tomb_grace, dead_grace, sched_delay, lb_min, sum_bits;
     uint32_t ablate;  // profiling only (env GS_ABLATE): 1 = skip packing, 2 = skip pass-1 stores (results invalid);
-                      // A/B, results valid: 8 = k_pass1v without its slow-group slots, 16 = k_pass1v records decoded at emit
+                      // A/B, results valid: 8 = k_pass1v without its slow-group slots
     double phi_thr, prior5;
     double prior5t;  // prior5 in ticks (x 64): the liveness sweep's division-free phi test
     float phi_thr_f, prior5t_f;  // the same in binary32: the sweep's first, full-rate test (2^-20 margin)
@@ -1658,7 +1658,7 @@ __global__ __launch_bounds__(XB, (KW == 4 ? (FUSE ? P1_WAVES : MV8 ? P1N_WAVES :
 #define P1V_AHEAD 1  // groups of 16 columns loaded ahead of the one being computed
 #endif
 #ifndef P1V_WAVES
-#define P1V_WAVES 6  // waves per SIMD k_pass1v is compiled for
+#define P1V_WAVES 5  // waves per SIMD k_pass1v is compiled for (r4i: 5 -> 2.19 ms per phase, 6 -> 2.25)
 #endif
 constexpr uint32_t B7 = 0x80808080u, L7 = 0x7F7F7F7Fu;
 // the 16-column plane layout: plane u16 g holds columns 16 g .. 16 g + 15, column 16 g + 4 q + i at bit 4 i + q
@@ -1702,7 +1702,7 @@ __device__ __forceinline__ uint32_t wave_scan_dpp(uint32_t x) {
 // would make the wave wait for the loads in flight for the next step.
 __device__ __forceinline__ void emit_v(uint16_t *gw16, uint2 *L, uint32_t &cnt, uint32_t c, bool act,
                                        const uint32_t (&nm)[4], const uint4 &sS, const uint4 &sR, uint32_t &alg,
-                                       uint32_t (&rec)[4], bool dec = false, const uint32_t *self_mv = nullptr) {
+                                       uint32_t (&rec)[4]) {
     const uint32_t my = act ? (uint32_t)(__popc(nm[0]) + __popc(nm[1]) + __popc(nm[2]) + __popc(nm[3])) : 0u;
     const uint32_t incl = wave_scan_dpp(my);
     const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
@@ -1722,12 +1722,7 @@ __device__ __forceinline__ void emit_v(uint16_t *gw16, uint2 *L, uint32_t &cnt, 
             for (int i = 0; i < 4; i++) {
                 if ((nm[q] >> (8 * i + 7)) & 1u) {
                     if (off < GS_CAND_CAP) {
-                        uint32_t w = ((s4[q] >> (8 * i)) & 0xFFu) | (((r4[q] >> (8 * i)) & 0xFFu) << 16);
-                        if (dec) {  // (A/B: decoded here)
-                            const uint32_t M = self_mv[c + 4u * q + i];
-                            w = mv_dec8(w & 0xFFu, M) | (mv_dec8(w >> 16, M) << 16);
-                        }
-                        L[off] = make_uint2(c + 4u * q + i, w);
+                        L[off] = make_uint2(c + 4u * q + i, ((s4[q] >> (8 * i)) & 0xFFu) | (((r4[q] >> (8 * i)) & 0xFFu) << 16));
                         rec[q] |= 0x80u << (8 * i);
                         alg += 8;
                     }
@@ -1862,7 +1857,7 @@ __device__ __forceinline__ void p1v_decode_records(const Dev &d, uint2 *L, uint3
 template <int AHEAD>
 __global__ __launch_bounds__(XB, P1V_WAVES) void k_pass1v(Dev d, const int32_t *ini, const int32_t *res, uint32_t n,
                                                           uint32_t t, uint32_t seq) {
-    static_assert(AHEAD == 1 || AHEAD == 2, "k_pass1v keeps one or two groups in flight ahead");
+    static_assert(AHEAD == 1, "k_pass1v double-buffers one group ahead (r4g: two ahead at 5 waves per SIMD, no faster)");
     __shared__ uint32_t s_col[XB / WAVE][P1V_K];
     __shared__ uint32_t s_out[XB / WAVE][P1V_K * P1V_SLOT];
     const uint32_t e = blockIdx.x;
@@ -1911,7 +1906,7 @@ __global__ __launch_bounds__(XB, P1V_WAVES) void k_pass1v(Dev d, const int32_t *
     }
     const uint8_t *h8 = reinterpret_cast<const uint8_t *>(d.hb), *m8 = reinterpret_cast<const uint8_t *>(d.mv);
     uint8_t *hw8 = reinterpret_cast<uint8_t *>(d.hb), *mw8 = reinterpret_cast<uint8_t *>(d.mv);
-    const bool hbst = !(d.ablate & 2u), spec = d.spec != 0u, decv = (d.ablate & 16u) != 0u;
+    const bool hbst = !(d.ablate & 2u), spec = d.spec != 0u;
     auto load = [&](uint32_t c, V16 &v) {
         v.hA = *reinterpret_cast<const uint4 *>(h8 + ra + c);
         v.hB = *reinterpret_cast<const uint4 *>(h8 + rb + c);
@@ -2011,7 +2006,6 @@ __global__ __launch_bounds__(XB, P1V_WAVES) void k_pass1v(Dev d, const int32_t *
     // path here (a whole-slow exchange, or more slow groups than slots).
     constexpr uint32_t STEP = WAVE * 16u;
     const uint32_t clast = (max(hi, 1u) - 1u) & ~15u;  // the wave's last group (a valid one for an empty half)
-    // (with AHEAD = 2 the prologue's second load may also fall past the end: clamped the same way)
     auto stream = [&](auto tag) {
         constexpr bool TABLE = decltype(tag)::value;
         uint32_t sbase = 0u;  // slow groups of the wave before this step (TABLE)
@@ -2020,7 +2014,7 @@ __global__ __launch_bounds__(XB, P1V_WAVES) void k_pass1v(Dev d, const int32_t *
             const bool act = c < hi;
             // unconditional (a lane past the end reloads the last group): a load under a branch would make
             // the wait for the current group's loads count as if the next group's were not in flight
-            load(c + AHEAD * STEP < hi ? c + AHEAD * STEP : clast, nx);
+            load(c + STEP < hi ? c + STEP : clast, nx);
             const uint32_t x4[4] = {v.hA.x, v.hA.y, v.hA.z, v.hA.w}, y4[4] = {v.hB.x, v.hB.y, v.hB.z, v.hB.w};
             const uint32_t ma4[4] = {v.mA.x, v.mA.y, v.mA.z, v.mA.w}, mb4[4] = {v.mB.x, v.mB.y, v.mB.z, v.mB.w};
             uint32_t nba[4] = {0u, 0u, 0u, 0u}, nab[4] = {0u, 0u, 0u, 0u};
@@ -2107,8 +2101,8 @@ __global__ __launch_bounds__(XB, P1V_WAVES) void k_pass1v(Dev d, const int32_t *
                 alg += 4;
             }
             uint32_t rBA[4] = {0u, 0u, 0u, 0u}, rAB[4] = {0u, 0u, 0u, 0u};  // recorded stale owners
-            emit_v(gBA, LBA, nBAc, c, act, nba, v.mB, v.mA, alg, rBA, decv, d.self_mv);  // b -> a: sender b, receiver a
-            emit_v(gAB, LAB, nABc, c, act, nab, v.mA, v.mB, alg, rAB, decv, d.self_mv);
+            emit_v(gBA, LBA, nBAc, c, act, nba, v.mB, v.mA, alg, rBA);  // b -> a: sender b, receiver a
+            emit_v(gAB, LAB, nABc, c, act, nab, v.mA, v.mB, alg, rAB);
             if (spec && act) {
                 // speculative merge (Dev::spec): each recorded stale owner whose two views are prefix views
                 // (GS_MV_INEXACT clear: bit 7 of both bytes) gets the sender's view now, in the 16 bytes this
@@ -2129,14 +2123,12 @@ __global__ __launch_bounds__(XB, P1V_WAVES) void k_pass1v(Dev d, const int32_t *
                 if (wB) { *reinterpret_cast<uint4 *>(mw8 + rb + c) = make_uint4(nB[0], nB[1], nB[2], nB[3]); alg += 16; }
             }
         };
-        // AHEAD + 1 buffers in rotation (the loop unrolled by that many steps: no register moves)
-        V16 bf[AHEAD + 1];
-#pragma unroll
-        for (int k = 0; k < AHEAD; k++) load(min(lo + (uint32_t)lane * 16u + k * STEP, clast), bf[k]);
-        for (uint32_t s0 = lo; s0 < hi; s0 += (AHEAD + 1) * STEP) {  // wave-uniform trip count (the scans need every lane)
-#pragma unroll
-            for (int k = 0; k <= AHEAD; k++)
-                if (k == 0 || s0 + k * STEP < hi) step(s0 + k * STEP, bf[k], bf[(k + AHEAD) % (AHEAD + 1)]);
+        // two buffers in turn (the loop unrolled by two steps: no register moves)
+        V16 b0, b1;
+        load(min(lo + (uint32_t)lane * 16u, clast), b0);
+        for (uint32_t s0 = lo; s0 < hi; s0 += 2u * STEP) {  // wave-uniform trip count (the scans need every lane)
+            step(s0, b0, b1);
+            if (s0 + STEP < hi) step(s0 + STEP, b1, b0);
         }
     };
     if (table)
@@ -2144,11 +2136,9 @@ __global__ __launch_bounds__(XB, P1V_WAVES) void k_pass1v(Dev d, const int32_t *
     else
         stream(std::false_type{});
     // this wave's records: bytes -> words (its own stores: visible to the wave after the fence)
-    if (!decv) {
-        __threadfence_block();
-        p1v_decode_records(d, LBA, nBAc, lane);
-        p1v_decode_records(d, LAB, nABc, lane);
-    }
+    __threadfence_block();
+    p1v_decode_records(d, LBA, nBAc, lane);
+    p1v_decode_records(d, LAB, nABc, lane);
     if (lane == 0) {
         d.cand_n[(size_t)e * 4 + 0 * 2 + wid] = nBAc;
         d.cand_n[(size_t)e * 4 + 1 * 2 + wid] = nABc;
@@ -2721,8 +2711,10 @@ __global__ __launch_bounds__(XB, (KW == 4 ? PK_WAVES : 1)) void k_settle(Dev d, 
     PackState pst{0u, false, false};
     uint32_t salg = 0;
     bool done = false;
+    // d.spec without d.lite: the speculative A/B path (GS_PACK=spec) sizes and settles from settle_sum; with
+    // d.lite (k_pass1v's merge) the lite / exact-packer path below restores what is not sent
     if (MODE == 1) {
-        if (d.spec) {
+        if (d.spec && !d.lite) {
             const SlotSum s = settle_sum<KW>(d, snd, rcv, ds, slot, wbuf, t, salg);
             if (lane == 0) {
                 io.tot[slot] = tot_word(s.T, 0u);  // (speculative A/B path: no chain skipping)
@@ -2762,7 +2754,7 @@ __global__ __launch_bounds__(XB, (KW == 4 ? PK_WAVES : 1)) void k_settle(Dev d, 
             return;
         }
         pst = PackState{(uint32_t)P, false, false};
-        if (d.spec && all <= d.mtu) {
+        if (d.spec && !d.lite && all <= d.mtu) {
             const uint4 ss = d.slot_stat[slot];
             if (!ss.w) {
                 done = true;
@@ -4405,13 +4397,16 @@ bool lite_ok(const gs_handle *h) {
            h->d.vlog && h->d.slot_stat && !h->d.ev && !(h->d.ablate & 1u);
 }
 // The same speculative merge in k_pass1v (GS_MV8 record phases, before k_lite): k_lite then only sizes the
-// deltas, and the exact packer restores what it does not send (env GS_P1SPEC=0: off, A/B)
+// deltas, and the exact packer restores what it does not send (a slot a chain step finds stopped restores
+// every record: pack_list).  Sliced phases only: there it halves the step-0 kernel (r4i: 0.23 vs 0.43 ms at
+// 2 slices); with one slice the merge's stores cost k_pass1v what they save k_lite (r4i: +0.40 / -0.41 ms,
+// 41.7 vs 41.4 ms per step).  Env GS_P1SPEC=0: off (A/B).
 bool spec_v_ok(const gs_handle *h) {
     static const bool on = [] {
         const char *e = getenv("GS_P1SPEC");
         return !(e && e[0] == '0');
     }();
-    return on && h->d.pl16 && !h->sliced && lite_ok(h);
+    return on && h->d.pl16 && h->sliced && lite_ok(h);
 }
 template <int MODE>
 int launch_lite(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t n, uint32_t tick, const SliceIO &io) {
@@ -4964,7 +4959,7 @@ int gs_phase_count(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_
         return rc ? rc : time_end(h, GS_KT_PASS1, e0);
     }
     // the speculative merge is decided here for the whole phase (gs_phase_pack / gs_phase_chain use it)
-    h->d.spec = spec_ok(h) ? 1u : 0u;
+    h->d.spec = spec_ok(h) || spec_v_ok(h) ? 1u : 0u;
     h->d.lite = lite_ok(h) ? 1u : 0u;
     if ((rc = launch_pass1(h, ini, res, n, tick))) return rc;
     if (h->d.lite && lite_fuse()) return launch_settle<1, true>(h, ini, res, n, tick, io, GS_KT_COUNT);
