@@ -4292,6 +4292,10 @@ struct gs_handle {
         uint32_t *list = nullptr;
         uint32_t cap = 0;  // exchanges the buffers hold
     } sc;
+    // gs_run_phase_group: each slice's kernels of a step run on a stream of its own (forked from and joined
+    // back into the group's stream around the step), so the slices' short launches overlap on the GPU
+    hipStream_t side = nullptr, home = nullptr;
+    hipEvent_t fj_fork = nullptr, fj_join = nullptr;
 };
 
 namespace {
@@ -4736,6 +4740,9 @@ void gs_destroy(gs_handle *h) {
                     (void *)h->sc.chain_all, (void *)h->sc.list, (void *)h->sc.pend})
         if (p) (void)hipFree(p);
     if (h->comm) (void)ncclCommDestroy(h->comm);
+    if (h->side) (void)hipStreamDestroy(h->side);
+    for (hipEvent_t e : {h->fj_fork, h->fj_join})
+        if (e) (void)hipEventDestroy(e);
     delete h;
 }
 
@@ -5097,23 +5104,54 @@ int gather_u64(gs_handle *const *hs, uint32_t nh, uint64_t *(*src)(gs_handle *),
 // totals (16 B per exchange and slice), packing step 0, then -- only for the (exchange, direction) slots
 // whose totals sum past the MTU, listed on the device, one host read -- G - 1 chain steps, each an
 // all-gather of those slots' chain states (8 B per slot and slice) and a resume on the next slice.
+// In-process slices (gs_run_phase_group): fork every slice onto its own stream after the work queued so far on
+// the group's stream, and join them back before a step that reads all slices (the gathers).  One RCCL slice per
+// process (nh = 1) runs on its own stream as it is.
+int fork_slices(gs_handle *const *hs, uint32_t nh) {
+    gs_handle *h0 = hs[0];
+    if (nh < 2) return GS_OK;
+    if (!h0->fj_fork) HIPCHK(h0, hipEventCreateWithFlags(&h0->fj_fork, hipEventDisableTiming));
+    HIPCHK(h0, hipEventRecord(h0->fj_fork, h0->stream));
+    for (uint32_t i = 0; i < nh; i++) {
+        gs_handle *h = hs[i];
+        if (!h->side) HIPCHK(h, hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
+        if (!h->fj_join) HIPCHK(h, hipEventCreateWithFlags(&h->fj_join, hipEventDisableTiming));
+        HIPCHK(h, hipStreamWaitEvent(h->side, h0->fj_fork, 0));
+        h->home = h->stream;
+        h->stream = h->side;
+    }
+    return GS_OK;
+}
+int join_slices(gs_handle *const *hs, uint32_t nh, int rc = GS_OK) {
+    if (nh < 2) return rc;
+    for (uint32_t i = 0; i < nh; i++) {  // streams restored first, whatever failed
+        gs_handle *h = hs[i];
+        const hipError_t e = hipEventRecord(h->fj_join, h->side);
+        h->stream = h->home;
+        if (e != hipSuccess && rc == GS_OK) rc = fail(h, GS_E_HIP, "hipEventRecord: %s", hipGetErrorString(e));
+    }
+    for (uint32_t i = 0; i < nh && rc == GS_OK; i++) HIPCHK(hs[0], hipStreamWaitEvent(hs[0]->stream, hs[i]->fj_join, 0));
+    return rc;
+}
 int sliced_phase(gs_handle *const *hs, uint32_t nh, const int32_t *ini, const int32_t *res, uint32_t n, uint32_t tick) {
     int rc;
     for (uint32_t i = 0; i < nh; i++) {
         if (!hs[i]->d.cand) return fail(hs[i], GS_E_UNSUPPORTED, "library-driven sliced phases need candidate records");
         if ((rc = ensure_scratch(hs[i], n))) return rc;
     }
-    for (uint32_t i = 0; i < nh; i++)
-        if ((rc = gs_phase_count(hs[i], ini, res, n, tick, hs[i]->sc.tot))) return rc;
+    if ((rc = fork_slices(hs, nh))) return rc;
+    for (uint32_t i = 0; i < nh && !rc; i++) rc = gs_phase_count(hs[i], ini, res, n, tick, hs[i]->sc.tot);
+    if ((rc = join_slices(hs, nh, rc))) return rc;
     if ((rc = gather_u64(hs, nh, [](gs_handle *h) { return h->sc.tot; }, [](gs_handle *h) { return h->sc.tot_all; },
                          (size_t)2 * n)))
         return rc;
-    for (uint32_t i = 0; i < nh; i++)
-        if ((rc = gs_phase_pack(hs[i], ini, res, n, tick, 0, hs[i]->sc.tot_all, nullptr, hs[i]->sc.chain))) return rc;
-    for (uint32_t i = 0; i < nh; i++)  // the overflowing slots, listed on the device (the same list on every slice)
-        if ((rc = gs_phase_overflow(hs[i], n, hs[i]->sc.tot_all, hs[i]->sc.chain, hs[i]->sc.list, hs[i]->sc.chainc,
-                                    nullptr)))
-            return rc;
+    if ((rc = fork_slices(hs, nh))) return rc;
+    for (uint32_t i = 0; i < nh && !rc; i++) {
+        rc = gs_phase_pack(hs[i], ini, res, n, tick, 0, hs[i]->sc.tot_all, nullptr, hs[i]->sc.chain);
+        // the overflowing slots, listed on the device (the same list on every slice)
+        if (!rc) rc = gs_phase_overflow(hs[i], n, hs[i]->sc.tot_all, hs[i]->sc.chain, hs[i]->sc.list, hs[i]->sc.chainc, nullptr);
+    }
+    if ((rc = join_slices(hs, nh, rc))) return rc;
     const uint32_t G = hs[0]->G;
     if (G < 2) return GS_OK;  // one slice: step 0 finished every slot
     gs_handle *h0 = hs[0];
@@ -5131,11 +5169,11 @@ int sliced_phase(gs_handle *const *hs, uint32_t nh, const int32_t *ini, const in
     };
     // step 1 before any host read, on the device count (a chain usually resolves in it: one read ends the phase)
     uint64_t pend = 0;
-    if ((rc = gather_chain(GS_CHAIN_CAP + 1u))) return rc;
-    for (uint32_t i = 0; i < nh; i++)
-        if ((rc = gs_phase_chain(hs[i], ini, res, n, tick, 1, hs[i]->sc.list, GS_CHAIN_DEVICE, hs[i]->sc.chain_all,
-                                 hs[i]->sc.chain, hs[i]->sc.chainc, hs[i]->sc.tot_all)))
-            return rc;
+    if ((rc = gather_chain(GS_CHAIN_CAP + 1u)) || (rc = fork_slices(hs, nh))) return rc;
+    for (uint32_t i = 0; i < nh && !rc; i++)
+        rc = gs_phase_chain(hs[i], ini, res, n, tick, 1, hs[i]->sc.list, GS_CHAIN_DEVICE, hs[i]->sc.chain_all,
+                            hs[i]->sc.chain, hs[i]->sc.chainc, hs[i]->sc.tot_all);
+    if ((rc = join_slices(hs, nh, rc))) return rc;
     if ((rc = gather_chain(GS_CHAIN_CAP + 1u)) || (rc = pending(0u, cnt0, pend))) return rc;
     if (!pend) return GS_OK;
     // still pending (or more slots than the device step takes): the count to the host, the remaining steps
@@ -5147,10 +5185,11 @@ int sliced_phase(gs_handle *const *hs, uint32_t nh, const int32_t *ini, const in
         // reads the same sum and all stop together
         if ((rc = gather_chain((size_t)count + 1)) || (rc = pending(count, nullptr, pend))) return rc;
         if (!pend) break;
-        for (uint32_t i = 0; i < nh; i++)
-            if ((rc = gs_phase_chain(hs[i], ini, res, n, tick, step, hs[i]->sc.list, count, hs[i]->sc.chain_all,
-                                     hs[i]->sc.chain, hs[i]->sc.chainc, hs[i]->sc.tot_all)))
-                return rc;
+        if ((rc = fork_slices(hs, nh))) return rc;
+        for (uint32_t i = 0; i < nh && !rc; i++)
+            rc = gs_phase_chain(hs[i], ini, res, n, tick, step, hs[i]->sc.list, count, hs[i]->sc.chain_all,
+                                hs[i]->sc.chain, hs[i]->sc.chainc, hs[i]->sc.tot_all);
+        if ((rc = join_slices(hs, nh, rc))) return rc;
     }
     return GS_OK;
 }

@@ -30,7 +30,7 @@ if [ -n "$PS" ]; then
 fi
 if [ -n "$SLICETRACE" ]; then  # kernel trace of a sliced rehearsal (gaps between launches: tools/gaps.py)
   for g in $SLICETRACE; do
-    (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace -d $GRAFT_REPO_ROOT/$O/st$g -o st --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --slices $g --steps 3 --warmup 1 --no-cpu-baseline --peer-select-steps 0 > $GRAFT_REPO_ROOT/$O/st$g.log 2>&1) || { tail -20 $O/st$g.log; exit 1; }
+    (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace -d $GRAFT_REPO_ROOT/$O/st$g -o st --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --slices $g --steps 3 --warmup 1 --no-cpu-baseline --peer-select-steps 0 $STARGS > $GRAFT_REPO_ROOT/$O/st$g.log 2>&1) || { tail -20 $O/st$g.log; exit 1; }
   done
   echo slicetrace
 fi
