@@ -1657,6 +1657,19 @@ __global__ __launch_bounds__(XB, (KW == 4 ? (FUSE ? P1_WAVES : MV8 ? P1N_WAVES :
 #ifndef P1V_AHEAD
 #define P1V_AHEAD 1  // groups of 16 columns loaded ahead of the one being computed
 #endif
+#ifndef P1V_LINE
+#define P1V_LINE 8  // k_pass1v's row stores cover whole 128-byte lines (8 lanes; 4: 64 B; 0: per lane): a partial
+                    // line written back costs the memory a read-modify-write (r4m, with the merge: 2.08 vs 2.26 ms)
+#endif
+// whether any lane of this lane's line (P1V_LINE consecutive lanes) has p set; every lane of the wave calls it
+__device__ __forceinline__ bool line_any_v(bool p) {
+    const uint64_t m = __ballot(p);
+    const uint32_t l = (uint32_t)__lane_id() & ~(uint32_t)(P1V_LINE - 1);
+    return ((m >> l) & ((1ull << P1V_LINE) - 1ull)) != 0ull;
+}
+#ifndef P1V_NT
+#define P1V_NT 1  // non-temporal row loads and heartbeat / max_version stores in k_pass1v (r4l: 1.81-1.86 vs 2.14-2.22 ms)
+#endif
 #ifndef P1V_WAVES
 #define P1V_WAVES 5  // waves per SIMD k_pass1v is compiled for (r4i: 5 -> 2.19 ms per phase, 6 -> 2.25)
 #endif
@@ -1908,10 +1921,21 @@ __global__ __launch_bounds__(XB, P1V_WAVES) void k_pass1v(Dev d, const int32_t *
     uint8_t *hw8 = reinterpret_cast<uint8_t *>(d.hb), *mw8 = reinterpret_cast<uint8_t *>(d.mv);
     const bool hbst = !(d.ablate & 2u), spec = d.spec != 0u;
     auto load = [&](uint32_t c, V16 &v) {
-        v.hA = *reinterpret_cast<const uint4 *>(h8 + ra + c);
-        v.hB = *reinterpret_cast<const uint4 *>(h8 + rb + c);
-        v.mA = *reinterpret_cast<const uint4 *>(m8 + ra + c);
-        v.mB = *reinterpret_cast<const uint4 *>(m8 + rb + c);
+        if (P1V_NT) {  // (A/B) the rows streamed non-temporally
+            const v4u_t x0 = __builtin_nontemporal_load(reinterpret_cast<const v4u_t *>(h8 + ra + c));
+            const v4u_t x1 = __builtin_nontemporal_load(reinterpret_cast<const v4u_t *>(h8 + rb + c));
+            const v4u_t x2 = __builtin_nontemporal_load(reinterpret_cast<const v4u_t *>(m8 + ra + c));
+            const v4u_t x3 = __builtin_nontemporal_load(reinterpret_cast<const v4u_t *>(m8 + rb + c));
+            v.hA = make_uint4(x0.x, x0.y, x0.z, x0.w);
+            v.hB = make_uint4(x1.x, x1.y, x1.z, x1.w);
+            v.mA = make_uint4(x2.x, x2.y, x2.z, x2.w);
+            v.mB = make_uint4(x3.x, x3.y, x3.z, x3.w);
+        } else {
+            v.hA = *reinterpret_cast<const uint4 *>(h8 + ra + c);
+            v.hB = *reinterpret_cast<const uint4 *>(h8 + rb + c);
+            v.mA = *reinterpret_cast<const uint4 *>(m8 + ra + c);
+            v.mB = *reinterpret_cast<const uint4 *>(m8 + rb + c);
+        }
         v.fl = d.p1flags[c >> 4];
     };
     // the per-column path's predicate for the group at column c (c < hi)
@@ -2046,9 +2070,18 @@ __global__ __launch_bounds__(XB, P1V_WAVES) void k_pass1v(Dev d, const int32_t *
                     nba[q] = (ev + L7) & B7 & ~e6;
                     nab[q] = e6;
                 }
+                if (P1V_LINE) {  // whole lines (the unchanged lanes' bytes are their rows' own)
+                    upAll = line_any_v(upAll != 0u) ? 1u : 0u;
+                    upBll = line_any_v(upBll != 0u) ? 1u : 0u;
+                }
                 if (hbst) {
-                    if (upAll) *reinterpret_cast<uint4 *>(hw8 + ra + c) = make_uint4(nw[0], nw[1], nw[2], nw[3]);
-                    if (upBll) *reinterpret_cast<uint4 *>(hw8 + rb + c) = make_uint4(nw[0], nw[1], nw[2], nw[3]);
+                    if (P1V_NT) {
+                        if (upAll) __builtin_nontemporal_store(v4u_t{nw[0], nw[1], nw[2], nw[3]}, reinterpret_cast<v4u_t *>(hw8 + ra + c));
+                        if (upBll) __builtin_nontemporal_store(v4u_t{nw[0], nw[1], nw[2], nw[3]}, reinterpret_cast<v4u_t *>(hw8 + rb + c));
+                    } else {
+                        if (upAll) *reinterpret_cast<uint4 *>(hw8 + ra + c) = make_uint4(nw[0], nw[1], nw[2], nw[3]);
+                        if (upBll) *reinterpret_cast<uint4 *>(hw8 + rb + c) = make_uint4(nw[0], nw[1], nw[2], nw[3]);
+                    }
                 }
                 alg += 64u + (upAll ? 16u : 0u) + (upBll ? 16u : 0u);
                 pA = pack16(repA);
@@ -2119,8 +2152,20 @@ __global__ __launch_bounds__(XB, P1V_WAVES) void k_pass1v(Dev d, const int32_t *
                     wA |= ba;
                     wB |= ab;
                 }
-                if (wA) { *reinterpret_cast<uint4 *>(mw8 + ra + c) = make_uint4(nA[0], nA[1], nA[2], nA[3]); alg += 16; }
-                if (wB) { *reinterpret_cast<uint4 *>(mw8 + rb + c) = make_uint4(nB[0], nB[1], nB[2], nB[3]); alg += 16; }
+                if (P1V_LINE) {  // whole lines: a partial line costs the memory a read-modify-write
+                    wA = line_any_v(wA != 0u);
+                    wB = line_any_v(wB != 0u);
+                }
+                if (wA) {
+                    if (P1V_NT) __builtin_nontemporal_store(v4u_t{nA[0], nA[1], nA[2], nA[3]}, reinterpret_cast<v4u_t *>(mw8 + ra + c));
+                    else *reinterpret_cast<uint4 *>(mw8 + ra + c) = make_uint4(nA[0], nA[1], nA[2], nA[3]);
+                    alg += 16;
+                }
+                if (wB) {
+                    if (P1V_NT) __builtin_nontemporal_store(v4u_t{nB[0], nB[1], nB[2], nB[3]}, reinterpret_cast<v4u_t *>(mw8 + rb + c));
+                    else *reinterpret_cast<uint4 *>(mw8 + rb + c) = make_uint4(nB[0], nB[1], nB[2], nB[3]);
+                    alg += 16;
+                }
             }
         };
         // two buffers in turn (the loop unrolled by two steps: no register moves)
@@ -3352,12 +3397,69 @@ __global__ __launch_bounds__(LB) void k_hb_lag(Dev d, uint32_t chunks) {
     if (j0 < d.ncol) {
         const size_t p0 = pix(d, o, j0);
         // one 16-byte load per region: the thread's heartbeat views (and GS_MV8 max_version views)
-        const uint4 hr = d.hb8 ? *reinterpret_cast<const uint4 *>(reinterpret_cast<const uint8_t *>(d.hb) + p0)
-                               : *reinterpret_cast<const uint4 *>(d.hb + p0);
-        const uint4 mr = d.mv8 ? *reinterpret_cast<const uint4 *>(reinterpret_cast<const uint8_t *>(d.mv) + p0)
-                               : make_uint4(0u, 0u, 0u, 0u);
+        // (8-bit views: streamed once per sweep, non-temporal)
+        uint4 hr, mr = make_uint4(0u, 0u, 0u, 0u);
+        if (d.hb8) {
+            const v4u_t x = __builtin_nontemporal_load(reinterpret_cast<const v4u_t *>(reinterpret_cast<const uint8_t *>(d.hb) + p0));
+            hr = make_uint4(x.x, x.y, x.z, x.w);
+        } else {
+            hr = *reinterpret_cast<const uint4 *>(d.hb + p0);
+        }
+        if (d.mv8) {
+            const v4u_t x = __builtin_nontemporal_load(reinterpret_cast<const v4u_t *>(reinterpret_cast<const uint8_t *>(d.mv) + p0));
+            mr = make_uint4(x.x, x.y, x.z, x.w);
+        }
         const uint32_t hw[4] = {hr.x, hr.y, hr.z, hr.w}, mw[4] = {mr.x, mr.y, mr.z, mr.w};
-        for (uint32_t q = 0; q < per / 4u && j0 + 4u * q < d.ncol; q++) {
+        // the headline's layout (canonical, GS_HB8 + GS_MV8): four views per 32-bit word against the owners'
+        // packed own values (SELF_PK: heartbeat mod 2^8 in byte 0, max_version in the high half), per-byte
+        // lags with borrow-isolated subtracts; only escaped columns and escape requests go column by column
+        const bool swar = !genm && d.hb8 && d.mv8 && d.self_pk;
+        if (swar) {
+#pragma unroll
+            for (uint32_t q = 0; q < 4u; q++) {
+                const uint32_t jq = j0 + 4u * q;
+                if (jq >= d.ncol) break;
+                const uint4 pk = *reinterpret_cast<const uint4 *>(d.self_pk + jq);
+                const uint32_t own8 = (pk.x & 0xFFu) | ((pk.y & 0xFFu) << 8) | ((pk.z & 0xFFu) << 16) | (pk.w << 24);
+                const uint32_t owm7 = ((pk.x >> 16) & 0x7Fu) | (((pk.y >> 16) & 0x7Fu) << 8) | (((pk.z >> 16) & 0x7Fu) << 16) |
+                                      (((pk.w >> 16) & 0x7Fu) << 24);
+                const uint32_t nv = min(d.ncol - jq, 4u);
+                const uint32_t vm7 = nv >= 4u ? B7 : B7 & ((1u << (8u * nv)) - 1u);  // bit 7 of the valid columns
+                uint32_t es[4] = {NONE, NONE, NONE, NONE};
+                uint32_t esc7 = 0u;
+                if (d.EC) {
+                    ld4(d.esc_slot + jq, es);
+#pragma unroll
+                    for (uint32_t i = 0; i < 4; i++) esc7 |= (uint32_t)(es[i] != NONE) << (8 * i + 7);
+                }
+                const uint32_t lagH = bsub(own8, hw[q]);                            // (own - view) mod 2^8
+                const uint32_t lagM = ((owm7 | B7) - (mw[q] & L7)) & L7;           // (own - view) mod 2^7
+                const uint32_t hb7 = lagH & B7 & ~esc7 & vm7;                       // heartbeat lag >= 2^7
+                const uint32_t hh7 = (lagH | (lagH << 1)) & B7 & ~esc7 & vm7;       // >= HOT_HB (64)
+                const uint32_t mb7 = (lagM << 1) & B7 & vm7;                        // max_version lag >= 2^6
+                const uint32_t mh7 = ((lagM << 1) | (lagM << 2)) & B7 & vm7;        // >= HOT_MV (32)
+                hot |= nib7(hh7 | mh7) << (4u * q);
+                bad += (uint32_t)__popc(mb7);
+                if (hb7) {
+                    if (d.EC) {
+                        for (uint32_t m = hb7; m; m &= m - 1u) {
+                            const uint32_t j = jq + ((uint32_t)__builtin_ctz(m) >> 3);
+                            atomicOr(&d.esc_req[j >> 5], 1u << (j & 31u));
+                        }
+                    } else {
+                        bad += (uint32_t)__popc(hb7);
+                    }
+                }
+                for (uint32_t m = esc7 & vm7; m; m &= m - 1u) {  // escaped columns: 16-bit views, exact while < 2^15
+                    const uint32_t i = (uint32_t)__builtin_ctz(m) >> 3;
+                    const uint32_t R = d.self_hb[jq + i];
+                    const uint32_t lag = (R - d.esc16[(size_t)o * d.EC + es[i]]) & 0xFFFFu;
+                    if (lag >= 0x8000u) bad++;
+                    hotc |= (uint32_t)(lag >= HOT_HB) << (4u * q + i);
+                }
+            }
+        }
+        for (uint32_t q = 0; !swar && q < per / 4u && j0 + 4u * q < d.ncol; q++) {
             const uint32_t jq = j0 + 4u * q;
             // the owners' own values, 4 columns per 16-byte load (L2)
             const uint4 ow = *reinterpret_cast<const uint4 *>(d.self_hb + jq);
@@ -4402,15 +4504,15 @@ bool lite_ok(const gs_handle *h) {
 }
 // The same speculative merge in k_pass1v (GS_MV8 record phases, before k_lite): k_lite then only sizes the
 // deltas, and the exact packer restores what it does not send (a slot a chain step finds stopped restores
-// every record: pack_list).  Sliced phases only: there it halves the step-0 kernel (r4i: 0.23 vs 0.43 ms at
-// 2 slices); with one slice the merge's stores cost k_pass1v what they save k_lite (r4i: +0.40 / -0.41 ms,
-// 41.7 vs 41.4 ms per step).  Env GS_P1SPEC=0: off (A/B).
+// every record: pack_list).  With whole-line row stores (P1V_LINE) the merge costs k_pass1v 0.27 ms and saves
+// k_lite 0.42 (r4m: 36.8 vs 38.0 ms per round); per-lane 16-byte stores made it cost as much as it saved (r4i).
+// In sliced phases it halves the step-0 kernel (r4i: 0.23 vs 0.43 ms at 2 slices).  Env GS_P1SPEC=0: off (A/B).
 bool spec_v_ok(const gs_handle *h) {
     static const bool on = [] {
         const char *e = getenv("GS_P1SPEC");
         return !(e && e[0] == '0');
     }();
-    return on && h->d.pl16 && h->sliced && lite_ok(h);
+    return on && h->d.pl16 && lite_ok(h);
 }
 template <int MODE>
 int launch_lite(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t n, uint32_t tick, const SliceIO &io) {
