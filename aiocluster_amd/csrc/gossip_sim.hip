@@ -929,8 +929,9 @@ __device__ __forceinline__ void pack_list(const Dev &d, uint32_t s, uint32_t r, 
     pack_begin(d, COUNT, pst, S, tail, stop);
     const bool specd = !COUNT && d.spec;
     // prefix candidates from the version log (eval_light): no hook events (their applies take the per-key
-    // path), no scheduled-for-deletion test due (a digest may leave owners out: from = 0), not speculative
-    const bool lightok = d.vlog && !d.ev && !ds.sched && !specd;
+    // path), no scheduled-for-deletion test due (a digest may leave owners out: from = 0).  Speculative slots
+    // too: eval_light and apply_cand's paths start from the record's pre-exchange words, never the merged row
+    const bool lightok = d.vlog && !d.ev && !ds.sched;
     uint32_t nr = 0, m1 = pst.m1;
     uint2 nxt = make_uint2(0u, 0u);
     if ((uint32_t)lane < n) nxt = L[lane];
@@ -1016,9 +1017,12 @@ __device__ __forceinline__ void lite_apply(const Dev &d, uint32_t rcv, size_t sl
 // k_lite's per-slot flags (Dev::slot_stat[slot].w): LITE_FULL = the exact packer must size / pack the slot,
 // LITE_DONE = k_lite completed it
 constexpr uint32_t LITE_FULL = 1u, LITE_DONE = 2u;
+// sched: the receiver's row may hold targets scheduled for deletion (its digest leaves them out, so their
+// NodeDeltas start from version 0): any recorded owner that is one sends the slot to the exact packer.
 template <bool APPLY = true>
 __device__ __forceinline__ bool pack_lite(const Dev &d, uint32_t rcv, size_t slot, uint32_t S0, WStats &st,
-                                          uint32_t &Tout, uint32_t *m1out = nullptr) {
+                                          uint32_t &Tout, uint32_t *m1out = nullptr, bool sched = false,
+                                          uint32_t t = 0u) {
     const int lane = lane_id();
     const uint32_t n0 = d.cand_n[slot * 2], n1 = d.cand_n[slot * 2 + 1];
     if (n0 > GS_CAND_CAP || n1 > GS_CAND_CAP) return false;  // a half continues in its bitmap
@@ -1041,6 +1045,11 @@ __device__ __forceinline__ bool pack_lite(const Dev &d, uint32_t rcv, size_t slo
             if (rc[u].x == NONE) continue;
             const uint32_t ms = rc[u].y & 0xFFFFu, mr = rc[u].y >> 16;  // sender / receiver words
             if (!rec_fast(rc[u].y) || ms <= mr) { bad = true; continue; }
+            if (sched) {  // owner rc.x left out of the receiver's digest (scheduled for deletion): from = 0
+                const size_t p = pix(d, rcv, rc[u].x);
+                if ((d.fd_state[p] & FD_MEMB) == FD_DEAD && is_sched(d.tod[p], t, d.sched_delay)) { bad = true; continue; }
+                alg += 1;
+            }
             ev[u] = d.vlog[(size_t)rc[u].x * d.VL + ms];
             ns[u] = d.nid_size[rc[u].x];
         }
@@ -2667,17 +2676,17 @@ template <int MODE>
 __device__ __forceinline__ uint32_t lite_slot(const Dev &d, int32_t ai, int32_t bi, uint32_t n, uint32_t t,
                                               const SliceIO &io, size_t slot, int wid, int lane) {
     const uint32_t rcv = wid == 0 ? (uint32_t)ai : (uint32_t)bi;
-    const bool sched = t >= d.row[rcv * 4 + 2];  // the receiver's digest may leave owners out: exact packer
+    const bool sched = t >= d.row[rcv * 4 + 2];  // the receiver's digest may leave owners out: checked per record
     WStats st{0, 0, 0, 0, 0};
     uint32_t T = 0, flag = LITE_FULL;
     if (MODE == 0) {
-        if (!sched && pack_lite<true>(d, rcv, slot, 0u, st, T)) {
+        if (pack_lite<true>(d, rcv, slot, 0u, st, T, nullptr, sched, t)) {
             flag = LITE_DONE;
             if (lane == 0) shard_add(d, C_DBYTES, T);
         }
     } else if (MODE == 1) {
         uint32_t m1 = NONE;
-        if (!sched && pack_lite<false>(d, rcv, slot, 0u, st, T, &m1)) {
+        if (pack_lite<false>(d, rcv, slot, 0u, st, T, &m1, sched, t)) {
             flag = 0u;
             const uint32_t kv = (uint32_t)wave_sum(st.kvs);  // for step 0 (MODE 2): it applies without re-sizing
             if (lane == 0) {
@@ -2692,12 +2701,12 @@ __device__ __forceinline__ uint32_t lite_slot(const Dev &d, int32_t ai, int32_t 
         const unsigned long long own = GS_TOT_BYTES(io.tot_all[(size_t)d.shard * n * 2 + slot]);
         // the count pass (MODE 1) sized this slot from the version log (slot_stat flag 0): apply only
         const uint4 ss = d.slot_stat[slot];
-        if (!sched && P + own <= d.mtu && ss.w == 0u) {
+        if (P + own <= d.mtu && ss.w == 0u) {  // (the count pass checked a scheduled receiver's records)
             lite_apply(d, rcv, slot, st);
             if (lane == 0) st.kvs = ss.y;
             T = (uint32_t)own;
         }
-        if (!sched && P + own <= d.mtu && (ss.w == 0u || pack_lite<true>(d, rcv, slot, (uint32_t)P, st, T))) {
+        if (P + own <= d.mtu && (ss.w == 0u || pack_lite<true>(d, rcv, slot, (uint32_t)P, st, T, nullptr, sched, t))) {
             flag = LITE_DONE;
             const uint32_t S = (uint32_t)P + T;  // every NodeDelta whole: pack_group's state after the last one
             const bool stop = S >= d.mtu || d.mtu - S < d.lb_min;
