@@ -51,7 +51,7 @@ constexpr int XB = 128;  // exchange workgroup: 2 waves
 #endif
 constexpr int LB = 256;  // liveness / elementwise workgroups
 #ifndef LIVE_PER
-#define LIVE_PER 32  // 1024-column chunks per k_liveness workgroup (r4g/r4h at 65,536: 32 -> 10.85 ms, 16 -> 11.0-11.1, 8 -> 11.9, 4 -> 13.6)
+#define LIVE_PER 64  // 1024-column chunks per k_liveness workgroup, at most (r4g/h/k/p at 65,536: 64 -> 10.5-10.8 ms, 32 -> 10.7-11.2, 16 -> 11.0-11.1, 8 -> 11.9, 4 -> 13.6)
 #endif
 constexpr int NSHARD = 64;
 // native vectors: the nontemporal load / store builtins take them (not HIP's uint4 struct)

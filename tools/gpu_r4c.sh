@@ -5,9 +5,17 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 O=gpurun_out/$TAG; mkdir -p $O
+if [ -n "$SMOKE" ]; then  # the driver's round-end smoke()
+  timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
+  tail -2 $O/smoke.log
+fi
 if [ -n "$TESTS" ]; then
   timeout -k 10 900 python -u -m pytest $TESTS -m gpu -x -v --durations=12 --timeout 400 --timeout-method thread > $O/gpu_tests.log 2>&1 || { tail -40 $O/gpu_tests.log; exit 1; }
   tail -14 $O/gpu_tests.log
+fi
+if [ -n "$BENCHFULL" ]; then  # the driver's bench command (cpu_baseline and peer_select legs included)
+  timeout -k 10 900 python -u bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_full.log 2>&1 || { tail -20 $O/bench_full.log; exit 1; }
+  tail -1 $O/bench_full.log | cut -c1-600
 fi
 if [ -n "$VARIANTS" ]; then
   ARGS=${ARGS:-"--steps 10 --warmup 2 --no-cpu-baseline --peer-select-steps 0"} bash tools/ab.sh || exit 1
