@@ -613,13 +613,18 @@ class GossipSim:
             s = np.asarray(hb).view(np.uint16).astype(np.uint32)
             out = (R - ((R - s) & np.uint32(0xFFFF))).astype(np.uint32)
         if "ESC_SLOT" in self.regions:
-            slot = self.region("ESC_SLOT", self.torch.int32, (self.np_,)).cpu().numpy().view(np.uint32)
+            torch = self.torch
+            slot = self.region("ESC_SLOT", torch.int32, (self.np_,)).cpu().numpy().view(np.uint32)
             cols = np.nonzero(slot != GS_NONE)[0]
             if len(cols):
+                # only the requested rows' escaped slots cross to the host (ESC16 is N x esc_cols x 2 B)
                 ec = int(self.c_esc_cols)
-                esc = self.region("ESC16", self.torch.int16, (self.n, ec)).cpu().numpy().view(np.uint16)
-                o = np.arange(self.n) if rows is None else np.asarray(rows, dtype=np.int64)
-                e = esc[o][:, slot[cols].astype(np.int64)].astype(np.uint32)  # [rows, escaped columns]
+                esc = self.region("ESC16", torch.int16, (self.n, ec))
+                if rows is not None or out.ndim == 1:
+                    o = np.arange(self.n) if rows is None else np.asarray(rows, dtype=np.int64).reshape(-1)
+                    esc = esc.index_select(0, torch.as_tensor(o, device=self.device))
+                sl = torch.as_tensor(slot[cols].astype(np.int64), device=self.device)
+                e = esc.index_select(1, sl).cpu().numpy().view(np.uint16).astype(np.uint32)  # [rows, escaped cols]
                 v = (R[cols] - ((R[cols] - e) & np.uint32(0xFFFF))).astype(np.uint32)
                 if out.ndim == 1:
                     out[cols] = v[0]

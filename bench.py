@@ -111,16 +111,18 @@ def cpu_baseline(sim, cfg, rd, sample: int, min_seconds: float = 10.0, threads: 
             os.sched_setaffinity(0, {pin[k]})  # Linux: pid 0 = the calling thread
 
     load0 = os.getloadavg()[0]
-    # one thread: every handle's pairs in turn, on restored rows, until ~min_seconds/3 are timed
+    # one thread: every handle's pairs in turn, each timed right after its own rows are restored -- as each of
+    # the T threads below restores its handle just before its timed pass (like for like: cache-warm rows in
+    # both legs; VERDICT r4: restoring all handles first left the single thread's rows cold)
     dt1, reps1, rate1 = 0.0, 0, []
     pin_to(T)
     while dt1 < min_seconds / 3 or reps1 < 3:
+        dt = 0.0
         for i in range(T):
             restore(i)
-        t0 = time.perf_counter()
-        for i in range(T):
+            t0 = time.perf_counter()
             run(i)
-        dt = time.perf_counter() - t0
+            dt += time.perf_counter() - t0
         dt1 += dt
         reps1 += 1
         rate1.append(len(pairs) / dt)
@@ -176,7 +178,8 @@ def cpu_baseline(sim, cfg, rd, sample: int, min_seconds: float = 10.0, threads: 
         "statistic": f"median of {repsT} timed passes (p10 {q(rateT, 10):.0f}, p90 {q(rateT, 90):.0f}; mean "
                      f"{len(pairs) * repsT / dtT:.0f})",
         "single_core_value": q(rate1, 50),
-        "single_core_statistic": f"median of {reps1} passes (p10 {q(rate1, 10):.0f}, p90 {q(rate1, 90):.0f})",
+        "single_core_statistic": f"median of {reps1} passes (p10 {q(rate1, 10):.0f}, p90 {q(rate1, 90):.0f}); each "
+                                 f"handle timed right after its own rows are restored, as in the threaded leg",
         "host": {"cpu_model": model, "cpus_allowed": len(cpus),
                  "pinning": (f"thread i on CPU {pin[0]}+i, single-thread runs on CPU {pin[T]}" if pin is not None
                              else "unpinned (fewer allowed CPUs than threads)"),
@@ -277,7 +280,8 @@ def pass1_kernel(wide_views: bool) -> str:
     return "k_pass1v"
 
 
-def roofline(sims, local_c, exch, kt, elapsed, torch, dev, rank, group, workload, p1name="k_pass1") -> dict:
+def roofline(sims, local_c, exch, kt, elapsed, torch, dev, rank, group, workload, p1name="k_pass1",
+             steps: int = 1) -> dict:
     """Roofline of the dominant kernel (by summed time; HBM-bound integer/byte work, no MFMA) plus the
     same figures for the other kernels of the round.
 
@@ -323,6 +327,10 @@ def roofline(sims, local_c, exch, kt, elapsed, torch, dev, rank, group, workload
     copy_gbs = copy_ceiling(torch, dev, sims[0].stream) if rank == 0 else None
     launches = kt["pass1"][1] or 1
     survey = (exch * 32 * ncols + packb) / launches
+    # the whole step: every phase kernel's and k_liveness' in-kernel algorithmic bytes of the timed rounds over
+    # the step's wall time (kernels not counted -- lag sweeps, round starts, owner writes -- add time, not bytes)
+    step_bytes = (alg + liveb) / max(steps, 1)
+    step_s = elapsed / max(steps, 1)
     return {
         "bound": "hbm",
         "kernel": d["kernel"] if group is None else d["kernel"] + " (one owner-column slice, per rank)",
@@ -349,8 +357,17 @@ def roofline(sims, local_c, exch, kt, elapsed, torch, dev, rank, group, workload
         "note": ("k_pass1v streams 8-bit heartbeat + max_version views (GS_HB8 + GS_MV8), 16 columns per lane, and "
                  "runs pass 1's per-column rules on 4 views per 32-bit word (DESIGN.md §4)") if d["kernel"] == "k_pass1v"
                 else None,
-        "survey_formula_bytes_per_phase": survey,
-        "survey_formula_gbs_over_pass1": survey / (kt["pass1"][0] / launches / 1e3) / 1e9 if kt["pass1"][0] else None,
+        "step_alg_bytes": step_bytes,
+        "step_achieved": step_bytes / step_s / 1e9,
+        "step_frac": step_bytes / step_s / 1e9 / HBM_PEAK_GBPS,
+        "step_basis": "(C_ALG + C_LIVEB) per timed round / ms_per_step: pass 1, k_lite, the exact packer and "
+                      "k_liveness in-kernel bytes over the whole round's wall time (launch gaps and kernels without a byte count "
+                      "kernels included)",
+        # the SURVEY §8(d) formula prices u32 heartbeat / max_version / last_gc rows (32 B per column per exchange);
+        # this layout streams 1-byte views, so this is what the u32 layout would have to move at this pass-1 time,
+        # an equivalent rate, NOT an achieved one (it exceeds the HBM peak)
+        "u32_layout_equiv_bytes_per_phase": survey,
+        "u32_layout_equiv_gbs_not_achieved": survey / (kt["pass1"][0] / launches / 1e3) / 1e9 if kt["pass1"][0] else None,
     }
 
 
@@ -535,6 +552,7 @@ def main():
     ap.add_argument("--wide-views", action="store_true", default=bool(os.environ.get("GS_WIDE_VIEWS")),
                     help="16-bit heartbeat and max_version views (default: GS_HB8 + GS_MV8, 8-bit views decoded "
                          "against the owner's own values, exact while every view lags < 2^8 / 2^7; swept)")
+    ap.add_argument("--hist-cap", type=int, default=64, help="writes kept per (owner, key) (gs_config.hist_cap)")
     ap.add_argument("--no-held", action="store_true",
                     help="version-only layout (GS_NO_HELD, config 4): needs an mtu no delta reaches")
     args = ap.parse_args()
@@ -581,7 +599,9 @@ def main():
                    else ""))
     t_setup = time.perf_counter()
     ids = synthetic_node_ids(n)
-    kw = dict(init="warm", device=str(dev), tombstones=False, fd_ring=False, hist_cap=16,
+    # hist_cap 64: HIST is 8 B x N x C x K (0.5 GB at 64); at 16 the writes per (owner, key) reached the cap's
+    # projection in ~100 rounds, well before the window horizon
+    kw = dict(init="warm", device=str(dev), tombstones=False, fd_ring=False, hist_cap=args.hist_cap,
               initial_ops=driver.boot_ops(n, K), held=not args.no_held, hb8=not args.wide_views,
               mv8=not args.wide_views)
     if world > 1 and args.slices > 1:
@@ -647,7 +667,7 @@ def main():
     # a sliced cluster: every rank runs the same exchanges on its columns -> count them once
     exch_total, elapsed_max = aggregate(exch if (group is None or rank == 0) else 0, elapsed, dist, dev)
     roof = roofline(sims[:1], local_c[:1], exch, kt, elapsed, torch, dev, rank, group, workload,
-                    pass1_kernel(args.wide_views))
+                    pass1_kernel(args.wide_views), steps=args.steps)
     cpu = None
     if rank == 0 and group is None and not args.no_cpu_baseline:
         rd = plans[R0 + args.steps]

@@ -112,7 +112,9 @@ typedef struct gs_config {
 enum gs_region {
     GS_R_HB = 0,      /* u16 [N][NP]   NodeState.heartbeat of owner j as seen by observer o, mod 2^16: decoded
                                         against GS_R_SELF_HB as R - ((R - s) mod 2^16), exact while every view
-                                        lags its owner's own heartbeat by less than 2^16 */
+                                        lags its owner's own heartbeat by less than 2^16.  With escape slots
+                                        (gs_config.esc_cols) the bytes of an escaped column (GS_R_ESC_SLOT[j] !=
+                                        GS_NONE) are STALE: its views live in GS_R_ESC16 [o][slot] */
     GS_R_MV,          /* u16 [N][NP]   NodeState.max_version (| GS_MV_INEXACT, see below); versions are
                                         bounded by K * (C - 1) <= 16,256, so 15 bits always suffice */
     GS_R_GC,          /* u32 [N][NP]   NodeState.last_gc_version (GS_TOMBSTONES only: without tombstone GC
@@ -486,9 +488,11 @@ int gs_reset_counters(gs_handle *h);
 int gs_sync(gs_handle *h);
 
 /* Copy-out (blocking, SURVEY §8(b) gs_read_*): observer rows [row_lo, row_hi) of a region indexed by
- * observer row (GS_R_HB, MV, GC, HELD, FD, FD_LAST, FD_STATE, FD_TOD, TS, RING, POS, ORD, ROW) into host memory
+ * observer row (GS_R_HB, MV, GC, HELD, FD, FD_LAST, FD_STATE, FD_TOD, TS, RING, POS, ORD, ROW, ESC16) into host memory
  * `out` of `cap` bytes, in the region's layout; *len = the bytes of those rows (set even when they exceed
- * cap, which fails).  GS_R_HELD rows are complete: the prefix views' ordinals are materialized first. */
+ * cap, which fails).  GS_R_HELD rows are complete: the prefix views' ordinals are materialized first.
+ * GS_R_HB rows are the stored bytes: an escaped owner column's views (GS_R_ESC_SLOT != GS_NONE) are read from
+ * GS_R_ESC16 (also a row region here), as GossipSim.decode_heartbeats does. */
 int gs_read_rows(gs_handle *h, int region, uint32_t row_lo, uint32_t row_hi, void *out, uint64_t cap, uint64_t *len);
 
 /* The latest tick any operation on h has used: GS_R_FD_LAST rows read with gs_read_rows are decoded against

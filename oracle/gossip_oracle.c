@@ -11,6 +11,7 @@
 #include "gossip_oracle.h"
 
 #include <math.h>
+#include <pthread.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -629,6 +630,101 @@ int32_t orc_liveness(orc *o, int32_t node, int64_t now) {
         for (int32_t r = 0; r < nres; r++) remove_node(o, b, res[r]); /* 619-620 */
     free(res);
     return q9;
+}
+
+/* ------------------------------------------------ threaded phases (checker speed) */
+/* A worker's view of the handle: the rows, configuration and sizes are shared (each thread touches its own
+ * rows only), the scratch (digests, deltas, schedules, temporaries) and the statistics are its own. */
+static void shadow_init(orc *sh, const orc *o) {
+    *sh = *o;
+    memset(&sh->st, 0, sizeof sh->st);
+    sh->ev_on = 0; sh->ev = NULL; sh->ev_n = sh->ev_cap = 0;
+    for (int d = 0; d < 2; d++) {
+        sh->dg[d].has = xcalloc(o->N, 1);
+        sh->dg[d].hb = xcalloc(o->N, sizeof(uint32_t));
+        sh->dg[d].gc = xcalloc(o->N, sizeof(uint32_t));
+        sh->dg[d].mv = xcalloc(o->N, sizeof(uint32_t));
+        sh->dg[d].list = xcalloc(o->N, sizeof(int32_t));
+        sh->sched[d] = xcalloc(o->N, 1);
+        sh->dl[d].cap_nd = 64;
+        sh->dl[d].nd = xcalloc(64, sizeof(ond));
+        sh->dl[d].cap_kv = 256;
+        sh->dl[d].kv = xcalloc(256, sizeof(okvu));
+    }
+    sh->tmp_stale = xcalloc(o->N, sizeof(int32_t));
+    sh->tmp_from = xcalloc(o->N, sizeof(uint32_t));
+    sh->tmp_keys = xcalloc(o->K, sizeof(int32_t));
+}
+
+static void shadow_fold(orc *o, orc *sh) {
+    o->st.exchanges += sh->st.exchanges;
+    o->st.node_deltas += sh->st.node_deltas;
+    o->st.kvs_sent += sh->st.kvs_sent;
+    o->st.delta_bytes += sh->st.delta_bytes;
+    o->st.hb_reports += sh->st.hb_reports;
+    o->st.truncated += sh->st.truncated;
+    for (int d = 0; d < 2; d++) {
+        free(sh->dg[d].has); free(sh->dg[d].hb); free(sh->dg[d].gc); free(sh->dg[d].mv); free(sh->dg[d].list);
+        free(sh->sched[d]); free(sh->dl[d].nd); free(sh->dl[d].kv);
+    }
+    free(sh->tmp_stale); free(sh->tmp_from); free(sh->tmp_keys);
+}
+
+typedef struct {
+    orc sh;
+    int kind; /* 0 phase, 1 round start, 2 liveness */
+    const int32_t *a, *b;
+    const uint8_t *up;
+    int32_t lo, hi, *q9;
+    int64_t now;
+} mt_job;
+
+static void *mt_run(void *arg) {
+    mt_job *j = arg;
+    for (int32_t i = j->lo; i < j->hi; i++) {
+        if (j->kind == 0) orc_exchange(&j->sh, j->a[i], j->b[i], j->now);
+        else if (j->up[i] && j->kind == 1) orc_begin_round(&j->sh, i, j->now);
+        else if (j->up[i]) j->q9[i] = orc_liveness(&j->sh, i, j->now);
+    }
+    return NULL;
+}
+
+static void mt_split(orc *o, int kind, const int32_t *a, const int32_t *b, const uint8_t *up, int32_t n, int64_t now,
+                     int32_t threads, int32_t *q9) {
+    if (o->ev_on) { fprintf(stderr, "oracle: threaded operations need hook events off\n"); abort(); }
+    if (threads < 1) threads = 1;
+    if (threads > n) threads = n > 0 ? n : 1;
+    mt_job *jobs = xcalloc((size_t)threads, sizeof(mt_job));
+    pthread_t *th = xcalloc((size_t)threads, sizeof(pthread_t));
+    for (int32_t t = 0; t < threads; t++) {
+        mt_job *j = &jobs[t];
+        shadow_init(&j->sh, o);
+        j->kind = kind; j->a = a; j->b = b; j->up = up; j->q9 = q9; j->now = now;
+        j->lo = (int32_t)((int64_t)n * t / threads);
+        j->hi = (int32_t)((int64_t)n * (t + 1) / threads);
+        if (t > 0 && pthread_create(&th[t], NULL, mt_run, j)) { fprintf(stderr, "oracle: pthread_create\n"); abort(); }
+    }
+    mt_run(&jobs[0]);
+    for (int32_t t = 1; t < threads; t++) pthread_join(th[t], NULL);
+    for (int32_t t = 0; t < threads; t++) shadow_fold(o, &jobs[t].sh);
+    free(jobs); free(th);
+}
+
+void orc_run_phase_mt(orc *o, const int32_t *a, const int32_t *b, int32_t n, int64_t now, int32_t threads) {
+    for (int32_t i = 0; i < n; i++) {  /* rows are allocated here, once, before the threads share the table */
+        row(o, a[i]);
+        row(o, b[i]);
+    }
+    mt_split(o, 0, a, b, NULL, n, now, threads, NULL);
+}
+
+void orc_begin_round_mt(orc *o, const uint8_t *up, int64_t now, int32_t threads) {
+    mt_split(o, 1, NULL, NULL, up, o->N, now, threads, NULL);
+}
+
+void orc_liveness_mt(orc *o, const uint8_t *up, int64_t now, int32_t threads, int32_t *q9) {
+    for (int32_t i = 0; i < o->N; i++) q9[i] = -1;
+    mt_split(o, 2, NULL, NULL, up, o->N, now, threads, q9);
 }
 
 /* ------------------------------------------------------------- readback */

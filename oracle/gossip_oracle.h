@@ -71,6 +71,14 @@ void orc_exchange(orc *o, int32_t a, int32_t b, int64_t now_us);
  * missing sampling window raised KeyError in FailureDetector.garbage_collect (Q9). */
 int32_t orc_liveness(orc *o, int32_t node, int64_t now_us);
 
+/* The same three operations over a whole phase / all up rows on `threads` host threads (checker speed for
+ * the long whole-array tests only).  A phase's exchanges touch disjoint rows and a round start or liveness
+ * sweep one row each, so the rows are split over the threads, each with scratch of its own; the result is
+ * the sequential one.  Hook events must be off.  q9[node] = orc_liveness's return for each up node (-1 else). */
+void orc_run_phase_mt(orc *o, const int32_t *a, const int32_t *b, int32_t n, int64_t now_us, int32_t threads);
+void orc_begin_round_mt(orc *o, const uint8_t *up, int64_t now_us, int32_t threads);
+void orc_liveness_mt(orc *o, const uint8_t *up, int64_t now_us, int32_t threads, int32_t *q9);
+
 /* ------------------------------------------------------------- readback */
 int32_t orc_node_count(const orc *o, int32_t obs);
 void    orc_node_order(const orc *o, int32_t obs, int32_t *out);

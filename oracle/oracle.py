@@ -66,6 +66,9 @@ def lib():
             "orc_begin_round": (None, [P, i32, i64]),
             "orc_exchange": (None, [P, i32, i32, i64]),
             "orc_liveness": (i32, [P, i32, i64]),
+            "orc_run_phase_mt": (None, [P, P, P, i32, i64, i32]),
+            "orc_begin_round_mt": (None, [P, P, i64, i32]),
+            "orc_liveness_mt": (None, [P, P, i64, i32, P]),
             "orc_node_count": (i32, [P, i32]),
             "orc_node_order": (None, [P, i32, pi32]),
             "orc_view": (None, [P, i32, i32, pu32]),
@@ -117,7 +120,10 @@ def us(seconds: float) -> int:
 class OracleSim:
     """The C oracle as a scenario backend (``aiocluster_amd.scenario.replay``)."""
 
-    def __init__(self, node_ids, keys, cfg: dict, init: str, initial_values, nid_sizes=None):
+    def __init__(self, node_ids, keys, cfg: dict, init: str, initial_values, nid_sizes=None, threads: int = 1):
+        """``threads`` > 1: phases, round starts and liveness sweeps split their rows over that many host
+        threads (orc_*_mt: the sequential result, checker speed for the long whole-array tests; no hook
+        events)."""
         from aiocluster_amd.pbsize import nodeid_size
 
         self.L = lib()
@@ -139,6 +145,8 @@ class OracleSim:
         self.value_ids = {"": 0}
         self.last_tick = 0
         self.q9_events = []
+        self.threads = int(threads)
+        self.events_on = False
         for j in range(self.n):
             self.L.orc_boot(self.h, j)
         if initial_values:
@@ -171,12 +179,24 @@ class OracleSim:
     def write(self, t: int, j: int, k: int, op: int, value: str):
         self.L.orc_write(self.h, j, k, op, self.intern(value), len(value.encode()), t * TICK_US)
 
+    def _mt(self) -> bool:
+        return self.threads > 1 and not self.events_on
+
     def begin_round(self, t: int, up):
+        if self._mt():
+            u = np.ascontiguousarray(np.asarray(up, dtype=np.uint8))
+            self.L.orc_begin_round_mt(self.h, u.ctypes.data_as(C.c_void_p), t * TICK_US, self.threads)
+            return
         for o in range(self.n):
             if up[o]:
                 self.L.orc_begin_round(self.h, o, t * TICK_US)
 
     def run_phase(self, t: int, pairs):
+        if self._mt():
+            p = np.ascontiguousarray(np.asarray(list(pairs), dtype=np.int32).reshape(-1, 2).T)
+            self.L.orc_run_phase_mt(self.h, p[0].ctypes.data_as(C.c_void_p), p[1].ctypes.data_as(C.c_void_p),
+                                    p.shape[1], t * TICK_US, self.threads)
+            return
         for a, b in pairs:
             self.L.orc_exchange(self.h, int(a), int(b), t * TICK_US)
 
@@ -185,6 +205,14 @@ class OracleSim:
 
     def liveness(self, t: int, up, r: int = -1):
         self.last_tick = t
+        if self._mt():
+            u = np.ascontiguousarray(np.asarray(up, dtype=np.uint8))
+            q9 = np.empty(self.n, np.int32)
+            self.L.orc_liveness_mt(self.h, u.ctypes.data_as(C.c_void_p), t * TICK_US, self.threads,
+                                   q9.ctypes.data_as(C.c_void_p))
+            for o in np.flatnonzero(q9 >= 0):
+                self.q9_events.append([r, int(o), int(q9[o])])
+            return
         for o in range(self.n):
             if up[o]:
                 q = self.L.orc_liveness(self.h, o, t * TICK_US)
@@ -192,6 +220,7 @@ class OracleSim:
                     self.q9_events.append([r, o, q])
 
     def enable_events(self):
+        self.events_on = True
         self.L.orc_enable_events(self.h, 1)
 
     def drain_events(self) -> np.ndarray:
@@ -258,24 +287,29 @@ class OracleSim:
     def state(self) -> list[dict]:
         return [self.observer_state(o) for o in range(self.n)]
 
+    _EXPORT = (("pos", np.int32, 0), ("hb", np.uint32, 0), ("mv", np.uint32, 0), ("gc", np.uint32, 0),
+               ("kv_version", np.uint32, 1), ("kv_status", np.int32, 1), ("kv_value_id", np.uint32, 1),
+               ("kv_ts", np.int64, 1), ("fd_last", np.int64, 0), ("fd_len", np.int32, 0), ("fd_sum", np.float64, 0),
+               ("live", np.int32, 0), ("tod", np.int64, 0))
+
     def export(self) -> dict:
-        rows = [self.export_row(o) for o in range(self.n)]
-        return {k: np.stack([r[k] for r in rows]) for k in rows[0]}
+        return self.export_rows(range(self.n))
+
+    def export_rows(self, rows) -> dict:
+        """Numpy arrays of the observer rows ``rows`` (see ``orc_export_row``), written in place; times in ticks."""
+        rows = list(rows)
+        R, N, K = len(rows), self.n, self.k
+        a = {name: np.empty((R, N, K) if kv else (R, N), dt) for name, dt, kv in self._EXPORT}
+        stride = {name: a[name].strides[0] for name, _, _ in self._EXPORT}
+        base = {name: a[name].ctypes.data for name, _, _ in self._EXPORT}
+        names = [name for name, _, _ in self._EXPORT]
+        for i, o in enumerate(rows):
+            self.L.orc_export_row(self.h, o, *[C.c_void_p(base[nm] + i * stride[nm]) for nm in names])
+        for n in ("kv_ts", "fd_last", "tod"):
+            x = a[n]
+            np.floor_divide(x, TICK_US, out=x, where=x >= 0)
+        return a
 
     def export_row(self, o: int) -> dict:
         """Numpy view of observer ``o`` (see ``orc_export_row``); times in ticks."""
-        N, K = self.n, self.k
-        a = {
-            "pos": np.empty(N, np.int32), "hb": np.empty(N, np.uint32), "mv": np.empty(N, np.uint32),
-            "gc": np.empty(N, np.uint32), "kv_version": np.empty((N, K), np.uint32),
-            "kv_status": np.empty((N, K), np.int32), "kv_value_id": np.empty((N, K), np.uint32),
-            "kv_ts": np.empty((N, K), np.int64), "fd_last": np.empty(N, np.int64), "fd_len": np.empty(N, np.int32),
-            "fd_sum": np.empty(N, np.float64), "live": np.empty(N, np.int32), "tod": np.empty(N, np.int64),
-        }
-        order = ["pos", "hb", "mv", "gc", "kv_version", "kv_status", "kv_value_id", "kv_ts", "fd_last", "fd_len",
-                 "fd_sum", "live", "tod"]
-        self.L.orc_export_row(self.h, o, *[a[n].ctypes.data_as(C.c_void_p) for n in order])
-        for n in ("kv_ts", "fd_last", "tod"):
-            m = a[n] >= 0
-            a[n][m] //= TICK_US
-        return a
+        return {k: v[0] for k, v in self.export_rows([o]).items()}

@@ -1,0 +1,102 @@
+"""Whole-array, long-run parity of the headline layout under the reference's own peer selection (VERDICT r4
+item 2).  GPU only.
+
+The 8-bit views (GS_HB8 + GS_MV8 with escape slots) are exact only while the lag sweeps keep every
+view within reach of its owner; under ``select_nodes_for_gossip`` (aiocluster/server.py:441-495, 656-717) the 8
+seeds answer in nearly every phase while the live sets are empty, so their columns fall behind, escape to 16-bit
+slots and come back.  Here every round of a long run is scheduled by the device's ``gs_select_peers`` +
+``gs_schedule_phases``; the C oracle (threaded over rows: ``orc_run_phase_mt``) replays the same phases, writes,
+round starts and liveness sweeps, and the WHOLE state -- every observer row, every owner column, every key,
+window and membership bit -- is compared every 10 rounds and at the end (heartbeats: state.py:280-287).
+"""
+
+import os
+
+import numpy as np
+import pytest
+from helpers import compare_exports, make_backend
+from oracle import OracleSim
+
+from aiocluster_amd._lib import GsError
+from aiocluster_amd.peers import PeerSelector
+from aiocluster_amd.scenario import make_scenario
+from aiocluster_amd.sim import GossipSim
+from aiocluster_amd.workload import WorkloadSpec, liveness_tick, phase_tick, round_tick
+
+pytestmark = pytest.mark.gpu
+
+
+def _scenario(n, k, rounds, seed):
+    spec = WorkloadSpec(n=n, k=k, fanout=3, seed=seed, init="warm", write_frac=0.05, down_frac=0.05, down_rounds=3)
+    return make_scenario(f"long{n}", spec, rounds)
+
+
+def _round(gpu, orc, sel, scen, r):
+    """Round r: the scenario's writes and up mask, the device's peer selection; the oracle replays the same
+    phases.  Returns the round's phase count."""
+    rd = scen["rounds"][r]
+    t = round_tick(r)
+    up = np.asarray(rd["up"], dtype=np.uint8)
+    for j, k, op, v in rd["writes"]:
+        gpu.write(t, j, k, op, v)
+        if orc is not None:
+            orc.write(t, j, k, op, v)
+    up_dev = gpu._dev(up, gpu.torch.uint8)
+    gpu.begin_round(t, up_dev)
+    if orc is not None:
+        orc.begin_round(t, up)
+    sel.select(up_dev, r)  # live / dead sets of the previous round's liveness (server.py:448-469)
+    phases, _, left = sel.schedule(up_dev, r)
+    assert left == 0, f"round {r}: {left} selected exchanges unscheduled"
+    sets = sel.scheduled_pairs(phases) if orc is not None else None
+    for p, (a, b, _) in enumerate(phases):
+        gpu.run_phase_arrays(phase_tick(r, p), a, b)
+        if orc is not None:
+            orc.run_phase(phase_tick(r, p), sorted(sets[p]))
+    gpu.update_node_liveness(liveness_tick(r, len(phases)), up_dev)
+    if orc is not None:
+        orc.liveness(liveness_tick(r, len(phases)), up, r)
+    return len(phases)
+
+
+def test_hb8mv8_160_selected_rounds_at_2048_whole_array_matches_oracle():
+    n, k, rounds, every = 2048, 16, 160, 10
+    scen = _scenario(n, k, rounds, seed=7)
+    gpu = make_backend(GossipSim, scen, tombstones=False, fd_ring=False, hb8=True, mv8=True)
+    orc = make_backend(OracleSim, scen, threads=min(16, os.cpu_count() or 1))
+    sel = PeerSelector(gpu, fanout=3, seeds=list(range(0, n, n // 8)), seed=7)
+    phases, compared, escaped_max = [], 0, 0
+    for r in range(rounds):
+        phases.append(_round(gpu, orc, sel, scen, r))
+        esc = int((gpu.region("ESC_SLOT", gpu.torch.int32, (gpu.np_,)) != -1).sum().item())
+        escaped_max = max(escaped_max, esc)
+        if (r + 1) % every == 0 or r == rounds - 1:
+            diff = compare_exports(gpu.export(), orc.export())
+            assert diff is None, f"round {r}: device vs oracle: {diff}"
+            compared += 1
+    gpu.check_heartbeat_lag()
+    c = gpu.check()  # raises on any err_* (err_hb_lag: a sweep found no free escape slot)
+    print(f"phases/round {min(phases)}-{max(phases)}, escapes {c['hb_escapes']}, releases {c['hb_releases']}, "
+          f"max escaped columns {escaped_max}, lag sweeps {c['lag_sweeps']}, whole-array compares {compared}")
+    assert c["hb_escapes"] > 0 and c["hb_releases"] > 0, c
+    assert c["exchanges"] == orc.stats()["exchanges"]
+    assert compared == rounds // every
+    gpu.close()
+    orc.close()
+
+
+def test_hb8mv8_without_free_escape_slots_raises_err_hb_lag():
+    """The same selected rounds with one escape slot: the hub columns outnumber it, so a sweep finds a view
+    lagging >= 2^7 with no slot free and counts err_hb_lag -- the run is reported inexact, never silently wrong."""
+    n, k, rounds = 2048, 16, 40
+    scen = _scenario(n, k, rounds, seed=7)
+    gpu = make_backend(GossipSim, scen, tombstones=False, fd_ring=False, hb8=True, mv8=True, esc_cols=1)
+    sel = PeerSelector(gpu, fanout=3, seeds=list(range(0, n, n // 8)), seed=7)
+    for r in range(rounds):
+        _round(gpu, None, sel, scen, r)
+        if gpu.counters()["err_hb_lag"]:
+            break
+    gpu.check_heartbeat_lag()
+    with pytest.raises(GsError, match="err_hb_lag"):
+        gpu.check()
+    gpu.close()

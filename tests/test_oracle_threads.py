@@ -40,3 +40,26 @@ def test_oracle_handles_are_independent_across_threads():
     assert st["exchanges"] > 1000 and st["truncated"] > 0, st
     for b in (alone, *pair):
         b.close()
+
+
+def test_threaded_phases_equal_sequential():
+    """orc_run_phase_mt / orc_begin_round_mt / orc_liveness_mt (rows split over host threads, each with
+    scratch of its own: the long whole-array GPU tests' checker) end every round bit-identical to the
+    sequential oracle, statistics and Q9 events included."""
+    spec = WorkloadSpec(n=80, k=6, fanout=3, seed=21, init="cold", write_frac=0.2, delete_frac=0.1,
+                        down_frac=0.15, down_rounds=3)
+    scen = make_scenario("mt80", spec, 14, {"mtu": 600, "window": 5, "tombstone_grace_s": 2,
+                                             "initial_interval_s": 1.0, "phi_threshold": 2.0, "dead_grace_s": 4})
+    seq = make_backend(OracleSim, scen)
+    par = make_backend(OracleSim, scen, threads=5)
+    from aiocluster_amd.scenario import replay_round
+
+    for r in range(len(scen["rounds"])):
+        replay_round(seq, scen, r)
+        replay_round(par, scen, r)
+        assert compare_exports(par.export(), seq.export()) is None, r
+    assert par.stats() == seq.stats()
+    assert par.q9_events == seq.q9_events
+    assert seq.stats()["truncated"] > 0
+    for b in (seq, par):
+        b.close()
