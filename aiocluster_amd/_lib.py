@@ -75,6 +75,7 @@ COUNTER_FIELDS = [
     "candidates", "live_pairs", "tomb_gc", "err_fd_overflow", "err_hist_full", "err_bad_index", "err_conflict",
     "err_fd_gc", "err_insert", "fd_gc", "q9", "pack_bytes", "err_holes", "err_hb_lag", "plane_flushes",
     "fd_saturated", "lite_slots", "lag_sweeps", "lite_bytes", "live_bytes", "hb_escapes", "hb_releases",
+    "pack_groups_max", "pack_steps_max",  # maxima (gs_read_counters takes the largest; sum_counters too)
 ]
 
 # Every symbol include/gossip_sim.h declares (checked by tests/test_abi.py).
@@ -84,11 +85,11 @@ EXPORTS = [
     "gs_read_counters", "gs_reset_counters", "gs_sync", "gs_shard_columns", "gs_phase_count", "gs_phase_pack", "gs_materialize_held", "gs_fd_census",
     "gs_select_peers", "gs_schedule_phases", "gs_set_events", "gs_emit_scratch_bytes", "gs_emit_digest", "gs_emit_delta",
     "gs_check_heartbeat_lag", "gs_stream_copy", "gs_stream_read", "gs_stream_write", "gs_set_timing", "gs_kernel_times",
-    "gs_phase_overflow", "gs_phase_chain", "gs_comm_id", "gs_comm_init", "gs_run_phase_group", "gs_read_rows",
+    "gs_phase_overflow", "gs_phase_chain", "gs_phase_pending", "gs_comm_id", "gs_comm_init", "gs_run_phase_group", "gs_read_rows",
     "gs_latest_tick", "gs_flush_reports", "gs_set_ring_rows",
 ]
 
-API_VERSION = 17
+API_VERSION = 18
 MAX_PHASES = 64  # GS_MAX_PHASES
 
 
@@ -204,6 +205,7 @@ def load():
         "gs_set_timing": (C.c_int, [P, C.c_int]),
         "gs_phase_overflow": (C.c_int, [P, u32, P, P, P, P, C.POINTER(u32)]),
         "gs_phase_chain": (C.c_int, [P, P, P, u32, u32, u32, P, u32, P, P, P, P]),
+        "gs_phase_pending": (C.c_int, [P, u32, P, u32, P, C.POINTER(u64), C.POINTER(u32)]),
         "gs_comm_id": (C.c_int, [P]),
         "gs_comm_init": (C.c_int, [P, P, u32, u32]),
         "gs_run_phase_group": (C.c_int, [P, u32, P, P, u32, u32]),
@@ -231,7 +233,12 @@ def load():
         "gs_emit_delta": (C.c_int, [P, C.POINTER(GsWire), u32, u32, u32, P, u64, C.POINTER(u64), P]),
     }
     for name, (res, args) in sig.items():
-        f = getattr(L, name)
+        try:
+            f = getattr(L, name)
+        except AttributeError:
+            if not os.environ.get("GS_LIB"):
+                raise GsError(f"{path} lacks {name}: rebuild it (__graft_entry__.build())")
+            continue  # an older A/B build named by GS_LIB: that entry point is absent (calling it fails loudly)
         f.restype = res
         f.argtypes = args
     del i32

@@ -76,12 +76,12 @@ enum Ctr {
     C_EXCH = 0, C_REPORTS, C_ND, C_KVS, C_TRUNC, C_DBYTES, C_ALG, C_HBW, C_CAND, C_LIVE, C_TOMBGC,
     C_E_FDOVF, C_E_HIST, C_E_IDX, C_E_CONFLICT, C_E_FDGC, C_E_INSERT, C_FDGC, C_Q9, C_PACKB, C_E_HOLES,
     C_E_HBLAG, C_FLUSH /* host-side: plane_flushes */, C_FDSAT, C_LITE, C_SWEEPS /* host-side: lag_sweeps */,
-    C_LITEB, C_LIVEB, C_ESC, C_ESCREL,
+    C_LITEB, C_LIVEB, C_ESC, C_ESCREL, C_PGMAX, C_PSMAX,
     C_CEN0 = 32, C_NUM = C_CEN0 + 6  // gs_fd_census scratch slots (not part of gs_counters)
 };
 constexpr int CROW = 40;  // u64 slots per counter shard row (the 32 gs_counters fields, then the census scratch)
 static_assert(C_NUM <= CROW, "counter region");
-static_assert(C_ESCREL < 32, "gs_counters fields");
+static_assert(C_PSMAX < 32, "gs_counters fields");
 static_assert(sizeof(gs_counters) == 32 * 8, "gs_counters layout");
 
 struct Dev {
@@ -156,6 +156,9 @@ struct Dev {
     // last lag sweep some view of j lagged by >= HOT_HB heartbeats or HOT_MV versions (GS_R_P1FLAGS)
     uint32_t *p1flags;
     uint32_t pl16;  // report planes in the 16-column layout of k_pass1v (plane16_bit), else the ballot layout
+    // the launch after a k_pass1v phase (k_pack_slice / k_settle<1>, set per launch by the host) first sets the
+    // phase's responders' small bits (k_p1v_fix's work, round 5: one launch fewer per phase)
+    uint32_t p1fix;
     // escaped owner columns (gs_config.esc_cols, k_pass1v handles): EC slots of 16-bit views [N][EC]; esc_slot[j] =
     // the slot of column j or NONE; esc_owner[s] = the column of slot s or NONE; esc_req = the sweep's scratch
     // (columns to escape, bitmap [NP/32], then the move count and list)
@@ -253,6 +256,10 @@ __device__ inline unsigned long long wave_sum(unsigned long long x) {
 __device__ inline void shard_add(const Dev &d, int c, unsigned long long v) {
     if (v) atomicAdd(&d.ctr[(blockIdx.x % NSHARD) * CROW + c], v);
 }
+// a maximum counter (C_PGMAX, C_PSMAX): gs_read_counters takes the largest over the shards
+__device__ inline void shard_max(const Dev &d, int c, unsigned long long v) {
+    if (v) atomicMax(&d.ctr[(blockIdx.x % NSHARD) * CROW + c], v);
+}
 
 enum EvKind { EV_KEY = 0, EV_JOIN = 1, EV_LEAVE = 2 };
 __device__ inline void emit_event(const Dev &d, uint32_t o, uint32_t j, uint32_t kk, uint32_t v_old, uint32_t v_new,
@@ -284,6 +291,9 @@ struct DigestSide {
 
 struct WStats {
     uint32_t nd, kvs, trunc, cand, alg;
+    // the exact packer's walk of one slot (wave-uniform): groups of 64 candidates it passed (evaluated or skipped)
+    // and its dependent steps (a group evaluated, a batch of TAIL_B groups skipped, a bitmap window compacted)
+    uint32_t grp = 0, stp = 0;
 };
 
 __device__ inline uint32_t byte_of(const uint32_t *w, int q) { return (w[q >> 2] >> (8 * (q & 3))) & 0xFFu; }
@@ -795,8 +805,57 @@ __device__ inline bool rec_fast(uint32_t mvw) { return !(mvw & (MV_INEXACT | (MV
 // from / max_version varints and the owner's smallest kv field over all its writes (GS_R_VLOG entry 0,
 // two L2-resident tables).  A candidate whose bound exceeds the budget cannot be sent (not even
 // truncated) and is skipped without its evaluation's round trips (returning nodes scan thousands).
-__device__ __forceinline__ uint32_t min1_lb(const Dev &d, uint32_t j, uint32_t ms, uint32_t from) {
-    return msgf(msgf(d.nid_size[j]) + ufield(from) + 1u + vlen(ms) + (d.vlog[(size_t)j * d.VL] & 0xFFFFu));
+// Round 5: a candidate one write behind (ms = mr + 1, the common case) has exactly one kv in its NodeDelta, write
+// ms itself, so its min1 is exact from VLOG entry ms at the same one load (eval_light's kv1); the entry-0 bound was
+// loose enough that a returning node's tail walk evaluated most of its groups.  sched: the receiver's
+// digest may leave owners out (from = 0): the entry-0 bound with from = 0.
+__device__ __forceinline__ uint32_t min1_lb(const Dev &d, uint32_t j, uint32_t ms, uint32_t mr, bool sched) {
+    ms &= MV_MASK;  // (flags cleared: a caller may evaluate this for a non-prefix word it then ignores)
+    mr &= MV_MASK;
+    const uint32_t from = sched ? 0u : mr;
+    const uint32_t v = !sched && ms == mr + 1u ? ms : 0u;
+    return msgf(msgf(d.nid_size[j]) + ufield(from) + 1u + vlen(ms) + (d.vlog[(size_t)j * d.VL + v] & 0xFFFFu));
+}
+
+constexpr int TAIL_B = 8;  // groups of 64 the first-fit skips (list_tail_skip, dir_tail_skip) load at once
+// list_tail_skip for the bitmap source (canonical): candidates [c0, lim) of a window's compacted positions
+// (wbuf[i - pend], all past the carried ones), TAIL_B groups of both rows' max_version words and bounds at once;
+// bitmap candidates were not merged speculatively, so nothing is restored.  Returns the first group holding a
+// candidate that may still be sent, or lim.
+__device__ __forceinline__ uint32_t dir_tail_skip(const Dev &d, uint32_t s, uint32_t r, bool sched, const uint16_t *wbuf,
+                                                  uint32_t win, uint32_t pend, uint32_t lim, uint32_t c0, uint32_t R,
+                                                  WStats &st) {
+    const int lane = lane_id();
+    while (c0 < lim) {
+        uint32_t j[TAIL_B], ms[TAIL_B], mr[TAIL_B];
+        bool ok[TAIL_B];
+#pragma unroll
+        for (int u = 0; u < TAIL_B; u++) {
+            const uint32_t i = c0 + (uint32_t)(u * WAVE + lane);
+            ok[u] = i < lim;
+            j[u] = ok[u] ? win + wbuf[i - pend] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < TAIL_B; u++) {
+            ms[u] = ok[u] ? mv_word(d, pix(d, s, j[u]), j[u]) : 0u;
+            mr[u] = ok[u] ? mv_word(d, pix(d, r, j[u]), j[u]) : 0u;
+        }
+        int uf = TAIL_B;
+#pragma unroll
+        for (int u = TAIL_B - 1; u >= 0; u--) {
+            const bool fast = !((ms[u] | mr[u]) & MV_INEXACT);
+            const bool keep = ok[u] && (!fast || min1_lb(d, j[u], ms[u], mr[u], sched) <= R);
+            if (__ballot(keep) != 0ull) uf = u;
+        }
+#pragma unroll
+        for (int u = 0; u < TAIL_B; u++)
+            if (u < uf && ok[u]) st.alg += 4;
+        st.stp++;
+        st.grp += (uint32_t)uf;
+        if (uf < TAIL_B) return c0 + (uint32_t)uf * WAVE;
+        c0 += TAIL_B * WAVE;
+    }
+    return lim;
 }
 
 // Bitmap source: positions [max(p0, pmin), cnt) of the sender's dict order (p0 = 0 in the general
@@ -846,6 +905,7 @@ __device__ __forceinline__ void pack_dir(const Dev &d, uint32_t s, uint32_t r, c
         const uint32_t incl = wave_incl_scan(cl);
         const uint32_t tot = __shfl(incl, WAVE - 1, WAVE);
         const bool last = win + WIN >= cnt;
+        st.stp++;
         if (tot) {
             __builtin_amdgcn_wave_barrier();
             uint32_t wp = incl - cl;
@@ -862,8 +922,14 @@ __device__ __forceinline__ void pack_dir(const Dev &d, uint32_t s, uint32_t r, c
         const uint32_t total = pend + tot;
         const uint32_t lim = last ? total : (total & ~(uint32_t)(WAVE - 1));
         for (uint32_t c0 = 0; c0 < lim && !stop; c0 += WAVE) {
+            if (!GENM && !COUNT && tail && d.vlog && c0 >= pend) {  // first-fit continuation: skip what cannot fit
+                c0 = dir_tail_skip(d, s, r, ds.sched, wbuf, win, pend, lim, c0, d.mtu - S, st);
+                if (c0 >= lim) break;
+            }
             const uint32_t ci = c0 + lane;
             bool cand = ci < lim;
+            st.grp++;
+            st.stp++;
             Cand<KW> c;
             c.emsg = 0;
             c.min1 = 0;
@@ -878,7 +944,7 @@ __device__ __forceinline__ void pack_dir(const Dev &d, uint32_t s, uint32_t r, c
                     st.alg += 4;
                     const bool fast = !((msw | mrw) & MV_INEXACT);
                     // tail mode: skip what cannot fit (min1_lb)
-                    if (!COUNT && tail && fast && min1_lb(d, j, msw, ds.sched ? 0u : mrw) > d.mtu - S) cand = false;
+                    if (!COUNT && tail && fast && min1_lb(d, j, msw, mrw, ds.sched) > d.mtu - S) cand = false;
                     else if (lightok && fast) {
                         eval_light<KW>(d, j, msw, mrw, c, st.alg);
                         light = true;
@@ -915,6 +981,49 @@ __device__ __forceinline__ void pack_dir(const Dev &d, uint32_t s, uint32_t r, c
 }
 
 
+// First-fit continuation (tail mode) over pass 1's records: every later candidate is tested against a budget
+// R that only shrinks, so a prefix record whose min1_lb exceeds R now is never sent.  Starting at group c0,
+// TAIL_B groups of records and their bounds are loaded at once (one round trip for TAIL_B groups instead of
+// one per group: a node back from an absence walks ~150 groups of stale owners past the mtu, and that walk
+// was the exact packer's critical path); groups with no possible candidate are skipped, their
+// speculatively merged receiver words restored (specd).  Returns the first group that holds a record that
+// may still be sent (a non-prefix record is always evaluated), or n.
+__device__ __forceinline__ uint32_t list_tail_skip(const Dev &d, uint32_t r, bool sched, const uint2 *L, uint32_t n,
+                                                   uint32_t c0, uint32_t R, bool specd, WStats &st) {
+    const int lane = lane_id();
+    while (c0 < n) {
+        uint2 rr[TAIL_B];
+        bool ok[TAIL_B];
+#pragma unroll
+        for (int u = 0; u < TAIL_B; u++) {
+            const uint32_t i = c0 + (uint32_t)(u * WAVE + lane);
+            ok[u] = i < n;
+            rr[u] = ok[u] ? L[i] : make_uint2(0u, 0u);
+        }
+        uint32_t lb[TAIL_B];
+#pragma unroll
+        for (int u = 0; u < TAIL_B; u++)
+            lb[u] = ok[u] && rec_fast(rr[u].y) ? min1_lb(d, rr[u].x, rr[u].y & 0xFFFFu, rr[u].y >> 16, sched) : 0u;
+        int uf = TAIL_B;
+#pragma unroll
+        for (int u = TAIL_B - 1; u >= 0; u--)
+            if (__ballot(ok[u] && (!rec_fast(rr[u].y) || lb[u] <= R)) != 0ull) uf = u;
+        if (specd) {
+#pragma unroll
+            for (int u = 0; u < TAIL_B; u++)
+                if (u < uf && ok[u] && rec_fast(rr[u].y)) {  // not sent: undo pass 1's merge
+                    mv_put(d, pix(d, r, rr[u].x), rr[u].y >> 16);
+                    st.alg += 4;
+                }
+        }
+        st.stp++;
+        st.grp += (uint32_t)uf;
+        if (uf < TAIL_B) return c0 + (uint32_t)uf * WAVE;
+        c0 += TAIL_B * WAVE;
+    }
+    return n;
+}
+
 // List source (canonical records): the n stale owners pass 1 recorded for one row half, in column
 // order, each with both views' max_version words (GS_R_CAND), so no row is read again.  The next
 // group's records are loaded one group ahead.  Dev::spec: once the delta is complete, the remaining
@@ -936,17 +1045,36 @@ __device__ __forceinline__ void pack_list(const Dev &d, uint32_t s, uint32_t r, 
     uint2 nxt = make_uint2(0u, 0u);
     if ((uint32_t)lane < n) nxt = L[lane];
     for (uint32_t c0 = 0; c0 < n && (specd || !stop); c0 += WAVE) {
+        if (stop) {  // specd only: nothing more is sent -- restore every remaining prefix record, TAIL_B groups at once
+            for (uint32_t b0 = c0; b0 < n; b0 += TAIL_B * WAVE) {
+#pragma unroll
+                for (int u = 0; u < TAIL_B; u++) {
+                    const uint32_t i = b0 + (uint32_t)(u * WAVE + lane);
+                    const uint2 cr = i < n ? L[i] : make_uint2(0u, MV_INEXACT);
+                    if (i < n && rec_fast(cr.y)) { mv_put(d, pix(d, r, cr.x), cr.y >> 16); st.alg += 4; }
+                }
+                st.stp++;
+                st.grp += TAIL_B;
+            }
+            break;
+        }
+        if (!COUNT && tail && d.vlog) {  // first-fit continuation: skip the groups that cannot send anything
+            const uint32_t c1 = list_tail_skip(d, r, ds.sched, L, n, c0, d.mtu - S, specd, st);
+            if (c1 >= n) break;
+            if (c1 != c0) {
+                c0 = c1;
+                nxt = c0 + lane < n ? L[c0 + lane] : make_uint2(0u, 0u);
+            }
+        }
         const uint32_t ci = c0 + lane;
         bool cand = ci < n;
         const uint2 cr = nxt;
         if (ci + WAVE < n) nxt = L[ci + WAVE];
-        if (stop) {  // specd only: nothing more is sent
-            if (cand && rec_fast(cr.y)) { mv_put(d, pix(d, r, cr.x), cr.y >> 16); st.alg += 4; }
-            continue;
-        }
+        st.grp++;
+        st.stp++;
         if (!COUNT && cand && tail && d.vlog && rec_fast(cr.y)) {  // tail mode: skip what cannot fit (min1_lb)
             const uint32_t mr = cr.y >> 16;
-            if (min1_lb(d, cr.x, cr.y & 0xFFFFu, ds.sched ? 0u : mr) > d.mtu - S) {
+            if (min1_lb(d, cr.x, cr.y & 0xFFFFu, mr, ds.sched) > d.mtu - S) {
                 cand = false;
                 if (specd) { mv_put(d, pix(d, r, cr.x), mr); st.alg += 4; }  // not sent: undo the merge
             }
@@ -1498,6 +1626,28 @@ __device__ inline PackState chain_unpack(uint64_t v) {
     return PackState{(uint32_t)v, ((v >> 32) & 1ull) != 0, ((v >> 33) & 1ull) != 0};
 }
 
+// In-process slice groups (gs_run_phase_group, round 5): one launch per step runs every slice of the group,
+// blockIdx.y = slice.  Each workgroup takes its slice's Dev and scratch pointers from a GroupArgs in device
+// memory (uploaded when they change: in a steady run never); the Dev fields that change per phase come by value
+// (DevDyn).  A single handle's launch passes ga = nullptr and uses its own arguments.
+constexpr uint32_t GRP_MAX = 8;
+struct DevDyn {
+    uint32_t t_round, spec, lite, p1fix;
+};
+struct GroupArgs {
+    Dev dv[GRP_MAX];
+    SliceIO io[GRP_MAX];  // tot (count), tot_all + chain (steps)
+    uint32_t *list[GRP_MAX];
+    uint64_t *chain_all[GRP_MAX], *chainc[GRP_MAX];
+};
+__device__ __forceinline__ void group_pick(Dev &d, const GroupArgs *ga, const DevDyn &dyn) {
+    d = ga->dv[blockIdx.y];
+    d.t_round = dyn.t_round;
+    d.spec = dyn.spec;
+    d.lite = dyn.lite;
+    d.p1fix = dyn.p1fix;
+}
+
 // Split canonical phase, kernel 1 of 2 (k_pass1 -> k_pack_slice): pass 1 alone, streaming both rows with
 // no LDS at all; the stale-owner bitmaps of both directions go to GS_R_SLICE_BITS ([e][2][NP/32],
 // natural bit order) for the packer.  Without LDS the occupancy is set by registers only, and the
@@ -1876,19 +2026,90 @@ __device__ __forceinline__ void p1v_decode_records(const Dev &d, uint2 *L, uint3
     }
 }
 
-template <int AHEAD>
+// k_lite's work for one (exchange, direction) slot (also run at the head of k_settle<LITE = true>, the sliced
+// phases' fused kernels); returns the slot's flag (slot_stat[slot].w, written here too)
+template <int MODE>
+__device__ __forceinline__ uint32_t lite_slot(const Dev &d, int32_t ai, int32_t bi, uint32_t n, uint32_t t,
+                                              const SliceIO &io, size_t slot, int wid, int lane) {
+    const uint32_t rcv = wid == 0 ? (uint32_t)ai : (uint32_t)bi;
+    const bool sched = t >= d.row[rcv * 4 + 2];  // the receiver's digest may leave owners out: checked per record
+    WStats st{0, 0, 0, 0, 0};
+    uint32_t T = 0, flag = LITE_FULL;
+    if (MODE == 0) {
+        if (pack_lite<true>(d, rcv, slot, 0u, st, T, nullptr, sched, t)) {
+            flag = LITE_DONE;
+            if (lane == 0) shard_add(d, C_DBYTES, T);
+        }
+    } else if (MODE == 1) {
+        uint32_t m1 = NONE;
+        if (pack_lite<false>(d, rcv, slot, 0u, st, T, &m1, sched, t)) {
+            flag = 0u;
+            const uint32_t kv = (uint32_t)wave_sum(st.kvs);  // for step 0 (MODE 2): it applies without re-sizing
+            if (lane == 0) {
+                io.tot[slot] = tot_word(T, m1);
+                d.slot_stat[slot].y = kv;
+            }
+            st.kvs = 0u;  // counted when sent (MODE 2 or the exact packer)
+        }
+    } else {
+        unsigned long long P = 0;
+        for (uint32_t g = 0; g < d.shard; g++) P += GS_TOT_BYTES(io.tot_all[(size_t)g * n * 2 + slot]);
+        const unsigned long long own = GS_TOT_BYTES(io.tot_all[(size_t)d.shard * n * 2 + slot]);
+        // the count pass (MODE 1) sized this slot from the version log (slot_stat flag 0): apply only
+        const uint4 ss = d.slot_stat[slot];
+        if (P + own <= d.mtu && ss.w == 0u) {  // (the count pass checked a scheduled receiver's records)
+            lite_apply(d, rcv, slot, st);
+            if (lane == 0) st.kvs = ss.y;
+            T = (uint32_t)own;
+        }
+        if (P + own <= d.mtu && (ss.w == 0u || pack_lite<true>(d, rcv, slot, (uint32_t)P, st, T, nullptr, sched, t))) {
+            flag = LITE_DONE;
+            const uint32_t S = (uint32_t)P + T;  // every NodeDelta whole: pack_group's state after the last one
+            const bool stop = S >= d.mtu || d.mtu - S < d.lb_min;
+            if (lane == 0) {
+                shard_add(d, C_DBYTES, T);
+                io.chain[slot] = (uint64_t)S | ((uint64_t)stop << 33);
+            }
+        }
+    }
+    if (lane == 0) {
+        d.slot_stat[slot].w = flag;
+        if (flag == LITE_DONE) shard_add(d, C_LITE, 1);
+    }
+    const unsigned long long s_alg = wave_sum(st.alg), s_nd = wave_sum(st.nd), s_kv = wave_sum(st.kvs);
+    const unsigned long long s_cd = wave_sum(st.cand);
+    if (lane == 0) {
+        shard_add(d, C_ALG, s_alg);
+        shard_add(d, C_PACKB, s_alg);
+        shard_add(d, C_LITEB, s_alg);  // k_lite's share of pack_bytes (its own roofline entry)
+        shard_add(d, C_ND, s_nd);
+        shard_add(d, C_KVS, s_kv);
+        shard_add(d, C_CAND, s_cd);
+    }
+    return flag;
+}
+
+// LM >= 0: k_lite's slot work (lite_slot<LM>: 0 = one slice, 1 = a sliced count pass) runs in the same workgroup
+// after the stream, wave w taking direction w -- no k_lite launch (round 5; env GS_P1LITE=0: the launch of its own)
+template <int AHEAD, int LM>
 __global__ __launch_bounds__(XB, P1V_WAVES) void k_pass1v(Dev d, const int32_t *ini, const int32_t *res, uint32_t n,
-                                                          uint32_t t, uint32_t seq) {
+                                                          uint32_t t, uint32_t seq, SliceIO io, const GroupArgs *ga,
+                                                          DevDyn dyn) {
     static_assert(AHEAD == 1, "k_pass1v double-buffers one group ahead (r4g: two ahead at 5 waves per SIMD, no faster)");
     __shared__ uint32_t s_col[XB / WAVE][P1V_K];
     __shared__ uint32_t s_out[XB / WAVE][P1V_K * P1V_SLOT];
     const uint32_t e = blockIdx.x;
     if (e >= n) return;
+    if (ga) {  // a slice of an in-process group (blockIdx.y)
+        group_pick(d, ga, dyn);
+        io = ga->io[blockIdx.y];
+    }
     // wid through readfirstlane: the half bounds, list and plane pointers derived from it stay scalar
     const int tid = threadIdx.x, lane = tid & (WAVE - 1), wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int32_t ai = ini[e], bi = res[e];
     if (ai < 0 || bi < 0 || (uint32_t)ai >= d.N || (uint32_t)bi >= d.N || ai == bi) {
         if (tid == 0) shard_add(d, C_E_IDX, 1);
+        if (LM >= 0 && lane == 0) d.slot_stat[(size_t)e * 2 + wid].w = LITE_DONE;  // (as k_lite: counted already)
         return;
     }
     const uint32_t a = (uint32_t)ai, b = (uint32_t)bi;
@@ -2204,14 +2425,24 @@ __global__ __launch_bounds__(XB, P1V_WAVES) void k_pass1v(Dev d, const int32_t *
         shard_add(d, C_HBW, s_hbw);
         if (wid == 0 && d.shard == 0) shard_add(d, C_EXCH, 1);  // slices: every slice runs every exchange
     }
+    if constexpr (LM >= 0) {
+        // both halves' records (and counts) are final after the barrier (one CU: workgroup-scope visibility);
+        // wave w sizes / completes direction w (0: the SynAck delta b -> a, 1: the Ack delta a -> b) as k_lite
+        // would, while the other workgroups on the CU stream their rows
+        __syncthreads();
+        lite_slot<LM>(d, ai, bi, n, t, io, (size_t)e * 2 + wid, wid, lane);
+    }
 }
 // After a k_pass1v phase: the responders' small bits (their own heartbeat rose by one in the phase; pass 1
 // read the bits as they were before it, consistently for every exchange of the phase)
+__device__ __forceinline__ void p1v_fix_one(const Dev &d, const int32_t *res, uint32_t e) {
+    const uint32_t jb = (uint32_t)res[e] - d.col_lo;
+    if ((uint32_t)res[e] < d.N && jb < d.ncol) set_small(d, jb, d.self_hb[jb]);
+}
 __global__ __launch_bounds__(LB) void k_p1v_fix(Dev d, const int32_t *res, uint32_t n) {
     const uint32_t e = blockIdx.x * LB + threadIdx.x;
     if (e >= n) return;
-    const uint32_t jb = (uint32_t)res[e] - d.col_lo;
-    if ((uint32_t)res[e] < d.N && jb < d.ncol) set_small(d, jb, d.self_hb[jb]);
+    p1v_fix_one(d, res, e);
 }
 
 // MODE 0: the whole exchange (one slice).  MODE 1: sharded count pass (pass 1, then the slice totals).
@@ -2378,6 +2609,8 @@ __global__ __launch_bounds__(XB, (KW == 4 ? XB_WAVES : 1)) void k_exchange(Dev d
         shard_add(d, C_KVS, s_kv);
         shard_add(d, C_TRUNC, s_tr);
         shard_add(d, C_CAND, s_cd);
+        shard_max(d, C_PGMAX, st.grp);
+        shard_max(d, C_PSMAX, st.stp);
         if (wid == 0) shard_add(d, C_EXCH, 1);
     }
 }
@@ -2397,6 +2630,7 @@ __global__ __launch_bounds__(XB, (KW == 4 ? PK_WAVES : 1)) void k_pack_slice(Dev
     const uint32_t e = e0 + blockIdx.x;
     if (e >= n) return;
     const int tid = threadIdx.x, lane = tid & (WAVE - 1), wid = tid >> 6;
+    if (d.p1fix && tid == 0) p1v_fix_one(d, res, e);  // k_p1v_fix's work (Dev::p1fix)
     const int32_t ai = ini[e], bi = res[e];
     if (ai < 0 || bi < 0 || (uint32_t)ai >= d.N || (uint32_t)bi >= d.N || ai == bi) return;  // counted already
     const uint32_t a = (uint32_t)ai, b = (uint32_t)bi;
@@ -2442,6 +2676,8 @@ __global__ __launch_bounds__(XB, (KW == 4 ? PK_WAVES : 1)) void k_pack_slice(Dev
         shard_add(d, C_KVS, s_kv);
         shard_add(d, C_TRUNC, s_tr);
         shard_add(d, C_CAND, s_cd);
+        shard_max(d, C_PGMAX, st.grp);
+        shard_max(d, C_PSMAX, st.stp);
     }
 }
 
@@ -2453,7 +2689,11 @@ __global__ __launch_bounds__(XB, (KW == 4 ? PK_WAVES : 1)) void k_pack_slice(Dev
 // counts, then the total -- GS_OVERFLOW_LIST_LEN(n) words in all.
 constexpr uint32_t OVB = 1024;
 __global__ __launch_bounds__(OVB) void k_ov_count(const uint64_t *tot_all, uint32_t slots, uint32_t G, uint32_t mtu,
-                                                  uint32_t *blkcnt) {
+                                                  uint32_t *blkcnt, const GroupArgs *ga) {
+    if (ga) {  // a slice of an in-process group (blockIdx.y)
+        tot_all = ga->io[blockIdx.y].tot_all;
+        blkcnt = ga->list[blockIdx.y] + slots;
+    }
     const uint32_t sl = blockIdx.x * OVB + threadIdx.x;
     uint64_t sum = 0;
     if (sl < slots)
@@ -2462,9 +2702,16 @@ __global__ __launch_bounds__(OVB) void k_ov_count(const uint64_t *tot_all, uint3
     if (threadIdx.x == 0) blkcnt[blockIdx.x] = (uint32_t)c;
 }
 __global__ __launch_bounds__(OVB) void k_ov_write(const uint64_t *tot_all, uint32_t slots, uint32_t G, uint32_t mtu,
-                                                  const uint64_t *chain, uint32_t *list, uint64_t *chainc) {
+                                                  const uint64_t *chain, uint32_t *list, uint64_t *chainc,
+                                                  const GroupArgs *ga) {
     __shared__ uint32_t s_w[OVB / WAVE];
     __shared__ uint32_t s_off;
+    if (ga) {  // a slice of an in-process group (blockIdx.y)
+        tot_all = ga->io[blockIdx.y].tot_all;
+        chain = ga->io[blockIdx.y].chain;
+        list = ga->list[blockIdx.y];
+        chainc = ga->chainc[blockIdx.y];
+    }
     const uint32_t nb = gridDim.x;
     const uint32_t *blkcnt = list + slots;
     if (threadIdx.x == 0) {
@@ -2497,20 +2744,32 @@ __global__ __launch_bounds__(OVB) void k_ov_write(const uint64_t *tot_all, uint3
 // the pending counts of all G slices (entry count of each gathered chainc) summed into *out.  cnt_dev: the count
 // is read on the device (GS_CHAIN_DEVICE: gathered rows of GS_CHAIN_CAP + 1 entries); a count above the cap gives
 // ~0 (the device step did not run: the host takes over)
+// out[1] = the count (gs_phase_pending; out may be host-mapped pinned memory: the host reads it after the wait)
 __global__ __launch_bounds__(WAVE) void k_sum_pending(const uint64_t *chain_all, uint32_t G, uint32_t count,
                                                       const uint32_t *cnt_dev, uint64_t *out) {
     const uint32_t c = cnt_dev ? *cnt_dev : count;
     const size_t stride = cnt_dev ? GS_CHAIN_CAP + 1u : (size_t)count + 1u;
     unsigned long long s = 0;
-    for (uint32_t g = threadIdx.x; g < G; g += WAVE) s += chain_all[(size_t)g * stride + c];
+    if (!cnt_dev || c <= GS_CHAIN_CAP)
+        for (uint32_t g = threadIdx.x; g < G; g += WAVE) s += chain_all[(size_t)g * stride + c];
     s = wave_sum(s);
-    if (threadIdx.x == 0) *out = cnt_dev && c > GS_CHAIN_CAP ? ~0ull : s;
+    if (threadIdx.x == 0) {
+        out[0] = cnt_dev && c > GS_CHAIN_CAP ? ~0ull : s;
+        out[1] = c;
+    }
 }
 
 // chainc[count] = this slice's listed slots still pending (the count itself read from the list's tail when
 // cnt_dev is set: gs_phase_overflow's count is not known to the host without a read)
 __global__ __launch_bounds__(OVB) void k_pending(const uint32_t *list, const uint32_t *cnt_dev, uint32_t count,
-                                                 const uint64_t *chain, uint64_t *chainc) {
+                                                 const uint64_t *chain, uint64_t *chainc, const GroupArgs *ga,
+                                                 uint32_t n) {
+    if (ga) {  // a slice of an in-process group (blockIdx.y)
+        if (cnt_dev) cnt_dev = ga->list[blockIdx.y] + 2u * n + (2u * n + OVB - 1u) / OVB;
+        list = ga->list[blockIdx.y];
+        chain = ga->io[blockIdx.y].chain;
+        chainc = ga->chainc[blockIdx.y];
+    }
     const uint32_t c = cnt_dev ? *cnt_dev : count;
     uint32_t p = 0;
     for (uint32_t i = threadIdx.x; i < c; i += OVB) p += chain[list[i]] == CHAIN_PENDING ? 1u : 0u;
@@ -2551,9 +2810,20 @@ template <int KW>
 __global__ __launch_bounds__(WAVE) void k_chain_step(Dev d, const int32_t *ini, const int32_t *res, uint32_t t,
                                                      const uint32_t *list, uint32_t count, const uint64_t *chain_all,
                                                      uint64_t *chain, uint64_t *chainc, const uint64_t *tot_all,
-                                                     uint32_t n, const uint32_t *cnt_dev) {
+                                                     uint32_t n, const uint32_t *cnt_dev, const GroupArgs *ga,
+                                                     DevDyn dyn) {
     __shared__ __attribute__((aligned(16))) uint16_t s_wbuf[WIN];
     const int lane = lane_id();
+    if (ga) {  // a slice of an in-process group (blockIdx.y): its own scratch
+        group_pick(d, ga, dyn);
+        const uint32_t y = blockIdx.y;
+        if (cnt_dev) cnt_dev = ga->list[y] + 2u * n + (2u * n + OVB - 1u) / OVB;
+        list = ga->list[y];
+        chain_all = ga->chain_all[y];
+        chain = ga->io[y].chain;
+        chainc = ga->chainc[y];
+        tot_all = ga->io[y].tot_all;
+    }
     // chain_all[g][count + 1]: entry count = g's pending slots; GS_CHAIN_DEVICE (cnt_dev): the count from the
     // device, rows of GS_CHAIN_CAP + 1 entries, nothing done above the cap (every slice sees the same count)
     if (cnt_dev) {
@@ -2596,6 +2866,8 @@ __global__ __launch_bounds__(WAVE) void k_chain_step(Dev d, const int32_t *ini, 
             shard_add(d, C_KVS, s_kv);
             shard_add(d, C_TRUNC, s_tr);
             shard_add(d, C_CAND, s_cd);
+            shard_max(d, C_PGMAX, st.grp);
+            shard_max(d, C_PSMAX, st.stp);
         }
         __builtin_amdgcn_wave_barrier();
     }
@@ -2670,79 +2942,24 @@ __device__ __forceinline__ SlotSum settle_sum(const Dev &d, uint32_t snd, uint32
 //          speculative slot whose whole delta fits over every slice and is clean here is complete.
 // Sequential semantics over the slices in column (= canonical dict) order, so the result is the
 // single-slice result bit for bit.
-// k_lite's work for one (exchange, direction) slot (also run at the head of k_settle<LITE = true>, the sliced
-// phases' fused kernels); returns the slot's flag (slot_stat[slot].w, written here too)
-template <int MODE>
-__device__ __forceinline__ uint32_t lite_slot(const Dev &d, int32_t ai, int32_t bi, uint32_t n, uint32_t t,
-                                              const SliceIO &io, size_t slot, int wid, int lane) {
-    const uint32_t rcv = wid == 0 ? (uint32_t)ai : (uint32_t)bi;
-    const bool sched = t >= d.row[rcv * 4 + 2];  // the receiver's digest may leave owners out: checked per record
-    WStats st{0, 0, 0, 0, 0};
-    uint32_t T = 0, flag = LITE_FULL;
-    if (MODE == 0) {
-        if (pack_lite<true>(d, rcv, slot, 0u, st, T, nullptr, sched, t)) {
-            flag = LITE_DONE;
-            if (lane == 0) shard_add(d, C_DBYTES, T);
-        }
-    } else if (MODE == 1) {
-        uint32_t m1 = NONE;
-        if (pack_lite<false>(d, rcv, slot, 0u, st, T, &m1, sched, t)) {
-            flag = 0u;
-            const uint32_t kv = (uint32_t)wave_sum(st.kvs);  // for step 0 (MODE 2): it applies without re-sizing
-            if (lane == 0) {
-                io.tot[slot] = tot_word(T, m1);
-                d.slot_stat[slot].y = kv;
-            }
-            st.kvs = 0u;  // counted when sent (MODE 2 or the exact packer)
-        }
-    } else {
-        unsigned long long P = 0;
-        for (uint32_t g = 0; g < d.shard; g++) P += GS_TOT_BYTES(io.tot_all[(size_t)g * n * 2 + slot]);
-        const unsigned long long own = GS_TOT_BYTES(io.tot_all[(size_t)d.shard * n * 2 + slot]);
-        // the count pass (MODE 1) sized this slot from the version log (slot_stat flag 0): apply only
-        const uint4 ss = d.slot_stat[slot];
-        if (P + own <= d.mtu && ss.w == 0u) {  // (the count pass checked a scheduled receiver's records)
-            lite_apply(d, rcv, slot, st);
-            if (lane == 0) st.kvs = ss.y;
-            T = (uint32_t)own;
-        }
-        if (P + own <= d.mtu && (ss.w == 0u || pack_lite<true>(d, rcv, slot, (uint32_t)P, st, T, nullptr, sched, t))) {
-            flag = LITE_DONE;
-            const uint32_t S = (uint32_t)P + T;  // every NodeDelta whole: pack_group's state after the last one
-            const bool stop = S >= d.mtu || d.mtu - S < d.lb_min;
-            if (lane == 0) {
-                shard_add(d, C_DBYTES, T);
-                io.chain[slot] = (uint64_t)S | ((uint64_t)stop << 33);
-            }
-        }
-    }
-    if (lane == 0) {
-        d.slot_stat[slot].w = flag;
-        if (flag == LITE_DONE) shard_add(d, C_LITE, 1);
-    }
-    const unsigned long long s_alg = wave_sum(st.alg), s_nd = wave_sum(st.nd), s_kv = wave_sum(st.kvs);
-    const unsigned long long s_cd = wave_sum(st.cand);
-    if (lane == 0) {
-        shard_add(d, C_ALG, s_alg);
-        shard_add(d, C_PACKB, s_alg);
-        shard_add(d, C_LITEB, s_alg);  // k_lite's share of pack_bytes (its own roofline entry)
-        shard_add(d, C_ND, s_nd);
-        shard_add(d, C_KVS, s_kv);
-        shard_add(d, C_CAND, s_cd);
-    }
-    return flag;
-}
-
 // LITE (sliced phases with Dev::lite, MODE 1 and 2): k_lite's slot work first, in the same wave, and the exact
 // count / pack only for the slots it leaves (one launch per step instead of two: a slice's kernels are short,
 // and their fixed cost per launch is what a sliced phase pays over one handle)
 template <int KW, int MODE, bool LITE = false>
 __global__ __launch_bounds__(XB, (KW == 4 ? PK_WAVES : 1)) void k_settle(Dev d, const int32_t *ini, const int32_t *res,
-                                                                        uint32_t n, uint32_t t, SliceIO io) {
+                                                                        uint32_t n, uint32_t t, SliceIO io,
+                                                                        const GroupArgs *ga, DevDyn dyn) {
     __shared__ __attribute__((aligned(16))) uint16_t s_wbuf[2 * WIN];
     const uint32_t e = blockIdx.x;
     if (e >= n) return;
+    if (ga) {  // a slice of an in-process group (blockIdx.y); the step comes by value
+        group_pick(d, ga, dyn);
+        const uint32_t step = io.step;
+        io = ga->io[blockIdx.y];
+        io.step = step;
+    }
     const int tid = threadIdx.x, lane = tid & (WAVE - 1), wid = tid >> 6;
+    if (d.p1fix && tid == 0) p1v_fix_one(d, res, e);  // k_p1v_fix's work (Dev::p1fix)
     const int32_t ai = ini[e], bi = res[e];
     const size_t slot = (size_t)e * 2 + wid;
     if (ai < 0 || bi < 0 || (uint32_t)ai >= d.N || (uint32_t)bi >= d.N || ai == bi) {  // counted already
@@ -2843,6 +3060,8 @@ __global__ __launch_bounds__(XB, (KW == 4 ? PK_WAVES : 1)) void k_settle(Dev d, 
         shard_add(d, C_KVS, st.kvs);
         shard_add(d, C_TRUNC, st.trunc);
         shard_add(d, C_CAND, st.cand);
+        shard_max(d, C_PGMAX, st.grp);
+        shard_max(d, C_PSMAX, st.stp);
     }
 }
 
@@ -2949,7 +3168,11 @@ template <int RING>
 #define LIVE_F32 1  // the phi decision's first test in binary32 (A/B: 0 = binary64 with a 2^-30 margin)
 #endif
 #ifndef LIVE_WAVES
-#define LIVE_WAVES 6  // waves per SIMD k_liveness is compiled for (<= 80 VGPRs: two chunks in flight)
+#define LIVE_WAVES 4  // waves per SIMD k_liveness is compiled for: 4 = 127 VGPRs, no spill with the fast path (r5e:
+                      // 12.02 ms vs 24.3 at 6 waves with 78 spills, 12.37 for round 4's code at 6 waves)
+#endif
+#ifndef LIVE_FAST
+#define LIVE_FAST 1  // round 5: the branch-free per-chunk fast path of k_liveness (0: the general path only, A/B)
 #endif
 #ifndef LIVE_NT
 #define LIVE_NT 1  // non-temporal loads / stores of the windows and state bytes (streamed once per round; r4c: 11.86 vs 12.21 ms)
@@ -3042,138 +3265,242 @@ __global__ __launch_bounds__(LB, LIVE_WAVES) void k_liveness(Dev d, const uint8_
             if (c0 < d.ncol) {
                 const size_t p = pix(d, o, c0);
                 // this thread's four columns: bit ph of q[i] = a report in phase ph
-                uint32_t q[4] = {0u, 0u, 0u, 0u};
-                if (d.pl16) {  // k_pass1v's layout: column 16 g + 4 q + i at bit 4 i + q of u16 g
-                    const uint32_t ui = (c0 & 255u) >> 4, qs = (c0 >> 2) & 3u;
-                    for (uint32_t m = vm; m; m &= m - 1u) {
-                        const uint32_t ph = (uint32_t)__builtin_ctz(m);
-                        const uint32_t u = (uint32_t)reinterpret_cast<const uint16_t *>(s_pl[wv][ph])[ui] >> qs;
-        #pragma unroll
-                        for (int i = 0; i < 4; i++) q[i] |= ((u >> (4 * i)) & 1u) << ph;
+                auto build_q = [&](uint32_t (&q)[4]) __attribute__((always_inline)) {
+                    q[0] = q[1] = q[2] = q[3] = 0u;
+                    if (d.pl16) {  // k_pass1v's layout: column 16 g + 4 q + i at bit 4 i + q of u16 g
+                        const uint32_t ui = (c0 & 255u) >> 4, qs = (c0 >> 2) & 3u;
+                        for (uint32_t m = vm; m; m &= m - 1u) {
+                            const uint32_t ph = (uint32_t)__builtin_ctz(m);
+                            const uint32_t u = (uint32_t)reinterpret_cast<const uint16_t *>(s_pl[wv][ph])[ui] >> qs;
+#pragma unroll
+                            for (int i = 0; i < 4; i++) q[i] |= ((u >> (4 * i)) & 1u) << ph;
+                        }
+                    } else {
+                        const uint32_t lb = plane_bit(c0);
+                        for (uint32_t m = vm; m; m &= m - 1u) {
+                            const uint32_t ph = (uint32_t)__builtin_ctz(m);
+#pragma unroll
+                            for (int i = 0; i < 4; i++) q[i] |= (uint32_t)((s_pl[wv][ph][i] >> lb) & 1ull) << ph;
+                        }
+                    }
+                };
+                uint32_t q[4];
+                build_q(q);
+                // Fast path (round 5): compact windows, no hook events, no row whose scheduled bound is recomputed,
+                // reports that telescope (max_interval >= NPL - 1 ticks): the four pairs branch-free -- selects, no
+                // per-pair exec-mask branches (the scalar unit's issue, shared by the CU's waves, was a third of the
+                // sweep's instruction stream) -- and committed unless some lane meets a rare case (a compact window
+                // that would fill up, a phi decision within the binary32 margin): then the whole chunk takes the
+                // general path below, from the same loaded values.
+                // the general path (every layout and case), on the chunk's values sc4, l4, s4 and report masks q
+                auto general = [&](const uint4 sc4, const uint2 l4, const uint32_t s4, const uint32_t (&q)[4])
+                                   __attribute__((always_inline)) {
+                    uint32_t sc[4] = {sc4.x, sc4.y, sc4.z, sc4.w};
+                    uint32_t lt[4] = {l4.x & 0xFFFFu, l4.x >> 16, l4.y & 0xFFFFu, l4.y >> 16};
+                    bool dw = false;
+                    uint32_t td[4] = {NONE, NONE, NONE, NONE};
+                    if (exact && (s4 & 0x02020202u)) { ld4(d.tod + p, td); alg += 16; }
+                    uint32_t s4n = s4;
+            #pragma unroll
+                    for (int i = 0; i < 4; i++) {
+                        uint32_t st = (s4 >> (8 * i)) & 0xFFu;
+                        Fd f = fd_get(d, st, lt[i], sc[i], t);  // t is at or after every report tick of this round
+                        uint32_t m = q[i];  // only if vm != 0: then the window was loaded
+                        if (m) {
+                            // report_heartbeat at ticks t_round + 1 + p for the phases p of m (failure_detector.py:32-38):
+                            // intervals between reports of one round are < NPL ticks, so with max_interval >= NPL - 1 all
+                            // but the first are appended and they telescope: (k - 1) intervals summing to p_last - p_first,
+                            // plus the first one if it is <= max_interval; a compact window that would fill up, and the
+                            // rings (their intervals one by one), replay report by report
+                            bool loop = (RING && rrow) || d.max_iv < NPL - 1u;
+                            if (!loop) {
+                                const uint32_t p1 = (uint32_t)__builtin_ctz(m), pk = 31u - (uint32_t)__builtin_clz(m);
+                                uint32_t app = (uint32_t)__popc(m) - 1u, add = pk - p1;
+                                if (f.last != NONE) {
+                                    const uint32_t iv = d.t_round + 1u + p1 - f.last;
+                                    if (iv <= d.max_iv) { app++; add += iv; }
+                                }
+                                if (f.cnt + app <= d.W) {
+                                    f.cnt += app;
+                                    f.sum += add;
+                                    f.last = d.t_round + 1u + pk;
+                                } else {
+                                    loop = true;
+                                }
+                            }
+                            if (loop) {
+                                while (m) {
+                                    const uint32_t bb = (uint32_t)__builtin_ctz(m);
+                                    m &= m - 1u;
+                                    f = fd_report_val(d, RING && rrow ? rrow + (size_t)(c0 + i) * d.W : nullptr, d.t_round + 1u + bb,
+                                                      f, alg, ovf);
+                                }
+                            }
+                            dw = true;
+                        }
+                        const uint32_t j = c0 + i;
+                        if (upo && j < d.ncol && d.col_lo + j != o && !(genm && ps[i] == NONE)) {
+                            live++;
+                            const bool has = f.last != NONE;
+                            const uint32_t len = RING && rrow ? (f.cnt < d.W ? f.cnt : d.W) : f.cnt;
+                            bool alive = false;
+                            if (has && len) {
+                                // phi <= threshold (failure_detector.py:43-53, 97-98) decided without the two binary64
+                                // divisions when it is clear by a margin: phi ~ elapsed (len + 5) / (sum + 5 prior) in
+                                // ticks.  First in binary32 (full rate: elapsed < 2^24 ticks, len + 5 and sum < 2^24 are
+                                // exact, the three roundings and the two constants' add < 2^-21 relative) with a 2^-20
+                                // margin, then in binary64 with 2^-30 (far above its rounding), the exact expression
+                                // otherwise
+            #if LIVE_F32
+                                const float lf = (float)(t - f.last) * (float)(len + 5u);
+                                const float rf = d.phi_thr_f * ((float)f.sum + d.prior5t_f);
+                                if (lf < rf * (1.0f - 0x1p-20f)) {
+                                    alive = true;
+                                } else if (!(lf > rf * (1.0f + 0x1p-20f))) {  // too close: the exact expression
+            #else
+                                const double lhs = (double)(t - f.last) * (double)(len + 5u);  // exact: < 2^43
+                                const double rhs = d.phi_thr * ((double)f.sum + d.prior5t);
+                                if (lhs < rhs * (1.0 - 0x1p-30)) {
+                                    alive = true;
+                                } else if (!(lhs > rhs * (1.0 + 0x1p-30))) {
+            #endif
+                                    const double mean = ((double)f.sum * TICK_S + d.prior5) / ((double)len + 5.0);
+                                    alive = ((double)(t - f.last) * TICK_S) / mean <= d.phi_thr;
+                                }
+                            }
+                            const uint32_t mb = st & FD_MEMB;
+                            // node join / leave: the live set against the previous call's (server.py:611-616)
+                            if (d.ev && alive != (mb == FD_LIVE))
+                                emit_event(d, o, d.col_lo + j, (alive ? EV_JOIN : EV_LEAVE) << 8, 0u, 0u, t, 0u);
+                            uint32_t sn = FD_LIVE;
+                            if (!alive) {
+                                sn = FD_DEAD;
+                                uint32_t tod = td[i];  // loaded for the dead pairs of a row being recomputed
+                                if (mb != FD_DEAD) { tod = t; d.tod[p + i] = t; alg += 4; }  // time_of_death recorded once
+                                if (has && (f.sum | f.cnt)) { f.sum = f.cnt = 0u; dw = true; }  // reset
+                                if (mb != FD_DEAD || exact) {
+                                    const uint32_t sat = tod + d.sched_delay;
+                                    if (sat < minS) minS = sat;
+                                }
+                                if (exact && (uint64_t)t >= (uint64_t)tod + d.dead_grace) gcdue++;
+                            }
+                            st = (st & ~(uint32_t)FD_MEMB) | sn;
+                        }
+                        // a window whose last report is >= FD_OLD_AGE old keeps only that fact (fd_get)
+                        if ((st & (FD_WIN | FD_OLD)) == FD_WIN && t - f.last >= FD_OLD_AGE) st |= FD_OLD;
+                        if (q[i]) st = fd_st(st, f);
+                        sc[i] = fd_sc(d, f);
+                        lt[i] = f.last & 0xFFFFu;
+                        s4n = (s4n & ~(0xFFu << (8 * i))) | (st << (8 * i));
+                    }
+                    if (dw) {
+                        if (LIVE_NT) {
+                            __builtin_nontemporal_store(v4u_t{sc[0], sc[1], sc[2], sc[3]}, reinterpret_cast<v4u_t *>(d.fd + p));
+                            __builtin_nontemporal_store(v2u_t{lt[0] | (lt[1] << 16), lt[2] | (lt[3] << 16)},
+                                                        reinterpret_cast<v2u_t *>(d.fd_last + p));
+                        } else {
+                            *reinterpret_cast<uint4 *>(d.fd + p) = make_uint4(sc[0], sc[1], sc[2], sc[3]);
+                            *reinterpret_cast<uint2 *>(d.fd_last + p) = make_uint2(lt[0] | (lt[1] << 16), lt[2] | (lt[3] << 16));
+                        }
+                        alg += 24;
+                    }
+                    if (s4n != s4) {
+                        if (LIVE_NT) __builtin_nontemporal_store(s4n, reinterpret_cast<uint32_t *>(d.fd_state + p));
+                        else *reinterpret_cast<uint32_t *>(d.fd_state + p) = s4n;
+                        alg += 4;
+                    }
+                    if (upo || vm) alg += 28;  // the four windows (sum | cnt, last tick) and state bytes read
+                };
+                bool done = false;  // (fast path committed)
+                uint4 gsc;          // the general path's inputs
+                uint2 gl;
+                uint32_t gs;
+                if (LIVE_FAST && RING == 0 && !exact && !genm && !d.ev && d.max_iv >= NPL - 1u) {
+                    const uint32_t sci[4] = {sc4.x, sc4.y, sc4.z, sc4.w};
+                    const uint32_t lti[4] = {l4.x & 0xFFFFu, l4.x >> 16, l4.y & 0xFFFFu, l4.y >> 16};
+                    uint32_t fsc[4], flt[4], fs4 = s4, flv = 0u, fmS = NONE;
+                    bool fdw = false, rare = false, nd[4];
+#pragma unroll
+                    for (int i = 0; i < 4; i++) {
+                        uint32_t st = (s4 >> (8 * i)) & 0xFFu;
+                        // fd_get as selects: last = NONE without a window, t - 2^15 for an old one
+                        const uint32_t l_dec = t - ((t - lti[i]) & 0xFFFFu);
+                        const uint32_t l_old = (st & FD_OLD) ? t - FD_OLD_AGE : l_dec;
+                        Fd f{(st & FD_WIN) ? l_old : NONE, sci[i] & ((1u << d.sum_bits) - 1u), sci[i] >> d.sum_bits};
+                        const uint32_t m = q[i];
+                        const bool hm = m != 0u;
+                        // telescoped replay (as the general path): ctz / highest bit of m, guarded for m = 0
+                        const uint32_t p1 = (uint32_t)__builtin_ctz(m | 0x80000000u);
+                        const uint32_t pk = 31u - (uint32_t)__builtin_clz(m | 1u);
+                        const uint32_t iv = d.t_round + 1u + p1 - f.last;
+                        const bool fo = f.last != NONE && iv <= d.max_iv;
+                        const uint32_t app = (uint32_t)__popc(m) - 1u + (fo ? 1u : 0u);
+                        const uint32_t add = pk - p1 + (fo ? iv : 0u);
+                        rare |= hm && f.cnt + app > d.W;
+                        f.cnt = hm ? f.cnt + app : f.cnt;
+                        f.sum = hm ? f.sum + add : f.sum;
+                        f.last = hm ? d.t_round + 1u + pk : f.last;
+                        fdw |= hm;
+                        const uint32_t j = c0 + i;
+                        const bool vp = upo & (j < d.ncol) & (d.col_lo + j != o);  // (canonical: every column known)
+                        flv += vp ? 1u : 0u;
+                        const bool hl = f.last != NONE && f.cnt != 0u;
+                        const float lf = (float)(t - f.last) * (float)(f.cnt + 5u);
+                        const float rf = d.phi_thr_f * ((float)f.sum + d.prior5t_f);
+                        const bool al = hl && lf < rf * (1.0f - 0x1p-20f);
+                        rare |= vp && hl && !al && !(lf > rf * (1.0f + 0x1p-20f));
+                        const uint32_t mb = st & FD_MEMB;
+                        nd[i] = vp && !al && mb != FD_DEAD;  // a new death: time_of_death recorded once
+                        fmS = nd[i] ? min(fmS, t + d.sched_delay) : fmS;
+                        const bool rst = vp && !al && f.last != NONE && (f.sum | f.cnt);  // reset
+                        f.sum = rst ? 0u : f.sum;
+                        f.cnt = rst ? 0u : f.cnt;
+                        fdw |= rst;
+                        st = vp ? ((st & ~(uint32_t)FD_MEMB) | (al ? (uint32_t)FD_LIVE : (uint32_t)FD_DEAD)) : st;
+                        st = ((st & (FD_WIN | FD_OLD)) == FD_WIN && t - f.last >= FD_OLD_AGE) ? st | FD_OLD : st;
+                        st = hm ? fd_st(st, f) : st;
+                        fsc[i] = fd_sc(d, f);
+                        flt[i] = f.last & 0xFFFFu;
+                        fs4 = (fs4 & ~(0xFFu << (8 * i))) | (st << (8 * i));
+                    }
+                    if (__ballot(rare) == 0ull) {
+                        done = true;
+                        if (fdw) {
+                            if (LIVE_NT) {
+                                __builtin_nontemporal_store(v4u_t{fsc[0], fsc[1], fsc[2], fsc[3]}, reinterpret_cast<v4u_t *>(d.fd + p));
+                                __builtin_nontemporal_store(v2u_t{flt[0] | (flt[1] << 16), flt[2] | (flt[3] << 16)},
+                                                            reinterpret_cast<v2u_t *>(d.fd_last + p));
+                            } else {
+                                *reinterpret_cast<uint4 *>(d.fd + p) = make_uint4(fsc[0], fsc[1], fsc[2], fsc[3]);
+                                *reinterpret_cast<uint2 *>(d.fd_last + p) = make_uint2(flt[0] | (flt[1] << 16), flt[2] | (flt[3] << 16));
+                            }
+                            alg += 24;
+                        }
+                        if (fs4 != s4) {
+                            if (LIVE_NT) __builtin_nontemporal_store(fs4, reinterpret_cast<uint32_t *>(d.fd_state + p));
+                            else *reinterpret_cast<uint32_t *>(d.fd_state + p) = fs4;
+                            alg += 4;
+                        }
+#pragma unroll
+                        for (int i = 0; i < 4; i++)
+                            if (nd[i]) { d.tod[p + i] = t; alg += 4; }
+                        live += flv;
+                        minS = min(minS, fmS);
+                        if (upo || vm) alg += 28;
+                    } else {
+                        // rare: the general path below on values reloaded here (nothing of this chunk was stored),
+                        // so the fast path's inputs need not stay live across it
+                        gsc = *reinterpret_cast<const uint4 *>(d.fd + p);
+                        gl = *reinterpret_cast<const uint2 *>(d.fd_last + p);
+                        gs = *reinterpret_cast<const uint32_t *>(d.fd_state + p);
+                        build_q(q);
                     }
                 } else {
-                    const uint32_t lb = plane_bit(c0);
-                    for (uint32_t m = vm; m; m &= m - 1u) {
-                        const uint32_t ph = (uint32_t)__builtin_ctz(m);
-        #pragma unroll
-                        for (int i = 0; i < 4; i++) q[i] |= (uint32_t)((s_pl[wv][ph][i] >> lb) & 1ull) << ph;
-                    }
+                    gsc = sc4;
+                    gl = l4;
+                    gs = s4;
                 }
-                uint32_t sc[4] = {sc4.x, sc4.y, sc4.z, sc4.w};
-                uint32_t lt[4] = {l4.x & 0xFFFFu, l4.x >> 16, l4.y & 0xFFFFu, l4.y >> 16};
-                bool dw = false;
-                uint32_t td[4] = {NONE, NONE, NONE, NONE};
-                if (exact && (s4 & 0x02020202u)) { ld4(d.tod + p, td); alg += 16; }
-                uint32_t s4n = s4;
-        #pragma unroll
-                for (int i = 0; i < 4; i++) {
-                    uint32_t st = (s4 >> (8 * i)) & 0xFFu;
-                    Fd f = fd_get(d, st, lt[i], sc[i], t);  // t is at or after every report tick of this round
-                    uint32_t m = q[i];  // only if vm != 0: then the window was loaded
-                    if (m) {
-                        // report_heartbeat at ticks t_round + 1 + p for the phases p of m (failure_detector.py:32-38):
-                        // intervals between reports of one round are < NPL ticks, so with max_interval >= NPL - 1 all
-                        // but the first are appended and they telescope: (k - 1) intervals summing to p_last - p_first,
-                        // plus the first one if it is <= max_interval; a compact window that would fill up, and the
-                        // rings (their intervals one by one), replay report by report
-                        bool loop = (RING && rrow) || d.max_iv < NPL - 1u;
-                        if (!loop) {
-                            const uint32_t p1 = (uint32_t)__builtin_ctz(m), pk = 31u - (uint32_t)__builtin_clz(m);
-                            uint32_t app = (uint32_t)__popc(m) - 1u, add = pk - p1;
-                            if (f.last != NONE) {
-                                const uint32_t iv = d.t_round + 1u + p1 - f.last;
-                                if (iv <= d.max_iv) { app++; add += iv; }
-                            }
-                            if (f.cnt + app <= d.W) {
-                                f.cnt += app;
-                                f.sum += add;
-                                f.last = d.t_round + 1u + pk;
-                            } else {
-                                loop = true;
-                            }
-                        }
-                        if (loop) {
-                            while (m) {
-                                const uint32_t bb = (uint32_t)__builtin_ctz(m);
-                                m &= m - 1u;
-                                f = fd_report_val(d, RING && rrow ? rrow + (size_t)(c0 + i) * d.W : nullptr, d.t_round + 1u + bb,
-                                                  f, alg, ovf);
-                            }
-                        }
-                        dw = true;
-                    }
-                    const uint32_t j = c0 + i;
-                    if (upo && j < d.ncol && d.col_lo + j != o && !(genm && ps[i] == NONE)) {
-                        live++;
-                        const bool has = f.last != NONE;
-                        const uint32_t len = RING && rrow ? (f.cnt < d.W ? f.cnt : d.W) : f.cnt;
-                        bool alive = false;
-                        if (has && len) {
-                            // phi <= threshold (failure_detector.py:43-53, 97-98) decided without the two binary64
-                            // divisions when it is clear by a margin: phi ~ elapsed (len + 5) / (sum + 5 prior) in
-                            // ticks.  First in binary32 (full rate: elapsed < 2^24 ticks, len + 5 and sum < 2^24 are
-                            // exact, the three roundings and the two constants' add < 2^-21 relative) with a 2^-20
-                            // margin, then in binary64 with 2^-30 (far above its rounding), the exact expression
-                            // otherwise
-        #if LIVE_F32
-                            const float lf = (float)(t - f.last) * (float)(len + 5u);
-                            const float rf = d.phi_thr_f * ((float)f.sum + d.prior5t_f);
-                            if (lf < rf * (1.0f - 0x1p-20f)) {
-                                alive = true;
-                            } else if (!(lf > rf * (1.0f + 0x1p-20f))) {  // too close: the exact expression
-        #else
-                            const double lhs = (double)(t - f.last) * (double)(len + 5u);  // exact: < 2^43
-                            const double rhs = d.phi_thr * ((double)f.sum + d.prior5t);
-                            if (lhs < rhs * (1.0 - 0x1p-30)) {
-                                alive = true;
-                            } else if (!(lhs > rhs * (1.0 + 0x1p-30))) {
-        #endif
-                                const double mean = ((double)f.sum * TICK_S + d.prior5) / ((double)len + 5.0);
-                                alive = ((double)(t - f.last) * TICK_S) / mean <= d.phi_thr;
-                            }
-                        }
-                        const uint32_t mb = st & FD_MEMB;
-                        // node join / leave: the live set against the previous call's (server.py:611-616)
-                        if (d.ev && alive != (mb == FD_LIVE))
-                            emit_event(d, o, d.col_lo + j, (alive ? EV_JOIN : EV_LEAVE) << 8, 0u, 0u, t, 0u);
-                        uint32_t sn = FD_LIVE;
-                        if (!alive) {
-                            sn = FD_DEAD;
-                            uint32_t tod = td[i];  // loaded for the dead pairs of a row being recomputed
-                            if (mb != FD_DEAD) { tod = t; d.tod[p + i] = t; alg += 4; }  // time_of_death recorded once
-                            if (has && (f.sum | f.cnt)) { f.sum = f.cnt = 0u; dw = true; }  // reset
-                            if (mb != FD_DEAD || exact) {
-                                const uint32_t sat = tod + d.sched_delay;
-                                if (sat < minS) minS = sat;
-                            }
-                            if (exact && (uint64_t)t >= (uint64_t)tod + d.dead_grace) gcdue++;
-                        }
-                        st = (st & ~(uint32_t)FD_MEMB) | sn;
-                    }
-                    // a window whose last report is >= FD_OLD_AGE old keeps only that fact (fd_get)
-                    if ((st & (FD_WIN | FD_OLD)) == FD_WIN && t - f.last >= FD_OLD_AGE) st |= FD_OLD;
-                    if (q[i]) st = fd_st(st, f);
-                    sc[i] = fd_sc(d, f);
-                    lt[i] = f.last & 0xFFFFu;
-                    s4n = (s4n & ~(0xFFu << (8 * i))) | (st << (8 * i));
-                }
-                if (dw) {
-                    if (LIVE_NT) {
-                        __builtin_nontemporal_store(v4u_t{sc[0], sc[1], sc[2], sc[3]}, reinterpret_cast<v4u_t *>(d.fd + p));
-                        __builtin_nontemporal_store(v2u_t{lt[0] | (lt[1] << 16), lt[2] | (lt[3] << 16)},
-                                                    reinterpret_cast<v2u_t *>(d.fd_last + p));
-                    } else {
-                        *reinterpret_cast<uint4 *>(d.fd + p) = make_uint4(sc[0], sc[1], sc[2], sc[3]);
-                        *reinterpret_cast<uint2 *>(d.fd_last + p) = make_uint2(lt[0] | (lt[1] << 16), lt[2] | (lt[3] << 16));
-                    }
-                    alg += 24;
-                }
-                if (s4n != s4) {
-                    if (LIVE_NT) __builtin_nontemporal_store(s4n, reinterpret_cast<uint32_t *>(d.fd_state + p));
-                    else *reinterpret_cast<uint32_t *>(d.fd_state + p) = s4n;
-                    alg += 4;
-                }
-                if (upo || vm) alg += 28;  // the four windows (sum | cnt, last tick) and state bytes read
+                if (!done) general(gsc, gl, gs, q);
             }
         };
         LW w0, w1;
@@ -4400,6 +4727,7 @@ struct gs_handle {
     struct {
         uint64_t *tot = nullptr, *tot_all = nullptr, *chain = nullptr, *chainc = nullptr, *chain_all = nullptr;
         uint64_t *pend = nullptr;  // device: the pending slots summed over the slices (sliced_phase's one read per step)
+        uint64_t *pin = nullptr, *pin_dev = nullptr;  // pinned host pair {pending, count} the kernel writes directly
         uint32_t *list = nullptr;
         uint32_t cap = 0;  // exchanges the buffers hold
     } sc;
@@ -4407,6 +4735,10 @@ struct gs_handle {
     // back into the group's stream around the step), so the slices' short launches overlap on the GPU
     hipStream_t side = nullptr, home = nullptr;
     hipEvent_t fj_fork = nullptr, fj_join = nullptr;
+    // gs_run_phase_group's batched launches: the group's GroupArgs in device memory and its host image as last
+    // uploaded (held by the group's first handle)
+    GroupArgs *grp = nullptr;
+    std::vector<uint8_t> grp_img;
 };
 
 namespace {
@@ -4605,16 +4937,42 @@ int check_phase(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t n
     return GS_OK;
 }
 
-// pass 1 of a record phase (k_pass1 without packing), speculative per Dev::spec
-int launch_pass1(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t n, uint32_t tick) {
+// k_lite's slot work at the end of k_pass1v (a record phase with Dev::lite on the byte-parallel pass 1); env
+// GS_P1LITE=0: k_lite (or k_settle<1, LITE>) as a launch of its own (A/B)
+// mode 0 (one slice): on by default (r5e: 2.27 ms per phase vs 2.10 + 0.235 in two launches); mode 1 (a sliced
+// count pass): off by default -- a slice's stream is short, and k_settle<1, LITE> at 8 waves per SIMD did the slot
+// work sooner (r5e, 8 slices: 0.304 + 0.061 vs 0.348 + 0.030 ms per phase); GS_P1LITE=0 / 1 / 2: off / mode 0 /
+// both (A/B)
+bool p1lite(const gs_handle *h, int mode = 0) {
+    static const int lvl = [] {
+        const char *e = getenv("GS_P1LITE");
+        return e ? atoi(e) : 1;
+    }();
+    return lvl > mode && h->d.pl16 && h->d.lite;
+}
+
+// pass 1 of a record phase (k_pass1 without packing), speculative per Dev::spec; lm >= 0 (k_pass1v only): the
+// slot work of k_lite<lm> in the same launch (io: the sliced count's totals)
+// a launch for every slice of an in-process group at once (grid.y = slices; gs_run_phase_group), or none
+struct GroupCtx {
+    const GroupArgs *ga = nullptr;
+    uint32_t nh = 1;
+    DevDyn dyn{};
+};
+int launch_pass1(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t n, uint32_t tick, int lm = -1,
+                 const SliceIO &io = SliceIO{}, bool defer_fix = false, const GroupCtx &gx = GroupCtx{}) {
     hipEvent_t e0 = nullptr;
     int rc = time_begin(h, e0);
     if (rc) return rc;
     if (h->d.pl16) {  // GS_MV8 record phases: the byte-parallel pass 1
-        k_pass1v<P1V_AHEAD><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, h->seq);
+        const dim3 grid(n, gx.nh);
+        if (lm == 0) k_pass1v<P1V_AHEAD, 0><<<grid, XB, 0, h->stream>>>(h->d, ini, res, n, tick, h->seq, io, gx.ga, gx.dyn);
+        else if (lm == 1) k_pass1v<P1V_AHEAD, 1><<<grid, XB, 0, h->stream>>>(h->d, ini, res, n, tick, h->seq, io, gx.ga, gx.dyn);
+        else k_pass1v<P1V_AHEAD, -1><<<grid, XB, 0, h->stream>>>(h->d, ini, res, n, tick, h->seq, io, gx.ga, gx.dyn);
         HIPCHK(h, hipGetLastError());
         rc = time_end(h, GS_KT_PASS1, e0);
         if (rc) return rc;
+        if (defer_fix) return GS_OK;  // the caller's next launch does it (Dev::p1fix)
         k_p1v_fix<<<(n + LB - 1) / LB, LB, 0, h->stream>>>(h->d, res, n);
         HIPCHK(h, hipGetLastError());
         return GS_OK;
@@ -4634,12 +4992,13 @@ int launch_pass1(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t 
 }
 template <int MODE, bool LITE = false>
 int launch_settle(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t n, uint32_t tick, const SliceIO &io,
-                  int kind) {
+                  int kind, const GroupCtx &gx = GroupCtx{}) {
     hipEvent_t e0 = nullptr;
     int rc = time_begin(h, e0);
     if (rc) return rc;
-    if (h->KP <= 16) k_settle<4, MODE, LITE><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, io);
-    else k_settle<KWB, MODE, LITE><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, io);
+    const dim3 grid(n, gx.nh);
+    if (h->KP <= 16) k_settle<4, MODE, LITE><<<grid, XB, 0, h->stream>>>(h->d, ini, res, n, tick, io, gx.ga, gx.dyn);
+    else k_settle<KWB, MODE, LITE><<<grid, XB, 0, h->stream>>>(h->d, ini, res, n, tick, io, gx.ga, gx.dyn);
     HIPCHK(h, hipGetLastError());
     return time_end(h, kind, e0);
 }
@@ -4667,14 +5026,17 @@ int run_split_phase(gs_handle *h, const int32_t *ini, const int32_t *res, uint32
         HIPCHK(h, hipGetLastError());
         return time_end(h, GS_KT_PASS1, e0);
     }
-    if ((rc = launch_pass1(h, ini, res, n, tick))) return rc;
-    if (h->d.ablate & 1u) return GS_OK;  // profiling only: no packing (results invalid)
+    const bool fl = p1lite(h), defer = fl && !(h->d.ablate & 1u);  // defer: the packer sets the small bits
     const SliceIO io{};
+    if ((rc = launch_pass1(h, ini, res, n, tick, fl ? 0 : -1, io, defer))) return rc;
+    if (h->d.ablate & 1u) return GS_OK;  // profiling only: no packing (results invalid)
     if (h->pack_mode == 0) return launch_settle<0>(h, ini, res, n, tick, io, GS_KT_PACK);
-    if (h->d.lite && (rc = launch_lite<0>(h, ini, res, n, tick, io))) return rc;
+    if (h->d.lite && !fl && (rc = launch_lite<0>(h, ini, res, n, tick, io))) return rc;
     if ((rc = time_begin(h, e0))) return rc;
+    h->d.p1fix = defer ? 1u : 0u;
     if (h->KP <= 16) k_pack_slice<4><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, io, 0u);
     else k_pack_slice<KWB><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, io, 0u);
+    h->d.p1fix = 0u;
     HIPCHK(h, hipGetLastError());
     return time_end(h, GS_KT_PACK, e0);
 }
@@ -4850,6 +5212,8 @@ void gs_destroy(gs_handle *h) {
     for (void *p : {(void *)h->sc.tot, (void *)h->sc.tot_all, (void *)h->sc.chain, (void *)h->sc.chainc,
                     (void *)h->sc.chain_all, (void *)h->sc.list, (void *)h->sc.pend})
         if (p) (void)hipFree(p);
+    if (h->sc.pin) (void)hipHostFree(h->sc.pin);
+    if (h->grp) (void)hipFree(h->grp);
     if (h->comm) (void)ncclCommDestroy(h->comm);
     if (h->side) (void)hipStreamDestroy(h->side);
     for (hipEvent_t e : {h->fj_fork, h->fj_join})
@@ -5079,6 +5443,20 @@ int gs_phase_count(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_
     // the speculative merge is decided here for the whole phase (gs_phase_pack / gs_phase_chain use it)
     h->d.spec = spec_ok(h) || spec_v_ok(h) ? 1u : 0u;
     h->d.lite = lite_ok(h) ? 1u : 0u;
+    if (p1lite(h, 1)) {  // the lite slot work ran in k_pass1v: the exact count of the slots it left (LITE_FULL) only
+        if ((rc = launch_pass1(h, ini, res, n, tick, 1, io, true))) return rc;
+        h->d.p1fix = 1u;  // and the responders' small bits (k_p1v_fix)
+        rc = launch_settle<1>(h, ini, res, n, tick, io, GS_KT_COUNT);
+        h->d.p1fix = 0u;
+        return rc;
+    }
+    if (h->d.lite && lite_fuse() && h->d.pl16) {  // lite + count in one launch, which also sets the small bits
+        if ((rc = launch_pass1(h, ini, res, n, tick, -1, io, true))) return rc;
+        h->d.p1fix = 1u;
+        rc = launch_settle<1, true>(h, ini, res, n, tick, io, GS_KT_COUNT);
+        h->d.p1fix = 0u;
+        return rc;
+    }
     if ((rc = launch_pass1(h, ini, res, n, tick))) return rc;
     if (h->d.lite && lite_fuse()) return launch_settle<1, true>(h, ini, res, n, tick, io, GS_KT_COUNT);
     if (h->d.lite && (rc = launch_lite<1>(h, ini, res, n, tick, io))) return rc;
@@ -5120,11 +5498,11 @@ int gs_phase_overflow(gs_handle *h, uint32_t n, const uint64_t *slice_bytes_all,
     if (!h->sliced || !h->d.cand) return fail(h, GS_E_UNSUPPORTED, "gs_phase_overflow needs a sliced canonical handle");
     if (!slice_bytes_all || !chain || !list || !chainc) return GS_E_INVALID;
     const uint32_t slots = 2 * n, nb = (slots + OVB - 1) / OVB;
-    k_ov_count<<<nb, OVB, 0, h->stream>>>(slice_bytes_all, slots, h->G, h->cfg.mtu, list + slots);
+    k_ov_count<<<nb, OVB, 0, h->stream>>>(slice_bytes_all, slots, h->G, h->cfg.mtu, list + slots, nullptr);
     HIPCHK(h, hipGetLastError());
-    k_ov_write<<<nb, OVB, 0, h->stream>>>(slice_bytes_all, slots, h->G, h->cfg.mtu, chain, list, chainc);
+    k_ov_write<<<nb, OVB, 0, h->stream>>>(slice_bytes_all, slots, h->G, h->cfg.mtu, chain, list, chainc, nullptr);
     HIPCHK(h, hipGetLastError());
-    k_pending<<<1, OVB, 0, h->stream>>>(list, list + slots + nb, 0u, chain, chainc);  // chainc[count]
+    k_pending<<<1, OVB, 0, h->stream>>>(list, list + slots + nb, 0u, chain, chainc, nullptr, n);  // chainc[count]
     HIPCHK(h, hipGetLastError());
     if (count) {  // count = NULL: no read back (another slice in this process reads the same count)
         HIPCHK(h, hipMemcpyAsync(count, list + slots + nb, 4, hipMemcpyDeviceToHost, h->stream));
@@ -5151,12 +5529,12 @@ int gs_phase_chain(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_
     const uint32_t grid = std::min<uint32_t>(dev ? GS_CHAIN_CAP : count, 2048u), c = dev ? 0u : count;
     if (h->KP <= 16)
         k_chain_step<4><<<grid, WAVE, 0, h->stream>>>(h->d, ini, res, tick, list, c, chain_all, chain, chainc,
-                                                       slice_bytes_all, n, cnt_dev);
+                                                       slice_bytes_all, n, cnt_dev, nullptr, DevDyn{});
     else
         k_chain_step<KWB><<<grid, WAVE, 0, h->stream>>>(h->d, ini, res, tick, list, c, chain_all, chain, chainc,
-                                                         slice_bytes_all, n, cnt_dev);
+                                                         slice_bytes_all, n, cnt_dev, nullptr, DevDyn{});
     HIPCHK(h, hipGetLastError());
-    k_pending<<<1, OVB, 0, h->stream>>>(list, cnt_dev, c, chain, chainc);  // chainc[count]
+    k_pending<<<1, OVB, 0, h->stream>>>(list, cnt_dev, c, chain, chainc, nullptr, n);  // chainc[count]
     HIPCHK(h, hipGetLastError());
     return time_end(h, GS_KT_PACK, e0);
 }
@@ -5176,9 +5554,24 @@ int ensure_scratch(gs_handle *h, uint32_t n) {
     HIPCHK(h, hipMalloc(&h->sc.chainc, s2 + 8));                 // [2 cap + 1]: the pending entry last
     HIPCHK(h, hipMalloc(&h->sc.tot_all, G * s2));
     HIPCHK(h, hipMalloc(&h->sc.chain_all, G * (s2 + 8)));      // [G][count + 1]
-    HIPCHK(h, hipMalloc(&h->sc.pend, 8));
+    HIPCHK(h, hipMalloc(&h->sc.pend, 16));
     HIPCHK(h, hipMalloc(&h->sc.list, (size_t)GS_OVERFLOW_LIST_LEN(cap) * 4));
     h->sc.cap = cap;
+    return GS_OK;
+}
+
+// k_sum_pending into the handle's pinned host pair (written by the kernel itself: no copy), then one wait
+int read_pending(gs_handle *h, uint32_t G, uint32_t count, const uint32_t *cnt_dev, const uint64_t *chain_all,
+                 uint64_t &pend, uint32_t &cnt) {
+    if (!h->sc.pin) {
+        HIPCHK(h, hipHostMalloc((void **)&h->sc.pin, 16, hipHostMallocMapped));
+        HIPCHK(h, hipHostGetDevicePointer((void **)&h->sc.pin_dev, h->sc.pin, 0));
+    }
+    k_sum_pending<<<1, WAVE, 0, h->stream>>>(chain_all, G, count, cnt_dev, h->sc.pin_dev);
+    HIPCHK(h, hipGetLastError());
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    pend = reinterpret_cast<volatile uint64_t *>(h->sc.pin)[0];
+    cnt = (uint32_t)reinterpret_cast<volatile uint64_t *>(h->sc.pin)[1];
     return GS_OK;
 }
 
@@ -5222,14 +5615,18 @@ int fork_slices(gs_handle *const *hs, uint32_t nh) {
     gs_handle *h0 = hs[0];
     if (nh < 2) return GS_OK;
     if (!h0->fj_fork) HIPCHK(h0, hipEventCreateWithFlags(&h0->fj_fork, hipEventDisableTiming));
-    HIPCHK(h0, hipEventRecord(h0->fj_fork, h0->stream));
+    // every stream, event and wait first; the handles switch streams only once nothing can fail (a
+    // failure half-way left the earlier handles on their side streams)
     for (uint32_t i = 0; i < nh; i++) {
         gs_handle *h = hs[i];
         if (!h->side) HIPCHK(h, hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
         if (!h->fj_join) HIPCHK(h, hipEventCreateWithFlags(&h->fj_join, hipEventDisableTiming));
-        HIPCHK(h, hipStreamWaitEvent(h->side, h0->fj_fork, 0));
-        h->home = h->stream;
-        h->stream = h->side;
+    }
+    HIPCHK(h0, hipEventRecord(h0->fj_fork, h0->stream));
+    for (uint32_t i = 0; i < nh; i++) HIPCHK(hs[i], hipStreamWaitEvent(hs[i]->side, h0->fj_fork, 0));
+    for (uint32_t i = 0; i < nh; i++) {
+        hs[i]->home = hs[i]->stream;
+        hs[i]->stream = hs[i]->side;
     }
     return GS_OK;
 }
@@ -5244,27 +5641,111 @@ int join_slices(gs_handle *const *hs, uint32_t nh, int rc = GS_OK) {
     for (uint32_t i = 0; i < nh && rc == GS_OK; i++) HIPCHK(hs[0], hipStreamWaitEvent(hs[0]->stream, hs[i]->fj_join, 0));
     return rc;
 }
+// gs_run_phase_group's batched steps (round 5): the slices of one process run each step as ONE launch (grid.y =
+// slice) instead of one launch per slice -- the in-process rehearsal of a G-GPU run otherwise paid G launches
+// (and their gaps) per step (1.67x one handle at 8 slices).  The default layout (GS_MV8 record phases
+// with the lite path, K <= 16), 2..GRP_MAX slices on one stream; env GS_GROUP_BATCH=0: a launch per slice (A/B).
+bool group_batch_ok(gs_handle *const *hs, uint32_t nh) {
+    static const bool on = [] {
+        const char *e = getenv("GS_GROUP_BATCH");
+        return !(e && e[0] == '0');
+    }();
+    if (!on || nh < 2 || nh > GRP_MAX || hs[0]->comm) return false;
+    for (uint32_t i = 0; i < nh; i++) {
+        const gs_handle *h = hs[i];
+        if (!h->d.cand || !h->d.pl16 || !lite_ok(h) || h->KP > 16 || !lite_fuse() || p1lite(h, 1)) return false;
+    }
+    return true;
+}
+// the group's GroupArgs: every slice's Dev (its per-phase fields zero: they come by value) and scratch pointers,
+// uploaded only when the image differs from the last one
+int group_upload(gs_handle *const *hs, uint32_t nh) {
+    gs_handle *h0 = hs[0];
+    std::vector<uint8_t> buf(sizeof(GroupArgs), 0u);
+    GroupArgs &img = *reinterpret_cast<GroupArgs *>(buf.data());
+    for (uint32_t i = 0; i < nh; i++) {
+        const gs_handle *h = hs[i];
+        memcpy(&img.dv[i], &h->d, sizeof(Dev));
+        img.dv[i].t_round = img.dv[i].spec = img.dv[i].lite = img.dv[i].p1fix = 0u;
+        img.io[i].tot = h->sc.tot;
+        img.io[i].tot_all = h->sc.tot_all;
+        img.io[i].chain_all = h->sc.chain_all;
+        img.io[i].chain = h->sc.chain;
+        img.list[i] = h->sc.list;
+        img.chain_all[i] = h->sc.chain_all;
+        img.chainc[i] = h->sc.chainc;
+    }
+    if (!h0->grp) HIPCHK(h0, hipMalloc(&h0->grp, sizeof(GroupArgs)));
+    if (h0->grp_img != buf) {
+        HIPCHK(h0, hipMemcpyAsync(h0->grp, buf.data(), buf.size(), hipMemcpyHostToDevice, h0->stream));
+        HIPCHK(h0, hipStreamSynchronize(h0->stream));  // (the source is this function's buffer)
+        h0->grp_img.swap(buf);
+    }
+    return GS_OK;
+}
+// count, gather, step 0, the overflow lists and chain step 1 of a sliced phase, batched over the group
+int group_steps(gs_handle *const *hs, uint32_t nh, const int32_t *ini, const int32_t *res, uint32_t n, uint32_t tick) {
+    int rc;
+    gs_handle *h0 = hs[0];
+    // per slice: gs_phase_count's checks and bookkeeping (a lag sweep or a window-age sweep may launch here)
+    for (uint32_t i = 0; i < nh; i++) {
+        gs_handle *h = hs[i];
+        if ((rc = check_phase(h, ini, res, n, tick))) return rc;
+        if ((rc = fd_age(h, tick)) || (rc = advance_planes(h, tick))) return rc;
+        h->seq += 1;
+        h->reports_pending = true;
+        h->last_phase_tick = tick;
+        h->hb_incs++;
+        h->d.spec = spec_ok(h) || spec_v_ok(h) ? 1u : 0u;
+        h->d.lite = lite_ok(h) ? 1u : 0u;
+        if (h->seq != h0->seq || h->d.t_round != h0->d.t_round || h->d.spec != h0->d.spec || h->d.lite != h0->d.lite)
+            return fail(h0, GS_E_INVALID, "gs_run_phase_group: slice %u is not in step with slice 0", i);
+    }
+    if ((rc = group_upload(hs, nh))) return rc;
+    GroupCtx gx;
+    gx.ga = h0->grp;
+    gx.nh = nh;
+    gx.dyn = DevDyn{h0->d.t_round, h0->d.spec, h0->d.lite, 0u};
+    SliceIO io{};  // (each slice's from GroupArgs; the step by value)
+    // count: pass 1, then lite + the slice totals in one launch, which also sets the responders' small bits
+    if ((rc = launch_pass1(h0, ini, res, n, tick, -1, io, true, gx))) return rc;
+    gx.dyn.p1fix = 1u;
+    if ((rc = launch_settle<1, true>(h0, ini, res, n, tick, io, GS_KT_COUNT, gx))) return rc;
+    gx.dyn.p1fix = 0u;
+    if ((rc = gather_u64(hs, nh, [](gs_handle *h) { return h->sc.tot; }, [](gs_handle *h) { return h->sc.tot_all; },
+                         (size_t)2 * n)))
+        return rc;
+    // step 0, then the overflowing slots listed on the device (the same list on every slice)
+    if ((rc = launch_settle<2, true>(h0, ini, res, n, tick, io, GS_KT_PACK, gx))) return rc;
+    const uint32_t slots = 2 * n, nb = (slots + OVB - 1) / OVB, G = h0->G;
+    const uint32_t *cnt0 = h0->sc.list + slots + nb;  // (each slice's own list tail, from GroupArgs)
+    k_ov_count<<<dim3(nb, nh), OVB, 0, h0->stream>>>(nullptr, slots, G, h0->cfg.mtu, nullptr, h0->grp);
+    HIPCHK(h0, hipGetLastError());
+    k_ov_write<<<dim3(nb, nh), OVB, 0, h0->stream>>>(nullptr, slots, G, h0->cfg.mtu, nullptr, nullptr, nullptr, h0->grp);
+    HIPCHK(h0, hipGetLastError());
+    k_pending<<<dim3(1, nh), OVB, 0, h0->stream>>>(nullptr, cnt0, 0u, nullptr, nullptr, h0->grp, n);
+    HIPCHK(h0, hipGetLastError());
+    // chain step 1 on the device count
+    if ((rc = gather_u64(hs, nh, [](gs_handle *h) { return h->sc.chainc; }, [](gs_handle *h) { return h->sc.chain_all; },
+                         GS_CHAIN_CAP + 1u)))
+        return rc;
+    hipEvent_t e0 = nullptr;
+    if ((rc = time_begin(h0, e0))) return rc;
+    k_chain_step<4><<<dim3(std::min<uint32_t>(GS_CHAIN_CAP, 2048u), nh), WAVE, 0, h0->stream>>>(
+        h0->d, ini, res, tick, nullptr, 0u, nullptr, nullptr, nullptr, nullptr, n, cnt0, h0->grp, gx.dyn);
+    HIPCHK(h0, hipGetLastError());
+    k_pending<<<dim3(1, nh), OVB, 0, h0->stream>>>(nullptr, cnt0, 0u, nullptr, nullptr, h0->grp, n);
+    HIPCHK(h0, hipGetLastError());
+    return time_end(h0, GS_KT_PACK, e0);
+}
+
 int sliced_phase(gs_handle *const *hs, uint32_t nh, const int32_t *ini, const int32_t *res, uint32_t n, uint32_t tick) {
     int rc;
     for (uint32_t i = 0; i < nh; i++) {
         if (!hs[i]->d.cand) return fail(hs[i], GS_E_UNSUPPORTED, "library-driven sliced phases need candidate records");
         if ((rc = ensure_scratch(hs[i], n))) return rc;
     }
-    if ((rc = fork_slices(hs, nh))) return rc;
-    for (uint32_t i = 0; i < nh && !rc; i++) rc = gs_phase_count(hs[i], ini, res, n, tick, hs[i]->sc.tot);
-    if ((rc = join_slices(hs, nh, rc))) return rc;
-    if ((rc = gather_u64(hs, nh, [](gs_handle *h) { return h->sc.tot; }, [](gs_handle *h) { return h->sc.tot_all; },
-                         (size_t)2 * n)))
-        return rc;
-    if ((rc = fork_slices(hs, nh))) return rc;
-    for (uint32_t i = 0; i < nh && !rc; i++) {
-        rc = gs_phase_pack(hs[i], ini, res, n, tick, 0, hs[i]->sc.tot_all, nullptr, hs[i]->sc.chain);
-        // the overflowing slots, listed on the device (the same list on every slice)
-        if (!rc) rc = gs_phase_overflow(hs[i], n, hs[i]->sc.tot_all, hs[i]->sc.chain, hs[i]->sc.list, hs[i]->sc.chainc, nullptr);
-    }
-    if ((rc = join_slices(hs, nh, rc))) return rc;
     const uint32_t G = hs[0]->G;
-    if (G < 2) return GS_OK;  // one slice: step 0 finished every slot
     gs_handle *h0 = hs[0];
     const uint32_t *cnt0 = h0->sc.list + 2u * n + (2u * n + OVB - 1u) / OVB;  // gs_phase_overflow's count entry
     auto gather_chain = [&](size_t entries) {
@@ -5272,19 +5753,34 @@ int sliced_phase(gs_handle *const *hs, uint32_t nh, const int32_t *ini, const in
                           entries);
     };
     auto pending = [&](uint32_t count, const uint32_t *cnt_dev, uint64_t &pend) {
-        k_sum_pending<<<1, WAVE, 0, h0->stream>>>(h0->sc.chain_all, G, count, cnt_dev, h0->sc.pend);
-        HIPCHK(h0, hipGetLastError());
-        HIPCHK(h0, hipMemcpyAsync(&pend, h0->sc.pend, 8, hipMemcpyDeviceToHost, h0->stream));
-        HIPCHK(h0, hipStreamSynchronize(h0->stream));
-        return GS_OK;
+        uint32_t c = 0;
+        return read_pending(h0, G, count, cnt_dev, h0->sc.chain_all, pend, c);
     };
-    // step 1 before any host read, on the device count (a chain usually resolves in it: one read ends the phase)
     uint64_t pend = 0;
-    if ((rc = gather_chain(GS_CHAIN_CAP + 1u)) || (rc = fork_slices(hs, nh))) return rc;
-    for (uint32_t i = 0; i < nh && !rc; i++)
-        rc = gs_phase_chain(hs[i], ini, res, n, tick, 1, hs[i]->sc.list, GS_CHAIN_DEVICE, hs[i]->sc.chain_all,
-                            hs[i]->sc.chain, hs[i]->sc.chainc, hs[i]->sc.tot_all);
-    if ((rc = join_slices(hs, nh, rc))) return rc;
+    if (group_batch_ok(hs, nh) && G == nh) {
+        if ((rc = group_steps(hs, nh, ini, res, n, tick))) return rc;
+    } else {
+        if ((rc = fork_slices(hs, nh))) return rc;
+        for (uint32_t i = 0; i < nh && !rc; i++) rc = gs_phase_count(hs[i], ini, res, n, tick, hs[i]->sc.tot);
+        if ((rc = join_slices(hs, nh, rc))) return rc;
+        if ((rc = gather_u64(hs, nh, [](gs_handle *h) { return h->sc.tot; }, [](gs_handle *h) { return h->sc.tot_all; },
+                             (size_t)2 * n)))
+            return rc;
+        if ((rc = fork_slices(hs, nh))) return rc;
+        for (uint32_t i = 0; i < nh && !rc; i++) {
+            rc = gs_phase_pack(hs[i], ini, res, n, tick, 0, hs[i]->sc.tot_all, nullptr, hs[i]->sc.chain);
+            // the overflowing slots, listed on the device (the same list on every slice)
+            if (!rc) rc = gs_phase_overflow(hs[i], n, hs[i]->sc.tot_all, hs[i]->sc.chain, hs[i]->sc.list, hs[i]->sc.chainc, nullptr);
+        }
+        if ((rc = join_slices(hs, nh, rc))) return rc;
+        if (G < 2) return GS_OK;  // one slice: step 0 finished every slot
+        // step 1 before any host read, on the device count (a chain usually resolves in it: one read ends the phase)
+        if ((rc = gather_chain(GS_CHAIN_CAP + 1u)) || (rc = fork_slices(hs, nh))) return rc;
+        for (uint32_t i = 0; i < nh && !rc; i++)
+            rc = gs_phase_chain(hs[i], ini, res, n, tick, 1, hs[i]->sc.list, GS_CHAIN_DEVICE, hs[i]->sc.chain_all,
+                                hs[i]->sc.chain, hs[i]->sc.chainc, hs[i]->sc.tot_all);
+        if ((rc = join_slices(hs, nh, rc))) return rc;
+    }
     if ((rc = gather_chain(GS_CHAIN_CAP + 1u)) || (rc = pending(0u, cnt0, pend))) return rc;
     if (!pend) return GS_OK;
     // still pending (or more slots than the device step takes): the count to the host, the remaining steps
@@ -5305,6 +5801,16 @@ int sliced_phase(gs_handle *const *hs, uint32_t nh, const int32_t *ini, const in
     return GS_OK;
 }
 }  // namespace
+}
+
+int gs_phase_pending(gs_handle *h, uint32_t n, const uint32_t *list, uint32_t count, const uint64_t *chain_all,
+                     uint64_t *pending, uint32_t *count_out) {
+    if (!h || !h->booted || !chain_all || !pending || !count_out) return GS_E_INVALID;
+    if (!h->sliced) return fail(h, GS_E_UNSUPPORTED, "gs_phase_pending needs a sliced handle");
+    const bool dev = count == GS_CHAIN_DEVICE;
+    if (dev && (!list || !n)) return GS_E_INVALID;
+    const uint32_t *cnt_dev = dev ? list + 2u * n + (2u * n + OVB - 1u) / OVB : nullptr;  // gs_phase_overflow's count
+    return read_pending(h, h->G, dev ? 0u : count, cnt_dev, chain_all, *pending, *count_out);
 }
 
 int gs_comm_id(void *id) {
@@ -5572,7 +6078,11 @@ int gs_read_counters(gs_handle *h, gs_counters *out) {
     HIPCHK(h, hipStreamSynchronize(h->stream));
     uint64_t acc[32] = {0};  // the gs_counters fields (the census scratch follows them in each row)
     for (int s = 0; s < NSHARD; s++)
-        for (int c = 0; c < 32; c++) acc[c] += buf[(size_t)s * CROW + c];
+        for (int c = 0; c < 32; c++) {
+            const uint64_t v = buf[(size_t)s * CROW + c];
+            if (c == C_PGMAX || c == C_PSMAX) acc[c] = std::max<uint64_t>(acc[c], v);  // maxima, not sums
+            else acc[c] += v;
+        }
     acc[C_FLUSH] = h->plane_flushes;
     acc[C_SWEEPS] = h->lag_sweeps;
     memcpy(out, acc, sizeof acc);

@@ -35,6 +35,8 @@ import numpy as np
 
 from ._lib import COUNTER_FIELDS, GS_CHAIN_CAP, GS_CHAIN_DEVICE, GsError, overflow_list_len
 
+MAX_FIELDS = ("pack_groups_max", "pack_steps_max")  # counters that are maxima, not sums
+
 CHAIN_PENDING = -1  # u64 ~0 viewed as int64 (gossip_sim.hip CHAIN_PENDING)
 TOT_BYTES_MASK = (1 << 40) - 1  # a slice total's DeltaPb bytes (GS_TOT_BYTES); the smallest NodeDelta above
 
@@ -52,7 +54,7 @@ class LocalComm:
         return torch.stack(parts)
 
     def sum_counters(self, per_slice: list[dict]) -> dict:
-        return {k: sum(c[k] for c in per_slice) for k in COUNTER_FIELDS}
+        return {k: (max if k in MAX_FIELDS else sum)(c[k] for c in per_slice) for k in COUNTER_FIELDS}
 
     def any(self, flag: bool) -> bool:
         return flag
@@ -112,19 +114,24 @@ class DistComm:
 
         (c,) = per_slice
         dev = "cpu" if self.dist.get_backend(self.group) == "gloo" else "cuda"
-        v = torch.tensor([c[k] for k in COUNTER_FIELDS], dtype=torch.int64, device=dev)
+        sums = [k for k in COUNTER_FIELDS if k not in MAX_FIELDS]
+        v = torch.tensor([c[k] for k in sums], dtype=torch.int64, device=dev)
+        m = torch.tensor([c[k] for k in MAX_FIELDS], dtype=torch.int64, device=dev)
         self.dist.all_reduce(v, group=self.group)
-        return dict(zip(COUNTER_FIELDS, (int(x) for x in v.tolist())))
+        self.dist.all_reduce(m, op=self.dist.ReduceOp.MAX, group=self.group)
+        out = dict(zip(sums, (int(x) for x in v.tolist())))
+        out.update(zip(MAX_FIELDS, (int(x) for x in m.tolist())))
+        return {k: out[k] for k in COUNTER_FIELDS}
 
     def any(self, flag: bool) -> bool:
         return flag  # decided from gathered data, identical on every rank
 
 
-def run_sliced_phase(slices, comm, mtu: int, t: int, ini, res) -> int:
+def run_sliced_phase(slices, comm, mtu: int, t: int, ini, res, cache: dict | None = None) -> int:
     """One phase on the slices this process drives; returns the pack steps taken (1 = no chain).
 
-    ``slices`` expose ``phase_count``, ``phase_pack``, ``phase_overflow`` and ``phase_chain``
-    (``GossipSim`` does).
+    ``slices`` expose ``phase_count``, ``phase_pack``, ``phase_overflow``, ``phase_chain`` and ``phase_pending``
+    (``GossipSim`` does).  ``cache``: the phase's scratch tensors kept across phases (per exchange count).
     """
     import torch
 
@@ -133,7 +140,20 @@ def run_sliced_phase(slices, comm, mtu: int, t: int, ini, res) -> int:
         return 0
     tots = [s.phase_count(t, ini, res) for s in slices]
     tot_all = comm.gather(tots)
-    chains = [torch.empty_like(x) for x in tots]
+    dev = tots[0].device
+    key = (n, str(dev), len(slices))
+    buf = None if cache is None else cache.get(key)
+    if buf is None:
+        buf = {
+            "chains": [torch.empty_like(x) for x in tots],
+            "lists": [torch.empty(overflow_list_len(n), dtype=torch.int32, device=dev) for _ in slices],
+            # [2n + 1] (the listed slots' states, then the pending entry), at least GS_CHAIN_CAP + 1
+            "chaincs": [torch.empty(max(2 * n, GS_CHAIN_CAP) + 1, dtype=torch.int64, device=dev) for _ in slices],
+        }
+        if cache is not None:
+            cache.clear()  # one exchange count at a time (phases of one schedule mostly share it)
+            cache[key] = buf
+    chains = buf["chains"]
     for s, ch in zip(slices, chains):
         s.phase_pack(t, ini, res, 0, tot_all, None, ch)
     if not all(s.has_records for s in slices):
@@ -145,10 +165,7 @@ def run_sliced_phase(slices, comm, mtu: int, t: int, ini, res) -> int:
             for s, ch in zip(slices, chains):
                 s.phase_pack(t, ini, res, step, tot_all, chain_all, ch)
         return comm.world
-    dev = tots[0].device
-    lists = [torch.empty(overflow_list_len(n), dtype=torch.int32, device=dev) for _ in slices]
-    # [2n + 1] (the listed slots' states, then the pending entry), at least GS_CHAIN_CAP + 1: the device step's rows
-    chaincs = [torch.empty(max(2 * n, GS_CHAIN_CAP) + 1, dtype=torch.int64, device=dev) for _ in slices]
+    lists, chaincs = buf["lists"], buf["chaincs"]
     # the overflowing slots, listed on the device (the same list on every slice); no count read
     for i in range(len(slices) - 1, -1, -1):
         slices[i].phase_overflow(tot_all, chains[i], lists[i], chaincs[i], read=False)
@@ -161,11 +178,9 @@ def run_sliced_phase(slices, comm, mtu: int, t: int, ini, res) -> int:
     for s, ch, lb, cc in zip(slices, chains, lists, chaincs):
         s.phase_chain(t, ini, res, 1, lb, GS_CHAIN_DEVICE, chain_all, ch, cc, tot_all)
     chain_all = comm.gather([cc[: cap + 1] for cc in chaincs])
-    ci = overflow_list_len(n) - 1  # gs_phase_overflow's count entry
-    cnt = lists[0][ci:ci + 1].to(torch.int64)
-    pend = torch.where(cnt > cap, torch.full_like(cnt, -1),
-                       chain_all.to(cnt.device).index_select(1, cnt.clamp(max=cap)).sum().reshape(1))
-    p_, count = (int(x) for x in torch.cat([pend, cnt]).tolist())  # the phase's one host read
+    # the phase's one host read: the pending slots summed over the slices and the device count (gs_phase_pending:
+    # one kernel writing a pinned host pair; -1 = more slots than the device step takes)
+    p_, count = slices[0].phase_pending(n, lists[0], GS_CHAIN_DEVICE, chain_all)
     if p_ == 0:
         return 2 if count else 1
     steps = 1 if count > cap else 2
@@ -196,6 +211,7 @@ class ShardGroup:
         self.n = self.slices[0].n
         self.chain_phases = 0
         self.phase_steps: list[int] = []  # pack steps each phase of this driver took (1 = no chain)
+        self._scratch: dict = {}  # run_sliced_phase's tensors, kept across phases
         self.native = native
         if native and len(self.slices) == 1 and isinstance(comm, DistComm):
             self._comm_init()
@@ -266,7 +282,7 @@ class ShardGroup:
                 s0._chk(s0.L.gs_run_phase_group(hs, len(self.slices), C.c_void_p(ini.data_ptr()),
                                                 C.c_void_p(res.data_ptr()), n, t), "gs_run_phase_group")
             return
-        steps = run_sliced_phase(self.slices, self.comm, self.mtu, t, ini, res)
+        steps = run_sliced_phase(self.slices, self.comm, self.mtu, t, ini, res, self._scratch)
         self.phase_steps.append(steps)
         if steps > 1:
             self.chain_phases += 1

@@ -437,6 +437,16 @@ class GossipSim:
                                         C.c_void_p(tot_all.data_ptr())),
                   "gs_phase_chain")
 
+    def phase_pending(self, n: int, list_buf, count: int, chain_all) -> tuple[int, int]:
+        """gs_phase_pending: (the listed slots still pending over all slices -- -1 when the device count exceeds
+        GS_CHAIN_CAP --, the count) after a chain step; ``count`` = GS_CHAIN_DEVICE reads it from ``list_buf``."""
+        pend, cnt = C.c_uint64(), C.c_uint32()
+        ca = chain_all if chain_all.device == self.device else chain_all.to(self.device)
+        self._chk(self.L.gs_phase_pending(self.h, n, C.c_void_p(list_buf.data_ptr()), count, C.c_void_p(ca.data_ptr()),
+                                          C.byref(pend), C.byref(cnt)), "gs_phase_pending")
+        p = int(pend.value)
+        return (-1 if p == (1 << 64) - 1 else p), int(cnt.value)
+
     def flush_reports(self, t: int):
         """gs_flush_reports: apply the open round's pending heartbeat reports to the windows now (a
         mid-round readback of GS_R_FD); the next phase must come after ``t``."""

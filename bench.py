@@ -297,6 +297,9 @@ def roofline(sims, local_c, exch, kt, elapsed, torch, dev, rank, group, workload
     liveb = sum(x["live_bytes"] for x in local_c)  # k_liveness's element bytes
     ncols = sum(s_.ncol for s_ in sims)
     fused = kt["pack"][1] == 0
+    # k_pass1v with k_lite's slot work in its epilogue (round 5; no k_lite launches): its bytes are pass 1's too
+    # (one slice only: a sliced count pass runs the slot work in k_settle<1, LITE> by default, GS_P1LITE < 2)
+    lite_in_p1 = group is None and kt.get("lite", (0.0, 0))[1] == 0 and liteb > 0 and not fused
     per = {}
     for kind, (ms, launches) in kt.items():
         if not launches:
@@ -304,7 +307,7 @@ def roofline(sims, local_c, exch, kt, elapsed, torch, dev, rank, group, workload
         avg_s = ms / launches / 1e3
         b = None
         if kind == "pass1":
-            b = (alg if fused else alg - packb) / launches
+            b = (alg if fused else alg - packb + (liteb if lite_in_p1 else 0)) / launches
         elif kind == "pack":
             b = (packb - liteb) / launches
         elif kind == "lite":
@@ -312,8 +315,9 @@ def roofline(sims, local_c, exch, kt, elapsed, torch, dev, rank, group, workload
         elif kind == "liveness":
             b = liveb / launches
         kname = p1name if kind == "pass1" else KERNEL_OF[kind]
+        shown = kname + (" (+ k_lite slot work in its epilogue)" if kind == "pass1" and lite_in_p1 else "")
         ent = {"kernel": ("k_pass1<fused>: pass 1, then packing + apply_delta in the same workgroup"
-                          if (fused and kind == "pass1") else kname),
+                          if (fused and kind == "pass1") else shown),
                "avg_launch_ms": avg_s * 1e3, "launches": launches, "share_of_step": ms / 1e3 / elapsed}
         if b is not None:
             ent.update(alg_bytes_per_launch=b, achieved=b / avg_s / 1e9, frac=b / avg_s / 1e9 / HBM_PEAK_GBPS)
@@ -355,7 +359,7 @@ def roofline(sims, local_c, exch, kt, elapsed, torch, dev, rank, group, workload
         "traffic_gbs": d.get("traffic_gbs"),
         "kernels": per,
         "note": ("k_pass1v streams 8-bit heartbeat + max_version views (GS_HB8 + GS_MV8), 16 columns per lane, and "
-                 "runs pass 1's per-column rules on 4 views per 32-bit word (DESIGN.md §4)") if d["kernel"] == "k_pass1v"
+                 "runs pass 1's per-column rules on 4 views per 32-bit word (DESIGN.md §4)") if d["kernel"].startswith("k_pass1v")
                 else None,
         "step_alg_bytes": step_bytes,
         "step_achieved": step_bytes / step_s / 1e9,

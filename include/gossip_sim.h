@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define GS_API_VERSION 17
+#define GS_API_VERSION 18
 #define GS_MAX_PHASES 64  /* gs_schedule_phases: phases per round */
 #define GS_TICK_US 15625u
 #define GS_NONE 0xFFFFFFFFu
@@ -238,7 +238,11 @@ typedef struct gs_counters {
                                   bytes, times of death, ring entries, the report planes they replayed */
     uint64_t hb_escapes;       /* owner columns moved to 16-bit escape slots by lag sweeps (gs_config.esc_cols) */
     uint64_t hb_releases;      /* escaped owner columns moved back to 8-bit views */
-    uint64_t reserved[2];
+    uint64_t pack_groups_max;  /* a MAXIMUM, not a sum: the most groups of 64 stale owners one (exchange, direction)
+                                  slot's exact packer walked (evaluated or skipped) in one phase since the reset */
+    uint64_t pack_steps_max;   /* a MAXIMUM: the longest dependent walk of one slot -- groups evaluated, batches of
+                                  groups skipped in first-fit continuation, bitmap windows -- the packer's
+                                  critical path */
 } gs_counters;
 
 /* Failure-detector membership census (gs_fd_census): (observer, target) pairs with the observer up and
@@ -337,6 +341,15 @@ int gs_phase_overflow(gs_handle *h, uint32_t n, const uint64_t *slice_bytes_all,
 int gs_phase_chain(gs_handle *h, const int32_t *initiators, const int32_t *responders, uint32_t n, uint32_t tick,
                    uint32_t step, const uint32_t *list, uint32_t count, const uint64_t *chain_all, uint64_t *chain,
                    uint64_t *chainc, const uint64_t *slice_bytes_all);
+
+/* The state after a chain step, read back in one wait (aiocluster_amd/shard.py's driver; the library's own sliced
+ * phases do the same): *pending = the listed slots still pending summed over the slices (entry `count` of each
+ * slice's row of chain_all, rows of count + 1 entries -- or of GS_CHAIN_CAP + 1 with count = GS_CHAIN_DEVICE, whose
+ * count is gs_phase_overflow's device count at the tail of `list`), UINT64_MAX when that device count exceeds
+ * GS_CHAIN_CAP (the device step did not run); *count_out = the count.  Replaces shard.py's torch reductions and
+ * read (round 5): one small kernel writing a pinned host pair, one stream wait. */
+int gs_phase_pending(gs_handle *h, uint32_t n, const uint32_t *list, uint32_t count, const uint64_t *chain_all,
+                     uint64_t *pending, uint32_t *count_out);
 /* count = GS_CHAIN_DEVICE: the count is not read back -- the kernels take it from `list` (gs_phase_overflow's count
  * entry), every slice gathered GS_CHAIN_CAP + 1 entries of its chainc into chain_all[G][GS_CHAIN_CAP + 1], and a
  * phase whose count exceeds GS_CHAIN_CAP is left to the host path (the step does nothing on any slice).  Lets a

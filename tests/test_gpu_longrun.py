@@ -26,14 +26,15 @@ from aiocluster_amd.workload import WorkloadSpec, liveness_tick, phase_tick, rou
 pytestmark = pytest.mark.gpu
 
 
-def _scenario(n, k, rounds, seed):
-    spec = WorkloadSpec(n=n, k=k, fanout=3, seed=seed, init="warm", write_frac=0.05, down_frac=0.05, down_rounds=3)
+def _scenario(n, k, rounds, seed, fanout=3):
+    spec = WorkloadSpec(n=n, k=k, fanout=fanout, seed=seed, init="warm", write_frac=0.05, down_frac=0.05,
+                        down_rounds=3)
     return make_scenario(f"long{n}", spec, rounds)
 
 
 def _round(gpu, orc, sel, scen, r):
     """Round r: the scenario's writes and up mask, the device's peer selection; the oracle replays the same
-    phases.  Returns the round's phase count."""
+    phases.  Returns (the round's phase count, its selected exchanges left unscheduled)."""
     rd = scen["rounds"][r]
     t = round_tick(r)
     up = np.asarray(rd["up"], dtype=np.uint8)
@@ -46,8 +47,9 @@ def _round(gpu, orc, sel, scen, r):
     if orc is not None:
         orc.begin_round(t, up)
     sel.select(up_dev, r)  # live / dead sets of the previous round's liveness (server.py:448-469)
+    # the first rounds after a warm start route every node's pick to the 8 seeds, more exchanges than 62 phases
+    # hold: those are counted (not run, on both sides), as in the bench's peer_select leg
     phases, _, left = sel.schedule(up_dev, r)
-    assert left == 0, f"round {r}: {left} selected exchanges unscheduled"
     sets = sel.scheduled_pairs(phases) if orc is not None else None
     for p, (a, b, _) in enumerate(phases):
         gpu.run_phase_arrays(phase_tick(r, p), a, b)
@@ -56,18 +58,24 @@ def _round(gpu, orc, sel, scen, r):
     gpu.update_node_liveness(liveness_tick(r, len(phases)), up_dev)
     if orc is not None:
         orc.liveness(liveness_tick(r, len(phases)), up, r)
-    return len(phases)
+    return len(phases), left
 
 
-def test_hb8mv8_160_selected_rounds_at_2048_whole_array_matches_oracle():
-    n, k, rounds, every = 2048, 16, 160, 10
-    scen = _scenario(n, k, rounds, seed=7)
+# (nodes, fanout, rounds, compare every): the seeds become hubs while the live sets are empty; at 2,048 nodes with
+# fanout 3 the hub lags stay below the escape bound (no escape, tools/esc_probe.py r5e), with fanout 1 -- or at
+# 4,096 nodes with fanout 3 -- all 8 seed columns escape and are released (r5e)
+@pytest.mark.parametrize("n,fanout,rounds,every", [(2048, 1, 160, 10), (4096, 3, 60, 20)])
+def test_hb8mv8_selected_rounds_whole_array_matches_oracle(n, fanout, rounds, every):
+    k = 16
+    scen = _scenario(n, k, rounds, seed=7, fanout=fanout)
     gpu = make_backend(GossipSim, scen, tombstones=False, fd_ring=False, hb8=True, mv8=True)
     orc = make_backend(OracleSim, scen, threads=min(16, os.cpu_count() or 1))
-    sel = PeerSelector(gpu, fanout=3, seeds=list(range(0, n, n // 8)), seed=7)
-    phases, compared, escaped_max = [], 0, 0
+    sel = PeerSelector(gpu, fanout=fanout, seeds=list(range(0, n, n // 8)), seed=7)
+    phases, compared, escaped_max, unscheduled = [], 0, 0, 0
     for r in range(rounds):
-        phases.append(_round(gpu, orc, sel, scen, r))
+        ph, left = _round(gpu, orc, sel, scen, r)
+        phases.append(ph)
+        unscheduled += left
         esc = int((gpu.region("ESC_SLOT", gpu.torch.int32, (gpu.np_,)) != -1).sum().item())
         escaped_max = max(escaped_max, esc)
         if (r + 1) % every == 0 or r == rounds - 1:
@@ -77,7 +85,8 @@ def test_hb8mv8_160_selected_rounds_at_2048_whole_array_matches_oracle():
     gpu.check_heartbeat_lag()
     c = gpu.check()  # raises on any err_* (err_hb_lag: a sweep found no free escape slot)
     print(f"phases/round {min(phases)}-{max(phases)}, escapes {c['hb_escapes']}, releases {c['hb_releases']}, "
-          f"max escaped columns {escaped_max}, lag sweeps {c['lag_sweeps']}, whole-array compares {compared}")
+          f"max escaped columns {escaped_max}, lag sweeps {c['lag_sweeps']}, whole-array compares {compared}, "
+          f"unscheduled exchanges {unscheduled}")
     assert c["hb_escapes"] > 0 and c["hb_releases"] > 0, c
     assert c["exchanges"] == orc.stats()["exchanges"]
     assert compared == rounds // every
@@ -89,9 +98,9 @@ def test_hb8mv8_without_free_escape_slots_raises_err_hb_lag():
     """The same selected rounds with one escape slot: the hub columns outnumber it, so a sweep finds a view
     lagging >= 2^7 with no slot free and counts err_hb_lag -- the run is reported inexact, never silently wrong."""
     n, k, rounds = 2048, 16, 40
-    scen = _scenario(n, k, rounds, seed=7)
+    scen = _scenario(n, k, rounds, seed=7, fanout=1)
     gpu = make_backend(GossipSim, scen, tombstones=False, fd_ring=False, hb8=True, mv8=True, esc_cols=1)
-    sel = PeerSelector(gpu, fanout=3, seeds=list(range(0, n, n // 8)), seed=7)
+    sel = PeerSelector(gpu, fanout=1, seeds=list(range(0, n, n // 8)), seed=7)
     for r in range(rounds):
         _round(gpu, None, sel, scen, r)
         if gpu.counters()["err_hb_lag"]:

@@ -94,6 +94,14 @@ class ToySlice:
             flat[slot] = chainc[i] = enc(S, tail, stop)
         chainc[count] = sum(int(flat[int(list_buf[i])]) == CHAIN_PENDING for i in range(count))
 
+    def phase_pending(self, n, list_buf, count, chain_all):
+        """gs_phase_pending: (pending slots summed over the slices, or -1 above the device cap; the count)"""
+        if count == GS_CHAIN_DEVICE:
+            count = int(list_buf[-1])
+            if count > GS_CHAIN_CAP:
+                return -1, count
+        return int(chain_all[:, count].sum()), count
+
     def phase_count(self, t, ini, res):
         """slice totals: bytes | the smallest candidate << 40 (0xFFFFFF: none), as gs_phase_count"""
         n = int(ini.numel())
@@ -212,7 +220,7 @@ def _gloo_worker(rank, world, port, q):
         steps = run_sliced_phase([s], DistComm(), MTU, 0, ini, ini)
         counters = DistComm().sum_counters([{k: rank + 1 for k in __import__("aiocluster_amd._lib").
                                              _lib.COUNTER_FIELDS}])
-        q.put((rank, steps, {k: v for k, v in s.sent.items()}, counters["exchanges"]))
+        q.put((rank, steps, {k: v for k, v in s.sent.items()}, (counters["exchanges"], counters["pack_steps_max"])))
     finally:
         dist.destroy_process_group()
 
@@ -244,6 +252,7 @@ def test_chain_protocol_gloo(world):
     steps0 = res[0][1]
     for (rank, steps, sent, ex), s in zip(res, slices):
         assert steps == steps0 and 2 <= steps <= world  # the same stop on every rank
-        assert ex == world * (world + 1) // 2  # 1 + 2 + ... summed over the ranks
+        assert ex[0] == world * (world + 1) // 2  # 1 + 2 + ... summed over the ranks
+        assert ex[1] == world  # a maximum counter: the largest over the ranks, not the sum
         s.sent = sent
     check(slices, cands, world, n)

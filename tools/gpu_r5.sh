@@ -1,12 +1,12 @@
 #!/bin/bash
 # Round-5 GPU call (gpurun): optional GPU tests, then named bench runs, each under its own limit; the first
 # failure ends the call.
-#   TAG=<tag> [TESTS="<pytest args>"] RUNS="name:ENV=V,ENV=V:<bench args>;name2::<bench args>" bash tools/gpu_r5.sh
+#   TAG=<tag> [TESTS="<pytest args>"] [KEXPR="<pytest -k expression>"] RUNS="name:ENV=V,ENV=V:<bench args>;name2::<bench args>" bash tools/gpu_r5.sh
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 O=gpurun_out/$TAG; mkdir -p $O
 if [ -n "$TESTS" ]; then
-  timeout -k 10 1000 python -u -m pytest $TESTS -m gpu -x -v --durations=15 --timeout 400 --timeout-method thread > $O/gpu_tests.log 2>&1 || { tail -40 $O/gpu_tests.log; exit 1; }
+  timeout -k 10 1000 python -u -m pytest $TESTS ${KEXPR:+-k "$KEXPR"} -m gpu -x -v --durations=15 --timeout 400 --timeout-method thread > $O/gpu_tests.log 2>&1 || { tail -40 $O/gpu_tests.log; exit 1; }
   tail -18 $O/gpu_tests.log
 fi
 summ() {
