@@ -805,16 +805,33 @@ __device__ inline bool rec_fast(uint32_t mvw) { return !(mvw & (MV_INEXACT | (MV
 // from / max_version varints and the owner's smallest kv field over all its writes (GS_R_VLOG entry 0,
 // two L2-resident tables).  A candidate whose bound exceeds the budget cannot be sent (not even
 // truncated) and is skipped without its evaluation's round trips (returning nodes scan thousands).
-// Round 5: a candidate one write behind (ms = mr + 1, the common case) has exactly one kv in its NodeDelta, write
-// ms itself, so its min1 is exact from VLOG entry ms at the same one load (eval_light's kv1); the entry-0 bound was
-// loose enough that a returning node's tail walk evaluated most of its groups.  sched: the receiver's
-// digest may leave owners out (from = 0): the entry-0 bound with from = 0.
+// Round 5: a candidate at most MIN1_EXACT writes behind gets its exact min1 (eval_light's kv1: the lowest write in
+// (mr, ms] that is the latest <= ms of its key, VLOG's next-version field > ms) from those VLOG entries, loaded
+// together; the entry-0 bound (the owner's smallest kv over all its writes) is kept past that lag and for a receiver
+// whose digest may leave owners out (from = 0).  The loose bound kept most of a returning node's groups alive: about
+// a quarter of its stale owners wrote more than once while it was away (the packer's critical path).
+#ifndef MIN1_EXACT
+#define MIN1_EXACT 1u  // lags with an exact bound (VLOG entries loaded per candidate; r5l: 4 -> 143 walk steps but 0.51
+                       // ms per phase against 0.38-0.40 at 1, the loads cost every tail candidate)
+#endif
 __device__ __forceinline__ uint32_t min1_lb(const Dev &d, uint32_t j, uint32_t ms, uint32_t mr, bool sched) {
     ms &= MV_MASK;  // (flags cleared: a caller may evaluate this for a non-prefix word it then ignores)
     mr &= MV_MASK;
     const uint32_t from = sched ? 0u : mr;
-    const uint32_t v = !sched && ms == mr + 1u ? ms : 0u;
-    return msgf(msgf(d.nid_size[j]) + ufield(from) + 1u + vlen(ms) + (d.vlog[(size_t)j * d.VL + v] & 0xFFFFu));
+    const uint32_t *vl = d.vlog + (size_t)j * d.VL;
+    uint32_t kv;
+    if (!sched && ms > mr && ms - mr <= MIN1_EXACT) {
+        uint32_t e[MIN1_EXACT];
+#pragma unroll
+        for (uint32_t k = 0; k < MIN1_EXACT; k++) e[k] = vl[min(mr + 1u + k, ms)];
+        kv = e[MIN1_EXACT - 1] & 0xFFFFu;  // (write ms qualifies; entries past it repeat it)
+#pragma unroll
+        for (int k = (int)MIN1_EXACT - 1; k >= 0; k--)
+            if (mr + 1u + (uint32_t)k == ms || (mr + 1u + (uint32_t)k < ms && (e[k] >> 16) > ms)) kv = e[k] & 0xFFFFu;
+    } else {
+        kv = vl[0] & 0xFFFFu;
+    }
+    return msgf(msgf(d.nid_size[j]) + ufield(from) + 1u + vlen(ms) + kv);
 }
 
 constexpr int TAIL_B = 8;  // groups of 64 the first-fit skips (list_tail_skip, dir_tail_skip) load at once
@@ -858,6 +875,63 @@ __device__ __forceinline__ uint32_t dir_tail_skip(const Dev &d, uint32_t s, uint
     return lim;
 }
 
+// First-fit continuation over the bitmap (canonical, GS_MV8; round 5): from position p on, a stale owner whose
+// smallest-NodeDelta bound exceeds the budget R is never sent (R only shrinks), so the walk jumps to the first
+// position that may be.  Dense, a window of WIN positions per step: each lane takes 16 positions -- its bitmap
+// bits, both rows' 16 max_version bytes and the owners' own max_versions in one round trip, then the bound's two
+// table entries of its stale ones in a second -- instead of compacting them and walking them 64 at a time
+// (a node back from an absence has ~30 such windows per half after its delta is full).  Returns that position
+// (a non-prefix view is always a candidate), or cnt.
+__device__ __forceinline__ uint32_t dir_tail_scan(const Dev &d, uint32_t s, uint32_t r, bool sched, const uint32_t *bits,
+                                                  uint32_t p, uint32_t cnt, uint32_t R, WStats &st) {
+    const int lane = lane_id();
+    const uint8_t *m8 = reinterpret_cast<const uint8_t *>(d.mv);
+    for (uint32_t w = p & ~15u; w < cnt; w += WIN) {
+        const uint32_t pb = w + 16u * (uint32_t)lane;
+        uint32_t m = 0u;
+        uint4 vs = make_uint4(0u, 0u, 0u, 0u), vr = vs, M[4] = {vs, vs, vs, vs};
+        if (pb < cnt) {
+            m = (bits[pb >> 5] >> (pb & 16u)) & 0xFFFFu;
+            vs = *reinterpret_cast<const uint4 *>(m8 + pix(d, s, pb));
+            vr = *reinterpret_cast<const uint4 *>(m8 + pix(d, r, pb));
+#pragma unroll
+            for (int k = 0; k < 4; k++) M[k] = *reinterpret_cast<const uint4 *>(d.self_mv + pb + 4u * k);
+            const uint32_t lim = cnt - pb;
+            if (lim < 16u) m &= (1u << lim) - 1u;
+            if (pb < p) m &= p - pb >= 16u ? 0u : ~((1u << (p - pb)) - 1u);
+        }
+        const uint32_t sv[4] = {vs.x, vs.y, vs.z, vs.w}, rv4[4] = {vr.x, vr.y, vr.z, vr.w};
+        uint32_t keep = 0u;
+#pragma unroll
+        for (int h = 0; h < 2; h++) {  // 8 positions at a time: their bound entries in flight together
+            uint32_t lb[8];
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                const int q = 8 * h + i;
+                lb[i] = 0u;
+                if ((m >> q) & 1u) {
+                    const uint32_t Mq = (q & 3) == 0 ? M[q >> 2].x : (q & 3) == 1 ? M[q >> 2].y : (q & 3) == 2 ? M[q >> 2].z : M[q >> 2].w;
+                    const uint32_t ms = mv_dec8((sv[q >> 2] >> (8 * (q & 3))) & 0xFFu, Mq);
+                    const uint32_t mr = mv_dec8((rv4[q >> 2] >> (8 * (q & 3))) & 0xFFu, Mq);
+                    lb[i] = (ms | mr) & MV_INEXACT ? 0u : min1_lb(d, pb + (uint32_t)q, ms, mr, sched);
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < 8; i++)
+                if ((m >> (8 * h + i)) & 1u && lb[i] <= R) keep |= 1u << (8 * h + i);
+        }
+        st.stp++;
+        st.grp += (wave_sum((uint32_t)__popc(m)) + WAVE - 1u) / WAVE;
+        const uint64_t any = __ballot(keep != 0u);
+        if (any) {
+            const int l = __builtin_ctzll(any);
+            const uint32_t kq = (uint32_t)__shfl((int)keep, l, WAVE);
+            return w + 16u * (uint32_t)l + (uint32_t)__builtin_ctz(kq);
+        }
+    }
+    return cnt;
+}
+
 // Bitmap source: positions [max(p0, pmin), cnt) of the sender's dict order (p0 = 0 in the general
 // layout; a multiple of 256 otherwise; pmin > p0: the positions before it came from pass 1's records).
 template <int KW, bool GENM, bool COUNT, bool REC = false>
@@ -880,7 +954,18 @@ __device__ __forceinline__ void pack_dir(const Dev &d, uint32_t s, uint32_t r, c
     // split path, so the walk would otherwise pay one dependent round trip per window)
     uint32_t wnext = 0;
     if (!GENM && p0 + 16u * lane < cnt) wnext = bits[(p0 + 16u * lane) >> 5];
+    uint32_t pfrom = pmin;  // positions before it are not candidates (records, or skipped by dir_tail_scan)
     for (uint32_t win = p0; win < cnt && !stop; win += WIN) {
+        if (!GENM && !COUNT && !REC && tail && d.vlog && d.mv8 && pend == 0u) {
+            // first-fit continuation: jump to the first position that may still send something
+            const uint32_t q = dir_tail_scan(d, s, r, ds.sched, bits, max(win, pfrom), cnt, d.mtu - S, st);
+            if (q >= cnt) break;
+            pfrom = q;
+            if (q >= win + WIN) {
+                win = q & ~15u;
+                wnext = win + 16u * lane < cnt ? bits[(win + 16u * lane) >> 5] : 0u;
+            }
+        }
         // -- compact this window's stale owners (sender order) into wbuf, 16 positions per lane
         uint32_t m = 0;
         const uint32_t pb = win + 16u * lane;
@@ -899,7 +984,7 @@ __device__ __forceinline__ void pack_dir(const Dev &d, uint32_t s, uint32_t r, c
             }
             const uint32_t lim = cnt - pb;
             if (lim < 16) m &= (1u << lim) - 1u;
-            if (pb < pmin) m &= pmin - pb >= 16u ? 0u : ~((1u << (pmin - pb)) - 1u);
+            if (pb < pfrom) m &= pfrom - pb >= 16u ? 0u : ~((1u << (pfrom - pb)) - 1u);
         }
         const uint32_t cl = (uint32_t)__popc(m);
         const uint32_t incl = wave_incl_scan(cl);
@@ -2091,7 +2176,7 @@ __device__ __forceinline__ uint32_t lite_slot(const Dev &d, int32_t ai, int32_t 
 
 // LM >= 0: k_lite's slot work (lite_slot<LM>: 0 = one slice, 1 = a sliced count pass) runs in the same workgroup
 // after the stream, wave w taking direction w -- no k_lite launch (round 5; env GS_P1LITE=0: the launch of its own)
-template <int AHEAD, int LM>
+template <int AHEAD, int LM, bool GRP = false>
 __global__ __launch_bounds__(XB, P1V_WAVES) void k_pass1v(Dev d, const int32_t *ini, const int32_t *res, uint32_t n,
                                                           uint32_t t, uint32_t seq, SliceIO io, const GroupArgs *ga,
                                                           DevDyn dyn) {
@@ -2100,8 +2185,8 @@ __global__ __launch_bounds__(XB, P1V_WAVES) void k_pass1v(Dev d, const int32_t *
     __shared__ uint32_t s_out[XB / WAVE][P1V_K * P1V_SLOT];
     const uint32_t e = blockIdx.x;
     if (e >= n) return;
-    if (ga) {  // a slice of an in-process group (blockIdx.y)
-        group_pick(d, ga, dyn);
+    if constexpr (GRP) {  // a slice of an in-process group (blockIdx.y; its own instantiation: the Dev copy
+        group_pick(d, ga, dyn);  // costs the single-handle kernel nothing)
         io = ga->io[blockIdx.y];
     }
     // wid through readfirstlane: the half bounds, list and plane pointers derived from it stay scalar
@@ -2801,7 +2886,7 @@ __global__ __launch_bounds__(LB) void k_gather_u64(GatherPtrs p, uint32_t G, uin
 // Chain step `step` >= 1 over the overflowing slots only (gs_phase_chain): one wave per listed slot; a
 // slot still pending on this slice continues from its predecessor's gathered state (chain_all =
 // [G][count] of every slice's chainc).  State goes to both chain (by slot) and chainc (by list index).
-template <int KW>
+template <int KW, bool GRP = false>
 // Resume point (gs_phase_chain): the nearest finished predecessor f; every slice between f and this one is
 // pending, and is skipped only if it cannot add a NodeDelta after f (f's delta is complete, or that slice's
 // smallest single-kv NodeDelta exceeds the budget f left: first-fit continuation tests each owner's
@@ -2814,7 +2899,7 @@ __global__ __launch_bounds__(WAVE) void k_chain_step(Dev d, const int32_t *ini, 
                                                      DevDyn dyn) {
     __shared__ __attribute__((aligned(16))) uint16_t s_wbuf[WIN];
     const int lane = lane_id();
-    if (ga) {  // a slice of an in-process group (blockIdx.y): its own scratch
+    if constexpr (GRP) {  // a slice of an in-process group (blockIdx.y): its own scratch
         group_pick(d, ga, dyn);
         const uint32_t y = blockIdx.y;
         if (cnt_dev) cnt_dev = ga->list[y] + 2u * n + (2u * n + OVB - 1u) / OVB;
@@ -2945,14 +3030,14 @@ __device__ __forceinline__ SlotSum settle_sum(const Dev &d, uint32_t snd, uint32
 // LITE (sliced phases with Dev::lite, MODE 1 and 2): k_lite's slot work first, in the same wave, and the exact
 // count / pack only for the slots it leaves (one launch per step instead of two: a slice's kernels are short,
 // and their fixed cost per launch is what a sliced phase pays over one handle)
-template <int KW, int MODE, bool LITE = false>
+template <int KW, int MODE, bool LITE = false, bool GRP = false>
 __global__ __launch_bounds__(XB, (KW == 4 ? PK_WAVES : 1)) void k_settle(Dev d, const int32_t *ini, const int32_t *res,
                                                                         uint32_t n, uint32_t t, SliceIO io,
                                                                         const GroupArgs *ga, DevDyn dyn) {
     __shared__ __attribute__((aligned(16))) uint16_t s_wbuf[2 * WIN];
     const uint32_t e = blockIdx.x;
     if (e >= n) return;
-    if (ga) {  // a slice of an in-process group (blockIdx.y); the step comes by value
+    if constexpr (GRP) {  // a slice of an in-process group (blockIdx.y); the step comes by value
         group_pick(d, ga, dyn);
         const uint32_t step = io.step;
         io = ga->io[blockIdx.y];
@@ -3168,11 +3253,7 @@ template <int RING>
 #define LIVE_F32 1  // the phi decision's first test in binary32 (A/B: 0 = binary64 with a 2^-30 margin)
 #endif
 #ifndef LIVE_WAVES
-#define LIVE_WAVES 4  // waves per SIMD k_liveness is compiled for: 4 = 127 VGPRs, no spill with the fast path (r5e:
-                      // 12.02 ms vs 24.3 at 6 waves with 78 spills, 12.37 for round 4's code at 6 waves)
-#endif
-#ifndef LIVE_FAST
-#define LIVE_FAST 1  // round 5: the branch-free per-chunk fast path of k_liveness (0: the general path only, A/B)
+#define LIVE_WAVES 6  // waves per SIMD k_liveness is compiled for (<= 80 VGPRs: two chunks in flight)
 #endif
 #ifndef LIVE_NT
 #define LIVE_NT 1  // non-temporal loads / stores of the windows and state bytes (streamed once per round; r4c: 11.86 vs 12.21 ms)
@@ -3265,242 +3346,138 @@ __global__ __launch_bounds__(LB, LIVE_WAVES) void k_liveness(Dev d, const uint8_
             if (c0 < d.ncol) {
                 const size_t p = pix(d, o, c0);
                 // this thread's four columns: bit ph of q[i] = a report in phase ph
-                auto build_q = [&](uint32_t (&q)[4]) __attribute__((always_inline)) {
-                    q[0] = q[1] = q[2] = q[3] = 0u;
-                    if (d.pl16) {  // k_pass1v's layout: column 16 g + 4 q + i at bit 4 i + q of u16 g
-                        const uint32_t ui = (c0 & 255u) >> 4, qs = (c0 >> 2) & 3u;
-                        for (uint32_t m = vm; m; m &= m - 1u) {
-                            const uint32_t ph = (uint32_t)__builtin_ctz(m);
-                            const uint32_t u = (uint32_t)reinterpret_cast<const uint16_t *>(s_pl[wv][ph])[ui] >> qs;
-#pragma unroll
-                            for (int i = 0; i < 4; i++) q[i] |= ((u >> (4 * i)) & 1u) << ph;
-                        }
-                    } else {
-                        const uint32_t lb = plane_bit(c0);
-                        for (uint32_t m = vm; m; m &= m - 1u) {
-                            const uint32_t ph = (uint32_t)__builtin_ctz(m);
-#pragma unroll
-                            for (int i = 0; i < 4; i++) q[i] |= (uint32_t)((s_pl[wv][ph][i] >> lb) & 1ull) << ph;
-                        }
-                    }
-                };
-                uint32_t q[4];
-                build_q(q);
-                // Fast path (round 5): compact windows, no hook events, no row whose scheduled bound is recomputed,
-                // reports that telescope (max_interval >= NPL - 1 ticks): the four pairs branch-free -- selects, no
-                // per-pair exec-mask branches (the scalar unit's issue, shared by the CU's waves, was a third of the
-                // sweep's instruction stream) -- and committed unless some lane meets a rare case (a compact window
-                // that would fill up, a phi decision within the binary32 margin): then the whole chunk takes the
-                // general path below, from the same loaded values.
-                // the general path (every layout and case), on the chunk's values sc4, l4, s4 and report masks q
-                auto general = [&](const uint4 sc4, const uint2 l4, const uint32_t s4, const uint32_t (&q)[4])
-                                   __attribute__((always_inline)) {
-                    uint32_t sc[4] = {sc4.x, sc4.y, sc4.z, sc4.w};
-                    uint32_t lt[4] = {l4.x & 0xFFFFu, l4.x >> 16, l4.y & 0xFFFFu, l4.y >> 16};
-                    bool dw = false;
-                    uint32_t td[4] = {NONE, NONE, NONE, NONE};
-                    if (exact && (s4 & 0x02020202u)) { ld4(d.tod + p, td); alg += 16; }
-                    uint32_t s4n = s4;
-            #pragma unroll
-                    for (int i = 0; i < 4; i++) {
-                        uint32_t st = (s4 >> (8 * i)) & 0xFFu;
-                        Fd f = fd_get(d, st, lt[i], sc[i], t);  // t is at or after every report tick of this round
-                        uint32_t m = q[i];  // only if vm != 0: then the window was loaded
-                        if (m) {
-                            // report_heartbeat at ticks t_round + 1 + p for the phases p of m (failure_detector.py:32-38):
-                            // intervals between reports of one round are < NPL ticks, so with max_interval >= NPL - 1 all
-                            // but the first are appended and they telescope: (k - 1) intervals summing to p_last - p_first,
-                            // plus the first one if it is <= max_interval; a compact window that would fill up, and the
-                            // rings (their intervals one by one), replay report by report
-                            bool loop = (RING && rrow) || d.max_iv < NPL - 1u;
-                            if (!loop) {
-                                const uint32_t p1 = (uint32_t)__builtin_ctz(m), pk = 31u - (uint32_t)__builtin_clz(m);
-                                uint32_t app = (uint32_t)__popc(m) - 1u, add = pk - p1;
-                                if (f.last != NONE) {
-                                    const uint32_t iv = d.t_round + 1u + p1 - f.last;
-                                    if (iv <= d.max_iv) { app++; add += iv; }
-                                }
-                                if (f.cnt + app <= d.W) {
-                                    f.cnt += app;
-                                    f.sum += add;
-                                    f.last = d.t_round + 1u + pk;
-                                } else {
-                                    loop = true;
-                                }
-                            }
-                            if (loop) {
-                                while (m) {
-                                    const uint32_t bb = (uint32_t)__builtin_ctz(m);
-                                    m &= m - 1u;
-                                    f = fd_report_val(d, RING && rrow ? rrow + (size_t)(c0 + i) * d.W : nullptr, d.t_round + 1u + bb,
-                                                      f, alg, ovf);
-                                }
-                            }
-                            dw = true;
-                        }
-                        const uint32_t j = c0 + i;
-                        if (upo && j < d.ncol && d.col_lo + j != o && !(genm && ps[i] == NONE)) {
-                            live++;
-                            const bool has = f.last != NONE;
-                            const uint32_t len = RING && rrow ? (f.cnt < d.W ? f.cnt : d.W) : f.cnt;
-                            bool alive = false;
-                            if (has && len) {
-                                // phi <= threshold (failure_detector.py:43-53, 97-98) decided without the two binary64
-                                // divisions when it is clear by a margin: phi ~ elapsed (len + 5) / (sum + 5 prior) in
-                                // ticks.  First in binary32 (full rate: elapsed < 2^24 ticks, len + 5 and sum < 2^24 are
-                                // exact, the three roundings and the two constants' add < 2^-21 relative) with a 2^-20
-                                // margin, then in binary64 with 2^-30 (far above its rounding), the exact expression
-                                // otherwise
-            #if LIVE_F32
-                                const float lf = (float)(t - f.last) * (float)(len + 5u);
-                                const float rf = d.phi_thr_f * ((float)f.sum + d.prior5t_f);
-                                if (lf < rf * (1.0f - 0x1p-20f)) {
-                                    alive = true;
-                                } else if (!(lf > rf * (1.0f + 0x1p-20f))) {  // too close: the exact expression
-            #else
-                                const double lhs = (double)(t - f.last) * (double)(len + 5u);  // exact: < 2^43
-                                const double rhs = d.phi_thr * ((double)f.sum + d.prior5t);
-                                if (lhs < rhs * (1.0 - 0x1p-30)) {
-                                    alive = true;
-                                } else if (!(lhs > rhs * (1.0 + 0x1p-30))) {
-            #endif
-                                    const double mean = ((double)f.sum * TICK_S + d.prior5) / ((double)len + 5.0);
-                                    alive = ((double)(t - f.last) * TICK_S) / mean <= d.phi_thr;
-                                }
-                            }
-                            const uint32_t mb = st & FD_MEMB;
-                            // node join / leave: the live set against the previous call's (server.py:611-616)
-                            if (d.ev && alive != (mb == FD_LIVE))
-                                emit_event(d, o, d.col_lo + j, (alive ? EV_JOIN : EV_LEAVE) << 8, 0u, 0u, t, 0u);
-                            uint32_t sn = FD_LIVE;
-                            if (!alive) {
-                                sn = FD_DEAD;
-                                uint32_t tod = td[i];  // loaded for the dead pairs of a row being recomputed
-                                if (mb != FD_DEAD) { tod = t; d.tod[p + i] = t; alg += 4; }  // time_of_death recorded once
-                                if (has && (f.sum | f.cnt)) { f.sum = f.cnt = 0u; dw = true; }  // reset
-                                if (mb != FD_DEAD || exact) {
-                                    const uint32_t sat = tod + d.sched_delay;
-                                    if (sat < minS) minS = sat;
-                                }
-                                if (exact && (uint64_t)t >= (uint64_t)tod + d.dead_grace) gcdue++;
-                            }
-                            st = (st & ~(uint32_t)FD_MEMB) | sn;
-                        }
-                        // a window whose last report is >= FD_OLD_AGE old keeps only that fact (fd_get)
-                        if ((st & (FD_WIN | FD_OLD)) == FD_WIN && t - f.last >= FD_OLD_AGE) st |= FD_OLD;
-                        if (q[i]) st = fd_st(st, f);
-                        sc[i] = fd_sc(d, f);
-                        lt[i] = f.last & 0xFFFFu;
-                        s4n = (s4n & ~(0xFFu << (8 * i))) | (st << (8 * i));
-                    }
-                    if (dw) {
-                        if (LIVE_NT) {
-                            __builtin_nontemporal_store(v4u_t{sc[0], sc[1], sc[2], sc[3]}, reinterpret_cast<v4u_t *>(d.fd + p));
-                            __builtin_nontemporal_store(v2u_t{lt[0] | (lt[1] << 16), lt[2] | (lt[3] << 16)},
-                                                        reinterpret_cast<v2u_t *>(d.fd_last + p));
-                        } else {
-                            *reinterpret_cast<uint4 *>(d.fd + p) = make_uint4(sc[0], sc[1], sc[2], sc[3]);
-                            *reinterpret_cast<uint2 *>(d.fd_last + p) = make_uint2(lt[0] | (lt[1] << 16), lt[2] | (lt[3] << 16));
-                        }
-                        alg += 24;
-                    }
-                    if (s4n != s4) {
-                        if (LIVE_NT) __builtin_nontemporal_store(s4n, reinterpret_cast<uint32_t *>(d.fd_state + p));
-                        else *reinterpret_cast<uint32_t *>(d.fd_state + p) = s4n;
-                        alg += 4;
-                    }
-                    if (upo || vm) alg += 28;  // the four windows (sum | cnt, last tick) and state bytes read
-                };
-                bool done = false;  // (fast path committed)
-                uint4 gsc;          // the general path's inputs
-                uint2 gl;
-                uint32_t gs;
-                if (LIVE_FAST && RING == 0 && !exact && !genm && !d.ev && d.max_iv >= NPL - 1u) {
-                    const uint32_t sci[4] = {sc4.x, sc4.y, sc4.z, sc4.w};
-                    const uint32_t lti[4] = {l4.x & 0xFFFFu, l4.x >> 16, l4.y & 0xFFFFu, l4.y >> 16};
-                    uint32_t fsc[4], flt[4], fs4 = s4, flv = 0u, fmS = NONE;
-                    bool fdw = false, rare = false, nd[4];
-#pragma unroll
-                    for (int i = 0; i < 4; i++) {
-                        uint32_t st = (s4 >> (8 * i)) & 0xFFu;
-                        // fd_get as selects: last = NONE without a window, t - 2^15 for an old one
-                        const uint32_t l_dec = t - ((t - lti[i]) & 0xFFFFu);
-                        const uint32_t l_old = (st & FD_OLD) ? t - FD_OLD_AGE : l_dec;
-                        Fd f{(st & FD_WIN) ? l_old : NONE, sci[i] & ((1u << d.sum_bits) - 1u), sci[i] >> d.sum_bits};
-                        const uint32_t m = q[i];
-                        const bool hm = m != 0u;
-                        // telescoped replay (as the general path): ctz / highest bit of m, guarded for m = 0
-                        const uint32_t p1 = (uint32_t)__builtin_ctz(m | 0x80000000u);
-                        const uint32_t pk = 31u - (uint32_t)__builtin_clz(m | 1u);
-                        const uint32_t iv = d.t_round + 1u + p1 - f.last;
-                        const bool fo = f.last != NONE && iv <= d.max_iv;
-                        const uint32_t app = (uint32_t)__popc(m) - 1u + (fo ? 1u : 0u);
-                        const uint32_t add = pk - p1 + (fo ? iv : 0u);
-                        rare |= hm && f.cnt + app > d.W;
-                        f.cnt = hm ? f.cnt + app : f.cnt;
-                        f.sum = hm ? f.sum + add : f.sum;
-                        f.last = hm ? d.t_round + 1u + pk : f.last;
-                        fdw |= hm;
-                        const uint32_t j = c0 + i;
-                        const bool vp = upo & (j < d.ncol) & (d.col_lo + j != o);  // (canonical: every column known)
-                        flv += vp ? 1u : 0u;
-                        const bool hl = f.last != NONE && f.cnt != 0u;
-                        const float lf = (float)(t - f.last) * (float)(f.cnt + 5u);
-                        const float rf = d.phi_thr_f * ((float)f.sum + d.prior5t_f);
-                        const bool al = hl && lf < rf * (1.0f - 0x1p-20f);
-                        rare |= vp && hl && !al && !(lf > rf * (1.0f + 0x1p-20f));
-                        const uint32_t mb = st & FD_MEMB;
-                        nd[i] = vp && !al && mb != FD_DEAD;  // a new death: time_of_death recorded once
-                        fmS = nd[i] ? min(fmS, t + d.sched_delay) : fmS;
-                        const bool rst = vp && !al && f.last != NONE && (f.sum | f.cnt);  // reset
-                        f.sum = rst ? 0u : f.sum;
-                        f.cnt = rst ? 0u : f.cnt;
-                        fdw |= rst;
-                        st = vp ? ((st & ~(uint32_t)FD_MEMB) | (al ? (uint32_t)FD_LIVE : (uint32_t)FD_DEAD)) : st;
-                        st = ((st & (FD_WIN | FD_OLD)) == FD_WIN && t - f.last >= FD_OLD_AGE) ? st | FD_OLD : st;
-                        st = hm ? fd_st(st, f) : st;
-                        fsc[i] = fd_sc(d, f);
-                        flt[i] = f.last & 0xFFFFu;
-                        fs4 = (fs4 & ~(0xFFu << (8 * i))) | (st << (8 * i));
-                    }
-                    if (__ballot(rare) == 0ull) {
-                        done = true;
-                        if (fdw) {
-                            if (LIVE_NT) {
-                                __builtin_nontemporal_store(v4u_t{fsc[0], fsc[1], fsc[2], fsc[3]}, reinterpret_cast<v4u_t *>(d.fd + p));
-                                __builtin_nontemporal_store(v2u_t{flt[0] | (flt[1] << 16), flt[2] | (flt[3] << 16)},
-                                                            reinterpret_cast<v2u_t *>(d.fd_last + p));
-                            } else {
-                                *reinterpret_cast<uint4 *>(d.fd + p) = make_uint4(fsc[0], fsc[1], fsc[2], fsc[3]);
-                                *reinterpret_cast<uint2 *>(d.fd_last + p) = make_uint2(flt[0] | (flt[1] << 16), flt[2] | (flt[3] << 16));
-                            }
-                            alg += 24;
-                        }
-                        if (fs4 != s4) {
-                            if (LIVE_NT) __builtin_nontemporal_store(fs4, reinterpret_cast<uint32_t *>(d.fd_state + p));
-                            else *reinterpret_cast<uint32_t *>(d.fd_state + p) = fs4;
-                            alg += 4;
-                        }
-#pragma unroll
-                        for (int i = 0; i < 4; i++)
-                            if (nd[i]) { d.tod[p + i] = t; alg += 4; }
-                        live += flv;
-                        minS = min(minS, fmS);
-                        if (upo || vm) alg += 28;
-                    } else {
-                        // rare: the general path below on values reloaded here (nothing of this chunk was stored),
-                        // so the fast path's inputs need not stay live across it
-                        gsc = *reinterpret_cast<const uint4 *>(d.fd + p);
-                        gl = *reinterpret_cast<const uint2 *>(d.fd_last + p);
-                        gs = *reinterpret_cast<const uint32_t *>(d.fd_state + p);
-                        build_q(q);
+                uint32_t q[4] = {0u, 0u, 0u, 0u};
+                if (d.pl16) {  // k_pass1v's layout: column 16 g + 4 q + i at bit 4 i + q of u16 g
+                    const uint32_t ui = (c0 & 255u) >> 4, qs = (c0 >> 2) & 3u;
+                    for (uint32_t m = vm; m; m &= m - 1u) {
+                        const uint32_t ph = (uint32_t)__builtin_ctz(m);
+                        const uint32_t u = (uint32_t)reinterpret_cast<const uint16_t *>(s_pl[wv][ph])[ui] >> qs;
+        #pragma unroll
+                        for (int i = 0; i < 4; i++) q[i] |= ((u >> (4 * i)) & 1u) << ph;
                     }
                 } else {
-                    gsc = sc4;
-                    gl = l4;
-                    gs = s4;
+                    const uint32_t lb = plane_bit(c0);
+                    for (uint32_t m = vm; m; m &= m - 1u) {
+                        const uint32_t ph = (uint32_t)__builtin_ctz(m);
+        #pragma unroll
+                        for (int i = 0; i < 4; i++) q[i] |= (uint32_t)((s_pl[wv][ph][i] >> lb) & 1ull) << ph;
+                    }
                 }
-                if (!done) general(gsc, gl, gs, q);
+                uint32_t sc[4] = {sc4.x, sc4.y, sc4.z, sc4.w};
+                uint32_t lt[4] = {l4.x & 0xFFFFu, l4.x >> 16, l4.y & 0xFFFFu, l4.y >> 16};
+                bool dw = false;
+                uint32_t td[4] = {NONE, NONE, NONE, NONE};
+                if (exact && (s4 & 0x02020202u)) { ld4(d.tod + p, td); alg += 16; }
+                uint32_t s4n = s4;
+        #pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    uint32_t st = (s4 >> (8 * i)) & 0xFFu;
+                    Fd f = fd_get(d, st, lt[i], sc[i], t);  // t is at or after every report tick of this round
+                    uint32_t m = q[i];  // only if vm != 0: then the window was loaded
+                    if (m) {
+                        // report_heartbeat at ticks t_round + 1 + p for the phases p of m (failure_detector.py:32-38):
+                        // intervals between reports of one round are < NPL ticks, so with max_interval >= NPL - 1 all
+                        // but the first are appended and they telescope: (k - 1) intervals summing to p_last - p_first,
+                        // plus the first one if it is <= max_interval; a compact window that would fill up, and the
+                        // rings (their intervals one by one), replay report by report
+                        bool loop = (RING && rrow) || d.max_iv < NPL - 1u;
+                        if (!loop) {
+                            const uint32_t p1 = (uint32_t)__builtin_ctz(m), pk = 31u - (uint32_t)__builtin_clz(m);
+                            uint32_t app = (uint32_t)__popc(m) - 1u, add = pk - p1;
+                            if (f.last != NONE) {
+                                const uint32_t iv = d.t_round + 1u + p1 - f.last;
+                                if (iv <= d.max_iv) { app++; add += iv; }
+                            }
+                            if (f.cnt + app <= d.W) {
+                                f.cnt += app;
+                                f.sum += add;
+                                f.last = d.t_round + 1u + pk;
+                            } else {
+                                loop = true;
+                            }
+                        }
+                        if (loop) {
+                            while (m) {
+                                const uint32_t bb = (uint32_t)__builtin_ctz(m);
+                                m &= m - 1u;
+                                f = fd_report_val(d, RING && rrow ? rrow + (size_t)(c0 + i) * d.W : nullptr, d.t_round + 1u + bb,
+                                                  f, alg, ovf);
+                            }
+                        }
+                        dw = true;
+                    }
+                    const uint32_t j = c0 + i;
+                    if (upo && j < d.ncol && d.col_lo + j != o && !(genm && ps[i] == NONE)) {
+                        live++;
+                        const bool has = f.last != NONE;
+                        const uint32_t len = RING && rrow ? (f.cnt < d.W ? f.cnt : d.W) : f.cnt;
+                        bool alive = false;
+                        if (has && len) {
+                            // phi <= threshold (failure_detector.py:43-53, 97-98) decided without the two binary64
+                            // divisions when it is clear by a margin: phi ~ elapsed (len + 5) / (sum + 5 prior) in
+                            // ticks.  First in binary32 (full rate: elapsed < 2^24 ticks, len + 5 and sum < 2^24 are
+                            // exact, the three roundings and the two constants' add < 2^-21 relative) with a 2^-20
+                            // margin, then in binary64 with 2^-30 (far above its rounding), the exact expression
+                            // otherwise
+        #if LIVE_F32
+                            const float lf = (float)(t - f.last) * (float)(len + 5u);
+                            const float rf = d.phi_thr_f * ((float)f.sum + d.prior5t_f);
+                            if (lf < rf * (1.0f - 0x1p-20f)) {
+                                alive = true;
+                            } else if (!(lf > rf * (1.0f + 0x1p-20f))) {  // too close: the exact expression
+        #else
+                            const double lhs = (double)(t - f.last) * (double)(len + 5u);  // exact: < 2^43
+                            const double rhs = d.phi_thr * ((double)f.sum + d.prior5t);
+                            if (lhs < rhs * (1.0 - 0x1p-30)) {
+                                alive = true;
+                            } else if (!(lhs > rhs * (1.0 + 0x1p-30))) {
+        #endif
+                                const double mean = ((double)f.sum * TICK_S + d.prior5) / ((double)len + 5.0);
+                                alive = ((double)(t - f.last) * TICK_S) / mean <= d.phi_thr;
+                            }
+                        }
+                        const uint32_t mb = st & FD_MEMB;
+                        // node join / leave: the live set against the previous call's (server.py:611-616)
+                        if (d.ev && alive != (mb == FD_LIVE))
+                            emit_event(d, o, d.col_lo + j, (alive ? EV_JOIN : EV_LEAVE) << 8, 0u, 0u, t, 0u);
+                        uint32_t sn = FD_LIVE;
+                        if (!alive) {
+                            sn = FD_DEAD;
+                            uint32_t tod = td[i];  // loaded for the dead pairs of a row being recomputed
+                            if (mb != FD_DEAD) { tod = t; d.tod[p + i] = t; alg += 4; }  // time_of_death recorded once
+                            if (has && (f.sum | f.cnt)) { f.sum = f.cnt = 0u; dw = true; }  // reset
+                            if (mb != FD_DEAD || exact) {
+                                const uint32_t sat = tod + d.sched_delay;
+                                if (sat < minS) minS = sat;
+                            }
+                            if (exact && (uint64_t)t >= (uint64_t)tod + d.dead_grace) gcdue++;
+                        }
+                        st = (st & ~(uint32_t)FD_MEMB) | sn;
+                    }
+                    // a window whose last report is >= FD_OLD_AGE old keeps only that fact (fd_get)
+                    if ((st & (FD_WIN | FD_OLD)) == FD_WIN && t - f.last >= FD_OLD_AGE) st |= FD_OLD;
+                    if (q[i]) st = fd_st(st, f);
+                    sc[i] = fd_sc(d, f);
+                    lt[i] = f.last & 0xFFFFu;
+                    s4n = (s4n & ~(0xFFu << (8 * i))) | (st << (8 * i));
+                }
+                if (dw) {
+                    if (LIVE_NT) {
+                        __builtin_nontemporal_store(v4u_t{sc[0], sc[1], sc[2], sc[3]}, reinterpret_cast<v4u_t *>(d.fd + p));
+                        __builtin_nontemporal_store(v2u_t{lt[0] | (lt[1] << 16), lt[2] | (lt[3] << 16)},
+                                                    reinterpret_cast<v2u_t *>(d.fd_last + p));
+                    } else {
+                        *reinterpret_cast<uint4 *>(d.fd + p) = make_uint4(sc[0], sc[1], sc[2], sc[3]);
+                        *reinterpret_cast<uint2 *>(d.fd_last + p) = make_uint2(lt[0] | (lt[1] << 16), lt[2] | (lt[3] << 16));
+                    }
+                    alg += 24;
+                }
+                if (s4n != s4) {
+                    if (LIVE_NT) __builtin_nontemporal_store(s4n, reinterpret_cast<uint32_t *>(d.fd_state + p));
+                    else *reinterpret_cast<uint32_t *>(d.fd_state + p) = s4n;
+                    alg += 4;
+                }
+                if (upo || vm) alg += 28;  // the four windows (sum | cnt, last tick) and state bytes read
             }
         };
         LW w0, w1;
@@ -4966,9 +4943,11 @@ int launch_pass1(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t 
     if (rc) return rc;
     if (h->d.pl16) {  // GS_MV8 record phases: the byte-parallel pass 1
         const dim3 grid(n, gx.nh);
-        if (lm == 0) k_pass1v<P1V_AHEAD, 0><<<grid, XB, 0, h->stream>>>(h->d, ini, res, n, tick, h->seq, io, gx.ga, gx.dyn);
-        else if (lm == 1) k_pass1v<P1V_AHEAD, 1><<<grid, XB, 0, h->stream>>>(h->d, ini, res, n, tick, h->seq, io, gx.ga, gx.dyn);
-        else k_pass1v<P1V_AHEAD, -1><<<grid, XB, 0, h->stream>>>(h->d, ini, res, n, tick, h->seq, io, gx.ga, gx.dyn);
+        if (gx.ga && lm == 1) k_pass1v<P1V_AHEAD, 1, true><<<grid, XB, 0, h->stream>>>(h->d, ini, res, n, tick, h->seq, io, gx.ga, gx.dyn);
+        else if (gx.ga) k_pass1v<P1V_AHEAD, -1, true><<<grid, XB, 0, h->stream>>>(h->d, ini, res, n, tick, h->seq, io, gx.ga, gx.dyn);
+        else if (lm == 0) k_pass1v<P1V_AHEAD, 0><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, h->seq, io, nullptr, DevDyn{});
+        else if (lm == 1) k_pass1v<P1V_AHEAD, 1><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, h->seq, io, nullptr, DevDyn{});
+        else k_pass1v<P1V_AHEAD, -1><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, h->seq, io, nullptr, DevDyn{});
         HIPCHK(h, hipGetLastError());
         rc = time_end(h, GS_KT_PASS1, e0);
         if (rc) return rc;
@@ -4997,8 +4976,9 @@ int launch_settle(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t
     int rc = time_begin(h, e0);
     if (rc) return rc;
     const dim3 grid(n, gx.nh);
-    if (h->KP <= 16) k_settle<4, MODE, LITE><<<grid, XB, 0, h->stream>>>(h->d, ini, res, n, tick, io, gx.ga, gx.dyn);
-    else k_settle<KWB, MODE, LITE><<<grid, XB, 0, h->stream>>>(h->d, ini, res, n, tick, io, gx.ga, gx.dyn);
+    if (gx.ga) k_settle<4, MODE, LITE, true><<<grid, XB, 0, h->stream>>>(h->d, ini, res, n, tick, io, gx.ga, gx.dyn);
+    else if (h->KP <= 16) k_settle<4, MODE, LITE><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, io, nullptr, DevDyn{});
+    else k_settle<KWB, MODE, LITE><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, io, nullptr, DevDyn{});
     HIPCHK(h, hipGetLastError());
     return time_end(h, kind, e0);
 }
@@ -5583,8 +5563,11 @@ int gather_u64(gs_handle *const *hs, uint32_t nh, uint64_t *(*src)(gs_handle *),
     if (!count) return GS_OK;
     if (nh == 1) {
         gs_handle *h = hs[0];
-        if (!h->comm) {  // GS_SLICED, one slice held alone (gs_run_phase_group): the gather is a copy
-            HIPCHK(h, hipMemcpyAsync(dst(h), src(h), count * 8, hipMemcpyDeviceToDevice, h->stream));
+        if (!h->comm) {  // one slice held alone (gs_run_phase_group): GS_SLICED's one slice, or a rehearsal of one
+            // GPU's share of a G-slice cluster, whose other slices gather as zeros (as shard.py's SoloComm)
+            if (h->G > 1) HIPCHK(h, hipMemsetAsync(dst(h), 0, (size_t)h->G * count * 8, h->stream));
+            HIPCHK(h, hipMemcpyAsync(dst(h) + (size_t)h->shard * count, src(h), count * 8, hipMemcpyDeviceToDevice,
+                                     h->stream));
             return GS_OK;
         }
         const ncclResult_t r = ncclAllGather(src(h), dst(h), count, ncclUint64, h->comm, h->stream);
@@ -5707,10 +5690,17 @@ int group_steps(gs_handle *const *hs, uint32_t nh, const int32_t *ini, const int
     gx.nh = nh;
     gx.dyn = DevDyn{h0->d.t_round, h0->d.spec, h0->d.lite, 0u};
     SliceIO io{};  // (each slice's from GroupArgs; the step by value)
-    // count: pass 1, then lite + the slice totals in one launch, which also sets the responders' small bits
-    if ((rc = launch_pass1(h0, ini, res, n, tick, -1, io, true, gx))) return rc;
+    // count: pass 1, then lite + the slice totals in one launch, which also sets the responders' small bits; env
+    // GS_GRP_P1LITE=1: the lite slot work in pass 1's epilogue instead, the count launch only for LITE_FULL slots
+    static const bool glite = [] {
+        const char *e = getenv("GS_GRP_P1LITE");
+        return e && e[0] == '1';
+    }();
+    if ((rc = launch_pass1(h0, ini, res, n, tick, glite ? 1 : -1, io, true, gx))) return rc;
     gx.dyn.p1fix = 1u;
-    if ((rc = launch_settle<1, true>(h0, ini, res, n, tick, io, GS_KT_COUNT, gx))) return rc;
+    rc = glite ? launch_settle<1>(h0, ini, res, n, tick, io, GS_KT_COUNT, gx)
+               : launch_settle<1, true>(h0, ini, res, n, tick, io, GS_KT_COUNT, gx);
+    if (rc) return rc;
     gx.dyn.p1fix = 0u;
     if ((rc = gather_u64(hs, nh, [](gs_handle *h) { return h->sc.tot; }, [](gs_handle *h) { return h->sc.tot_all; },
                          (size_t)2 * n)))
@@ -5731,7 +5721,7 @@ int group_steps(gs_handle *const *hs, uint32_t nh, const int32_t *ini, const int
         return rc;
     hipEvent_t e0 = nullptr;
     if ((rc = time_begin(h0, e0))) return rc;
-    k_chain_step<4><<<dim3(std::min<uint32_t>(GS_CHAIN_CAP, 2048u), nh), WAVE, 0, h0->stream>>>(
+    k_chain_step<4, true><<<dim3(std::min<uint32_t>(GS_CHAIN_CAP, 2048u), nh), WAVE, 0, h0->stream>>>(
         h0->d, ini, res, tick, nullptr, 0u, nullptr, nullptr, nullptr, nullptr, n, cnt0, h0->grp, gx.dyn);
     HIPCHK(h0, hipGetLastError());
     k_pending<<<dim3(1, nh), OVB, 0, h0->stream>>>(nullptr, cnt0, 0u, nullptr, nullptr, h0->grp, n);
@@ -5841,8 +5831,12 @@ int gs_run_phase_group(gs_handle *const *hs, uint32_t n_handles, const int32_t *
                        uint32_t tick) {
     if (!hs || !n_handles || !hs[0]) return GS_E_INVALID;
     gs_handle *h0 = hs[0];
-    if (n_handles != h0->G) return fail(h0, GS_E_INVALID, "gs_run_phase_group: %u handles for %u slices", n_handles, h0->G);
-    for (uint32_t i = 0; i < n_handles; i++) {
+    // every slice of the cluster, or one slice held alone (a rehearsal of one GPU's share: the others gather as
+    // zeros -- exact for that slice only when the mtu cannot bind, config 4's contract)
+    if (n_handles != h0->G && n_handles != 1)
+        return fail(h0, GS_E_INVALID, "gs_run_phase_group: %u handles for %u slices", n_handles, h0->G);
+    if (n_handles == 1 && h0->comm) return gs_run_phase(h0, ini, res, n, tick);
+    for (uint32_t i = 0; i < n_handles && n_handles > 1; i++) {
         if (!hs[i] || hs[i]->shard != i || hs[i]->G != h0->G || hs[i]->N != h0->N || hs[i]->stream != h0->stream)
             return fail(h0, GS_E_INVALID, "gs_run_phase_group: handle %u is not slice %u of this cluster on one stream", i, i);
     }

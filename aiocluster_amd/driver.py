@@ -81,8 +81,6 @@ def begin(sims, rd):
 
 def run_phases(sims, rd, events=None, group=None, phases=None):
     """The round's phases (``phases`` overrides the plan's: (a, b, n, tick) tuples)."""
-    from .shard import run_sliced_phase
-
     s0 = sims[0]
     for a, b, n, t in (rd["phases"] if phases is None else phases):
         if not n:
@@ -99,8 +97,8 @@ def run_phases(sims, rd, events=None, group=None, phases=None):
         if group is None:
             s0._chk(s0.L.gs_run_phase(s0.h, C.c_void_p(a.data_ptr()), C.c_void_p(b.data_ptr()), n, t),
                     "gs_run_phase")
-        else:
-            run_sliced_phase(sims, group.comm, group.mtu, t, a, b)
+        else:  # the group's own driver: shard.py's (its scratch kept across phases), or the library's (native)
+            group.run_phase_arrays(t, a, b)
         if events is not None:
             e1.record(s0.stream)
             events.append((e0, e1))

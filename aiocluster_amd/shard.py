@@ -274,7 +274,7 @@ class ShardGroup:
             import ctypes as C
 
             n = int(ini.numel())
-            if len(self.slices) == 1:
+            if len(self.slices) == 1 and not isinstance(self.comm, SoloComm):
                 s0._chk(s0.L.gs_run_phase(s0.h, C.c_void_p(ini.data_ptr()), C.c_void_p(res.data_ptr()), n, t),
                         "gs_run_phase")
             else:

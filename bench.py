@@ -199,6 +199,7 @@ def aggregate(exchanges: float, elapsed: float, dist=None, dev=None) -> tuple[fl
         return float(exchanges), float(elapsed)
     import torch
 
+    dev = dev if dist.get_backend() == "nccl" else "cpu"  # (gloo rehearsals: host tensors)
     ex = torch.tensor([float(exchanges)], dtype=torch.float64, device=dev)
     tm = torch.tensor([float(elapsed)], dtype=torch.float64, device=dev)
     dist.all_reduce(ex, op=dist.ReduceOp.SUM)
@@ -577,11 +578,19 @@ def main():
     import torch
 
     dist = None
+    # GS_BENCH_BACKEND=gloo: a rehearsal of the multi-rank run on fewer GPUs than ranks (ranks share devices,
+    # the gathers go through host memory) -- the bench's rank plumbing end to end, not a measurement
+    backend = os.environ.get("GS_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % max(1, torch.cuda.device_count())
     if world > 1:
         import torch.distributed as dist
 
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -616,7 +625,7 @@ def main():
         group = ShardGroup(sims, DistComm(), cfg["mtu"], native=args.native_comm)
     elif args.rehearse_slices > 1:
         sims = [GossipSim(ids, key_names(K), cfg, shards=args.rehearse_slices, shard=0, **kw)]
-        group = ShardGroup(sims, SoloComm(args.rehearse_slices), cfg["mtu"])
+        group = ShardGroup(sims, SoloComm(args.rehearse_slices), cfg["mtu"], native=args.native_comm)
     elif args.slices > 1:
         sims = [GossipSim(ids, key_names(K), cfg, shards=args.slices, shard=g, **kw) for g in range(args.slices)]
         group = ShardGroup(sims, LocalComm(args.slices), cfg["mtu"], native=args.native_comm)

@@ -365,7 +365,10 @@ int gs_phase_pending(gs_handle *h, uint32_t n, const uint32_t *list, uint32_t co
  * gs_comm_init(h, id, n_shards, shard) on its slice (ncclCommInitRank), and gs_run_phase on a sliced
  * handle runs the whole phase (one blocking host read of the overflow count, as gs_phase_overflow).
  * gs_run_phase_group: the same phase for all G slices of one cluster held by this process (one device,
- * one stream; the gathers are device copies) -- the one-GPU rehearsal and test of the same driver. */
+ * one stream; the gathers are device copies; each step one launch for all slices, grid.y = slice) -- the
+ * one-GPU rehearsal and test of the same driver.  n_handles = 1 of G > 1 slices: that slice held alone, the
+ * others' totals and chain states gathered as zeros (a timing rehearsal of one GPU's share; exact for its
+ * columns only when the mtu cannot bind, config 4's contract). */
 #define GS_COMM_ID_BYTES 128
 int gs_comm_id(void *id);
 int gs_comm_init(gs_handle *h, const void *id, uint32_t nranks, uint32_t rank);
