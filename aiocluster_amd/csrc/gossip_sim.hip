@@ -2879,8 +2879,10 @@ struct GatherPtrs {
 __global__ __launch_bounds__(LB) void k_gather_u64(GatherPtrs p, uint32_t G, uint64_t count) {
     uint64_t *dst = p.dst[blockIdx.y];
     const uint64_t total = (uint64_t)G * count;
-    for (uint64_t x = (uint64_t)blockIdx.x * LB + threadIdx.x; x < total; x += (uint64_t)gridDim.x * LB)
-        dst[x] = p.src[x / count][x % count];
+    for (uint64_t x = (uint64_t)blockIdx.x * LB + threadIdx.x; x < total; x += (uint64_t)gridDim.x * LB) {
+        const uint64_t *s = p.src[x / count];  // (null: a slice held by no one here, gathered as zeros)
+        dst[x] = s ? s[x % count] : 0ull;
+    }
 }
 
 // Chain step `step` >= 1 over the overflowing slots only (gs_phase_chain): one wave per listed slot; a
@@ -3259,16 +3261,24 @@ template <int RING>
 #define LIVE_NT 1  // non-temporal loads / stores of the windows and state bytes (streamed once per round; r4c: 11.86 vs 12.21 ms)
 #endif
 __global__ __launch_bounds__(LB, LIVE_WAVES) void k_liveness(Dev d, const uint8_t *up, uint32_t t, uint32_t chunks,
-                                                 uint32_t per, bool replay, bool decide) {
+                                                 uint32_t per, uint32_t rows, bool replay, bool decide) {
     // [wave][phase][the wave's 4 plane words of this chunk]: each wave stages and reads only its own
     // words (lane l: phase l / 2, words 2 (l % 2) + {0, 1}), so the chunks need no workgroup barrier
     __shared__ __attribute__((aligned(16))) uint64_t s_pl[LB / WAVE][NPL][4];
-    __shared__ uint32_t s_vm;
+    // a row's chunks in `groups` workgroups; or, with one group per row, `rows` consecutive rows per workgroup
+    // (a slice's short rows: the workgroup's start and its counter atomics paid once per `rows` rows)
     const uint32_t groups = (chunks + per - 1) / per;
-    const uint32_t o = blockIdx.x / groups, cb0 = (blockIdx.x % groups) * per;
+    const uint32_t ob = groups == 1u ? blockIdx.x * rows : blockIdx.x / groups;
+    const uint32_t oe = groups == 1u ? min(d.N, ob + rows) : ob + 1u;
+    const uint32_t cb0 = groups == 1u ? 0u : (blockIdx.x % groups) * per;
+    const uint32_t cb1 = min(chunks, cb0 + per);
+    const bool genm = !(d.flags & GS_CANONICAL);
+    const uint32_t wv = threadIdx.x >> 6, ln = threadIdx.x & 63u;
+    uint32_t live = 0, ovf = 0, alg = 0, gcs = 0;
+    unsigned long long plb = 0;  // report-plane bytes staged (C_LIVEB)
+    for (uint32_t o = ob; o < oe; o++) {
     const bool upo = decide && up[o] != 0;
     const bool exact = upo && (d.row[o * 4 + 3] & 2u);  // recompute row word 2 (k_reset_sched)
-    const bool genm = !(d.flags & GS_CANONICAL);
     // this row's interval rings: every row has them (RING: GS_FD_RING), or this is a sampled ring row
     uint16_t *rrow = nullptr;
     if (RING == 1) {
@@ -3277,18 +3287,11 @@ __global__ __launch_bounds__(LB, LIVE_WAVES) void k_liveness(Dev d, const uint8_
         const uint32_t rs = d.ring_slot[o];
         if (rs != NONE) rrow = d.ring + (size_t)rs * d.NP * d.W;
     }
-    uint32_t minS = NONE, live = 0, gcdue = 0, ovf = 0, alg = 0;
+    uint32_t minS = NONE, gcdue = 0;
     // phases of the current round in which row o was in an exchange (its plane rows are valid);
-    // replay = false once this round's reports were replayed (the host closes the round)
-    if (threadIdx.x < 64) {
-        const bool v = replay && threadIdx.x < NPL && d.pstamp[o * NPL + threadIdx.x] == d.t_round + 1u + threadIdx.x;
-        const uint32_t m = (uint32_t)__ballot(v);
-        if (threadIdx.x == 0) s_vm = m;
-    }
-    __syncthreads();
-    const uint32_t vm = s_vm;
-    const uint32_t cb1 = min(chunks, cb0 + per);
-    const uint32_t wv = threadIdx.x >> 6, ln = threadIdx.x & 63u;
+    // replay = false once this round's reports were replayed (the host closes the round).  Each wave
+    // ballots the stamps itself (no workgroup barrier between rows)
+    const uint32_t vm = (uint32_t)__ballot(replay && ln < NPL && d.pstamp[o * NPL + ln] == d.t_round + 1u + ln);
     // A down row without valid planes (its node was in no exchange) has nothing to replay or decide.  The
     // chunks stream double-buffered: the next chunk's windows, states and plane words are loaded (always, at
     // a clamped or shared address past the end, so that no wait counts them as absent) before the current
@@ -3488,25 +3491,31 @@ __global__ __launch_bounds__(LB, LIVE_WAVES) void k_liveness(Dev d, const uint8_
         }
     }
     // earliest scheduled-for-deletion tick of this row
-    for (int dd = 32; dd >= 1; dd >>= 1) {
-        const uint32_t y = __shfl_xor(minS, dd, WAVE);
-        if (y < minS) minS = y;
+    if (__ballot(minS != NONE)) {
+        for (int dd = 32; dd >= 1; dd >>= 1) {
+            const uint32_t y = __shfl_xor(minS, dd, WAVE);
+            if (y < minS) minS = y;
+        }
+        if (ln == 0) atomicMin(&d.row[o * 4 + 2], minS);
+    }
+    if (genm) {
+        if (__ballot(gcdue != 0) && ln == 0) atomicOr(&d.row[o * 4 + 3], 1u);  // k_fd_gc collects this row
+    } else {
+        gcs += gcdue;  // removal would break the canonical layout
+    }
+    plb += (unsigned long long)__popc(vm) * 32u * (cb1 - cb0);
     }
     // in-kernel algorithmic bytes (C_LIVEB): windows, states, times of death and ring entries read and
     // written (fd_report_val's per-report 16 B estimate is replaced by these element counts), and the
     // report planes staged (32 B per valid phase per wave and chunk)
-    const unsigned long long sl = wave_sum(live), sg = wave_sum(gcdue), so = wave_sum(ovf), sa = wave_sum(alg);
-    if ((threadIdx.x & 63) == 0) {
-        if (minS != NONE) atomicMin(&d.row[o * 4 + 2], minS);
+    const unsigned long long sl = wave_sum(live), sg = wave_sum(gcs), so = wave_sum(ovf), sa = wave_sum(alg);
+    if (ln == 0) {
         if (sl) shard_add(d, C_LIVE, sl);
-        shard_add(d, C_LIVEB, sa + (unsigned long long)__popc(vm) * 32u * (cb1 - cb0));
+        shard_add(d, C_LIVEB, sa + plb);
         // a full compact window that needed an eviction: an error, except with sampled rings, where the
         // compact rows are documented as exact only up to W intervals (fd_saturated)
         if (so) shard_add(d, d.ring_slot ? C_FDSAT : C_E_FDOVF, so);
-        if (sg) {
-            if (genm) atomicOr(&d.row[o * 4 + 3], 1u);  // k_fd_gc collects this row
-            else shard_add(d, C_E_FDGC, sg);  // removal would break the canonical layout
-        }
+        if (sg) shard_add(d, C_E_FDGC, sg);
     }
 }
 
@@ -4866,16 +4875,24 @@ int launch_liveness(gs_handle *h, const uint8_t *up, uint32_t tick, bool replay,
         const int v = e ? atoi(e) : 0;
         return v >= 1 && v <= 64 ? (uint32_t)v : (uint32_t)LIVE_PER;
     }();
+    static const uint32_t live_rows = [] {  // env GS_LIVE_ROWS: rows per workgroup when a row is one group (A/B)
+        const char *e = getenv("GS_LIVE_ROWS");
+        const int v = e ? atoi(e) : 0;
+        return v >= 1 && v <= 64 ? (uint32_t)v : 0u;
+    }();
     const uint32_t per = live_per, groups = (chunks + per - 1) / per;
+    // short rows (a slice's columns): several rows per workgroup, up to `per` chunks of work
+    const uint32_t rows = groups > 1 ? 1u : live_rows ? live_rows : std::max(1u, std::min(per / chunks, h->N / 256u));
+    const uint32_t grid = groups > 1 ? groups * h->N : (h->N + rows - 1) / rows;
     hipEvent_t e0 = nullptr;
     int rc = time_begin(h, e0);
     if (rc) return rc;
     if (h->cfg.flags & GS_FD_RING)
-        k_liveness<1><<<groups * h->N, LB, 0, h->stream>>>(h->d, up, tick, chunks, per, replay, decide);
+        k_liveness<1><<<grid, LB, 0, h->stream>>>(h->d, up, tick, chunks, per, rows, replay, decide);
     else if (h->d.ring_slot)
-        k_liveness<2><<<groups * h->N, LB, 0, h->stream>>>(h->d, up, tick, chunks, per, replay, decide);
+        k_liveness<2><<<grid, LB, 0, h->stream>>>(h->d, up, tick, chunks, per, rows, replay, decide);
     else
-        k_liveness<0><<<groups * h->N, LB, 0, h->stream>>>(h->d, up, tick, chunks, per, replay, decide);
+        k_liveness<0><<<grid, LB, 0, h->stream>>>(h->d, up, tick, chunks, per, rows, replay, decide);
     HIPCHK(h, hipGetLastError());
     return time_end(h, GS_KT_LIVENESS, e0);
 }
@@ -5565,9 +5582,15 @@ int gather_u64(gs_handle *const *hs, uint32_t nh, uint64_t *(*src)(gs_handle *),
         gs_handle *h = hs[0];
         if (!h->comm) {  // one slice held alone (gs_run_phase_group): GS_SLICED's one slice, or a rehearsal of one
             // GPU's share of a G-slice cluster, whose other slices gather as zeros (as shard.py's SoloComm)
-            if (h->G > 1) HIPCHK(h, hipMemsetAsync(dst(h), 0, (size_t)h->G * count * 8, h->stream));
-            HIPCHK(h, hipMemcpyAsync(dst(h) + (size_t)h->shard * count, src(h), count * 8, hipMemcpyDeviceToDevice,
-                                     h->stream));
+            // (one k_gather_u64 launch with null sources for the others: zeros and the copy together)
+            if (h->G > GATHER_MAX) return fail(h, GS_E_INVALID, "gather over %u slices (at most %u)", h->G, GATHER_MAX);
+            GatherPtrs p{};
+            p.src[h->shard] = src(h);
+            p.dst[0] = dst(h);
+            const uint64_t total = (uint64_t)h->G * count;
+            const uint32_t bx = (uint32_t)std::min<uint64_t>((total + LB - 1) / LB, 4096u);
+            k_gather_u64<<<dim3(bx, 1), LB, 0, h->stream>>>(p, h->G, count);
+            HIPCHK(h, hipGetLastError());
             return GS_OK;
         }
         const ncclResult_t r = ncclAllGather(src(h), dst(h), count, ncclUint64, h->comm, h->stream);
