@@ -3261,24 +3261,16 @@ template <int RING>
 #define LIVE_NT 1  // non-temporal loads / stores of the windows and state bytes (streamed once per round; r4c: 11.86 vs 12.21 ms)
 #endif
 __global__ __launch_bounds__(LB, LIVE_WAVES) void k_liveness(Dev d, const uint8_t *up, uint32_t t, uint32_t chunks,
-                                                 uint32_t per, uint32_t rows, bool replay, bool decide) {
+                                                 uint32_t per, bool replay, bool decide) {
     // [wave][phase][the wave's 4 plane words of this chunk]: each wave stages and reads only its own
     // words (lane l: phase l / 2, words 2 (l % 2) + {0, 1}), so the chunks need no workgroup barrier
     __shared__ __attribute__((aligned(16))) uint64_t s_pl[LB / WAVE][NPL][4];
-    // a row's chunks in `groups` workgroups; or, with one group per row, `rows` consecutive rows per workgroup
-    // (a slice's short rows: the workgroup's start and its counter atomics paid once per `rows` rows)
+    __shared__ uint32_t s_vm;
     const uint32_t groups = (chunks + per - 1) / per;
-    const uint32_t ob = groups == 1u ? blockIdx.x * rows : blockIdx.x / groups;
-    const uint32_t oe = groups == 1u ? min(d.N, ob + rows) : ob + 1u;
-    const uint32_t cb0 = groups == 1u ? 0u : (blockIdx.x % groups) * per;
-    const uint32_t cb1 = min(chunks, cb0 + per);
-    const bool genm = !(d.flags & GS_CANONICAL);
-    const uint32_t wv = threadIdx.x >> 6, ln = threadIdx.x & 63u;
-    uint32_t live = 0, ovf = 0, alg = 0, gcs = 0;
-    unsigned long long plb = 0;  // report-plane bytes staged (C_LIVEB)
-    for (uint32_t o = ob; o < oe; o++) {
+    const uint32_t o = blockIdx.x / groups, cb0 = (blockIdx.x % groups) * per;
     const bool upo = decide && up[o] != 0;
     const bool exact = upo && (d.row[o * 4 + 3] & 2u);  // recompute row word 2 (k_reset_sched)
+    const bool genm = !(d.flags & GS_CANONICAL);
     // this row's interval rings: every row has them (RING: GS_FD_RING), or this is a sampled ring row
     uint16_t *rrow = nullptr;
     if (RING == 1) {
@@ -3287,11 +3279,18 @@ __global__ __launch_bounds__(LB, LIVE_WAVES) void k_liveness(Dev d, const uint8_
         const uint32_t rs = d.ring_slot[o];
         if (rs != NONE) rrow = d.ring + (size_t)rs * d.NP * d.W;
     }
-    uint32_t minS = NONE, gcdue = 0;
+    uint32_t minS = NONE, live = 0, gcdue = 0, ovf = 0, alg = 0;
     // phases of the current round in which row o was in an exchange (its plane rows are valid);
-    // replay = false once this round's reports were replayed (the host closes the round).  Each wave
-    // ballots the stamps itself (no workgroup barrier between rows)
-    const uint32_t vm = (uint32_t)__ballot(replay && ln < NPL && d.pstamp[o * NPL + ln] == d.t_round + 1u + ln);
+    // replay = false once this round's reports were replayed (the host closes the round)
+    if (threadIdx.x < 64) {
+        const bool v = replay && threadIdx.x < NPL && d.pstamp[o * NPL + threadIdx.x] == d.t_round + 1u + threadIdx.x;
+        const uint32_t m = (uint32_t)__ballot(v);
+        if (threadIdx.x == 0) s_vm = m;
+    }
+    __syncthreads();
+    const uint32_t vm = s_vm;
+    const uint32_t cb1 = min(chunks, cb0 + per);
+    const uint32_t wv = threadIdx.x >> 6, ln = threadIdx.x & 63u;
     // A down row without valid planes (its node was in no exchange) has nothing to replay or decide.  The
     // chunks stream double-buffered: the next chunk's windows, states and plane words are loaded (always, at
     // a clamped or shared address past the end, so that no wait counts them as absent) before the current
@@ -3491,31 +3490,25 @@ __global__ __launch_bounds__(LB, LIVE_WAVES) void k_liveness(Dev d, const uint8_
         }
     }
     // earliest scheduled-for-deletion tick of this row
-    if (__ballot(minS != NONE)) {
-        for (int dd = 32; dd >= 1; dd >>= 1) {
-            const uint32_t y = __shfl_xor(minS, dd, WAVE);
-            if (y < minS) minS = y;
-        }
-        if (ln == 0) atomicMin(&d.row[o * 4 + 2], minS);
-    }
-    if (genm) {
-        if (__ballot(gcdue != 0) && ln == 0) atomicOr(&d.row[o * 4 + 3], 1u);  // k_fd_gc collects this row
-    } else {
-        gcs += gcdue;  // removal would break the canonical layout
-    }
-    plb += (unsigned long long)__popc(vm) * 32u * (cb1 - cb0);
+    for (int dd = 32; dd >= 1; dd >>= 1) {
+        const uint32_t y = __shfl_xor(minS, dd, WAVE);
+        if (y < minS) minS = y;
     }
     // in-kernel algorithmic bytes (C_LIVEB): windows, states, times of death and ring entries read and
     // written (fd_report_val's per-report 16 B estimate is replaced by these element counts), and the
     // report planes staged (32 B per valid phase per wave and chunk)
-    const unsigned long long sl = wave_sum(live), sg = wave_sum(gcs), so = wave_sum(ovf), sa = wave_sum(alg);
-    if (ln == 0) {
+    const unsigned long long sl = wave_sum(live), sg = wave_sum(gcdue), so = wave_sum(ovf), sa = wave_sum(alg);
+    if ((threadIdx.x & 63) == 0) {
+        if (minS != NONE) atomicMin(&d.row[o * 4 + 2], minS);
         if (sl) shard_add(d, C_LIVE, sl);
-        shard_add(d, C_LIVEB, sa + plb);
+        shard_add(d, C_LIVEB, sa + (unsigned long long)__popc(vm) * 32u * (cb1 - cb0));
         // a full compact window that needed an eviction: an error, except with sampled rings, where the
         // compact rows are documented as exact only up to W intervals (fd_saturated)
         if (so) shard_add(d, d.ring_slot ? C_FDSAT : C_E_FDOVF, so);
-        if (sg) shard_add(d, C_E_FDGC, sg);
+        if (sg) {
+            if (genm) atomicOr(&d.row[o * 4 + 3], 1u);  // k_fd_gc collects this row
+            else shard_add(d, C_E_FDGC, sg);  // removal would break the canonical layout
+        }
     }
 }
 
@@ -4326,7 +4319,7 @@ __global__ __launch_bounds__(LB) void k_sel_count(Dev d, const uint8_t *up, uint
 // The seed probe (server.py:700-717) of row o and the resolved picks out: thread 0 of the resolve kernels.
 __device__ void sel_seed_probe(const Dev &d, uint32_t o, uint32_t L, uint32_t D, uint32_t F, uint64_t seed,
                                uint32_t round, const int32_t *seeds, uint32_t n_seeds, const uint32_t *s_hit,
-                               int32_t *oo) {
+                               int32_t *oo, const uint32_t *pre = nullptr) {
     bool has_seed = false;
     uint32_t S = 0;
     for (uint32_t q = 0; q < n_seeds; q++) {
@@ -4337,7 +4330,11 @@ __device__ void sel_seed_probe(const Dev &d, uint32_t o, uint32_t L, uint32_t D,
     uint32_t pick = NONE;
     if (S && (!has_seed || L < S)) {
         uint32_t c[4];
-        sel_rand(seed, round, o, SEL_SEED, c);
+        if (pre) {  // (drawn earlier by another lane: the same counter, the same values)
+            for (int q = 0; q < 4; q++) c[q] = pre[q];
+        } else {
+            sel_rand(seed, round, o, SEL_SEED, c);
+        }
         const double ps = (L + D) == 0u ? 1.0 : (double)S / (double)(L + D);
         if (L == 0u || unit53(c[0], c[1]) <= ps) {
             uint32_t k = below(c[2], S);
@@ -4392,6 +4389,32 @@ __global__ __launch_bounds__(LB) void k_sel_count16(Dev d, const uint8_t *up, ui
     }
 }
 
+// Floyd's sample of k distinct ranks of [0, n) (n = L live, or P known when none is live) and the dead probe,
+// by rank, into so[0..F] (NONE where absent: so[] starts all NONE)
+// pre (optional): the draws of counters (round, o, slot) already made, pre[4 i + q] for slot i < F, then SEL_DEAD
+__device__ inline void sel_ranks(uint32_t o, uint32_t L, uint32_t D, uint32_t P, uint32_t F, uint64_t seed,
+                                 uint32_t round, uint32_t *so, const uint32_t *pre = nullptr) {
+    const uint32_t n = L ? L : P, k = F < n ? F : n;
+    uint32_t c[4];
+    for (uint32_t i = 0; i < k; i++) {
+        const uint32_t t = n - k + i;
+        if (pre) c[0] = pre[4 * i];
+        else sel_rand(seed, round, o, i, c);
+        uint32_t r = below(c[0], t + 1);
+        for (uint32_t q = 0; q < i; q++)
+            if (so[q] == r) { r = t; break; }
+        so[i] = r;
+    }
+    if (D) {
+        if (pre) {
+            for (int q = 0; q < 4; q++) c[q] = pre[4 * F + q];
+        } else {
+            sel_rand(seed, round, o, SEL_DEAD, c);
+        }
+        const double pd = (double)D / (double)(L + 1u);
+        if (pd > unit53(c[0], c[1])) so[F] = below(c[2], D);
+    }
+}
 // Floyd's sample of k distinct ranks of [0, n) and the dead probe, by rank; targets resolved next.
 // sel[o][0..F) = live (or peer) ranks, sel[o][F] = dead rank, NONE where absent.
 __global__ __launch_bounds__(LB) void k_sel_pick(Dev d, const uint8_t *up, const uint32_t *scnt, uint32_t F,
@@ -4401,22 +4424,7 @@ __global__ __launch_bounds__(LB) void k_sel_pick(Dev d, const uint8_t *up, const
     uint32_t *so = sel + (size_t)o * (F + 2);
     for (uint32_t i = 0; i < F + 2; i++) so[i] = NONE;
     if (!up[o]) return;
-    const uint32_t L = scnt[o * 4 + 0], D = scnt[o * 4 + 1], P = scnt[o * 4 + 2];
-    const uint32_t n = L ? L : P, k = F < n ? F : n;
-    uint32_t c[4];
-    for (uint32_t i = 0; i < k; i++) {
-        const uint32_t t = n - k + i;
-        sel_rand(seed, round, o, i, c);
-        uint32_t r = below(c[0], t + 1);
-        for (uint32_t q = 0; q < i; q++)
-            if (so[q] == r) { r = t; break; }
-        so[i] = r;
-    }
-    if (D) {
-        sel_rand(seed, round, o, SEL_DEAD, c);
-        const double pd = (double)D / (double)(L + 1u);
-        if (pd > unit53(c[0], c[1])) so[F] = below(c[2], D);
-    }
+    sel_ranks(o, scnt[o * 4 + 0], scnt[o * 4 + 1], scnt[o * 4 + 2], F, seed, round, so);
 }
 
 // k-th set bit (k < popc(m)) of a 16-bit mask
@@ -4490,6 +4498,134 @@ __global__ __launch_bounds__(LB) void k_sel_resolve16(Dev d, const uint8_t *up, 
         __syncthreads();
     }
     if (threadIdx.x == 0) sel_seed_probe(d, o, L, scnt[o * 4 + 1], F, seed, round, seeds, n_seeds, s_hit, oo);
+}
+
+// Canonical layout, ncol <= SEL_ROW_IT * 4096: k_sel_count16 + k_sel_pick + k_sel_resolve16 in one workgroup per
+// row that reads the row's state bytes once -- each thread keeps its 16-column live / dead masks of every
+// 4,096-column step in registers: the counts, the ranks (thread 0), then one block scan of all steps at once
+// (one barrier instead of two per step)
+constexpr uint32_t SEL_ROW_IT = 16;
+__global__ __launch_bounds__(LB, 4) void k_sel_row16(Dev d, const uint8_t *up, uint32_t F, uint64_t seed, uint32_t round,
+                                                  const int32_t *seeds, uint32_t n_seeds, uint32_t *scnt, int32_t *out) {
+    // the live / dead masks of every step in LDS (16 KB: registers would hold the occupancy to 2 waves per SIMD)
+    __shared__ uint16_t s_m[SEL_ROW_IT][2][LB];
+    __shared__ uint32_t s_w[SEL_ROW_IT][LB / WAVE][2];
+    __shared__ uint32_t s_rank[10], s_hit[10], s_cnt[2], s_rnd[10 * 4];
+    const uint32_t o = blockIdx.x;
+    int32_t *oo = out + (size_t)o * (F + 2);
+    if (!up[o]) {
+        for (uint32_t i = threadIdx.x; i < F + 2; i += LB) oo[i] = -1;
+        return;
+    }
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    if (threadIdx.x < F + 2) {  // the row's Philox draws, one lane each (thread 0 only does the arithmetic)
+        uint32_t c[4];
+        sel_rand(seed, round, o, threadIdx.x < F ? threadIdx.x : threadIdx.x == F ? SEL_DEAD : SEL_SEED, c);
+        for (int q = 0; q < 4; q++) s_rnd[4 * threadIdx.x + q] = c[q];
+    }
+    const uint8_t *row = d.fd_state + (size_t)o * d.NP;
+    const uint32_t nit = (d.ncol + LB * 16u - 1u) / (LB * 16u);
+    uint32_t L = 0, D = 0;
+#pragma unroll
+    for (uint32_t h = 0; h < SEL_ROW_IT; h += 8) {  // eight steps' loads in flight at a time
+        uint4 v[8];
+#pragma unroll
+        for (uint32_t u = 0; u < 8; u++) {
+            // unconditional (a clamped address, masked below): loads under a branch would be waited for one by one
+            const uint32_t j0 = (h + u) * LB * 16u + threadIdx.x * 16u;
+            v[u] = *reinterpret_cast<const uint4 *>(row + min(j0, d.NP - 16u));
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < 8; u++) {
+            const uint32_t it = h + u, j0 = it * LB * 16u + threadIdx.x * 16u;
+            const bool inrow = it < nit && j0 < d.ncol;
+            const uint32_t wd[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+            uint32_t a = 0u, b = 0u;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const uint32_t jq = j0 + 4u * q;
+                uint32_t keep = inrow ? 0x01010101u : 0u;  // (k_sel_count16's column mask: in range, not o's own)
+                if (jq + 4u > d.ncol) keep = jq >= d.ncol ? 0u : (keep >> (8u * (jq + 4u - d.ncol)));
+                const uint32_t js = o - d.col_lo - jq;
+                if (js < 4u) keep &= ~(0x01u << (8u * js));
+                // bit 0 of each byte -> 4 adjacent bits: bytes 0..3 times 2^21, 2^14, 2^7, 1 land on bits 21..24
+                a |= (((memb_live4(wd[q]) & keep) * 0x204081u) >> 21 & 0xFu) << (4 * q);
+                b |= (((memb_dead4(wd[q]) & keep) * 0x204081u) >> 21 & 0xFu) << (4 * q);
+            }
+            s_m[it][0][threadIdx.x] = (uint16_t)a;
+            s_m[it][1][threadIdx.x] = (uint16_t)b;
+            L += (uint32_t)__popc(a);
+            D += (uint32_t)__popc(b);
+        }
+    }
+    {
+        const unsigned long long l = wave_sum(L), dd = wave_sum(D);
+        if (lane == 0) { s_w[0][w][0] = (uint32_t)l; s_w[0][w][1] = (uint32_t)dd; }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t a = 0, b = 0;
+            for (uint32_t i = 0; i < LB / WAVE; i++) { a += s_w[0][i][0]; b += s_w[0][i][1]; }
+            const uint32_t P = d.ncol - (o - d.col_lo < d.ncol ? 1u : 0u);  // known: every column but o's own
+            scnt[o * 4 + 0] = a;
+            scnt[o * 4 + 1] = b;
+            scnt[o * 4 + 2] = P;
+            s_cnt[0] = a;
+            s_cnt[1] = b;
+            uint32_t so[10];
+            for (uint32_t i = 0; i < F + 2; i++) so[i] = NONE;
+            sel_ranks(o, a, b, P, F, seed, round, so, s_rnd);
+            for (uint32_t i = 0; i < F + 1; i++) {
+                s_rank[i] = so[i];
+                s_hit[i] = NONE;
+            }
+        }
+        __syncthreads();
+    }
+    L = s_cnt[0];
+    const bool from_live = L != 0;
+    // the pool (live, or every known column when none is live) and dead ranks of every step, one block scan
+    auto pool = [&](uint32_t it) {
+        if (from_live) return (uint32_t)s_m[it][0][threadIdx.x];
+        const uint32_t j0 = it * LB * 16u + threadIdx.x * 16u;  // every valid column
+        uint32_t m = j0 >= d.ncol ? 0u : d.ncol - j0 >= 16u ? 0xFFFFu : (1u << (d.ncol - j0)) - 1u;
+        const uint32_t js = o - d.col_lo - j0;
+        if (js < 16u) m &= ~(1u << js);
+        return m;
+    };
+    uint32_t ex[SEL_ROW_IT];  // the wave-exclusive scans: pool | dead << 16 (each < 2^10)
+#pragma unroll
+    for (uint32_t it = 0; it < SEL_ROW_IT; it++) {
+        const uint32_t c2 = (uint32_t)__popc(pool(it)) | ((uint32_t)__popc((uint32_t)s_m[it][1][threadIdx.x]) << 16);
+        const uint32_t i2 = wave_scan_dpp(c2);  // (both halves at once: no carry out of the low one)
+        ex[it] = i2 - c2;
+        if (lane == 63) { s_w[it][w][0] = i2 & 0xFFFFu; s_w[it][w][1] = i2 >> 16; }
+    }
+    __syncthreads();
+    uint32_t bp = 0, bd = 0;  // ranks before this step
+#pragma unroll
+    for (uint32_t it = 0; it < SEL_ROW_IT; it++) {  // (unrolled: ex[] stays in registers)
+        uint32_t op = bp + (ex[it] & 0xFFFFu), od = bd + (ex[it] >> 16);
+#pragma unroll
+        for (uint32_t i = 0; i < LB / WAVE; i++) {
+            const uint32_t xp = s_w[it][i][0], xd = s_w[it][i][1];
+            if (i < w) { op += xp; od += xd; }
+            bp += xp;
+            bd += xd;
+        }
+        const uint32_t j0 = it * LB * 16u + threadIdx.x * 16u;
+        const uint32_t mp = pool(it), md = s_m[it][1][threadIdx.x];
+        const uint32_t cp = (uint32_t)__popc(mp), cd = (uint32_t)__popc(md);
+        if (cp) {
+            for (uint32_t i = 0; i < F; i++) {
+                const uint32_t r = s_rank[i];
+                if (r != NONE && r >= op && r < op + cp) s_hit[i] = j0 + nth_bit16(mp, r - op);
+            }
+        }
+        const uint32_t r = s_rank[F];
+        if (cd && r != NONE && r >= od && r < od + cd) s_hit[F] = j0 + nth_bit16(md, r - od);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) sel_seed_probe(d, o, L, s_cnt[1], F, seed, round, seeds, n_seeds, s_hit, oo, s_rnd + 4 * (F + 1));
 }
 
 // Resolve ranks to node ids in column order (one workgroup per row), then the seed probe.
@@ -4614,16 +4750,35 @@ __global__ __launch_bounds__(LB) void k_luby_left(const int32_t *out, const uint
     const unsigned long long m = __ballot(l);
     if ((threadIdx.x & 63) == 0 && m) atomicAdd(left, (uint32_t)__popcll(m));
 }
-// scatter the scheduled exchanges into per-phase (initiator, responder) arrays
+// scatter the scheduled exchanges into per-phase (initiator, responder) arrays: each workgroup ranks its
+// SCAT_PER x LB exchanges per phase in LDS and takes one range per phase with a single global atomic (a
+// returning atomic per exchange, or per wave and phase, serialises on the 16 or so phase counters: 0.59 ms)
+constexpr uint32_t SCAT_PER = 4;
 __global__ __launch_bounds__(LB) void k_luby_scatter(const int32_t *out, const uint32_t *eph, uint32_t E, uint32_t F,
                                                      const uint32_t *poff, uint32_t *pfill, int32_t *ini,
                                                      int32_t *res) {
-    const uint32_t e = blockIdx.x * LB + threadIdx.x;
-    if (e >= E || eph[e] == NONE) return;
-    const uint32_t p = eph[e];
-    const uint32_t slot = poff[p] + atomicAdd(&pfill[p], 1u);
-    ini[slot] = (int32_t)(e / (F + 2));
-    res[slot] = out[e];
+    __shared__ uint32_t s_cnt[GS_MAX_PHASES], s_base[GS_MAX_PHASES];
+    if (threadIdx.x < GS_MAX_PHASES) s_cnt[threadIdx.x] = 0u;
+    __syncthreads();
+    uint32_t p[SCAT_PER], loc[SCAT_PER];
+#pragma unroll
+    for (uint32_t k = 0; k < SCAT_PER; k++) {
+        const uint32_t e = (blockIdx.x * SCAT_PER + k) * LB + threadIdx.x;
+        p[k] = e < E ? eph[e] : NONE;
+        loc[k] = p[k] != NONE ? atomicAdd(&s_cnt[p[k]], 1u) : 0u;
+    }
+    __syncthreads();
+    if (threadIdx.x < GS_MAX_PHASES && s_cnt[threadIdx.x])
+        s_base[threadIdx.x] = atomicAdd(&pfill[threadIdx.x], s_cnt[threadIdx.x]);
+    __syncthreads();
+#pragma unroll
+    for (uint32_t k = 0; k < SCAT_PER; k++) {
+        if (p[k] == NONE) continue;
+        const uint32_t e = (blockIdx.x * SCAT_PER + k) * LB + threadIdx.x;
+        const uint32_t slot = poff[p[k]] + s_base[p[k]] + loc[k];
+        ini[slot] = (int32_t)(e / (F + 2));
+        res[slot] = out[e];
+    }
 }
 
 // ------------------------------------------------------------------ measurement kernels
@@ -4875,24 +5030,16 @@ int launch_liveness(gs_handle *h, const uint8_t *up, uint32_t tick, bool replay,
         const int v = e ? atoi(e) : 0;
         return v >= 1 && v <= 64 ? (uint32_t)v : (uint32_t)LIVE_PER;
     }();
-    static const uint32_t live_rows = [] {  // env GS_LIVE_ROWS: rows per workgroup when a row is one group (A/B)
-        const char *e = getenv("GS_LIVE_ROWS");
-        const int v = e ? atoi(e) : 0;
-        return v >= 1 && v <= 64 ? (uint32_t)v : 0u;
-    }();
     const uint32_t per = live_per, groups = (chunks + per - 1) / per;
-    // short rows (a slice's columns): several rows per workgroup, up to `per` chunks of work
-    const uint32_t rows = groups > 1 ? 1u : live_rows ? live_rows : std::max(1u, std::min(per / chunks, h->N / 256u));
-    const uint32_t grid = groups > 1 ? groups * h->N : (h->N + rows - 1) / rows;
     hipEvent_t e0 = nullptr;
     int rc = time_begin(h, e0);
     if (rc) return rc;
     if (h->cfg.flags & GS_FD_RING)
-        k_liveness<1><<<grid, LB, 0, h->stream>>>(h->d, up, tick, chunks, per, rows, replay, decide);
+        k_liveness<1><<<groups * h->N, LB, 0, h->stream>>>(h->d, up, tick, chunks, per, replay, decide);
     else if (h->d.ring_slot)
-        k_liveness<2><<<grid, LB, 0, h->stream>>>(h->d, up, tick, chunks, per, rows, replay, decide);
+        k_liveness<2><<<groups * h->N, LB, 0, h->stream>>>(h->d, up, tick, chunks, per, replay, decide);
     else
-        k_liveness<0><<<grid, LB, 0, h->stream>>>(h->d, up, tick, chunks, per, rows, replay, decide);
+        k_liveness<0><<<groups * h->N, LB, 0, h->stream>>>(h->d, up, tick, chunks, per, replay, decide);
     HIPCHK(h, hipGetLastError());
     return time_end(h, GS_KT_LIVENESS, e0);
 }
@@ -6155,6 +6302,11 @@ int gs_select_peers(gs_handle *h, const uint8_t *up, uint32_t fanout, const int3
     uint32_t *scnt = (uint32_t *)scratch;
     uint32_t *sel = scnt + (size_t)h->N * 4;
     const bool canon = (h->cfg.flags & GS_CANONICAL) != 0;
+    if (canon && h->ncol <= SEL_ROW_IT * LB * 16u && !getenv("GS_SEL_SPLIT")) {  // one read of each row
+        k_sel_row16<<<h->N, LB, 0, h->stream>>>(h->d, up, fanout, seed, round, seeds, n_seeds, scnt, targets);
+        HIPCHK(h, hipGetLastError());
+        return GS_OK;
+    }
     if (canon) k_sel_count16<<<h->N, LB, 0, h->stream>>>(h->d, up, scnt);
     else k_sel_count<<<h->N, LB, 0, h->stream>>>(h->d, up, scnt);
     HIPCHK(h, hipGetLastError());
@@ -6189,9 +6341,11 @@ int gs_schedule_phases(gs_handle *h, const uint8_t *up, uint32_t fanout, const i
     const uint32_t gE = (std::max(E, N) + LB - 1) / LB;
     // the two minimum buffers alternate by the GLOBAL iteration index, so each pick resets exactly
     // the buffer the next iteration (of this phase or the next) reduces into, whatever iters is
-    uint32_t g = 0, nleft = 0;
-    for (uint32_t p0 = 0; p0 < max_phases; p0 += 16) {
-        const uint32_t p1 = std::min(max_phases, p0 + 16u);
+    uint32_t g = 0, nleft = 0, chk = 0;
+    // phases in blocks: 16 first (a round's schedule needs about 15-17 at fanout 3), then 4 at a time (the last few
+    // exchanges), each block followed by one count of the exchanges still without a phase
+    for (uint32_t p0 = 0, p1; p0 < max_phases; p0 = p1, chk++) {
+        p1 = std::min(max_phases, p0 + (p0 ? 4u : 16u));
         for (uint32_t p = p0; p < p1; p++)
             for (uint32_t it = 0; it < iters; it++, g++) {
                 unsigned long long *b0 = best + (size_t)(g & 1) * N, *b1 = best + (size_t)((g + 1) & 1) * N;
@@ -6200,11 +6354,11 @@ int gs_schedule_phases(gs_handle *h, const uint8_t *up, uint32_t fanout, const i
                 k_luby_pick<<<gE, LB, 0, s>>>(targets, up, eph, busy, b0, b1, E, N, fanout, seed, round, p, it,
                                               pcount);
             }
-        // after every 16 phases: stop once every valid exchange has a phase
-        HIPCHK(h, hipMemsetAsync(left + p0 / 16, 0, 4, s));
-        k_luby_left<<<(E + LB - 1) / LB, LB, 0, s>>>(targets, up, eph, E, fanout, left + p0 / 16);
+        // stop once every valid exchange has a phase
+        HIPCHK(h, hipMemsetAsync(left + chk, 0, 4, s));
+        k_luby_left<<<(E + LB - 1) / LB, LB, 0, s>>>(targets, up, eph, E, fanout, left + chk);
         HIPCHK(h, hipGetLastError());
-        HIPCHK(h, hipMemcpyAsync(&nleft, left + p0 / 16, 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(h, hipMemcpyAsync(&nleft, left + chk, 4, hipMemcpyDeviceToHost, s));
         HIPCHK(h, hipStreamSynchronize(s));
         if (!nleft) break;
     }
@@ -6215,7 +6369,8 @@ int gs_schedule_phases(gs_handle *h, const uint8_t *up, uint32_t fanout, const i
     off[0] = 0;
     for (uint32_t p = 0; p < max_phases; p++) off[p + 1] = off[p] + cnt[p];
     HIPCHK(h, hipMemcpyAsync(poff, off.data(), max_phases * 4, hipMemcpyHostToDevice, s));
-    k_luby_scatter<<<(E + LB - 1) / LB, LB, 0, s>>>(targets, eph, E, fanout, poff, pfill, initiators, responders);
+    k_luby_scatter<<<(E + SCAT_PER * LB - 1) / (SCAT_PER * LB), LB, 0, s>>>(targets, eph, E, fanout, poff, pfill,
+                                                                        initiators, responders);
     HIPCHK(h, hipGetLastError());
     HIPCHK(h, hipStreamSynchronize(s));
     memcpy(phase_offsets, off.data(), (max_phases + 1) * 4);
