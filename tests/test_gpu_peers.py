@@ -153,3 +153,30 @@ def test_rounds_with_many_phases_match_oracle(fanout, flushes):
     # a round replays its planes mid-round when it runs a phase more than 32 ticks after the round start
     late = sum(1 for rd in scen["rounds"] if any(len(ph) for ph in rd["phases"][32:]))
     assert c["plane_flushes"] == late and (late > 0) == flushes
+
+
+@pytest.mark.parametrize("rounds", [0, 6])
+def test_canonical_selection_past_one_scan_step_matches_restatement(rounds):
+    """k_sel_row16 (the canonical layout's counts, ranks and resolve from one read of each row) ranks a row's
+    columns in steps of 4,096: at 4,500 nodes a row spans two, the second partial, so the ranks carried from
+    the first step into the second are checked.  Round 0 (no liveness yet: every observer draws from its
+    known set) and after 6 rounds with down churn (live and dead sets, dead probes)."""
+    n = 4500
+    spec = WorkloadSpec(n=n, k=4, fanout=3, seed=5, init="warm", write_frac=0.05, down_frac=0.1, down_rounds=3)
+    scen = make_scenario(f"selstep{n}", spec, rounds + 1, {"initial_interval_s": 1.0, "phi_threshold": 3.0})
+    gpu = make_backend(GossipSim, scen, fd_ring=False)
+    assert gpu.canonical
+    for r in range(rounds):
+        replay_round(gpu, scen, r)
+    up = np.asarray(scen["rounds"][rounds]["up"], dtype=np.uint8)
+    seeds = [0, 4099, 4321]
+    sel = PeerSelector(gpu, fanout=3, seeds=seeds, seed=77)
+    got = sel.select(gpu._dev(up, gpu.torch.uint8), rounds).cpu().numpy()
+    st = gpu._host()["FD_STATE"][:, :n]  # the device's own live / dead sets (export()'s decoding)
+    live = (st == 1).astype(np.int32)
+    tod = np.where(st >= 2, st.astype(np.int64) - 2, -1)
+    want = peer_select.select_peers(live, tod, np.ones((n, n), dtype=bool), up, 3, seeds, 77, rounds)
+    assert np.array_equal(got, want)
+    if rounds:
+        assert (got[:, 3] >= 0).any()  # dead probes happened
+    gpu.close()
