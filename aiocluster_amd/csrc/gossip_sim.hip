@@ -3697,23 +3697,29 @@ __global__ __launch_bounds__(LB) void k_fd_age(Dev d, uint32_t t) {
 // < 64 versions: the bounds under which pass 1 compares two 8-bit views without their owner's value.
 // One workgroup per (row, chunk of LB x 16 columns); each thread reads 16 views (u8) or 8 (u16).
 constexpr uint32_t HOT_HB = 64, HOT_MV = 32, HOT_ROW_MIN = 16;
+// One workgroup per (LAG_ROWS consecutive observer rows, 4,096-column chunk): a row's chunk is 16 bytes per
+// region and thread, too little for a workgroup of its own (one per row: 1 M workgroups at 65,536 nodes, 4.1 ms
+// per sweep, 2.1 TB/s); the next row's views are loaded while this row's are checked.
+constexpr uint32_t LAG_ROWS = 16;
 __global__ __launch_bounds__(LB) void k_hb_lag(Dev d, uint32_t chunks) {
-    __shared__ uint32_t s_hot;
+    __shared__ uint32_t s_hot[LAG_ROWS];
+    __shared__ uint16_t s_hm[LAG_ROWS][LB];  // each row's hot views of this thread's 16 columns
     const bool genm = !(d.flags & GS_CANONICAL);
-    const uint32_t o = blockIdx.x / chunks, cb = blockIdx.x % chunks;
+    const uint32_t rb = blockIdx.x / chunks, cb = blockIdx.x % chunks;
     const uint32_t per = d.hb8 ? 16u : 8u;
     const uint32_t j0 = (cb * LB + threadIdx.x) * per;
-    uint32_t bad = 0, hot = 0;  // hot: bit k = view k of this thread's (at most 16)
-    uint32_t hotc = 0;           // ... of an escaped column: always marks the column (k_esc_plan's release test)
+    const uint32_t o0 = rb * LAG_ROWS, nrow = min(LAG_ROWS, d.N - o0);
+    uint32_t bad = 0;
+    uint32_t hotc = 0;  // views of escaped columns: always mark the column (k_esc_plan's release test)
     if (d.p1flags) {
-        if (threadIdx.x == 0) s_hot = 0u;
+        if (threadIdx.x < LAG_ROWS) s_hot[threadIdx.x] = 0u;
         __syncthreads();
     }
-    if (j0 < d.ncol) {
-        const size_t p0 = pix(d, o, j0);
-        // one 16-byte load per region: the thread's heartbeat views (and GS_MV8 max_version views)
-        // (8-bit views: streamed once per sweep, non-temporal)
-        uint4 hr, mr = make_uint4(0u, 0u, 0u, 0u);
+    // one 16-byte load per region and row: the thread's heartbeat views (and GS_MV8 max_version views)
+    // (8-bit views: streamed once per sweep, non-temporal), one row ahead
+    auto ldv = [&](uint32_t o, uint4 &hr, uint4 &mr) {
+        const size_t p0 = pix(d, o, j0 < d.ncol ? j0 : 0u);
+        mr = make_uint4(0u, 0u, 0u, 0u);
         if (d.hb8) {
             const v4u_t x = __builtin_nontemporal_load(reinterpret_cast<const v4u_t *>(reinterpret_cast<const uint8_t *>(d.hb) + p0));
             hr = make_uint4(x.x, x.y, x.z, x.w);
@@ -3724,29 +3730,48 @@ __global__ __launch_bounds__(LB) void k_hb_lag(Dev d, uint32_t chunks) {
             const v4u_t x = __builtin_nontemporal_load(reinterpret_cast<const v4u_t *>(reinterpret_cast<const uint8_t *>(d.mv) + p0));
             mr = make_uint4(x.x, x.y, x.z, x.w);
         }
+    };
+    uint4 nh, nm;
+    ldv(o0, nh, nm);
+    // the headline's layout (canonical, GS_HB8 + GS_MV8): four views per 32-bit word against the owners'
+    // packed own values (SELF_PK: heartbeat mod 2^8 in byte 0, max_version in the high half), per-byte
+    // lags with borrow-isolated subtracts; only escaped columns and escape requests go column by column.
+    // The owners' values and escape slots are the same for every row: loaded once (L2 reads 4x the rows' bytes)
+    const bool swar = !genm && d.hb8 && d.mv8 && d.self_pk;
+    uint32_t own8v[4] = {0u, 0u, 0u, 0u}, owm7v[4] = {0u, 0u, 0u, 0u}, vm7v[4] = {0u, 0u, 0u, 0u}, esc7v[4] = {0u, 0u, 0u, 0u};
+    uint32_t esv[4][4];
+#pragma unroll
+    for (uint32_t q = 0; q < 4u; q++) {
+        const uint32_t jq = j0 + 4u * q;
+#pragma unroll
+        for (uint32_t i = 0; i < 4; i++) esv[q][i] = NONE;
+        if (!swar || jq >= d.ncol) continue;  // (vm7v[q] = 0: the step's bits all clear)
+        const uint4 pk = *reinterpret_cast<const uint4 *>(d.self_pk + jq);
+        own8v[q] = (pk.x & 0xFFu) | ((pk.y & 0xFFu) << 8) | ((pk.z & 0xFFu) << 16) | (pk.w << 24);
+        owm7v[q] = ((pk.x >> 16) & 0x7Fu) | (((pk.y >> 16) & 0x7Fu) << 8) | (((pk.z >> 16) & 0x7Fu) << 16) |
+                   (((pk.w >> 16) & 0x7Fu) << 24);
+        const uint32_t nv = min(d.ncol - jq, 4u);
+        vm7v[q] = nv >= 4u ? B7 : B7 & ((1u << (8u * nv)) - 1u);  // bit 7 of the valid columns
+        if (d.EC) {
+            ld4(d.esc_slot + jq, esv[q]);
+#pragma unroll
+            for (uint32_t i = 0; i < 4; i++) esc7v[q] |= (uint32_t)(esv[q][i] != NONE) << (8 * i + 7);
+        }
+    }
+    for (uint32_t r = 0; r < nrow; r++) {
+    const uint32_t o = o0 + r;
+    const uint4 hr = nh, mr = nm;
+    ldv(o0 + min(r + 1u, nrow - 1u), nh, nm);  // (the last row reloads itself: no wait counts a load as absent)
+    uint32_t hot = 0;  // bit k = view k of this thread's (at most 16)
+    if (j0 < d.ncol) {
+        const size_t p0 = pix(d, o, j0);
         const uint32_t hw[4] = {hr.x, hr.y, hr.z, hr.w}, mw[4] = {mr.x, mr.y, mr.z, mr.w};
-        // the headline's layout (canonical, GS_HB8 + GS_MV8): four views per 32-bit word against the owners'
-        // packed own values (SELF_PK: heartbeat mod 2^8 in byte 0, max_version in the high half), per-byte
-        // lags with borrow-isolated subtracts; only escaped columns and escape requests go column by column
-        const bool swar = !genm && d.hb8 && d.mv8 && d.self_pk;
         if (swar) {
 #pragma unroll
             for (uint32_t q = 0; q < 4u; q++) {
                 const uint32_t jq = j0 + 4u * q;
-                if (jq >= d.ncol) break;
-                const uint4 pk = *reinterpret_cast<const uint4 *>(d.self_pk + jq);
-                const uint32_t own8 = (pk.x & 0xFFu) | ((pk.y & 0xFFu) << 8) | ((pk.z & 0xFFu) << 16) | (pk.w << 24);
-                const uint32_t owm7 = ((pk.x >> 16) & 0x7Fu) | (((pk.y >> 16) & 0x7Fu) << 8) | (((pk.z >> 16) & 0x7Fu) << 16) |
-                                      (((pk.w >> 16) & 0x7Fu) << 24);
-                const uint32_t nv = min(d.ncol - jq, 4u);
-                const uint32_t vm7 = nv >= 4u ? B7 : B7 & ((1u << (8u * nv)) - 1u);  // bit 7 of the valid columns
-                uint32_t es[4] = {NONE, NONE, NONE, NONE};
-                uint32_t esc7 = 0u;
-                if (d.EC) {
-                    ld4(d.esc_slot + jq, es);
-#pragma unroll
-                    for (uint32_t i = 0; i < 4; i++) esc7 |= (uint32_t)(es[i] != NONE) << (8 * i + 7);
-                }
+                const uint32_t own8 = own8v[q], owm7 = owm7v[q], vm7 = vm7v[q], esc7 = esc7v[q];
+                const uint32_t *es = esv[q];
                 const uint32_t lagH = bsub(own8, hw[q]);                            // (own - view) mod 2^8
                 const uint32_t lagM = ((owm7 | B7) - (mw[q] & L7)) & L7;           // (own - view) mod 2^7
                 const uint32_t hb7 = lagH & B7 & ~esc7 & vm7;                       // heartbeat lag >= 2^7
@@ -3815,16 +3840,23 @@ __global__ __launch_bounds__(LB) void k_hb_lag(Dev d, uint32_t chunks) {
             }
         }
     }
+    if (d.p1flags) {  // this row's hot views in its chunk (counted for the row's hot test below)
+        const unsigned long long wn = wave_sum((uint32_t)__popc(hot));
+        if ((threadIdx.x & 63) == 0 && wn) atomicAdd(&s_hot[r], (uint32_t)wn);
+        s_hm[r][threadIdx.x] = (uint16_t)hot;
+    }
+    }
     if (d.p1flags) {  // k_pass1v's hot rows and columns (cleared by k_hot_clear before the sweep)
-        const uint32_t nh = (uint32_t)__popc(hot);
-        const unsigned long long wn = wave_sum(nh);
-        if ((threadIdx.x & 63) == 0 && wn) atomicAdd(&s_hot, (uint32_t)wn);
         __syncthreads();
-        if (s_hot >= HOT_ROW_MIN) {
-            if (threadIdx.x == 0) atomicOr(&d.row[o * 4 + 3], 4u);
-            hot = 0u;
+        uint32_t col = hotc;
+        for (uint32_t r = 0; r < nrow; r++) {
+            if (s_hot[r] >= HOT_ROW_MIN) {  // a hot row: its views take the per-column path, not its columns
+                if (threadIdx.x == 0) atomicOr(&d.row[(o0 + r) * 4 + 3], 4u);
+            } else {
+                col |= s_hm[r][threadIdx.x];
+            }
         }
-        if (hot | hotc) atomicOr(&d.p1flags[j0 >> 4], (hot | hotc) << 16);  // 16 views: one 16-column group
+        if (col && j0 < d.ncol) atomicOr(&d.p1flags[j0 >> 4], col << 16);  // 16 views: one 16-column group
     }
     const unsigned long long sb = wave_sum(bad);
     if ((threadIdx.x & 63) == 0) shard_add(d, C_E_HBLAG, sb);
@@ -5504,7 +5536,7 @@ int gs_check_heartbeat_lag(gs_handle *h) {
         k_hot_clear<<<(std::max(h->N, h->NP / 16u) + LB - 1) / LB, LB, 0, h->stream>>>(h->d);
         HIPCHK(h, hipGetLastError());
     }
-    k_hb_lag<<<h->N * chunks, LB, 0, h->stream>>>(h->d, chunks);
+    k_hb_lag<<<(h->N + LAG_ROWS - 1) / LAG_ROWS * chunks, LB, 0, h->stream>>>(h->d, chunks);
     HIPCHK(h, hipGetLastError());
     if (h->d.EC) {  // escaped owner columns: moves decided, then copied (one pass over the rows)
         k_esc_plan<<<1, 1024, 0, h->stream>>>(h->d);
