@@ -76,6 +76,7 @@ COUNTER_FIELDS = [
     "err_fd_gc", "err_insert", "fd_gc", "q9", "pack_bytes", "err_holes", "err_hb_lag", "plane_flushes",
     "fd_saturated", "lite_slots", "lag_sweeps", "lite_bytes", "live_bytes", "hb_escapes", "hb_releases",
     "pack_groups_max", "pack_steps_max",  # maxima (gs_read_counters takes the largest; sum_counters too)
+    "heavy_slots",
 ]
 
 # Every symbol include/gossip_sim.h declares (checked by tests/test_abi.py).
@@ -86,11 +87,17 @@ EXPORTS = [
     "gs_select_peers", "gs_schedule_phases", "gs_set_events", "gs_emit_scratch_bytes", "gs_emit_digest", "gs_emit_delta",
     "gs_check_heartbeat_lag", "gs_stream_copy", "gs_stream_read", "gs_stream_write", "gs_set_timing", "gs_kernel_times",
     "gs_phase_overflow", "gs_phase_chain", "gs_phase_pending", "gs_comm_id", "gs_comm_init", "gs_run_phase_group", "gs_read_rows",
-    "gs_latest_tick", "gs_flush_reports", "gs_set_ring_rows",
+    "gs_latest_tick", "gs_flush_reports", "gs_set_ring_rows", "gs_mark",
 ]
 
-API_VERSION = 18
+API_VERSION = 20
 MAX_PHASES = 64  # GS_MAX_PHASES
+MAX_SCHED_PHASES = 65536  # GS_MAX_SCHED_PHASES
+
+
+def sched_scratch_bytes(n: int, fanout: int, max_phases: int) -> int:
+    """GS_SCHED_SCRATCH_BYTES: gs_schedule_phases' device scratch."""
+    return 4 * n * (fanout + 2) + 12 * max_phases + 32 + 24 * n
 
 
 class GsConfig(C.Structure):
@@ -115,7 +122,7 @@ class GsConfig(C.Structure):
 
 
 class GsCounters(C.Structure):
-    _fields_ = [(n, C.c_uint64) for n in COUNTER_FIELDS] + [("reserved", C.c_uint64 * (32 - len(COUNTER_FIELDS)))]
+    _fields_ = [(n, C.c_uint64) for n in COUNTER_FIELDS] + [("reserved", C.c_uint64 * (40 - len(COUNTER_FIELDS)))]
 
 
 CENSUS_FIELDS = ["up_pairs", "up_dead", "up_live", "down_pairs", "down_live"]
@@ -228,19 +235,28 @@ def load():
         "gs_stream_copy": (C.c_int, [P, P, u64, P]),
         "gs_stream_read": (C.c_int, [P, u64, u32, P, P]),
         "gs_stream_write": (C.c_int, [P, u64, u32, P]),
+        "gs_mark": (C.c_int, [u32, P]),
         "gs_emit_scratch_bytes": (C.c_int, [P, C.POINTER(u64)]),
         "gs_emit_digest": (C.c_int, [P, C.POINTER(GsWire), u32, u32, P, u64, C.POINTER(u64), P]),
         "gs_emit_delta": (C.c_int, [P, C.POINTER(GsWire), u32, u32, u32, P, u64, C.POINTER(u64), P]),
     }
+    missing = []
     for name, (res, args) in sig.items():
         try:
             f = getattr(L, name)
         except AttributeError:
             if not os.environ.get("GS_LIB"):
                 raise GsError(f"{path} lacks {name}: rebuild it (__graft_entry__.build())")
-            continue  # an older A/B build named by GS_LIB: that entry point is absent (calling it fails loudly)
+            missing.append(name)  # an older A/B build named by GS_LIB: that entry point is absent
+            continue
         f.restype = res
         f.argtypes = args
+    if missing:
+        import sys
+
+        print(f"[aiocluster_amd] GS_LIB={path} lacks {', '.join(missing)} (older A/B build): calls to them raise",
+              file=sys.stderr, flush=True)
+    L.gs_missing = frozenset(missing)
     del i32
     _LIB = L
     return L

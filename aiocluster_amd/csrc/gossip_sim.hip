@@ -76,13 +76,14 @@ enum Ctr {
     C_EXCH = 0, C_REPORTS, C_ND, C_KVS, C_TRUNC, C_DBYTES, C_ALG, C_HBW, C_CAND, C_LIVE, C_TOMBGC,
     C_E_FDOVF, C_E_HIST, C_E_IDX, C_E_CONFLICT, C_E_FDGC, C_E_INSERT, C_FDGC, C_Q9, C_PACKB, C_E_HOLES,
     C_E_HBLAG, C_FLUSH /* host-side: plane_flushes */, C_FDSAT, C_LITE, C_SWEEPS /* host-side: lag_sweeps */,
-    C_LITEB, C_LIVEB, C_ESC, C_ESCREL, C_PGMAX, C_PSMAX,
-    C_CEN0 = 32, C_NUM = C_CEN0 + 6  // gs_fd_census scratch slots (not part of gs_counters)
+    C_LITEB, C_LIVEB, C_ESC, C_ESCREL, C_PGMAX, C_PSMAX, C_HEAVY,
+    C_CEN0 = 40, C_NUM = C_CEN0 + 6  // gs_fd_census scratch slots (not part of gs_counters)
 };
-constexpr int CROW = 40;  // u64 slots per counter shard row (the 32 gs_counters fields, then the census scratch)
+constexpr int CFIELDS = 40;  // gs_counters fields (the last ones reserved)
+constexpr int CROW = 48;     // u64 slots per counter shard row (the gs_counters fields, then the census scratch)
 static_assert(C_NUM <= CROW, "counter region");
-static_assert(C_PSMAX < 32, "gs_counters fields");
-static_assert(sizeof(gs_counters) == 32 * 8, "gs_counters layout");
+static_assert(C_HEAVY < CFIELDS, "gs_counters fields");
+static_assert(sizeof(gs_counters) == CFIELDS * 8, "gs_counters layout");
 
 struct Dev {
     uint32_t N, NP, K, KP, C, mtu, flags, W;
@@ -128,6 +129,12 @@ struct Dev {
     // ticks after it (the planes were replayed into the windows mid-round), the tick before the
     // first phase after that replay; plane p holds the phase at tick t_round + 1 + p
     uint32_t t_round;
+    // sub-phases (round 6): several phases at one tick -- every exchange select_nodes_for_gossip chose, however
+    // many phases its hubs need (server.py:476-493).  Plane p of the base holds the phase of VIRTUAL tick
+    // v_round + 1 + p (pstamp holds virtual ticks, unique over the handle's life) at real tick
+    // min(t_round + 1 + p, t_cap) (plane_tick); vt = the virtual tick of the phase being launched (set per phase by
+    // the host).  Without sub-phases v_round = t_round, vt = the phase's tick and t_cap = NONE: the round-5 layout.
+    uint32_t v_round, vt, t_cap;
     // speculative max-version merge (canonical record phases): pass 1 already wrote
     // max(sender, receiver) into the receiver's max_version word of every recorded candidate whose two
     // views are prefix views; the packers restore the receiver's word of such a candidate when it is not
@@ -170,6 +177,11 @@ struct Dev {
 // gs_set_events).  ev == nullptr: off
     uint32_t *ev, *ev_count;
     uint32_t ev_cap;
+    // the exact packer's heavy slots (round 6): k_pack_slice lists a slot with more than heavy_t stale owners here
+    // ([0] = count, then slot ids) instead of walking it, and k_pack_heavy packs it with a workgroup of its own;
+    // nullptr: no hand-off (set per launch by the host, one-slice record phases only)
+    uint32_t *heavy;
+    uint32_t heavy_t;
     uint32_t ev_wseq;  // owner-write ops issued since gs_set_events (the seq of the next call's op 0)
 };
 
@@ -183,6 +195,8 @@ __host__ __device__ inline uint32_t sfield(uint32_t n) { return n ? 1u + vlen(n)
 __host__ __device__ inline uint32_t msgf(uint32_t n) { return 1u + vlen(n) + n; }
 
 __device__ inline size_t pix(const Dev &d, uint32_t o, uint32_t j) { return (size_t)o * d.NP + j; }
+// the real tick of report plane p of the current plane base (sub-phases share the tick t_cap)
+__device__ inline uint32_t plane_tick(const Dev &d, uint32_t p) { return min(d.t_round + 1u + p, d.t_cap); }
 __device__ inline size_t hix(const Dev &d, uint32_t j, uint32_t w, uint32_t k) {
     return ((size_t)j * d.C + w) * d.K + k;
 }
@@ -1717,7 +1731,7 @@ __device__ inline PackState chain_unpack(uint64_t v) {
 // (DevDyn).  A single handle's launch passes ga = nullptr and uses its own arguments.
 constexpr uint32_t GRP_MAX = 8;
 struct DevDyn {
-    uint32_t t_round, spec, lite, p1fix;
+    uint32_t t_round, spec, lite, p1fix, v_round, vt, t_cap;
 };
 struct GroupArgs {
     Dev dv[GRP_MAX];
@@ -1728,6 +1742,9 @@ struct GroupArgs {
 __device__ __forceinline__ void group_pick(Dev &d, const GroupArgs *ga, const DevDyn &dyn) {
     d = ga->dv[blockIdx.y];
     d.t_round = dyn.t_round;
+    d.v_round = dyn.v_round;
+    d.vt = dyn.vt;
+    d.t_cap = dyn.t_cap;
     d.spec = dyn.spec;
     d.lite = dyn.lite;
     d.p1fix = dyn.p1fix;
@@ -1795,12 +1812,16 @@ __global__ __launch_bounds__(XB, (KW == 4 ? (FUSE ? P1_WAVES : MV8 ? P1N_WAVES :
     uint32_t nBAc = 0, nABc = 0;
     uint32_t alg = 0, reports = 0, hbw = 0;
     bool anynew = false;
-    const uint32_t ph = t - d.t_round - 1u;
+    const uint32_t ph = d.vt - d.v_round - 1u;  // this phase's plane (host-checked: < NPL)
+    if (ph >= NPL) {  // (never: plane_slot checks it; a guard, so that a host bug cannot write past the planes)
+        if (tid == 0) shard_add(d, C_E_IDX, 1);
+        return;
+    }
     uint64_t *planeA = d.pend + ((size_t)a * NPL + ph) * d.PW;
     uint64_t *planeB = d.pend + ((size_t)b * NPL + ph) * d.PW;
     if (tid == 0) {
-        d.pstamp[a * NPL + ph] = t;
-        d.pstamp[b * NPL + ph] = t;
+        d.pstamp[a * NPL + ph] = d.vt;
+        d.pstamp[b * NPL + ph] = d.vt;
     }
     // responder inc_heartbeat (server.py:524): the owner's own heartbeat R is raised once, here; the
     // view hb[b][b] is raised in the loop.  Other exchanges of the phase decode column b against R or
@@ -2217,12 +2238,16 @@ __global__ __launch_bounds__(XB, P1V_WAVES) void k_pass1v(Dev d, const int32_t *
     uint2 *LBA = d.cand + ((size_t)e * 4 + 0 * 2 + wid) * GS_CAND_CAP;
     uint2 *LAB = d.cand + ((size_t)e * 4 + 1 * 2 + wid) * GS_CAND_CAP;
     uint32_t nBAc = 0, nABc = 0, alg = 0, reports = 0, hbw = 0;
-    const uint32_t ph = t - d.t_round - 1u;
+    const uint32_t ph = d.vt - d.v_round - 1u;  // this phase's plane (host-checked: < NPL)
+    if (ph >= NPL) {  // (never: plane_slot checks it; a guard, so that a host bug cannot write past the planes)
+        if (tid == 0) shard_add(d, C_E_IDX, 1);
+        return;
+    }
     uint16_t *planeA = reinterpret_cast<uint16_t *>(d.pend + ((size_t)a * NPL + ph) * d.PW);
     uint16_t *planeB = reinterpret_cast<uint16_t *>(d.pend + ((size_t)b * NPL + ph) * d.PW);
     if (tid == 0) {
-        d.pstamp[a * NPL + ph] = t;
-        d.pstamp[b * NPL + ph] = t;
+        d.pstamp[a * NPL + ph] = d.vt;
+        d.pstamp[b * NPL + ph] = d.vt;
     }
     const uint32_t ja = a - d.col_lo, jb = b - d.col_lo;  // this slice's columns of a and b (>= ncol: not here)
     // responder inc_heartbeat (server.py:524): the owner's own heartbeat is raised here (the per-column path
@@ -2569,12 +2594,16 @@ __global__ __launch_bounds__(XB, (KW == 4 ? XB_WAVES : 1)) void k_exchange(Dev d
     const size_t ra = (size_t)a * d.NP, rb = (size_t)b * d.NP;
     uint32_t alg = 0, reports = 0, hbw = 0;
     bool anynew = false;
-    const uint32_t ph = t - d.t_round - 1u;  // phase of this round (host-checked: < NPL)
+    const uint32_t ph = d.vt - d.v_round - 1u;  // phase of this round (host-checked: < NPL)
+    if (ph >= NPL) {  // (never: plane_slot checks it; a guard, so that a host bug cannot write past the planes)
+        if (tid == 0) shard_add(d, C_E_IDX, 1);
+        return;
+    }
     uint64_t *planeA = d.pend + ((size_t)a * NPL + ph) * d.PW;
     uint64_t *planeB = d.pend + ((size_t)b * NPL + ph) * d.PW;
     if (tid == 0) {  // both plane rows are rewritten below: valid for this phase
-        d.pstamp[a * NPL + ph] = t;
-        d.pstamp[b * NPL + ph] = t;
+        d.pstamp[a * NPL + ph] = d.vt;
+        d.pstamp[b * NPL + ph] = d.vt;
     }
     // software-pipelined: the next group's loads are in flight while this group computes and stores
     // (different owners, so the early loads never read a location this group writes)
@@ -2721,6 +2750,13 @@ __global__ __launch_bounds__(XB, (KW == 4 ? PK_WAVES : 1)) void k_pack_slice(Dev
     const uint32_t a = (uint32_t)ai, b = (uint32_t)bi;
     const size_t slot = (size_t)e * 2 + wid;
     if (io.step == 0 && d.lite && (d.slot_stat[slot].w & LITE_DONE)) return;  // k_lite completed it
+    if (d.heavy && d.cand_n[slot * 2] + d.cand_n[slot * 2 + 1] > d.heavy_t) {  // k_pack_heavy packs it
+        if (tid == (wid << 6)) {
+            d.heavy[1u + atomicAdd(d.heavy, 1u)] = (uint32_t)slot;
+            shard_add(d, C_HEAVY, 1);
+        }
+        return;
+    }
     PackState pst;
     if (io.step == 0) {
         uint64_t P = 0;
@@ -2763,6 +2799,268 @@ __global__ __launch_bounds__(XB, (KW == 4 ? PK_WAVES : 1)) void k_pack_slice(Dev
         shard_add(d, C_CAND, s_cd);
         shard_max(d, C_PGMAX, st.grp);
         shard_max(d, C_PSMAX, st.stp);
+    }
+}
+
+// ---- the exact packer's heavy slots (round 6).  A slot with thousands of stale owners -- a
+// node back from an absence -- kept k_pack_slice's two-wave workgroup walking for ~270 dependent steps (the launch
+// lasts as long as its heaviest slot) while the others were long done.  k_pack_slice hands such slots to this
+// kernel (Dev::heavy), which packs each with HW_WAVES waves, HT candidates per block in sender order:
+//  * whole-fit prefix (state.py:392-398): the block's candidates are evaluated in parallel, a block scan of their
+//    DeltaPb sizes finds the first one that does not fit whole, every candidate before it is sent whole (applied in
+//    parallel: distinct owners);
+//  * first-fit continuation (state.py:392-413): every later candidate is tested against the budget R left, which
+//    only shrinks, so one whose smallest NodeDelta (its lowest-version kv alone, min1) exceeds R now is never sent:
+//    the block filters its candidates in parallel (min1_lb first, the exact min1 for those that pass), and one wave
+//    runs pack_group's sequential first-fit over the survivors alone, in sender order;
+//  * a speculatively merged record (Dev::spec) that is not sent gets its receiver word restored, as in pack_list.
+// Bit-exact with pack_records: the same candidates, the same order, the same decisions.
+#ifndef HW_WAVES
+#define HW_WAVES 4
+#endif
+constexpr int HT = HW_WAVES * WAVE;   // threads per heavy workgroup: one candidate each per block
+constexpr uint32_t HWIN = 16u * HT;   // bitmap positions compacted per window (16 per thread)
+struct HeavyLds {
+    uint32_t wsum[HW_WAVES];
+    uint32_t first, S, stop, tail, nsurv, steps, groups;
+    uint32_t cj[HT], cm[HT];  // the block's candidates: owner column, sender | receiver max_version words << 16
+    uint16_t surv[HT];        // survivors' block indices in sender order
+    uint16_t wl[HWIN];        // a bitmap window's stale positions (offsets from the window start)
+    uint8_t crec[HT];         // candidate from pass 1's records (merged speculatively if both views are prefixes)
+};
+// block-wide exclusive scan of x (all threads call); returns the exclusive prefix, *total the block's sum
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, HeavyLds &sh, uint32_t *total) {
+    const int lane = lane_id(), wv = (int)(threadIdx.x >> 6);
+    const uint32_t inc = wave_incl_scan(x);
+    if (lane == WAVE - 1) sh.wsum[wv] = inc;
+    __syncthreads();
+    uint32_t pre = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < HW_WAVES; w++) {
+        const uint32_t v = sh.wsum[w];
+        if (w < wv) pre += v;
+        tot += v;
+    }
+    __syncthreads();  // (wsum is reused by the next scan)
+    *total = tot;
+    return pre + inc - x;
+}
+
+// one block of candidates (thread i: the i-th, if has), in sender order after every earlier block's
+template <int KW>
+__device__ __forceinline__ void heavy_block(const Dev &d, uint32_t s, uint32_t r, const DigestSide &ds, uint32_t t,
+                                            bool has, uint32_t j, uint32_t mvw, bool rec, bool specd, bool lightok,
+                                            HeavyLds &sh, WStats &st, bool &tomb) {
+    const int tid = (int)threadIdx.x, lane = lane_id();
+    const uint32_t mtu = d.mtu;
+    uint32_t S = sh.S;
+    bool tail = sh.tail != 0u;
+    const bool fastrec = rec_fast(mvw);
+    if (sh.stop) {  // the delta is complete: nothing more is sent; restore the merged records
+        if (has && rec && specd && fastrec) { mv_put(d, pix(d, r, j), mvw >> 16); st.alg += 4; }
+        return;
+    }
+    const uint32_t msw = mvw & 0xFFFFu, mrw = mvw >> 16;
+    Cand<KW> c;
+    c.emsg = 0;
+    c.min1 = 0;
+    c.light = false;
+    c.fast = false;
+    bool ev = false;
+    auto eval = [&]() {
+        if (lightok && fastrec) {
+            eval_light<KW>(d, j, msw & MV_MASK, mrw & MV_MASK, c, st.alg);
+        } else {
+            CandKeys<KW> ck;
+            eval_cand<KW, false, true>(d, s, r, ds, j, t, c, ck, st.alg, mvw);
+        }
+        st.cand++;
+        ev = true;
+    };
+    uint32_t f = 0;  // block index from which the candidates are in first-fit continuation
+    if (!tail) {
+        if (has) eval();
+        const uint32_t em = has ? c.emsg : 0u;
+        uint32_t total;
+        const uint32_t ex = block_excl_scan(em, sh, &total);
+        bool whole;
+        if (S + total <= mtu) {
+            whole = em != 0u;
+            f = HT;
+            if (tid == 0) {
+                const uint32_t S1 = S + total;
+                sh.S = S1;
+                if (S1 >= mtu || mtu - S1 < d.lb_min) sh.stop = 1u;
+            }
+        } else {
+            if (tid == 0) sh.first = HT;
+            __syncthreads();
+            if (em && S + ex + em > mtu) atomicMin(&sh.first, (uint32_t)tid);
+            __syncthreads();
+            f = sh.first;
+            whole = em != 0u && (uint32_t)tid < f;
+            if ((uint32_t)tid == f) { sh.S = S + ex; sh.tail = 1u; }
+        }
+        if (whole) {  // sent whole: one lane per NodeDelta, distinct owners
+            apply_cand<KW>(d, s, r, c, NONE, t, tomb, st.alg, specd && rec);
+            st.nd++;
+            st.kvs += c.nkv;
+        } else if (has && (uint32_t)tid < f && specd && rec && c.fast) {  // no kvs to send: restore
+            mv_put(d, pix(d, r, j), mrw);
+            st.alg += 4;
+        }
+        __syncthreads();
+        if (f >= HT) return;  // (stop, if set, takes effect from the next block)
+        S = sh.S;
+        tail = true;
+    }
+    // first-fit continuation over candidates f.. of the block: keep those whose min1 fits the budget left now
+    const uint32_t R = mtu - S;
+    bool surv = false;
+    if (has && (uint32_t)tid >= f) {
+        if (!ev && fastrec && d.vlog && min1_lb(d, j, msw, mrw, ds.sched) > R) {
+            st.alg += 4;  // the bound's version-log entry
+        } else {
+            if (!ev) eval();
+            surv = c.emsg != 0u && c.min1 <= R;
+        }
+        if (!surv && rec && specd && fastrec) { mv_put(d, pix(d, r, j), mrw); st.alg += 4; }  // not sent: restore
+    }
+    uint32_t nsurv;
+    const uint32_t at = block_excl_scan(surv ? 1u : 0u, sh, &nsurv);
+    if (surv) sh.surv[at] = (uint16_t)tid;
+    sh.cj[tid] = j;
+    sh.cm[tid] = mvw;
+    sh.crec[tid] = rec ? 1u : 0u;
+    __syncthreads();
+    if (tid < WAVE) {  // one wave: pack_group's sequential first-fit over the survivors, 64 at a time
+        bool tl = true, sp = false;
+        uint32_t nr = 0, steps = 0;
+        for (uint32_t g0 = 0; g0 < nsurv; g0 += WAVE) {
+            const bool cand = g0 + (uint32_t)lane < nsurv;
+            const uint32_t i = cand ? sh.surv[g0 + lane] : 0u;
+            const uint32_t jj = sh.cj[i], mm = sh.cm[i];
+            const bool rc = sh.crec[i] != 0u;
+            const uint32_t ms = mm & 0xFFFFu, mr = mm >> 16;
+            if (sp) {  // complete: restore the rest of the merged survivors
+                if (cand && rc && specd && rec_fast(mm)) { mv_put(d, pix(d, r, jj), mr); st.alg += 4; }
+                continue;
+            }
+            Cand<KW> cc;
+            cc.emsg = 0;
+            cc.min1 = 0;
+            cc.light = false;
+            cc.fast = false;
+            if (cand) {
+                if (lightok && rec_fast(mm)) {
+                    eval_light<KW>(d, jj, ms & MV_MASK, mr & MV_MASK, cc, st.alg);
+                } else {
+                    CandKeys<KW> ck;
+                    eval_cand<KW, false, true>(d, s, r, ds, jj, t, cc, ck, st.alg, mm);
+                }
+            }
+            pack_group<KW, false, false>(d, s, r, t, cc, cand, S, tl, sp, st, tomb, nullptr, nr, specd && rc);
+            steps++;
+        }
+        if (lane == 0) {
+            sh.S = S;
+            sh.stop = sp ? 1u : 0u;
+            sh.tail = 1u;
+            sh.steps += steps;
+        }
+    }
+    __syncthreads();
+}
+
+template <int KW>
+__global__ __launch_bounds__(HT) void k_pack_heavy(Dev d, const int32_t *ini, const int32_t *res, uint32_t t,
+                                                   const uint32_t *heavy) {
+    __shared__ HeavyLds sh;
+    const uint32_t count = heavy[0];
+    const int tid = (int)threadIdx.x, lane = lane_id();
+    const uint32_t H = half_cols(d), words = d.NP / 32;
+    WStats st{0, 0, 0, 0, 0};
+    bool tomb = false;
+    for (uint32_t hi = blockIdx.x; hi < count; hi += gridDim.x) {
+        const uint32_t slot = heavy[1u + hi], e = slot >> 1;
+        const bool w0 = (slot & 1u) == 0u;
+        const uint32_t a = (uint32_t)ini[e], b = (uint32_t)res[e];  // (k_pack_slice listed valid exchanges only)
+        const uint32_t snd = w0 ? b : a, rcv = w0 ? a : b;
+        const DigestSide ds{rcv, d.ncol, t >= d.row[rcv * 4 + 2]};
+        const bool specd = d.spec != 0u, lightok = d.vlog && !d.ev && !ds.sched;
+        if (tid == 0) { sh.S = 0u; sh.stop = 0u; sh.tail = 0u; sh.steps = 0u; sh.groups = 0u; }
+        __syncthreads();
+        const uint32_t S0 = 0u;
+        bool tb = false;
+        for (uint32_t hf = 0; hf < 2; hf++) {
+            const uint32_t nh = d.cand_n[(size_t)slot * 2 + hf];
+            const uint2 *L = d.cand + ((size_t)slot * 2 + hf) * GS_CAND_CAP;
+            const uint32_t nl = min(nh, GS_CAND_CAP);
+            for (uint32_t b0 = 0; b0 < nl; b0 += HT) {  // pass 1's records (continue when complete: restores)
+                if (sh.stop && !specd) break;
+                const uint32_t i = b0 + (uint32_t)tid;
+                const bool has = i < nl;
+                const uint2 rr = has ? L[i] : make_uint2(0u, 0u);
+                if (has) st.alg += 8;  // the record
+                heavy_block<KW>(d, snd, rcv, ds, t, has, rr.x, rr.y, true, specd, lightok, sh, st, tb);
+                if (tid == 0) sh.groups += (min(nl - b0, (uint32_t)HT) + WAVE - 1) / WAVE;
+            }
+            if (nh <= GS_CAND_CAP || sh.stop) continue;
+            // past the half's records: its bitmap, compacted window by window (those owners were not merged)
+            const uint32_t pmin = L[GS_CAND_CAP - 1].x + 1u, end = min(H * (hf + 1u), d.ncol);
+            const uint32_t *bits = d.sbits + (size_t)slot * words;
+            for (uint32_t w = pmin & ~15u; w < end && !sh.stop; w += HWIN) {
+                const uint32_t pb = w + 16u * (uint32_t)tid;
+                uint32_t m = 0u;
+                if (pb < end) {
+                    m = (bits[pb >> 5] >> (pb & 16u)) & 0xFFFFu;
+                    st.alg += 2;
+                    if (end - pb < 16u) m &= (1u << (end - pb)) - 1u;
+                    if (pb < pmin) m &= pmin - pb >= 16u ? 0u : ~((1u << (pmin - pb)) - 1u);
+                }
+                uint32_t cnt;
+                uint32_t wp = block_excl_scan((uint32_t)__popc(m), sh, &cnt);
+                while (m) {
+                    const uint32_t bb = (uint32_t)__builtin_ctz(m);
+                    m &= m - 1u;
+                    sh.wl[wp++] = (uint16_t)(16u * (uint32_t)tid + bb);
+                }
+                __syncthreads();
+                for (uint32_t b0 = 0; b0 < cnt && !sh.stop; b0 += HT) {
+                    const uint32_t i = b0 + (uint32_t)tid;
+                    const bool has = i < cnt;
+                    uint32_t j = 0u, mvw = 0u;
+                    if (has) {
+                        j = w + sh.wl[i];
+                        mvw = mv_word(d, pix(d, snd, j), j) | (mv_word(d, pix(d, rcv, j), j) << 16);
+                        st.alg += 2;
+                    }
+                    heavy_block<KW>(d, snd, rcv, ds, t, has, j, mvw, false, specd, lightok, sh, st, tb);
+                    if (tid == 0) sh.groups += (min(cnt - b0, (uint32_t)HT) + WAVE - 1) / WAVE;
+                }
+                if (tid == 0) sh.steps++;
+                __syncthreads();  // (wl is rewritten by the next window)
+            }
+        }
+        const uint32_t S1 = sh.S;
+        tomb = tomb || tb;
+        if (__syncthreads_or(tb) && tid == 0) d.row[rcv * 4 + 1] = 1u;
+        if (tid == 0) {
+            shard_add(d, C_DBYTES, S1 - S0);
+            shard_max(d, C_PGMAX, sh.groups);
+            shard_max(d, C_PSMAX, sh.steps);
+        }
+        __syncthreads();  // (sh is reset for the next slot)
+    }
+    const unsigned long long s_alg = wave_sum(st.alg), s_nd = wave_sum(st.nd), s_kv = wave_sum(st.kvs);
+    const unsigned long long s_tr = wave_sum(st.trunc), s_cd = wave_sum(st.cand);
+    if (lane == 0) {
+        shard_add(d, C_ALG, s_alg);
+        shard_add(d, C_PACKB, s_alg);
+        shard_add(d, C_ND, s_nd);
+        shard_add(d, C_KVS, s_kv);
+        shard_add(d, C_TRUNC, s_tr);
+        shard_add(d, C_CAND, s_cd);
     }
 }
 
@@ -3283,7 +3581,7 @@ __global__ __launch_bounds__(LB, LIVE_WAVES) void k_liveness(Dev d, const uint8_
     // phases of the current round in which row o was in an exchange (its plane rows are valid);
     // replay = false once this round's reports were replayed (the host closes the round)
     if (threadIdx.x < 64) {
-        const bool v = replay && threadIdx.x < NPL && d.pstamp[o * NPL + threadIdx.x] == d.t_round + 1u + threadIdx.x;
+        const bool v = replay && threadIdx.x < NPL && d.pstamp[o * NPL + threadIdx.x] == d.v_round + 1u + threadIdx.x;
         const uint32_t m = (uint32_t)__ballot(v);
         if (threadIdx.x == 0) s_vm = m;
     }
@@ -3377,23 +3675,25 @@ __global__ __launch_bounds__(LB, LIVE_WAVES) void k_liveness(Dev d, const uint8_
                     Fd f = fd_get(d, st, lt[i], sc[i], t);  // t is at or after every report tick of this round
                     uint32_t m = q[i];  // only if vm != 0: then the window was loaded
                     if (m) {
-                        // report_heartbeat at ticks t_round + 1 + p for the phases p of m (failure_detector.py:32-38):
-                        // intervals between reports of one round are < NPL ticks, so with max_interval >= NPL - 1 all
-                        // but the first are appended and they telescope: (k - 1) intervals summing to p_last - p_first,
-                        // plus the first one if it is <= max_interval; a compact window that would fill up, and the
-                        // rings (their intervals one by one), replay report by report
+                        // report_heartbeat at ticks plane_tick(p) for the phases p of m (failure_detector.py:32-38):
+                        // non-decreasing, and less than NPL ticks apart within a base, so with max_interval >= NPL - 1
+                        // all but the first are appended (sub-phases at one tick append 0 s, as the reference does
+                        // for two reports at one time) and they telescope: (k - 1) intervals summing to
+                        // tick(p_last) - tick(p_first), plus the first one if it is <= max_interval; a compact window
+                        // that would fill up, and the rings (their intervals one by one), replay report by report
                         bool loop = (RING && rrow) || d.max_iv < NPL - 1u;
                         if (!loop) {
                             const uint32_t p1 = (uint32_t)__builtin_ctz(m), pk = 31u - (uint32_t)__builtin_clz(m);
-                            uint32_t app = (uint32_t)__popc(m) - 1u, add = pk - p1;
+                            const uint32_t t1 = plane_tick(d, p1), tk = plane_tick(d, pk);
+                            uint32_t app = (uint32_t)__popc(m) - 1u, add = tk - t1;
                             if (f.last != NONE) {
-                                const uint32_t iv = d.t_round + 1u + p1 - f.last;
+                                const uint32_t iv = t1 - f.last;
                                 if (iv <= d.max_iv) { app++; add += iv; }
                             }
                             if (f.cnt + app <= d.W) {
                                 f.cnt += app;
                                 f.sum += add;
-                                f.last = d.t_round + 1u + pk;
+                                f.last = tk;
                             } else {
                                 loop = true;
                             }
@@ -3402,7 +3702,7 @@ __global__ __launch_bounds__(LB, LIVE_WAVES) void k_liveness(Dev d, const uint8_
                             while (m) {
                                 const uint32_t bb = (uint32_t)__builtin_ctz(m);
                                 m &= m - 1u;
-                                f = fd_report_val(d, RING && rrow ? rrow + (size_t)(c0 + i) * d.W : nullptr, d.t_round + 1u + bb,
+                                f = fd_report_val(d, RING && rrow ? rrow + (size_t)(c0 + i) * d.W : nullptr, plane_tick(d, bb),
                                                   f, alg, ovf);
                             }
                         }
@@ -4721,8 +5021,10 @@ __global__ __launch_bounds__(LB) void k_sel_resolve(Dev d, const uint8_t *up, co
 // out[e]; exchanges whose responder is down fail before any state change, as a refused
 // connection does, and are not scheduled).  Per phase p, IT rounds of a deterministic Luby
 // matching: an unscheduled exchange whose two endpoints are free in p takes p if its priority
-// key is the smallest at both endpoints.  Up to 64 phases (busy = one bit per phase and node);
-// exchanges left after the last phase are counted, not run.
+// key is the smallest at both endpoints.  busy = one bit per phase and node for 64 phases at a time (bit p mod 64;
+// the host clears it every 64 phases: a phase's bits are read only while it is being filled).  Up to
+// GS_MAX_SCHED_PHASES phases (round 6: the hubs of the reference's selection -- every node picks a seed while its
+// live set is empty -- need as many phases as their degree); exchanges left after the last are counted, not run.
 __device__ inline uint32_t fmix32(uint32_t h) {
     h ^= h >> 16; h *= 0x85EBCA6Bu; h ^= h >> 13; h *= 0xC2B2AE35u; h ^= h >> 16;
     return h;
@@ -4740,7 +5042,7 @@ __device__ inline bool luby_active(const int32_t *out, const uint8_t *up, const 
                                    uint32_t &b) {
     if (eph[e] != NONE) return false;
     if (!luby_valid(out, up, e, F, a, b)) return false;
-    return !((busy[a] >> p) & 1ull) && !((busy[b] >> p) & 1ull);
+    return !((busy[a] >> (p & 63u)) & 1ull) && !((busy[b] >> (p & 63u)) & 1ull);
 }
 __device__ inline unsigned long long luby_key(uint64_t seed, uint32_t round, uint32_t e, uint32_t p, uint32_t it) {
     const uint32_t h = fmix32(e ^ fmix32((uint32_t)seed ^ fmix32(round * 0x9E3779B9u + p * 0x632BE5ABu + it)));
@@ -4768,12 +5070,12 @@ __global__ __launch_bounds__(LB) void k_luby_pick(const int32_t *out, const uint
     const unsigned long long k = luby_key(seed, round, x, p, it);
     if (best[a] == k && best[b] == k) {
         eph[x] = p;
-        atomicOr(&busy[a], 1ull << p);
-        atomicOr(&busy[b], 1ull << p);
+        atomicOr(&busy[a], 1ull << (p & 63u));
+        atomicOr(&busy[b], 1ull << (p & 63u));
         atomicAdd(&pcount[p], 1u);
     }
 }
-// valid exchanges not scheduled yet (pcount[64])
+// valid exchanges not scheduled yet
 __global__ __launch_bounds__(LB) void k_luby_left(const int32_t *out, const uint8_t *up, const uint32_t *eph,
                                                   uint32_t E, uint32_t F, uint32_t *left) {
     const uint32_t e = blockIdx.x * LB + threadIdx.x;
@@ -4784,7 +5086,8 @@ __global__ __launch_bounds__(LB) void k_luby_left(const int32_t *out, const uint
 }
 // scatter the scheduled exchanges into per-phase (initiator, responder) arrays: each workgroup ranks its
 // SCAT_PER x LB exchanges per phase in LDS and takes one range per phase with a single global atomic (a
-// returning atomic per exchange, or per wave and phase, serialises on the 16 or so phase counters: 0.59 ms)
+// returning atomic per exchange, or per wave and phase, serialises on the 16 or so phase counters: 0.59 ms).
+// Phases past the first 64 (hub exchanges only, a few per phase) take a global atomic each.
 constexpr uint32_t SCAT_PER = 4;
 __global__ __launch_bounds__(LB) void k_luby_scatter(const int32_t *out, const uint32_t *eph, uint32_t E, uint32_t F,
                                                      const uint32_t *poff, uint32_t *pfill, int32_t *ini,
@@ -4797,7 +5100,7 @@ __global__ __launch_bounds__(LB) void k_luby_scatter(const int32_t *out, const u
     for (uint32_t k = 0; k < SCAT_PER; k++) {
         const uint32_t e = (blockIdx.x * SCAT_PER + k) * LB + threadIdx.x;
         p[k] = e < E ? eph[e] : NONE;
-        loc[k] = p[k] != NONE ? atomicAdd(&s_cnt[p[k]], 1u) : 0u;
+        loc[k] = p[k] < GS_MAX_PHASES ? atomicAdd(&s_cnt[p[k]], 1u) : 0u;
     }
     __syncthreads();
     if (threadIdx.x < GS_MAX_PHASES && s_cnt[threadIdx.x])
@@ -4807,7 +5110,7 @@ __global__ __launch_bounds__(LB) void k_luby_scatter(const int32_t *out, const u
     for (uint32_t k = 0; k < SCAT_PER; k++) {
         if (p[k] == NONE) continue;
         const uint32_t e = (blockIdx.x * SCAT_PER + k) * LB + threadIdx.x;
-        const uint32_t slot = poff[p[k]] + s_base[p[k]] + loc[k];
+        const uint32_t slot = poff[p[k]] + (p[k] < GS_MAX_PHASES ? s_base[p[k]] + loc[k] : atomicAdd(&pfill[p[k]], 1u));
         ini[slot] = (int32_t)(e / (F + 2));
         res[slot] = out[e];
     }
@@ -4858,6 +5161,11 @@ __global__ __launch_bounds__(256) void k_read(const V *__restrict__ src, uint64_
     if (acc == 0x9E3779B9u) atomicAdd(sink, 1ull);  // keeps the loads; practically never taken
 }
 
+// gs_mark: empty one-wave dispatches whose names bracket a region of a kernel trace (bench.py's timed rounds), so
+// tools/pmc_summary.py averages exactly the dispatches between them
+__global__ __launch_bounds__(WAVE) void k_mark_begin() {}
+__global__ __launch_bounds__(WAVE) void k_mark_end() {}
+
 }  // namespace
 
 // ====================================================================== C ABI
@@ -4870,6 +5178,12 @@ struct gs_handle {
     bool reports_pending;             // phases ran since the last gs_liveness
     bool round_open;                  // gs_begin_round ran and gs_liveness has not closed the round yet
     uint32_t last_phase_tick;
+    // sub-phases (Dev::v_round): the last phase's virtual tick (monotonic over the handle's life); a phase has run
+    // at last_phase_tick since the last round start / flush (a further phase at that tick is then a sub-phase);
+    // the plane base still needs its virtual base (set by the base's first phase)
+    uint32_t last_vt = 0;
+    bool sub_ok = false;
+    bool base_fresh = true;
     uint64_t plane_flushes;           // mid-round report replays (rounds with phases > 16 ticks after the base)
     uint64_t lag_sweeps = 0;          // k_hb_lag sweeps run (gs_counters.lag_sweeps)
     uint32_t hb_incs;                 // rounds + phases since the last heartbeat-lag check (gs_check_heartbeat_lag)
@@ -4891,6 +5205,7 @@ struct gs_handle {
     bool age_init = false;            // age_tick holds the first operation's tick (fd_age)
     // gs_set_timing: HIP events around each kernel launch of a kind (gs_ktimes), on the library's stream
     bool timing;
+    uint32_t *heavy_buf = nullptr;  // k_pack_heavy's slot list (Dev::heavy): [0] = count, then up to N slot ids
     std::vector<std::pair<hipEvent_t, hipEvent_t>> tev[GS_KT_KINDS];
     std::vector<hipEvent_t> evpool;
     std::string err;
@@ -5076,17 +5391,39 @@ int launch_liveness(gs_handle *h, const uint8_t *up, uint32_t tick, bool replay,
     return time_end(h, GS_KT_LIVENESS, e0);
 }
 
-// A phase more than NPL ticks after the plane base: replay the pending report planes into the sampling
-// windows now (nothing reads a window before the round's liveness sweep, and the replay applies the
-// same reports in the same tick order), then start a new plane base just before this phase.
-int advance_planes(gs_handle *h, uint32_t tick) {
-    if (tick - h->d.t_round <= NPL) return GS_OK;
-    if (h->reports_pending) {
-        int rc = launch_liveness(h, nullptr, tick, true, false);
-        if (rc) return rc;
-        h->plane_flushes++;
+// The report plane of a new phase at `tick` (sets Dev::vt).  A phase at a later tick takes plane tick - t_round - 1
+// of the base, as before; a sub-phase (a further phase at the previous phase's tick) takes the next plane, at the
+// same real tick (Dev::t_cap).  A phase past the base's NPL planes -- or at a later tick after sub-phases, whose
+// planes clamp to t_cap -- first replays the pending report planes into the sampling windows (nothing reads a
+// window before the round's liveness sweep, and the replay applies the same reports in the same tick order), then
+// starts a new plane base just before this phase.
+uint32_t plane_tick_host(const Dev &d, uint32_t p) { return std::min(d.t_round + 1u + p, d.t_cap); }
+int plane_slot(gs_handle *h, uint32_t tick, bool sub) {
+    Dev &d = h->d;
+    if (h->base_fresh) {  // the base's first phase: every plane's virtual tick is above every earlier phase's
+        d.v_round = std::max(d.t_round, h->last_vt);
+        d.t_cap = NONE;
+        h->base_fresh = false;
     }
-    h->d.t_round = tick - 1u;
+    uint32_t vt = sub ? h->last_vt + 1u : tick + (d.v_round - d.t_round);
+    const bool full = vt - d.v_round > NPL || (!sub && d.t_cap != NONE && tick > d.t_cap);
+    if (full) {
+        if (h->reports_pending) {
+            int rc = launch_liveness(h, nullptr, tick, true, false);
+            if (rc) return rc;
+            h->plane_flushes++;
+        }
+        d.t_round = tick - 1u;
+        vt = std::max(tick, h->last_vt + 1u);
+        d.v_round = vt - 1u;
+        d.t_cap = NONE;
+    }
+    if (sub) d.t_cap = tick;  // this plane and every later one of the base: the shared tick
+    if (vt - d.v_round - 1u >= NPL || plane_tick_host(d, vt - d.v_round - 1u) != tick)
+        return fail(h, GS_E_INVALID, "plane_slot: tick %u (virtual %u) does not map to a plane of the base (%u, %u, %u)",
+                    tick, vt, d.t_round, d.v_round, d.t_cap);
+    d.vt = vt;
+    h->last_vt = vt;
     return GS_OK;
 }
 
@@ -5095,7 +5432,8 @@ int check_phase(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t n
     if (!h || !h->booted) return GS_E_INVALID;
     if (!h->round_open)
         return fail(h, GS_E_INVALID, "phases run between gs_begin_round and gs_liveness (the round is closed)");
-    if (pack ? tick != h->last_phase_tick : tick <= h->last_phase_tick)
+    // a phase runs after the round start (or flush) at a tick >= the previous phase's: an equal tick is a sub-phase
+    if (pack ? tick != h->last_phase_tick : (tick < h->last_phase_tick || (tick == h->last_phase_tick && !h->sub_ok)))
         return fail(h, GS_E_INVALID, "phase tick %u %s (tick %u)", tick,
                     pack ? "is not the tick of the last gs_phase_count" : "not after the round start / previous phase",
                     h->last_phase_tick);
@@ -5187,6 +5525,28 @@ bool lite_fuse() {
     return on;
 }
 
+// k_pack_heavy (round 6): on unless env GS_HEAVY=0 (A/B); a slot goes there past GS_HEAVY_T stale owners (default
+// HEAVY_T); a grid of at most HEAVY_GRID workgroups loops over the listed slots
+#ifndef HEAVY_T
+#define HEAVY_T 2048u
+#endif
+constexpr uint32_t HEAVY_GRID = 4096u;
+bool heavy_on() {
+    static const bool on = [] {
+        const char *e = getenv("GS_HEAVY");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+uint32_t heavy_t() {
+    static const uint32_t v = [] {
+        const char *e = getenv("GS_HEAVY_T");
+        const long x = e ? atol(e) : 0;
+        return x > 0 ? (uint32_t)x : (uint32_t)HEAVY_T;
+    }();
+    return v;
+}
+
 // One canonical one-slice phase on the caller's stream (GS_PACK, A/B runs): default k_pass1 with the
 // speculative merge, then k_settle; "fused": k_pass1<FUSE = true> (pass 1, then packing and apply in the
 // same workgroup); "split": k_pass1, then k_pack_slice.
@@ -5210,10 +5570,23 @@ int run_split_phase(gs_handle *h, const int32_t *ini, const int32_t *res, uint32
     if (h->d.lite && !fl && (rc = launch_lite<0>(h, ini, res, n, tick, io))) return rc;
     if ((rc = time_begin(h, e0))) return rc;
     h->d.p1fix = defer ? 1u : 0u;
+    // slots with more than heavy_t stale owners go to k_pack_heavy (K <= 16, prefix views, no hook events)
+    const bool hv = heavy_on() && h->KP <= 16 && h->d.vlog && !h->d.ev && h->d.cand;
+    if (hv) {
+        if (!h->heavy_buf) HIPCHK(h, hipMalloc(&h->heavy_buf, ((size_t)h->N + 4) * 4));
+        HIPCHK(h, hipMemsetAsync(h->heavy_buf, 0, 4, h->stream));
+        h->d.heavy = h->heavy_buf;
+        h->d.heavy_t = heavy_t();
+    }
     if (h->KP <= 16) k_pack_slice<4><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, io, 0u);
     else k_pack_slice<KWB><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, io, 0u);
     h->d.p1fix = 0u;
+    h->d.heavy = nullptr;
     HIPCHK(h, hipGetLastError());
+    if (hv) {
+        k_pack_heavy<4><<<std::min(2u * n, HEAVY_GRID), HT, 0, h->stream>>>(h->d, ini, res, tick, h->heavy_buf);
+        HIPCHK(h, hipGetLastError());
+    }
     return time_end(h, GS_KT_PACK, e0);
 }
 
@@ -5259,6 +5632,7 @@ int gs_create(const gs_config *cfg, gs_handle **out) {
         return GS_E_INVALID;
     gs_handle *h = new gs_handle();
     h->cfg = c;
+    h->d.t_cap = NONE;  // no sub-phases yet (plane_tick)
     h->N = c.n_nodes;
     h->G = G;
     h->sliced = G > 1 || (c.flags & GS_SLICED);
@@ -5390,6 +5764,7 @@ void gs_destroy(gs_handle *h) {
         if (p) (void)hipFree(p);
     if (h->sc.pin) (void)hipHostFree(h->sc.pin);
     if (h->grp) (void)hipFree(h->grp);
+    if (h->heavy_buf) (void)hipFree(h->heavy_buf);
     if (h->comm) (void)ncclCommDestroy(h->comm);
     if (h->side) (void)hipStreamDestroy(h->side);
     for (hipEvent_t e : {h->fj_fork, h->fj_join})
@@ -5520,6 +5895,8 @@ int gs_begin_round(gs_handle *h, const uint8_t *up, uint32_t tick) {
     }
     if (int rc = fd_age(h, tick)) return rc;  // the tick axis of the 16-bit report ticks (and gs_latest_tick)
     h->d.t_round = tick;
+    h->base_fresh = true;
+    h->sub_ok = false;
     h->last_phase_tick = tick;
     k_begin_round<<<h->N, LB, 0, h->stream>>>(h->d, up, tick);
     HIPCHK(h, hipGetLastError());
@@ -5565,7 +5942,8 @@ int gs_run_phase(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t 
         return n ? sliced_phase(&h, 1, ini, res, n, tick) : GS_OK;
     }
     if (!n) return GS_OK;
-    if ((rc = fd_age(h, tick)) || (rc = advance_planes(h, tick))) return rc;
+    if ((rc = fd_age(h, tick)) || (rc = plane_slot(h, tick, h->sub_ok && tick == h->last_phase_tick))) return rc;
+    h->sub_ok = true;
     const bool genm = !(h->cfg.flags & GS_CANONICAL);
     const size_t lds = exchange_lds(h);
     const SliceIO io{};
@@ -5599,7 +5977,8 @@ int gs_phase_count(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_
     if (!h->sliced) return fail(h, GS_E_UNSUPPORTED, "gs_phase_count needs a sliced handle (n_shards > 1 or GS_SLICED)");
     if (!n) return GS_OK;
     if (!slice_bytes) return GS_E_INVALID;
-    if ((rc = fd_age(h, tick)) || (rc = advance_planes(h, tick))) return rc;
+    if ((rc = fd_age(h, tick)) || (rc = plane_slot(h, tick, h->sub_ok && tick == h->last_phase_tick))) return rc;
+    h->sub_ok = true;
     const size_t lds = exchange_lds(h);
     SliceIO io{};
     io.tot = slice_bytes;
@@ -5852,6 +6231,7 @@ int group_upload(gs_handle *const *hs, uint32_t nh) {
         const gs_handle *h = hs[i];
         memcpy(&img.dv[i], &h->d, sizeof(Dev));
         img.dv[i].t_round = img.dv[i].spec = img.dv[i].lite = img.dv[i].p1fix = 0u;
+        img.dv[i].v_round = img.dv[i].vt = img.dv[i].t_cap = 0u;
         img.io[i].tot = h->sc.tot;
         img.io[i].tot_all = h->sc.tot_all;
         img.io[i].chain_all = h->sc.chain_all;
@@ -5876,21 +6256,23 @@ int group_steps(gs_handle *const *hs, uint32_t nh, const int32_t *ini, const int
     for (uint32_t i = 0; i < nh; i++) {
         gs_handle *h = hs[i];
         if ((rc = check_phase(h, ini, res, n, tick))) return rc;
-        if ((rc = fd_age(h, tick)) || (rc = advance_planes(h, tick))) return rc;
+        if ((rc = fd_age(h, tick)) || (rc = plane_slot(h, tick, h->sub_ok && tick == h->last_phase_tick))) return rc;
+        h->sub_ok = true;
         h->seq += 1;
         h->reports_pending = true;
         h->last_phase_tick = tick;
         h->hb_incs++;
         h->d.spec = spec_ok(h) || spec_v_ok(h) ? 1u : 0u;
         h->d.lite = lite_ok(h) ? 1u : 0u;
-        if (h->seq != h0->seq || h->d.t_round != h0->d.t_round || h->d.spec != h0->d.spec || h->d.lite != h0->d.lite)
+        if (h->seq != h0->seq || h->d.t_round != h0->d.t_round || h->d.spec != h0->d.spec || h->d.lite != h0->d.lite ||
+            h->d.v_round != h0->d.v_round || h->d.vt != h0->d.vt || h->d.t_cap != h0->d.t_cap)
             return fail(h0, GS_E_INVALID, "gs_run_phase_group: slice %u is not in step with slice 0", i);
     }
     if ((rc = group_upload(hs, nh))) return rc;
     GroupCtx gx;
     gx.ga = h0->grp;
     gx.nh = nh;
-    gx.dyn = DevDyn{h0->d.t_round, h0->d.spec, h0->d.lite, 0u};
+    gx.dyn = DevDyn{h0->d.t_round, h0->d.spec, h0->d.lite, 0u, h0->d.v_round, h0->d.vt, h0->d.t_cap};
     SliceIO io{};  // (each slice's from GroupArgs; the step by value)
     // count: pass 1, then lite + the slice totals in one launch, which also sets the responders' small bits; env
     // GS_GRP_P1LITE=1: the lite slot work in pass 1's epilogue instead, the count launch only for LITE_FULL slots
@@ -6033,11 +6415,16 @@ int gs_run_phase_group(gs_handle *const *hs, uint32_t n_handles, const int32_t *
                        uint32_t tick) {
     if (!hs || !n_handles || !hs[0]) return GS_E_INVALID;
     gs_handle *h0 = hs[0];
-    // every slice of the cluster, or one slice held alone (a rehearsal of one GPU's share: the others gather as
-    // zeros -- exact for that slice only when the mtu cannot bind, config 4's contract)
+    // every slice of the cluster, or slice 0 held alone (a rehearsal of one GPU's share: the others gather as
+    // zeros).  Slice 0 is exact alone whatever the mtu: the packer walks owners in slice order, so slice 0's
+    // NodeDeltas start every delta and never depend on the other slices' totals.  Any other slice held alone would
+    // pack from a zero predecessor total, silently wrong once the mtu binds, so it is refused.
     if (n_handles != h0->G && n_handles != 1)
         return fail(h0, GS_E_INVALID, "gs_run_phase_group: %u handles for %u slices", n_handles, h0->G);
     if (n_handles == 1 && h0->comm) return gs_run_phase(h0, ini, res, n, tick);
+    if (n_handles == 1 && h0->G > 1 && h0->shard != 0)
+        return fail(h0, GS_E_UNSUPPORTED, "gs_run_phase_group: slice %u held alone packs from its predecessors' "
+                    "totals, which only a communicator or the whole group provides (slice 0 alone is exact)", h0->shard);
     for (uint32_t i = 0; i < n_handles && n_handles > 1; i++) {
         if (!hs[i] || hs[i]->shard != i || hs[i]->G != h0->G || hs[i]->N != h0->N || hs[i]->stream != h0->stream)
             return fail(h0, GS_E_INVALID, "gs_run_phase_group: handle %u is not slice %u of this cluster on one stream", i, i);
@@ -6112,6 +6499,8 @@ int gs_flush_reports(gs_handle *h, uint32_t tick) {
         h->reports_pending = false;
     }
     h->d.t_round = tick;  // the next phase (after tick) starts a new plane base
+    h->base_fresh = true;
+    h->sub_ok = false;
     h->last_phase_tick = tick;
     return GS_OK;
 }
@@ -6272,9 +6661,9 @@ int gs_read_counters(gs_handle *h, gs_counters *out) {
     std::vector<unsigned long long> buf((size_t)NSHARD * CROW);
     HIPCHK(h, hipMemcpyAsync(buf.data(), h->reg[GS_R_COUNTERS], buf.size() * 8, hipMemcpyDeviceToHost, h->stream));
     HIPCHK(h, hipStreamSynchronize(h->stream));
-    uint64_t acc[32] = {0};  // the gs_counters fields (the census scratch follows them in each row)
+    uint64_t acc[CFIELDS] = {0};  // the gs_counters fields (the census scratch follows them in each row)
     for (int s = 0; s < NSHARD; s++)
-        for (int c = 0; c < 32; c++) {
+        for (int c = 0; c < CFIELDS; c++) {
             const uint64_t v = buf[(size_t)s * CROW + c];
             if (c == C_PGMAX || c == C_PSMAX) acc[c] = std::max<uint64_t>(acc[c], v);  // maxima, not sums
             else acc[c] += v;
@@ -6354,30 +6743,35 @@ int gs_schedule_phases(gs_handle *h, const uint8_t *up, uint32_t fanout, const i
                        uint32_t round, uint32_t iters, uint32_t max_phases, void *scratch, int32_t *initiators,
                        int32_t *responders, uint32_t *phase_offsets, uint32_t *unscheduled) {
     if (!h || !up || !targets || !scratch || !initiators || !responders || !phase_offsets || !unscheduled ||
-        fanout < 1 || fanout > 8 || iters < 1 || max_phases < 1 || max_phases > GS_MAX_PHASES)
+        fanout < 1 || fanout > 8 || iters < 1 || max_phases < 1 || max_phases > GS_MAX_SCHED_PHASES)
         return GS_E_INVALID;
     const uint32_t N = h->N, E = N * (fanout + 2);
-    // scratch: eph[E] | pcount[64] | pfill[64] | poff[64] | left[64] | busy[N] (u64) | best[2][N] (u64)
+    // scratch (GS_SCHED_SCRATCH_BYTES): eph[E] | pcount[P] | pfill[P] | poff[P] | left[4] | busy[N] (u64) |
+    // best[2][N] (u64)
+    const uint32_t P = max_phases;
     uint32_t *eph = (uint32_t *)scratch;
     uint32_t *pcount = eph + E;
-    uint32_t *pfill = pcount + 64;
-    uint32_t *poff = pfill + 64;
-    uint32_t *left = poff + 64;
-    unsigned long long *busy = (unsigned long long *)(((uintptr_t)(left + 64) + 15) & ~(uintptr_t)15);
+    uint32_t *pfill = pcount + P;
+    uint32_t *poff = pfill + P;
+    uint32_t *left = poff + P;
+    unsigned long long *busy = (unsigned long long *)(((uintptr_t)(left + 4) + 15) & ~(uintptr_t)15);
     unsigned long long *best = busy + N;
     hipStream_t s = h->stream;
     HIPCHK(h, hipMemsetAsync(eph, 0xFF, (size_t)E * 4, s));
-    HIPCHK(h, hipMemsetAsync(pcount, 0, 4 * 64 * 4, s));
+    HIPCHK(h, hipMemsetAsync(pcount, 0, ((size_t)3 * P + 4) * 4, s));
     HIPCHK(h, hipMemsetAsync(busy, 0, (size_t)N * 8, s));
     HIPCHK(h, hipMemsetAsync(best, 0xFF, (size_t)N * 16, s));
     const uint32_t gE = (std::max(E, N) + LB - 1) / LB;
     // the two minimum buffers alternate by the GLOBAL iteration index, so each pick resets exactly
     // the buffer the next iteration (of this phase or the next) reduces into, whatever iters is
-    uint32_t g = 0, nleft = 0, chk = 0;
+    uint32_t g = 0, nleft = 0;
     // phases in blocks: 16 first (a round's schedule needs about 15-17 at fanout 3), then 4 at a time (the last few
     // exchanges), each block followed by one count of the exchanges still without a phase
-    for (uint32_t p0 = 0, p1; p0 < max_phases; p0 = p1, chk++) {
+    for (uint32_t p0 = 0, p1; p0 < max_phases; p0 = p1) {
         p1 = std::min(max_phases, p0 + (p0 ? 4u : 16u));
+        // busy holds bit p mod 64: a block starting a new window of 64 phases starts from clear bits (blocks are
+        // 16 then 4 phases, so windows start at block boundaries)
+        if (p0 && (p0 & 63u) == 0) HIPCHK(h, hipMemsetAsync(busy, 0, (size_t)N * 8, s));
         for (uint32_t p = p0; p < p1; p++)
             for (uint32_t it = 0; it < iters; it++, g++) {
                 unsigned long long *b0 = best + (size_t)(g & 1) * N, *b1 = best + (size_t)((g + 1) & 1) * N;
@@ -6387,15 +6781,15 @@ int gs_schedule_phases(gs_handle *h, const uint8_t *up, uint32_t fanout, const i
                                               pcount);
             }
         // stop once every valid exchange has a phase
-        HIPCHK(h, hipMemsetAsync(left + chk, 0, 4, s));
-        k_luby_left<<<(E + LB - 1) / LB, LB, 0, s>>>(targets, up, eph, E, fanout, left + chk);
+        HIPCHK(h, hipMemsetAsync(left, 0, 4, s));
+        k_luby_left<<<(E + LB - 1) / LB, LB, 0, s>>>(targets, up, eph, E, fanout, left);
         HIPCHK(h, hipGetLastError());
-        HIPCHK(h, hipMemcpyAsync(&nleft, left + chk, 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(h, hipMemcpyAsync(&nleft, left, 4, hipMemcpyDeviceToHost, s));
         HIPCHK(h, hipStreamSynchronize(s));
         if (!nleft) break;
     }
-    uint32_t cnt[GS_MAX_PHASES];
-    HIPCHK(h, hipMemcpyAsync(cnt, pcount, sizeof cnt, hipMemcpyDeviceToHost, s));
+    std::vector<uint32_t> cnt(max_phases);
+    HIPCHK(h, hipMemcpyAsync(cnt.data(), pcount, (size_t)max_phases * 4, hipMemcpyDeviceToHost, s));
     HIPCHK(h, hipStreamSynchronize(s));
     std::vector<uint32_t> off(max_phases + 1);
     off[0] = 0;
@@ -6461,6 +6855,15 @@ int gs_stream_read(const void *src, uint64_t bytes, uint32_t width, uint64_t *si
     else
         k_read<uint4><<<32768, 256, 0, (hipStream_t)stream>>>((const uint4 *)src, bytes / 16,
                                                               (unsigned long long *)sink);
+    return hipGetLastError() == hipSuccess ? GS_OK : GS_E_HIP;
+}
+
+int gs_mark(uint32_t which, void *stream) {
+    if (which > 1) return GS_E_INVALID;
+    if (which == 0)
+        k_mark_begin<<<1, WAVE, 0, (hipStream_t)stream>>>();
+    else
+        k_mark_end<<<1, WAVE, 0, (hipStream_t)stream>>>();
     return hipGetLastError() == hipSuccess ? GS_OK : GS_E_HIP;
 }
 

@@ -115,7 +115,7 @@ def run_round(sims, rd, events=None, group=None, sel=None):
     """One gossip round on the slices this process drives (one GossipSim when unsliced).  With ``sel``
     (a PeerSelector) the round's exchanges come from the device's select_nodes_for_gossip + phase
     schedule instead of the workload's explicit schedule (``rd`` gains "exchanges", "unscheduled")."""
-    from .workload import TICKS_PER_ROUND, phase_tick
+    from .workload import TICKS_PER_ROUND, liveness_tick, phase_tick
 
     begin(sims, rd)
     phases = None
@@ -125,7 +125,8 @@ def run_round(sims, rd, events=None, group=None, sel=None):
         phases = [(a, b, n, phase_tick(rd["r"], p)) for p, (a, b, n) in enumerate(ph)]
         rd["exchanges"] = offs[-1]
         rd["unscheduled"] = left
-        rd["t_live"] = rd["t"] + 1 + len(phases)
+        rd["t_live"] = liveness_tick(rd["r"], len(phases))  # sub-phases share the budget's last tick
+        rd["phases_run"] = len(phases)
     if rd["t_live"] >= rd["t"] + TICKS_PER_ROUND:
         raise ValueError(f"round {rd['r']}: liveness tick {rd['t_live']} reaches the next round's tick")
     run_phases(sims, rd, events, group, phases)

@@ -18,25 +18,24 @@ import ctypes as C
 
 import numpy as np
 
-from ._lib import MAX_PHASES, GsError
+from ._lib import MAX_SCHED_PHASES, GsError, sched_scratch_bytes
 
 
 class PeerSelector:
     """Device buffers for one cluster's per-round peer selection and phase schedule."""
 
-    def __init__(self, sim, fanout: int = 3, seeds=(), seed: int = 0, iters: int = 4, max_phases: int = 62):
+    def __init__(self, sim, fanout: int = 3, seeds=(), seed: int = 0, iters: int = 4,
+                 max_phases: int = MAX_SCHED_PHASES):
         if sim.shards > 1:
             raise GsError("peer selection needs the whole matrix (one slice)")
         if not 1 <= fanout <= 8:
             raise GsError("fanout must be in 1..8")
-        from .workload import MAX_PHASES_PER_ROUND
-
         torch = sim.torch
-        # the workload's tick model: phase p at round tick + 1 + p, liveness after the last phase, all before
-        # the next round's tick (TICKS_PER_ROUND apart)
-        top = min(MAX_PHASES, MAX_PHASES_PER_ROUND)
-        if not 1 <= max_phases <= top:
-            raise GsError(f"max_phases must be in 1..{top}")
+        # the workload's tick model: phase p at round tick + 1 + min(p, MAX_PHASES_PER_ROUND - 1) -- the phases past
+        # the tick budget are sub-phases at its last tick (workload.phase_tick), so every selected exchange runs
+        # (server.py:476-493) -- and liveness after them, before the next round's tick
+        if not 1 <= max_phases <= MAX_SCHED_PHASES:
+            raise GsError(f"max_phases must be in 1..{MAX_SCHED_PHASES}")
         self.sim, self.fanout, self.seed, self.iters = sim, int(fanout), int(seed), int(iters)
         self.max_phases = int(max_phases)
         n, F = sim.n, self.fanout
@@ -45,7 +44,7 @@ class PeerSelector:
         self.n_seeds = len(set(seeds))
         self.targets = torch.empty((n, F + 2), dtype=torch.int32, device=dev)
         self.sel_scratch = torch.empty(4 * n * (F + 6), dtype=torch.uint8, device=dev)
-        self.sched_scratch = torch.empty(4 * n * (F + 2) + 24 * n + 1040, dtype=torch.uint8, device=dev)
+        self.sched_scratch = torch.empty(sched_scratch_bytes(n, F, self.max_phases), dtype=torch.uint8, device=dev)
         self.ini = torch.empty(n * (F + 2), dtype=torch.int32, device=dev)
         self.res = torch.empty(n * (F + 2), dtype=torch.int32, device=dev)
 
@@ -71,9 +70,11 @@ class PeerSelector:
                                       C.c_void_p(self.targets.data_ptr()), self.seed, r, self.iters, P,
                                       C.c_void_p(self.sched_scratch.data_ptr()), C.c_void_p(self.ini.data_ptr()),
                                       C.c_void_p(self.res.data_ptr()), off, C.byref(left)), "gs_schedule_phases")
-        offs = list(off)
-        phases = [(self.ini[offs[p]:offs[p + 1]], self.res[offs[p]:offs[p + 1]], offs[p + 1] - offs[p])
-                  for p in range(P) if offs[p + 1] > offs[p]]
+        offs = np.frombuffer(off, dtype=np.uint32).astype(np.int64)
+        nz = np.flatnonzero(offs[1:] > offs[:-1]).tolist()
+        phases = [(self.ini[offs[p]:offs[p + 1]], self.res[offs[p]:offs[p + 1]], int(offs[p + 1] - offs[p]))
+                  for p in nz]
+        offs = offs.tolist()
         return phases, offs, int(left.value)
 
     def scheduled_pairs(self, phases) -> list[set]:
@@ -95,6 +96,7 @@ def run_selected_round(sim, sel: PeerSelector, r: int, up, writes=None, tick0: i
     phases, offs, left = sel.schedule(up_dev, r)
     if left:
         raise GsError(f"round {r}: {left} selected exchanges did not fit in {sel.max_phases} phases")
+    # phases past the tick budget share its last tick (sub-phases: workload.phase_tick)
     for p, (a, b, n) in enumerate(phases):
         sim.run_phase_arrays(phase_tick(r, p), a, b)
     sim.update_node_liveness(liveness_tick(r, len(phases)), up_dev)

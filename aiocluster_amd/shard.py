@@ -141,18 +141,22 @@ def run_sliced_phase(slices, comm, mtu: int, t: int, ini, res, cache: dict | Non
     tots = [s.phase_count(t, ini, res) for s in slices]
     tot_all = comm.gather(tots)
     dev = tots[0].device
-    key = (n, str(dev), len(slices))
+    # scratch sized for the largest phase seen on this device and slice count (peer-selected schedules change the
+    # exchange count nearly every phase: views of one allocation, not a reallocation per phase)
+    key = (str(dev), len(slices))
     buf = None if cache is None else cache.get(key)
-    if buf is None:
+    if buf is None or buf["n"] < n:
         buf = {
-            "chains": [torch.empty_like(x) for x in tots],
+            "n": n,
+            "chains": [torch.empty((n, 2), dtype=torch.int64, device=dev) for _ in slices],
             "lists": [torch.empty(overflow_list_len(n), dtype=torch.int32, device=dev) for _ in slices],
             # [2n + 1] (the listed slots' states, then the pending entry), at least GS_CHAIN_CAP + 1
             "chaincs": [torch.empty(max(2 * n, GS_CHAIN_CAP) + 1, dtype=torch.int64, device=dev) for _ in slices],
         }
         if cache is not None:
-            cache.clear()  # one exchange count at a time (phases of one schedule mostly share it)
             cache[key] = buf
+    buf = {"chains": [x[:n] for x in buf["chains"]], "lists": [x[: overflow_list_len(n)] for x in buf["lists"]],
+           "chaincs": [x[: max(2 * n, GS_CHAIN_CAP) + 1] for x in buf["chaincs"]]}
     chains = buf["chains"]
     for s, ch in zip(slices, chains):
         s.phase_pack(t, ini, res, 0, tot_all, None, ch)

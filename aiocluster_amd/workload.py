@@ -44,11 +44,14 @@ def round_tick(r: int) -> int:
 
 
 def phase_tick(r: int, p: int) -> int:
-    return round_tick(r) + 1 + p
+    """Tick of phase p of round r.  Phases past the tick budget (a schedule by the reference's own selection, whose
+    hubs need more phases than a round has ticks) are sub-phases at the budget's last tick: the reference runs
+    every selected exchange (server.py:476-493), concurrently, so several at one time."""
+    return round_tick(r) + 1 + min(p, MAX_PHASES_PER_ROUND - 1)
 
 
 def liveness_tick(r: int, n_phases: int) -> int:
-    return round_tick(r) + 1 + n_phases
+    return round_tick(r) + 1 + min(n_phases, MAX_PHASES_PER_ROUND)
 
 
 def synthetic_node_ids(n: int) -> list[NodeId]:

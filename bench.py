@@ -115,7 +115,7 @@ def cpu_baseline(sim, cfg, rd, sample: int, min_seconds: float = 10.0, threads: 
     # the T threads below restores its handle just before its timed pass (like for like: cache-warm rows in
     # both legs; VERDICT r4: restoring all handles first left the single thread's rows cold)
     dt1, reps1, rate1 = 0.0, 0, []
-    pin_to(T)
+    pin_to(0)  # the threaded leg's first core (a different core made the two legs incomparable)
     while dt1 < min_seconds / 3 or reps1 < 3:
         dt = 0.0
         for i in range(T):
@@ -126,6 +126,7 @@ def cpu_baseline(sim, cfg, rd, sample: int, min_seconds: float = 10.0, threads: 
         dt1 += dt
         reps1 += 1
         rate1.append(len(pairs) / dt)
+    pin_to(T)  # the main thread (it only waits at the barriers) off the workers' cores
     # T threads (ctypes drops the GIL during each oracle call), a barrier around every timed pass
     import threading
     bar = threading.Barrier(T + 1)
@@ -178,10 +179,12 @@ def cpu_baseline(sim, cfg, rd, sample: int, min_seconds: float = 10.0, threads: 
         "statistic": f"median of {repsT} timed passes (p10 {q(rateT, 10):.0f}, p90 {q(rateT, 90):.0f}; mean "
                      f"{len(pairs) * repsT / dtT:.0f})",
         "single_core_value": q(rate1, 50),
+        "threaded_per_core_value": q(rateT, 50) / T,
         "single_core_statistic": f"median of {reps1} passes (p10 {q(rate1, 10):.0f}, p90 {q(rate1, 90):.0f}); each "
                                  f"handle timed right after its own rows are restored, as in the threaded leg",
         "host": {"cpu_model": model, "cpus_allowed": len(cpus),
-                 "pinning": (f"thread i on CPU {pin[0]}+i, single-thread runs on CPU {pin[T]}" if pin is not None
+                 "pinning": (f"thread i on CPU {pin[0]}+i, the single-thread leg on CPU {pin[0]} (thread 0's)"
+                             if pin is not None
                              else "unpinned (fewer allowed CPUs than threads)"),
                  "loadavg_1min_before": load0},
         "sample": f"{len(pairs)} exchanges (disjoint pairs of the first phase of the round after the timed ones) "
@@ -191,6 +194,58 @@ def cpu_baseline(sim, cfg, rd, sample: int, min_seconds: float = 10.0, threads: 
                   f"per pass",
         "parity_check": f"{len(rows)} device rows after that phase + liveness == oracle rows (bit-exact)",
     }
+
+
+class ObjComm:
+    """Object collectives for the sliced parity check over a gloo group of the bench's ranks (host pickles, so
+    the same code runs beside an RCCL group): ``gather`` collects every rank's list on rank 0, ``allmax``."""
+
+    def __init__(self, dist):
+        self.dist = dist
+        self.group = dist.new_group(backend="gloo")
+        self.rank, self.world = dist.get_rank(), dist.get_world_size()
+
+    def gather(self, xs: list):
+        out = [None] * self.world if self.rank == 0 else None
+        self.dist.gather_object(xs, out, dst=0, group=self.group)
+        return [x for part in out for x in part] if self.rank == 0 else None
+
+    def allmax(self, x: int) -> int:
+        import torch
+
+        t = torch.tensor([int(x)], dtype=torch.int64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX, group=self.group)
+        return int(t.item())
+
+    def bcast(self, obj):
+        box = [obj]
+        self.dist.broadcast_object_list(box, src=0, group=self.group)
+        return box[0]
+
+
+def sliced_parity(group, cfg, rd, sample: int, dist) -> dict | None:
+    """Bit-exact check of a sliced run (every rank calls it; rank 0 returns the result): oracle/rowcheck's
+    ``check_sliced_phase_rows`` -- the rows of ``sample`` exchanges of ``rd``'s first phase, copied out of every
+    slice and joined into whole-cluster rows, vs the same exchanges + liveness in the C oracle.  Raises on a
+    mismatch, on every rank, like the single-GPU CPU-baseline check."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import rowcheck  # test infrastructure: the checker
+
+    comm = ObjComm(dist) if dist is not None else None
+    t0 = time.perf_counter()
+    res, info = rowcheck.check_sliced_phase_rows(group, cfg, rd, sample=sample, comm=comm)
+    ok = all(r["exact"] for r in res) if res is not None else None
+    if comm is not None:
+        ok = comm.bcast(ok)
+    if not ok:
+        raise SystemExit(f"sliced full-size parity FAILED: {res}")
+    if res is None:
+        return None
+    return {"exact": True, "per_slice": res, **info, "seconds": time.perf_counter() - t0,
+            "what": "rows of the sampled exchanges of the first phase of the round after the timed ones, copied "
+                    "from every slice after gs_begin_round and joined into whole-cluster rows (every owner column, "
+                    "so the MTU walk across slices is covered); the phase ran on the devices through the sliced "
+                    "driver, then the liveness sweep; each slice's columns == the C oracle's (bit-exact)"}
 
 
 def aggregate(exchanges: float, elapsed: float, dist=None, dev=None) -> tuple[float, float]:
@@ -409,7 +464,7 @@ def config4_leg(args, world: int, rank: int, dist, dev) -> dict:
     comm = DistComm() if world == C4_GPUS else SoloComm(C4_GPUS, 0)
     grp = ShardGroup([sim], comm, cfg["mtu"])
     S, W, T = args.config4_settle, 1, args.config4_steps
-    plans = driver.prepare(spec, S + W + T, torch, dev)
+    plans = driver.prepare(spec, S + W + T + 1, torch, dev)
     torch.cuda.synchronize(dev)
     setup = time.perf_counter() - t0
     for r in range(S + W):
@@ -435,7 +490,23 @@ def config4_leg(args, world: int, rank: int, dist, dev) -> dict:
     exch = sum(plans[r]["exchanges"] for r in range(S + W, S + W + T))
     assert c["exchanges"] == exch, (c["exchanges"], exch)
     _, el_max = aggregate(0.0, el, dist, dev)
-    hz = sim.horizon(rounds=S + W + T)
+    # parity of this leg: the next round's first phase, sampled rows vs the C oracle
+    par = None
+    if args.parity_sample:
+        rd = plans[S + W + T]
+        driver.begin([sim], rd)
+        if world == C4_GPUS:  # whole-cluster rows joined from the 8 slices
+            par = sliced_parity(grp, cfg, rd, min(args.parity_sample, 8), dist)
+        else:  # slice 0 alone: the other columns inert in the oracle, exact under config 4's mtu (no truncation)
+            sys.path.insert(0, os.path.join(REPO, "oracle"))
+            import rowcheck
+
+            diff, info = rowcheck.check_phase_rows(sim, cfg, rd, sample=min(args.parity_sample, 8), group=grp)
+            if diff is not None:
+                raise SystemExit(f"config-4 slice parity FAILED: {diff}")
+            par = {"exact": True, "scope": "slice 0's columns (the others inert; exact: mtu 2^30)",
+                   **{k: int(info[k]) for k in ("rows", "node_deltas", "hb_reports")}}
+    hz = sim.horizon(rounds=S + W + T + (1 if par is not None else 0))
     sim.close()
     del sim, grp
     torch.cuda.empty_cache()
@@ -460,6 +531,7 @@ def config4_leg(args, world: int, rank: int, dist, dev) -> dict:
         "kernel_ms_per_step": {k: v[0] / T for k, v in kt.items() if v[1]},
         "counters": {k: v for k, v in c.items() if not k.startswith("err_")},
         "exactness": hz,
+        "parity_check": par,
     }
 
 
@@ -489,12 +561,22 @@ def peer_select_rounds(sims, plans, r0: int, steps: int, args, n: int, dev) -> d
         "steps": steps,
         "ms_per_step": dt / steps * 1e3,
         "exchanges_per_step": exch / steps,
-        "phases_per_round": [rd["t_live"] - rd["t"] - 1 for rd in rds],
+        "phases_per_round": [rd["phases_run"] for rd in rds],
         "unscheduled_exchanges": sum(rd["unscheduled"] for rd in rds),
         "note": "same cluster state and workload as the headline; the schedule comes from the device's "
                 "select_nodes_for_gossip + Luby phases instead of the workload generator's permutations "
-                "(selection, scheduling and the phase-offset read back are inside the timed region)",
+                "(selection, scheduling and the phase-offset read back are inside the timed region); phases past the "
+                "round's 62-tick budget run as sub-phases at its last tick, so every selected exchange runs",
     }
+
+
+def mark(sim, which: int) -> None:
+    """An empty marker dispatch (gs_mark: k_mark_begin / k_mark_end) on the library's stream: rocprofv3 traces then
+    show exactly which dispatches the timed rounds made (tools/pmc_summary.py selects them by position)."""
+    from aiocluster_amd import _lib
+
+    rc = _lib.load().gs_mark(which, C.c_void_p(sim.stream.cuda_stream))
+    assert rc == 0, rc
 
 
 def launch_ranks(n: int) -> int:
@@ -533,6 +615,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--slices", type=int, default=1, help="owner-column slices in this process (1-GPU rehearsal)")
     ap.add_argument("--mtu", type=int, default=65507)
+    ap.add_argument("--parity-sample", type=int, default=16,
+                    help="sliced runs (--gpus N > 1, --slices G): after the timed rounds, check this many exchanges "
+                         "of the next round's first phase against the C oracle on whole-cluster rows joined from "
+                         "every slice (0 = skip)")
     ap.add_argument("--peer-select", action="store_true",
                     help="schedule each round with the device's select_nodes_for_gossip (gs_select_peers) and "
                          "Luby phases (gs_schedule_phases) instead of the workload's permutation schedule")
@@ -649,7 +735,8 @@ def main():
         ts = time.perf_counter()
         driver.run_round(sims, plans[r], group=group, sel=sel)
         torch.cuda.synchronize(dev)
-        log(f"settle round {r}: {(time.perf_counter() - ts) * 1e3:.1f} ms, {plans[r]['exchanges']} exchanges")
+        log(f"settle round {r}: {(time.perf_counter() - ts) * 1e3:.1f} ms, {plans[r]['exchanges']} exchanges"
+            + (f", {plans[r]['phases_run']} phases" if sel is not None else ""))
     for r in range(args.settle, R0):
         driver.run_round(sims, plans[r], group=group, sel=sel)
     torch.cuda.synchronize(dev)
@@ -661,9 +748,11 @@ def main():
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize(dev)
+    mark(sims[0], 0)  # k_mark_begin / k_mark_end bracket the timed dispatches in a kernel trace (tools/pmc_summary.py)
     t0 = time.perf_counter()
     for r in range(R0, R0 + args.steps):
         driver.run_round(sims, plans[r], None, group, sel)
+    mark(sims[0], 1)
     torch.cuda.synchronize(dev)
     if dist is not None:
         dist.barrier()
@@ -686,6 +775,13 @@ def main():
         rd = plans[R0 + args.steps]
         driver.begin(sims, rd)
         cpu = cpu_baseline(sim, cfg, rd, args.cpu_sample, args.cpu_seconds, args.cpu_threads)
+    par = None
+    if group is not None and args.rehearse_slices <= 1 and args.parity_sample:
+        # the sliced run's own parity evidence: the round after the timed ones, phase 0's
+        # first exchanges, whole-cluster rows joined from every slice vs the C oracle
+        rd = plans[R0 + args.steps]
+        driver.begin(sims, rd)
+        par = sliced_parity(group, cfg, rd, args.parity_sample, dist)
     ps = None
     if ps_steps:
         ps = peer_select_rounds(sims, plans, R0 + args.steps + 1, ps_steps, args, n, dev)
@@ -695,7 +791,8 @@ def main():
         errs = {k: v for k, v in sims[0].counters().items() if k.startswith("err_") and v}
         ps["device_errors"] = errs
         ps["exact"] = not errs
-    rounds_run = R0 + args.steps + (1 if cpu is not None else 0) + (ps_steps + 1 if ps is not None else 0)
+    rounds_run = (R0 + args.steps + (1 if (cpu is not None or par is not None) else 0)
+                  + (ps_steps + 1 if ps is not None else 0))
     horizon = sims[0].horizon(rounds=rounds_run)
     sliced = group is not None  # (the config-4 leg below releases the headline's handles first)
     c4 = None
@@ -734,10 +831,18 @@ def main():
                                 else f"slice 0 of {args.rehearse_slices} (rehearsal)" if args.rehearse_slices > 1
                                 else f"owner-column slices x{args.slices} in one process" if sliced
                                 else "1 GPU"),
-                **({"unscheduled_exchanges": unscheduled} if sel is not None else {}),
+                **({"unscheduled_exchanges": unscheduled,
+                    # every round of the run, settle and warmup included (round 5 dropped the exchanges past 62
+                    # phases in the settle rounds, where the seed hubs are busiest: VERDICT r5)
+                    "unscheduled_exchanges_all_rounds": sum(plans[r].get("unscheduled", 0)
+                                                            for r in range(R0 + args.steps)),
+                    "max_phases_per_round": max(plans[r].get("phases_run", 0) for r in range(R0 + args.steps)),
+                    "rounds_with_sub_phases": sum(plans[r].get("phases_run", 0) > 62 for r in range(R0 + args.steps))}
+                   if sel is not None else {}),
             },
             "roofline": roof,
             "cpu_baseline": cpu,
+            **({"parity_check": par} if par is not None else {}),
             "peer_select": ps,
             **({"ABLATION_RESULTS_INVALID": os.environ["GS_ABLATE"]} if os.environ.get("GS_ABLATE") else {}),
             "counters": {**{k: v for k, v in c.items() if not k.startswith("err_")}, "inexact_views": inexact},

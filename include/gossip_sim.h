@@ -28,8 +28,14 @@
 extern "C" {
 #endif
 
-#define GS_API_VERSION 18
-#define GS_MAX_PHASES 64  /* gs_schedule_phases: phases per round */
+#define GS_API_VERSION 20
+#define GS_MAX_PHASES 64  /* report bit planes' phases per plane base window of the scheduler (busy bits) */
+/* gs_schedule_phases: phases of one round's schedule.  Every selected exchange runs (server.py:476-493): phases
+ * past the workload's tick budget are sub-phases, run at one tick (gs_run_phase at the previous phase's tick). */
+#define GS_MAX_SCHED_PHASES 65536u
+/* DEVICE scratch bytes of gs_schedule_phases for N nodes, fanout F, max_phases P */
+#define GS_SCHED_SCRATCH_BYTES(N, F, P) \
+    (4ull * (N) * ((F) + 2) + 12ull * (P) + 32ull + 24ull * (N))
 #define GS_TICK_US 15625u
 #define GS_NONE 0xFFFFFFFFu
 #define GS_CAND_CAP 1024u /* GS_R_CAND records per exchange, direction and row half */
@@ -144,7 +150,7 @@ enum gs_region {
     GS_R_NID_SIZE,    /* u16 [NP]      NodeIdPb size per owner column (entities.py:62-72) */
     GS_R_KEY_LEN,     /* u8  [KP]      UTF-8 key length per key index */
     GS_R_STAMP,       /* u32 [N rounded to 64] per-node phase stamp (conflict check) */
-    GS_R_COUNTERS,    /* u64 [64][40]  sharded gs_counters (summed by gs_read_counters) and census scratch */
+    GS_R_COUNTERS,    /* u64 [64][48]  sharded gs_counters (summed by gs_read_counters) and census scratch */
     GS_R_SLICE_BITS,  /* u32 [N/2][2][NP/32] stale-owner bitmaps per exchange and direction: between
                                         gs_phase_count and gs_phase_pack (n_shards > 1), and between the two
                                         kernels of a canonical one-slice gs_run_phase */
@@ -243,6 +249,9 @@ typedef struct gs_counters {
     uint64_t pack_steps_max;   /* a MAXIMUM: the longest dependent walk of one slot -- groups evaluated, batches of
                                   groups skipped in first-fit continuation, bitmap windows -- the packer's
                                   critical path */
+    uint64_t heavy_slots;      /* (exchange, direction) slots the exact packer handed to its heavy-slot kernel
+                                  (k_pack_heavy: more stale owners than the hand-off threshold) */
+    uint64_t reserved[7];
 } gs_counters;
 
 /* Failure-detector membership census (gs_fd_census): (observer, target) pairs with the observer up and
@@ -295,11 +304,14 @@ int gs_begin_round(gs_handle *h, const uint8_t *up, uint32_t tick);
  * Syn/SynAck/Ack = server.py:327-376 + 524, i.e. compute_digest, _report_heartbeat,
  * compute_partial_delta_respecting_mtu and apply_delta on both sides.  At most n_nodes/2 exchanges;
  * the round must still be open (no gs_liveness since the last gs_begin_round) and `tick` must be
- * later than the round start and than the round's previous phase.  The failure detector's
- * report_heartbeat calls are recorded per phase (GS_R_PEND bit planes, GS_PLANES per row) and applied to the
- * sampling windows, in tick order, by the gs_liveness that closes the round (nothing reads a
- * window in between); a phase more than GS_PLANES ticks after the planes' base replays the pending planes
- * into the windows first (counted in plane_flushes). */
+ * later than the round start and not earlier than the round's previous phase: a phase at the previous
+ * phase's tick is a sub-phase (the exchanges a schedule needs past its tick budget, e.g. the 8 seeds'
+ * hundreds of exchanges while every live set is empty: the reference runs every selected exchange,
+ * server.py:476-493; its reports at one time append 0-s intervals, failure_detector.py:32-38).  The failure
+ * detector's report_heartbeat calls are recorded per phase (GS_R_PEND bit planes, GS_PLANES per row) and
+ * applied to the sampling windows, in tick order, by the gs_liveness that closes the round (nothing reads a
+ * window in between); a phase past the planes' base's GS_PLANES planes replays the pending planes into the
+ * windows first (counted in plane_flushes). */
 int gs_run_phase(gs_handle *h, const int32_t *initiators, const int32_t *responders, uint32_t n, uint32_t tick);
 /* Owner-column sliced phase (n_shards > 1; gs_run_phase refuses sliced handles).  The slices of one
  * cluster run, per phase, on the same initiators/responders:
@@ -366,9 +378,10 @@ int gs_phase_pending(gs_handle *h, uint32_t n, const uint32_t *list, uint32_t co
  * handle runs the whole phase (one blocking host read of the overflow count, as gs_phase_overflow).
  * gs_run_phase_group: the same phase for all G slices of one cluster held by this process (one device,
  * one stream; the gathers are device copies; each step one launch for all slices, grid.y = slice) -- the
- * one-GPU rehearsal and test of the same driver.  n_handles = 1 of G > 1 slices: that slice held alone, the
- * others' totals and chain states gathered as zeros (a timing rehearsal of one GPU's share; exact for its
- * columns only when the mtu cannot bind, config 4's contract). */
+ * one-GPU rehearsal and test of the same driver.  n_handles = 1 of G > 1 slices: slice 0 held alone, the
+ * others' totals and chain states gathered as zeros (a timing rehearsal of one GPU's share; exact for slice 0's
+ * columns, whose NodeDeltas start every delta); any other slice alone returns GS_E_UNSUPPORTED (it would pack
+ * from a zero predecessor total). */
 #define GS_COMM_ID_BYTES 128
 int gs_comm_id(void *id);
 int gs_comm_init(gs_handle *h, const void *id, uint32_t nranks, uint32_t rank);
@@ -429,13 +442,13 @@ int gs_set_events(gs_handle *h, uint32_t *records, uint32_t capacity, uint32_t *
 int gs_select_peers(gs_handle *h, const uint8_t *up, uint32_t fanout, const int32_t *seeds, uint32_t n_seeds,
                     uint64_t seed, uint32_t round, int32_t *targets, void *scratch);
 /* The round's exchanges (initiator o, responder targets[o][s], responder up) in <= max_phases
- * (<= GS_MAX_PHASES) conflict-free phases: per phase `iters` rounds of a deterministic Luby matching
+ * (<= GS_MAX_SCHED_PHASES) conflict-free phases: per phase `iters` rounds of a deterministic Luby matching
  * (an exchange whose endpoints are free in that phase takes it if its priority key is the smallest at
  * both).  Writes the exchanges of phase p to DEVICE initiators/responders[phase_offsets[p] ..
  * phase_offsets[p+1]) (order within a phase unspecified: exchanges of one phase commute) and the host
  * array phase_offsets[max_phases + 1]; *unscheduled (host) = valid exchanges (responder up) left
  * after max_phases phases, which are not run (0 unless the round needs more phases).  DEVICE scratch
- * of 4 * N * (fanout + 2) + 24 * N + 1040 bytes.  Blocking. */
+ * of GS_SCHED_SCRATCH_BYTES(N, fanout, max_phases) bytes.  Blocking. */
 int gs_schedule_phases(gs_handle *h, const uint8_t *up, uint32_t fanout, const int32_t *targets, uint64_t seed,
                        uint32_t round, uint32_t iters, uint32_t max_phases, void *scratch, int32_t *initiators,
                        int32_t *responders, uint32_t *phase_offsets, uint32_t *unscheduled);
@@ -479,6 +492,10 @@ int gs_stream_copy(void *dst, const void *src, uint64_t bytes, void *stream);
 int gs_stream_read(const void *src, uint64_t bytes, uint32_t width, uint64_t *sink, void *stream);
 /* a write-only stream of `bytes` at `width` = 4, 8 or 16 B per lane: the known byte count for WRITE_SIZE */
 int gs_stream_write(void *dst, uint64_t bytes, uint32_t width, void *stream);
+/* a trace marker: which = 0 launches the empty kernel k_mark_begin, 1 k_mark_end, on `stream`.  bench.py brackets
+ * its timed rounds with them so that a rocprofv3 kernel trace / PMC pass can select exactly those dispatches
+ * (tools/pmc_summary.py). */
+int gs_mark(uint32_t which, void *stream);
 
 /* Per-kernel timing (measurement): with timing on, every launch of the kinds below is bracketed by HIP
  * events on the library's stream; gs_kernel_times (blocking) returns the summed milliseconds and launch

@@ -711,6 +711,22 @@ static void mt_split(orc *o, int kind, const int32_t *a, const int32_t *b, const
 }
 
 void orc_run_phase_mt(orc *o, const int32_t *a, const int32_t *b, int32_t n, int64_t now, int32_t threads) {
+    /* the threads share rows only if the phase's exchanges are disjoint (a conflict-free phase): a node in two
+     * pairs would race, so such a phase runs sequentially, in list order */
+    uint8_t *seen = (uint8_t *)calloc((size_t)o->N, 1);
+    int disjoint = seen != NULL;
+    for (int32_t i = 0; i < n && disjoint; i++) {
+        if (a[i] < 0 || b[i] < 0 || a[i] >= o->N || b[i] >= o->N || a[i] == b[i] || seen[a[i]] || seen[b[i]]) {
+            disjoint = 0;
+            break;
+        }
+        seen[a[i]] = seen[b[i]] = 1;
+    }
+    free(seen);
+    if (!disjoint) {
+        for (int32_t i = 0; i < n; i++) orc_exchange(o, a[i], b[i], now);
+        return;
+    }
     for (int32_t i = 0; i < n; i++) {  /* rows are allocated here, once, before the threads share the table */
         row(o, a[i]);
         row(o, b[i]);

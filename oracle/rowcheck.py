@@ -87,15 +87,16 @@ class RowOracle:
         except Exception:
             pass
 
-    def load(self, rows, handles=None, owner=None):
+    def load(self, rows, handles=None, owner=None, g=None):
         """Copy observer rows ``rows`` of the device's current state into every handle in ``handles``
         (default: one new handle), or, with ``owner`` (one handle per row), each row into its own
-        handle only.  Returns the handles."""
+        handle only.  ``g``: host copies of those rows already taken (``join_host_rows``).  Returns the
+        handles."""
         sim = self.sim
         rows = [int(o) for o in rows]
         handles = handles or [self.new_handle()]
-        g = sim._host(rows)
-        n, K, Cc = sim.n, sim.k, sim.hist_cap
+        g = sim._host(rows) if g is None else g
+        n, K = sim.n, sim.k
         lo, nc = self.lo, self.nc
 
         def full(x, fill=0):
@@ -107,6 +108,7 @@ class RowOracle:
             out[lo:lo + nc] = x[:nc]
             return out
 
+        Cc = g["HIST_VER"].shape[1]  # hist_cap, or fewer entries (host_rows trims what no loaded row holds)
         hist_ver = full(g["HIST_VER"])
         hist_vid = full(g["HIST_VID"])
         meta = full(g["HIST_META"])
@@ -285,3 +287,105 @@ def check_phase_rows(sim, cfg: dict, rd: dict, sample: int = 64, phase: int = 0,
     info = {**ro.stats(h), "rows": len(rows)}
     ro.close()
     return diff, info
+
+
+# -- the whole cluster's rows from owner-column slices (multi-GPU bench parity: VERDICT r5 item 5)
+
+
+class ClusterView:
+    """The attributes ``RowOracle`` reads of a ``GossipSim``, for the WHOLE cluster of a sliced run: rows loaded
+    from host copies joined over every slice (``join_host_rows``), so the oracle holds complete rows and the
+    check is exact whatever the MTU does (no inert columns)."""
+
+    def __init__(self, sim, hist_cap: int):
+        self.n, self.k, self.hist_cap = sim.n, sim.k, hist_cap
+        self.canonical, self.shards, self.col_lo, self.ncol = True, 1, 0, sim.n
+        self.node_ids, self.keys = sim.node_ids, sim.keys
+        self.flags, self.ring_rows = 0, []
+
+
+def host_rows(sim, g: dict, cmax: int | None = None) -> dict:
+    """Host copies ``g`` (``sim._host(rows)``) of observer rows of one slice, cut to the slice's own columns
+    (``[:, :ncol]``), with the owner tables (HIST_*) cut to their first ``cmax`` write ordinals (default: all)."""
+    nc = sim.ncol
+    out = {"col_lo": sim.col_lo, "ncol": nc}
+    for k, v in g.items():
+        if k == "rows" or k in ("ROW", "ORD"):
+            out[k] = v
+        elif k.startswith("HIST_"):
+            out[k] = np.ascontiguousarray(v[:, :cmax]) if cmax is not None else v
+        else:
+            out[k] = np.ascontiguousarray(v[:, :nc])
+    return out
+
+
+def join_host_rows(parts: list[dict]) -> dict:
+    """``host_rows`` of every slice, in slice order, joined along the owner axis into whole-cluster rows."""
+    parts = sorted(parts, key=lambda p: p["col_lo"])
+    lo = 0
+    for p in parts:
+        if p["col_lo"] != lo:
+            raise ValueError(f"slices do not tile the owner columns: {p['col_lo']} != {lo}")
+        lo += p["ncol"]
+    g = {"rows": parts[0]["rows"], "ROW": parts[0]["ROW"]}
+    for k in parts[0]:
+        if k in ("rows", "ROW", "ORD", "col_lo", "ncol"):
+            continue
+        g[k] = np.concatenate([p[k] for p in parts], axis=0 if k.startswith("HIST_") else 1)
+    return g
+
+
+def check_sliced_phase_rows(group, cfg: dict, rd: dict, sample: int = 16, phase: int = 0, comm=None):
+    """Full-size parity of a SLICED cluster (one slice per rank, or G slices in this process): ``group`` (a
+    ``ShardGroup``) has just run ``gs_begin_round`` of round ``rd``.  The rows of the first ``sample`` exchanges
+    of phase ``phase`` are copied out of every slice and joined on rank 0 into whole-cluster rows (all owner
+    columns: the MTU walk across slices is checked too, unlike the inert-column ``RowOracle`` of one slice); the
+    whole phase then runs on the devices through the group's own sliced driver (count, gather, pack, chain steps)
+    and the round is closed by the liveness sweep; rank 0 runs the sampled exchanges and the liveness of their
+    rows in the oracle and compares every slice's columns of the device rows with the oracle's.
+
+    ``comm``: object collectives ``gather(list) -> list | None`` (every slice's objects on rank 0) and
+    ``allmax(int) -> int``; default: the slices of this process only.  Returns, on rank 0, a list with one dict
+    per slice ({"slice", "cols": [lo, hi), "rows", "diff", "exact"}) and an info dict; ``(None, None)``
+    elsewhere."""
+    from aiocluster_amd import driver
+
+    sims = group.slices
+    gather = comm.gather if comm is not None else (lambda xs: xs)
+    allmax = comm.allmax if comm is not None else (lambda x: x)
+    a_all, b_all, n, t = rd["phases"][phase]
+    a = a_all[:sample].cpu().numpy().tolist()
+    b = b_all[:sample].cpu().numpy().tolist()
+    rows = a + b
+    assert len(set(rows)) == len(rows), "a phase's exchanges are disjoint"
+    gs = [s_._host(rows) for s_ in sims]
+    # the oracle's owner tables need the write ordinals the loaded rows hold (not hist_cap of them)
+    cmax = allmax(max(int(g_["HELD"][:, : s_.ncol].max()) for s_, g_ in zip(sims, gs))) + 1
+    before = gather([host_rows(s_, g_, cmax) for s_, g_ in zip(sims, gs)])
+    del gs
+    driver.run_phases(sims, rd, phases=[rd["phases"][phase]], group=group)
+    driver.end(sims, rd, tick=t + 1)
+    after = gather([(s_.col_lo, s_.ncol, s_.export_rows(rows)) for s_ in sims])
+    if before is None:
+        return None, None
+    g = join_host_rows(before)
+    view = ClusterView(sims[0], cmax)
+    ro = RowOracle(view, cfg)
+    (h,) = ro.load(rows, g=g)
+    for x, y in zip(a, b):
+        ro.exchange(h, x, y, t)
+    for o in rows:
+        if rd["up_host"][o]:
+            ro.liveness(h, o, t + 1)
+    want = ro.export_rows(h, rows)
+    st = ro.stats(h)
+    ro.close()
+    res = []
+    for i, (lo, nc, got) in enumerate(sorted(after, key=lambda x: x[0])):
+        w = {k: v[:, lo:lo + nc] for k, v in want.items()}
+        diff = compare_exports(got, w)
+        res.append({"slice": i, "cols": [int(lo), int(lo + nc)], "rows": len(rows), "diff": diff,
+                    "exact": diff is None})
+    info = {"exchanges": len(a), "rows": len(rows), "tick": int(t), "hist_entries": int(cmax),
+            **{k: int(st[k]) for k in ("node_deltas", "hb_reports", "truncated")}}
+    return res, info

@@ -324,7 +324,7 @@ def test_hb8mv8_100_selected_rounds_at_16384_match_oracle():
             ph, offs, left = sel.schedule(rd["up"], rd["r"])
             assert left == 0
             rd["phases"] = [(a, b, m, ptick(rd["r"], p)) for p, (a, b, m) in enumerate(ph)]
-            rd["t_live"] = rd["t"] + 1 + len(ph)
+            rd["t_live"] = liveness_tick(rd["r"], len(ph))
             assert rd["t_live"] < rd["t"] + TICKS_PER_ROUND
             if r == 6:
                 slot = sim.region("ESC_SLOT", torch.int32, (sim.np_,))

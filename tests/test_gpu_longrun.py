@@ -47,8 +47,9 @@ def _round(gpu, orc, sel, scen, r):
     if orc is not None:
         orc.begin_round(t, up)
     sel.select(up_dev, r)  # live / dead sets of the previous round's liveness (server.py:448-469)
-    # the first rounds after a warm start route every node's pick to the 8 seeds, more exchanges than 62 phases
-    # hold: those are counted (not run, on both sides), as in the bench's peer_select leg
+    # the first rounds after a warm start route every node's pick to the 8 seeds: more phases than the round has
+    # ticks; those past the budget are sub-phases at its last tick (workload.phase_tick), so every selected exchange
+    # runs, on both sides (server.py:476-493)
     phases, _, left = sel.schedule(up_dev, r)
     sets = sel.scheduled_pairs(phases) if orc is not None else None
     for p, (a, b, _) in enumerate(phases):
@@ -72,6 +73,7 @@ def test_hb8mv8_selected_rounds_whole_array_matches_oracle(n, fanout, rounds, ev
     orc = make_backend(OracleSim, scen, threads=min(16, os.cpu_count() or 1))
     sel = PeerSelector(gpu, fanout=fanout, seeds=list(range(0, n, n // 8)), seed=7)
     phases, compared, escaped_max, unscheduled = [], 0, 0, 0
+    from aiocluster_amd.workload import MAX_PHASES_PER_ROUND
     for r in range(rounds):
         ph, left = _round(gpu, orc, sel, scen, r)
         phases.append(ph)
@@ -86,7 +88,10 @@ def test_hb8mv8_selected_rounds_whole_array_matches_oracle(n, fanout, rounds, ev
     c = gpu.check()  # raises on any err_* (err_hb_lag: a sweep found no free escape slot)
     print(f"phases/round {min(phases)}-{max(phases)}, escapes {c['hb_escapes']}, releases {c['hb_releases']}, "
           f"max escaped columns {escaped_max}, lag sweeps {c['lag_sweeps']}, whole-array compares {compared}, "
-          f"unscheduled exchanges {unscheduled}")
+          f"unscheduled exchanges {unscheduled}, rounds with sub-phases "
+          f"{sum(p > MAX_PHASES_PER_ROUND for p in phases)}, plane flushes {c['plane_flushes']}")
+    assert unscheduled == 0  # every selected exchange ran (round 5 dropped those past 62 phases)
+    assert max(phases) > MAX_PHASES_PER_ROUND  # ... including rounds past the tick budget (sub-phases)
     assert c["hb_escapes"] > 0 and c["hb_releases"] > 0, c
     assert c["exchanges"] == orc.stats()["exchanges"]
     assert compared == rounds // every

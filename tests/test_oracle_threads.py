@@ -63,3 +63,27 @@ def test_threaded_phases_equal_sequential():
     assert seq.stats()["truncated"] > 0
     for b in (seq, par):
         b.close()
+
+
+def test_threaded_phase_with_overlapping_pairs_runs_sequentially():
+    """orc_run_phase_mt on a pair list that is NOT conflict-free (node 3 in two pairs) must not race: it falls back
+    to the sequential order, so the result equals orc_exchange pair by pair."""
+    spec = WorkloadSpec(n=64, k=6, fanout=3, seed=5, init="warm", write_frac=0.3, down_frac=0.0, down_rounds=1)
+    scen = make_scenario("ovl64", spec, 3, {"mtu": 900})
+    seq = make_backend(OracleSim, scen)
+    par = make_backend(OracleSim, scen, threads=4)
+    from aiocluster_amd.scenario import replay_round
+
+    for r in range(len(scen["rounds"])):
+        replay_round(seq, scen, r)
+        replay_round(par, scen, r)
+    t = seq.last_tick + 1
+    pairs = [(3, 10), (11, 12), (3, 20), (21, 22), (20, 30), (40, 41)]
+    seq.begin_round(t, [1] * 64)
+    par.begin_round(t, [1] * 64)
+    for a, b in pairs:
+        seq.exchange(a, b, t + 1)
+    par.run_phase(t + 1, pairs)
+    assert compare_exports(par.export(), seq.export()) is None
+    for b in (seq, par):
+        b.close()

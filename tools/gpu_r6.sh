@@ -1,7 +1,7 @@
 #!/bin/bash
-# Round-5 GPU call (gpurun): optional GPU tests, then named bench runs, each under its own limit; the first
+# GPU call (gpurun): optional GPU tests, then named bench runs, each under its own limit; the first
 # failure ends the call.
-#   TAG=<tag> [TESTS="<pytest args>"] [KEXPR="<pytest -k expression>"] RUNS="name:ENV=V,ENV=V:<bench args>;name2::<bench args>" bash tools/gpu_r5.sh
+#   TAG=<tag> [TESTS="<pytest args>"] [KEXPR="<pytest -k expression>"] RUNS="name:ENV=V,ENV=V:<bench args>;name2::<bench args>" bash tools/gpu_r6.sh
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 O=gpurun_out/$TAG; mkdir -p $O
@@ -19,6 +19,8 @@ print('$2', 'value', round(d['value']), 'ms/step', round(d['ms_per_step'],2), 's
       'cpu', d['cpu_baseline'] and (round(d['cpu_baseline']['value']), round(d['cpu_baseline']['single_core_value'])),
       'ps', d['peer_select'] and (round(d['peer_select']['value']), d['peer_select']['phases_per_round'], d['peer_select'].get('exact')),
       'c4', d.get('config4') and (round(d['config4']['ms_per_step'],2), d['config4']['kernel_ms_per_step']),
+      'parity', d.get('parity_check') and [x['exact'] for x in d['parity_check']['per_slice']],
+      'sched', {k: d['config'][k] for k in ('unscheduled_exchanges_all_rounds', 'max_phases_per_round', 'rounds_with_sub_phases') if k in d['config']},
       'extra', d.get('slice_stats'))"
 }
 IFS=';' read -ra RUNL <<< "$RUNS"

@@ -15,8 +15,12 @@ width of the kernel's dominant streams:
     k_pack_slice  8 B (candidate records; the rest are gathers, which no stream calibrates)
     k_settle      8 B (likewise: candidate records, owner-table gathers)
     k_liveness    16 B per lane (two 16-B window loads + one 16-B state load per 4 columns)
-Only the launches inside bench.py's timed region are averaged (the last N of each kernel, N from the
-bench's JSON line).  The entry written to profiles/pmc_summary.json carries the source hash of the
+Only the dispatches inside bench.py's timed region are averaged: bench.py brackets its timed rounds with two
+empty marker kernels (gs_mark: k_mark_begin, k_mark_end) on the library's stream, and every average here --
+trace durations, FETCH/WRITE_SIZE, SQ counters -- takes exactly the dispatches whose Dispatch_Id lies between
+the two markers of that pass.  (Round 5's version took each kernel's last N dispatches, which mixed the
+peer-selected rounds bench runs after the timed ones into the averages: VERDICT r5.)  The launch counts in the
+window are checked against the bench line's HIP-event launch counts.  The entry written to profiles/pmc_summary.json carries the source hash of the
 kernels it measured, so bench.py ignores it once the kernels change.
 
 Usage: python tools/pmc_summary.py gpurun_out/prof_<tag> <tag>
@@ -34,12 +38,17 @@ from collections import defaultdict
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
-KERNELS = ("k_pass1v", "k_pass1", "k_pack_slice", "k_settle", "k_lite", "k_liveness", "k_exchange", "k_count", "k_begin_round",
-           "k_owner_writes", "k_reset_sched", "k_warm", "k_boot_self", "k_phi_row")
+KERNELS = ("k_mark_begin", "k_mark_end", "k_pass1v", "k_pass1", "k_pack_slice", "k_settle", "k_lite", "k_liveness", "k_exchange", "k_count", "k_begin_round",
+           "k_owner_writes", "k_reset_sched", "k_warm", "k_boot_self", "k_phi_row", "k_hb_lag", "k_p1v_fix", "k_fd_age",
+           "k_esc_plan", "k_esc_move", "k_hot_clear", "k_chain_step", "k_ov_count", "k_ov_write", "k_pending",
+           "k_gather_u64", "k_sum_pending", "k_copy16")
 WIDTH = {"k_pass1v": 16, "k_pass1": 4, "k_pack_slice": 8, "k_settle": 8, "k_lite": 8, "k_liveness": 16, "k_exchange": 8, "k_count": 8}
 KIND = {"k_pass1v": "pass1", "k_pass1": "pass1", "k_pack_slice": "pack", "k_settle": "count", "k_lite": "lite", "k_liveness": "liveness",
         "k_exchange": "pass1", "k_count": "count"}
 CAL_BYTES = 1 << 30
+# the bench line's roofline.kernels kinds -> the kernel each times (pass 1: k_pass1v in the headline's layout)
+KIND_KERNEL = {"pass1": "k_pass1v", "pack": "k_pack_slice", "liveness": "k_liveness", "count": "k_settle",
+               "lite": "k_lite"}
 
 
 def short(name: str) -> str:
@@ -76,53 +85,91 @@ def bench_line(root: str, sub: str) -> dict | None:
 
 
 def timed_launches(line: dict | None) -> dict:
-    """Launches of each kernel inside bench.py's timed region (its roofline.kernels[kind].launches)."""
+    """Launches of each kernel inside bench.py's timed region by the bench line's HIP-event counts
+    (roofline.kernels[kind].launches): the cross-check of the marker window."""
     if not line:
         return {}
     per = line.get("roofline", {}).get("kernels", {})
     return {k: per[kind]["launches"] for k, kind in KIND.items() if kind in per}
 
 
-def trace_avg(root: str, last: dict) -> dict:
-    """Average duration (ms) of each kernel over its last `last[k]` launches of the kernel trace."""
-    d = defaultdict(list)
+def marker_window(rows: list[tuple[int, str]]) -> tuple[int, int] | None:
+    """(first, last) Dispatch_Id strictly between the k_mark_begin and the following k_mark_end dispatch."""
+    beg = end = None
+    for did, name in sorted(rows):
+        if name == "k_mark_begin" and beg is None:
+            beg = did
+        elif name == "k_mark_end" and beg is not None:
+            end = did
+            break
+    return (beg, end) if beg is not None and end is not None else None
+
+
+def trace_window(root: str) -> tuple[dict, dict]:
+    """Every kernel dispatched between the markers of the kernel-trace pass: launches, average / total duration,
+    and the window's span and GPU-busy time (the union of the dispatches' intervals)."""
+    rows = []
     for path in glob.glob(os.path.join(root, "kt", "**", "*kernel_trace.csv"), recursive=True):
         for row in csv.DictReader(open(path)):
-            k = short(row["Kernel_Name"])
-            if k in last:
-                d[k].append((int(row["Start_Timestamp"]), (int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) / 1e6))
-    out = {}
-    for k, v in d.items():
-        v.sort()
-        tail = v[-last[k]:]
-        out[k] = {"launches": len(tail), "avg_ms": sum(x for _, x in tail) / len(tail)}
-    return out
+            rows.append((int(row["Dispatch_Id"]), short(row["Kernel_Name"]), int(row["Start_Timestamp"]),
+                         int(row["End_Timestamp"])))
+    win = marker_window([(r[0], r[1]) for r in rows])
+    if win is None:
+        return {}, {"error": "no k_mark_begin / k_mark_end pair in the kernel trace"}
+    d = defaultdict(list)
+    iv = []
+    for did, k, t0, t1 in rows:
+        if win[0] < did < win[1]:
+            d[k].append((t1 - t0) / 1e6)
+            iv.append((t0, t1))
+    out = {k: {"launches": len(v), "avg_ms": sum(v) / len(v), "total_ms": sum(v)} for k, v in d.items()}
+    iv.sort()
+    busy, cur0, cur1 = 0, None, None
+    for a, b in iv:
+        if cur1 is None or a > cur1:
+            if cur1 is not None:
+                busy += cur1 - cur0
+            cur0, cur1 = a, b
+        else:
+            cur1 = max(cur1, b)
+    if cur1 is not None:
+        busy += cur1 - cur0
+    info = {"dispatch_ids": list(win), "dispatches": sum(len(v) for v in d.values()),
+            "span_ms": (iv[-1][1] - iv[0][0]) / 1e6 if iv else 0.0, "busy_ms": busy / 1e6}
+    return out, info
 
 
-def counters(root: str, sub: str, name: str, last: dict | None = None) -> tuple[dict, dict]:
-    """Average counter value per launch and per workgroup, over each kernel's last `last[k]` dispatches."""
-    rows = defaultdict(list)
+def counters(root: str, sub: str, name: str, windowed: bool = True) -> tuple[dict, dict]:
+    """Average counter value per launch and per workgroup of each kernel; with ``windowed`` only over the
+    dispatches between that pass's k_mark_begin and k_mark_end (bench.py's timed rounds)."""
+    rows = []
     for path in glob.glob(os.path.join(root, sub, "**", "*counter_collection.csv"), recursive=True):
         for row in csv.DictReader(open(path)):
             if row.get("Counter_Name") == name:
-                k = short(row["Kernel_Name"])
                 wg = float(row.get("Grid_Size", 0) or 0) / max(1.0, float(row.get("Workgroup_Size", 1) or 1))
-                rows[k].append((int(row.get("Dispatch_Id", 0) or 0), float(row["Counter_Value"]), wg))
+                rows.append((int(row.get("Dispatch_Id", 0) or 0), short(row["Kernel_Name"]),
+                             float(row["Counter_Value"]), wg))
+    if windowed:
+        # the markers are dispatches too, with counter rows of their own
+        win = marker_window([(r[0], r[1]) for r in rows])
+        if win is None:
+            raise SystemExit(f"{sub}: no k_mark_begin / k_mark_end pair among the {name} rows")
+        rows = [r for r in rows if win[0] < r[0] < win[1]]
+    by = defaultdict(list)
+    for did, k, v, wg in rows:
+        by[k].append((v, wg))
     avg, per_wg = {}, {}
-    for k, v in rows.items():
-        v.sort()
-        if last and k in last:
-            v = v[-last[k]:]
-        avg[k] = sum(x[1] for x in v) / len(v)
-        u = sum(x[2] for x in v)
+    for k, v in by.items():
+        avg[k] = sum(x[0] for x in v) / len(v)
+        u = sum(x[1] for x in v)
         if u > 0:
-            per_wg[k] = sum(x[1] for x in v) / u
+            per_wg[k] = sum(x[0] for x in v) / u
     return avg, per_wg
 
 
 def calibration(root: str) -> dict:
-    f, _ = counters(root, "cal_fetch", "FETCH_SIZE")
-    w, _ = counters(root, "cal_write", "WRITE_SIZE")
+    f, _ = counters(root, "cal_fetch", "FETCH_SIZE", windowed=False)
+    w, _ = counters(root, "cal_write", "WRITE_SIZE", windowed=False)
     cal = {}
     for width in (4, 8, 16):
         r, wr = f.get(f"read{width}"), w.get(f"write{width}")
@@ -135,12 +182,19 @@ def main(root: str, tag: str):
     from bench import kernel_source_hash
 
     line = bench_line(root, "kt")
-    last = timed_launches(line)
     ks = kernel_stats(root)
-    timed = trace_avg(root, last)
+    timed, window = trace_window(root)
+    # the marker window must hold exactly the launches the bench line's HIP events counted
+    window["launch_check"] = {k: {"window": timed.get(k, {}).get("launches"), "hip_events": n}
+                              for k, n in timed_launches(line).items()}
+    window["launch_check_ok"] = all(v["window"] == v["hip_events"] for v in window["launch_check"].values())
+    hip_avg = {KIND_KERNEL.get(kind, kind): v["avg_launch_ms"]
+               for kind, v in ((line or {}).get("roofline", {}).get("kernels", {}) or {}).items()}
+    window["hip_event_avg_ms"] = hip_avg
+    window["trace_over_hip_events"] = {k: timed[k]["avg_ms"] / v for k, v in hip_avg.items() if k in timed and v}
     cal = calibration(root)
-    fetch, fetch_wg = counters(root, "fetch", "FETCH_SIZE", timed_launches(bench_line(root, "fetch")))
-    write, write_wg = counters(root, "write", "WRITE_SIZE", timed_launches(bench_line(root, "write")))
+    fetch, fetch_wg = counters(root, "fetch", "FETCH_SIZE")
+    write, write_wg = counters(root, "write", "WRITE_SIZE")
     kern = {}
     for k in WIDTH:
         if k not in fetch or k not in write:
@@ -162,11 +216,11 @@ def main(root: str, tag: str):
     workload = (line or {}).get("config", {}).get("workload")
     src = kernel_source_hash()
     summary = {"tag": tag, "workload": workload, "source_hash": src, "calibration": cal, "kernel_stats": ks,
-               "timed_region": timed, "kernels": kern, "bench": line}
+               "timed_window": window, "timed_region": timed, "kernels": kern, "bench": line}
     sq = {}
     for name in ("SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU",
                  "SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_WAVES"):
-        avg, _ = counters(root, "sq", name, timed_launches(bench_line(root, "sq")))
+        avg, _ = counters(root, "sq", name)
         for k, v in avg.items():
             sq.setdefault(k, {})[name] = v
     if sq:
