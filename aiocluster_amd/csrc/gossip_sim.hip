@@ -182,6 +182,13 @@ struct Dev {
     // nullptr: no hand-off (set per launch by the host, one-slice record phases only)
     uint32_t *heavy;
     uint32_t heavy_t;
+    // one-slice prefix-view handles (round 6): sm[c] = the smallest possible NodeDelta of any owner column >= c --
+    // min over j >= c of msgf(msgf(NodeIdPb bytes of j) + 2 + the smallest kv field j ever wrote, GS_R_VLOG entry
+    // 0), a lower bound of every candidate's min1 -- rebuilt after every gs_owner_writes (k_sm_build); sm[ncol] =
+    // 0xFFFF.  First-fit continuation stops as soon as the budget left is below sm at the next candidate's column:
+    // no later candidate can add a NodeDelta (R only shrinks).  nullptr: not built (sliced handles: the chain's
+    // later slices hold the other columns)
+    uint16_t *sm;
     uint32_t ev_wseq;  // owner-write ops issued since gs_set_events (the seq of the next call's op 0)
 };
 
@@ -970,6 +977,10 @@ __device__ __forceinline__ void pack_dir(const Dev &d, uint32_t s, uint32_t r, c
     if (!GENM && p0 + 16u * lane < cnt) wnext = bits[(p0 + 16u * lane) >> 5];
     uint32_t pfrom = pmin;  // positions before it are not candidates (records, or skipped by dir_tail_scan)
     for (uint32_t win = p0; win < cnt && !stop; win += WIN) {
+        if (!GENM && !COUNT && !REC && tail && d.sm && pend == 0u && d.mtu - S < d.sm[max(win, pfrom)]) {
+            stop = true;  // no later candidate can fit (Dev::sm); bitmap candidates were not merged: nothing to restore
+            break;
+        }
         if (!GENM && !COUNT && !REC && tail && d.vlog && d.mv8 && pend == 0u) {
             // first-fit continuation: jump to the first position that may still send something
             const uint32_t q = dir_tail_scan(d, s, r, ds.sched, bits, max(win, pfrom), cnt, d.mtu - S, st);
@@ -1144,6 +1155,11 @@ __device__ __forceinline__ void pack_list(const Dev &d, uint32_t s, uint32_t r, 
     uint2 nxt = make_uint2(0u, 0u);
     if ((uint32_t)lane < n) nxt = L[lane];
     for (uint32_t c0 = 0; c0 < n && (specd || !stop); c0 += WAVE) {
+        // first-fit continuation: no later candidate can fit once the budget is below their smallest NodeDelta
+        if (!COUNT && !stop && tail && d.sm && d.mtu - S < d.sm[L[c0].x]) {
+            stop = true;
+            if (!specd) break;
+        }
         if (stop) {  // specd only: nothing more is sent -- restore every remaining prefix record, TAIL_B groups at once
             for (uint32_t b0 = c0; b0 < n; b0 += TAIL_B * WAVE) {
 #pragma unroll
@@ -1255,6 +1271,9 @@ __device__ __forceinline__ bool pack_lite(const Dev &d, uint32_t rcv, size_t slo
     if (n0 > GS_CAND_CAP || n1 > GS_CAND_CAP) return false;  // a half continues in its bitmap
     const uint2 *L0 = d.cand + slot * 2 * GS_CAND_CAP, *L1 = L0 + GS_CAND_CAP;
     const uint32_t nt = n0 + n1;
+    // every recorded owner is a NodeDelta of >= lb_min bytes (or the slot is not a lite one): past that many the
+    // whole delta cannot fit, so the exact packer takes the slot without this pass sizing it
+    if (APPLY && (uint64_t)nt * d.lb_min > (uint64_t)(d.mtu - min(S0, d.mtu))) return false;
     uint32_t sum = 0, kvs = 0, alg = 0, m1 = NONE;
     bool bad = false;
     for (uint32_t c0 = 0; c0 < nt; c0 += WAVE * LITE_B) {
@@ -2181,6 +2200,11 @@ __device__ __forceinline__ uint32_t lite_slot(const Dev &d, int32_t ai, int32_t 
     if (lane == 0) {
         d.slot_stat[slot].w = flag;
         if (flag == LITE_DONE) shard_add(d, C_LITE, 1);
+        // a heavy slot (Dev::heavy): listed for k_pack_heavy, which runs beside k_pack_slice
+        if (MODE == 0 && flag == LITE_FULL && d.heavy && d.cand_n[slot * 2] + d.cand_n[slot * 2 + 1] > d.heavy_t) {
+            d.heavy[1u + atomicAdd(d.heavy, 1u)] = (uint32_t)slot;
+            shard_add(d, C_HEAVY, 1);
+        }
     }
     const unsigned long long s_alg = wave_sum(st.alg), s_nd = wave_sum(st.nd), s_kv = wave_sum(st.kvs);
     const unsigned long long s_cd = wave_sum(st.cand);
@@ -2750,13 +2774,8 @@ __global__ __launch_bounds__(XB, (KW == 4 ? PK_WAVES : 1)) void k_pack_slice(Dev
     const uint32_t a = (uint32_t)ai, b = (uint32_t)bi;
     const size_t slot = (size_t)e * 2 + wid;
     if (io.step == 0 && d.lite && (d.slot_stat[slot].w & LITE_DONE)) return;  // k_lite completed it
-    if (d.heavy && d.cand_n[slot * 2] + d.cand_n[slot * 2 + 1] > d.heavy_t) {  // k_pack_heavy packs it
-        if (tid == (wid << 6)) {
-            d.heavy[1u + atomicAdd(d.heavy, 1u)] = (uint32_t)slot;
-            shard_add(d, C_HEAVY, 1);
-        }
-        return;
-    }
+    // a heavy slot: the lite slot work listed it (Dev::heavy) and k_pack_heavy packs it
+    if (d.heavy && d.cand_n[slot * 2] + d.cand_n[slot * 2 + 1] > d.heavy_t) return;
     PackState pst;
     if (io.step == 0) {
         uint64_t P = 0;
@@ -2805,29 +2824,56 @@ __global__ __launch_bounds__(XB, (KW == 4 ? PK_WAVES : 1)) void k_pack_slice(Dev
 // ---- the exact packer's heavy slots (round 6).  A slot with thousands of stale owners -- a
 // node back from an absence -- kept k_pack_slice's two-wave workgroup walking for ~270 dependent steps (the launch
 // lasts as long as its heaviest slot) while the others were long done.  k_pack_slice hands such slots to this
-// kernel (Dev::heavy), which packs each with HW_WAVES waves, HT candidates per block in sender order:
-//  * whole-fit prefix (state.py:392-398): the block's candidates are evaluated in parallel, a block scan of their
-//    DeltaPb sizes finds the first one that does not fit whole, every candidate before it is sent whole (applied in
-//    parallel: distinct owners);
+// kernel (Dev::heavy), which packs each with HW_WAVES waves, in sender order:
+//  * whole-fit prefix (state.py:392-398): blocks of HT candidates are evaluated in parallel, a block scan of their
+//    DeltaPb sizes finds the first one that does not fit whole, and every candidate before it is sent whole
+//    (applied in parallel: distinct owners);
 //  * first-fit continuation (state.py:392-413): every later candidate is tested against the budget R left, which
-//    only shrinks, so one whose smallest NodeDelta (its lowest-version kv alone, min1) exceeds R now is never sent:
-//    the block filters its candidates in parallel (min1_lb first, the exact min1 for those that pass), and one wave
-//    runs pack_group's sequential first-fit over the survivors alone, in sender order;
+//    only shrinks, so one whose smallest NodeDelta (its lowest-version kv alone, min1) exceeds R now is never sent,
+//    and once R is below the smallest NodeDelta of any owner (lb_min) nothing is: super-blocks of HT x HTB
+//    candidates are filtered in parallel (min1_lb first, the exact min1 for those that pass), and one wave runs
+//    pack_group's sequential first-fit over the survivors alone, in sender order;
 //  * a speculatively merged record (Dev::spec) that is not sent gets its receiver word restored, as in pack_list.
 // Bit-exact with pack_records: the same candidates, the same order, the same decisions.
 #ifndef HW_WAVES
 #define HW_WAVES 4
 #endif
-constexpr int HT = HW_WAVES * WAVE;   // threads per heavy workgroup: one candidate each per block
-constexpr uint32_t HWIN = 16u * HT;   // bitmap positions compacted per window (16 per thread)
+#ifndef HTB
+#define HTB 8  // candidates per thread in a first-fit super-block (candidate k * HT + thread)
+#endif
+#ifndef HPK
+#define HPK 4  // consecutive candidates per thread in a whole-fit block
+#endif
+constexpr int HT = HW_WAVES * WAVE;           // threads per heavy workgroup
+constexpr uint32_t HSB = (uint32_t)HT * HTB;  // candidates per first-fit super-block
+constexpr uint32_t HPB = (uint32_t)HT * HPK;  // candidates per whole-fit block
+constexpr uint32_t HWIN = 16u * HT;           // bitmap positions compacted per window (16 per thread)
 struct HeavyLds {
     uint32_t wsum[HW_WAVES];
-    uint32_t first, S, stop, tail, nsurv, steps, groups;
-    uint32_t cj[HT], cm[HT];  // the block's candidates: owner column, sender | receiver max_version words << 16
-    uint16_t surv[HT];        // survivors' block indices in sender order
-    uint16_t wl[HWIN];        // a bitmap window's stale positions (offsets from the window start)
-    uint8_t crec[HT];         // candidate from pass 1's records (merged speculatively if both views are prefixes)
+    uint32_t wcnt[HTB][HW_WAVES];
+    uint32_t first, S, stop, tail, steps, groups;
+    uint16_t surv[HSB];  // first-fit survivors in sender order (offsets from the super-block's start)
+    uint32_t pe[HPB];    // a whole-fit block's candidates: DeltaPb bytes | kv count << 16 | prefix views << 24
+    uint16_t wl[HWIN];   // a bitmap window's stale positions (offsets from the window start)
 };
+// a candidate source: pass 1's records of a row half, or a compacted bitmap window (rows read for the words)
+struct HSrc {
+    const uint2 *L;  // records, or nullptr: the window wl at column w
+    uint32_t w;
+};
+__device__ __forceinline__ void hsrc_get(const Dev &d, const HSrc &src, const HeavyLds &sh, uint32_t q, uint32_t s,
+                                         uint32_t r, uint32_t &j, uint32_t &mvw, uint32_t &alg) {
+    if (src.L) {
+        const uint2 x = src.L[q];
+        j = x.x;
+        mvw = x.y;
+        alg += 8;
+    } else {
+        j = src.w + sh.wl[q];
+        mvw = mv_word(d, pix(d, s, j), j) | (mv_word(d, pix(d, r, j), j) << 16);
+        alg += 2;
+    }
+}
 // block-wide exclusive scan of x (all threads call); returns the exclusive prefix, *total the block's sum
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, HeavyLds &sh, uint32_t *total) {
     const int lane = lane_id(), wv = (int)(threadIdx.x >> 6);
@@ -2846,104 +2892,199 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, HeavyLds &sh, ui
     return pre + inc - x;
 }
 
-// one block of candidates (thread i: the i-th, if has), in sender order after every earlier block's
 template <int KW>
-__device__ __forceinline__ void heavy_block(const Dev &d, uint32_t s, uint32_t r, const DigestSide &ds, uint32_t t,
-                                            bool has, uint32_t j, uint32_t mvw, bool rec, bool specd, bool lightok,
-                                            HeavyLds &sh, WStats &st, bool &tomb) {
-    const int tid = (int)threadIdx.x, lane = lane_id();
-    const uint32_t mtu = d.mtu;
-    uint32_t S = sh.S;
-    bool tail = sh.tail != 0u;
-    const bool fastrec = rec_fast(mvw);
-    if (sh.stop) {  // the delta is complete: nothing more is sent; restore the merged records
-        if (has && rec && specd && fastrec) { mv_put(d, pix(d, r, j), mvw >> 16); st.alg += 4; }
-        return;
-    }
-    const uint32_t msw = mvw & 0xFFFFu, mrw = mvw >> 16;
-    Cand<KW> c;
+__device__ __forceinline__ void heavy_eval(const Dev &d, uint32_t s, uint32_t r, const DigestSide &ds, uint32_t t,
+                                           uint32_t j, uint32_t mvw, bool lightok, Cand<KW> &c, WStats &st) {
     c.emsg = 0;
     c.min1 = 0;
     c.light = false;
     c.fast = false;
-    bool ev = false;
-    auto eval = [&]() {
-        if (lightok && fastrec) {
-            eval_light<KW>(d, j, msw & MV_MASK, mrw & MV_MASK, c, st.alg);
-        } else {
-            CandKeys<KW> ck;
-            eval_cand<KW, false, true>(d, s, r, ds, j, t, c, ck, st.alg, mvw);
+    if (lightok && rec_fast(mvw)) {
+        eval_light<KW>(d, j, mvw & MV_MASK, (mvw >> 16) & MV_MASK, c, st.alg);
+    } else {
+        CandKeys<KW> ck;
+        eval_cand<KW, false, true>(d, s, r, ds, j, t, c, ck, st.alg, mvw);
+    }
+    st.cand++;
+}
+
+// whole-fit prefix: candidates [pos, pos + HPB) of src (thread i: the HPK consecutive ones from pos + i HPK, those
+// < len), none of them in first-fit continuation yet.  Sends whole every candidate before the first that does not
+// fit; returns how many candidates it consumed (HPB, or that first one's offset: first-fit continuation, sh.tail,
+// resumes there).  Each candidate's size, kv count and prefix flag wait in LDS (sh.pe) through the scan; a sent
+// prefix candidate's apply is one max_version store (none if pass 1 merged it), any other is evaluated again
+template <int KW>
+__device__ __forceinline__ uint32_t heavy_prefix(const Dev &d, uint32_t s, uint32_t r, const DigestSide &ds, uint32_t t,
+                                                 const HSrc &src, uint32_t pos, uint32_t len, bool specd, bool lightok,
+                                                 HeavyLds &sh, WStats &st, bool &tomb) {
+    const int tid = (int)threadIdx.x;
+    const uint32_t mtu = d.mtu, S = sh.S;
+    const uint32_t q0 = pos + (uint32_t)tid * HPK;
+    uint32_t *pe = sh.pe + (uint32_t)tid * HPK;
+    uint32_t sum = 0;
+#pragma unroll 1
+    for (uint32_t k = 0; k < HPK; k++) {
+        uint32_t x = 0u;
+        if (q0 + k < len) {
+            uint32_t j, m;
+            hsrc_get(d, src, sh, q0 + k, s, r, j, m, st.alg);
+            Cand<KW> c;
+            heavy_eval<KW>(d, s, r, ds, t, j, m, lightok, c, st);
+            x = c.emsg | (c.nkv << 16) | (c.fast ? 1u << 24 : 0u);
+            sum += c.emsg;
         }
-        st.cand++;
-        ev = true;
-    };
-    uint32_t f = 0;  // block index from which the candidates are in first-fit continuation
-    if (!tail) {
-        if (has) eval();
-        const uint32_t em = has ? c.emsg : 0u;
-        uint32_t total;
-        const uint32_t ex = block_excl_scan(em, sh, &total);
-        bool whole;
-        if (S + total <= mtu) {
-            whole = em != 0u;
-            f = HT;
-            if (tid == 0) {
-                const uint32_t S1 = S + total;
-                sh.S = S1;
-                if (S1 >= mtu || mtu - S1 < d.lb_min) sh.stop = 1u;
+        pe[k] = x;
+    }
+    uint32_t total;
+    const uint32_t ex = block_excl_scan(sum, sh, &total);
+    uint32_t f = HPB;  // offset (from pos) of the first candidate that does not fit whole
+    if (S + total <= mtu) {
+        if (tid == 0) {
+            const uint32_t S1 = S + total;
+            sh.S = S1;
+            if (S1 >= mtu || mtu - S1 < d.lb_min) sh.stop = 1u;
+        }
+    } else {
+        if (tid == 0) sh.first = HPB;
+        __syncthreads();
+        uint32_t run = S + ex;
+#pragma unroll 1
+        for (uint32_t k = 0; k < HPK; k++) {
+            const uint32_t em = pe[k] & 0xFFFFu;
+            if (em && run + em > mtu) {
+                atomicMin(&sh.first, (uint32_t)tid * HPK + k);
+                break;
             }
-        } else {
-            if (tid == 0) sh.first = HT;
-            __syncthreads();
-            if (em && S + ex + em > mtu) atomicMin(&sh.first, (uint32_t)tid);
-            __syncthreads();
-            f = sh.first;
-            whole = em != 0u && (uint32_t)tid < f;
-            if ((uint32_t)tid == f) { sh.S = S + ex; sh.tail = 1u; }
-        }
-        if (whole) {  // sent whole: one lane per NodeDelta, distinct owners
-            apply_cand<KW>(d, s, r, c, NONE, t, tomb, st.alg, specd && rec);
-            st.nd++;
-            st.kvs += c.nkv;
-        } else if (has && (uint32_t)tid < f && specd && rec && c.fast) {  // no kvs to send: restore
-            mv_put(d, pix(d, r, j), mrw);
-            st.alg += 4;
+            run += em;
         }
         __syncthreads();
-        if (f >= HT) return;  // (stop, if set, takes effect from the next block)
-        S = sh.S;
-        tail = true;
-    }
-    // first-fit continuation over candidates f.. of the block: keep those whose min1 fits the budget left now
-    const uint32_t R = mtu - S;
-    bool surv = false;
-    if (has && (uint32_t)tid >= f) {
-        if (!ev && fastrec && d.vlog && min1_lb(d, j, msw, mrw, ds.sched) > R) {
-            st.alg += 4;  // the bound's version-log entry
-        } else {
-            if (!ev) eval();
-            surv = c.emsg != 0u && c.min1 <= R;
+        f = sh.first;
+        if ((uint32_t)tid == f / HPK) {  // the thread holding candidate f: the bytes before it
+            uint32_t bb = S + ex;
+            for (uint32_t k = 0; k < f % HPK; k++) bb += pe[k] & 0xFFFFu;
+            sh.S = bb;
+            sh.tail = 1u;
         }
-        if (!surv && rec && specd && fastrec) { mv_put(d, pix(d, r, j), mrw); st.alg += 4; }  // not sent: restore
     }
-    uint32_t nsurv;
-    const uint32_t at = block_excl_scan(surv ? 1u : 0u, sh, &nsurv);
-    if (surv) sh.surv[at] = (uint16_t)tid;
-    sh.cj[tid] = j;
-    sh.cm[tid] = mvw;
-    sh.crec[tid] = rec ? 1u : 0u;
+    const bool merged = specd && src.L != nullptr;  // pass 1 merged the records' receiver words (prefix views)
+#pragma unroll 1
+    for (uint32_t k = 0; k < HPK; k++) {
+        if ((uint32_t)tid * HPK + k >= f || q0 + k >= len) break;
+        const uint32_t x = pe[k], em = x & 0xFFFFu;
+        const bool fast = (x >> 24) & 1u;
+        if (!em && !(merged && fast)) continue;
+        uint32_t j, m;
+        hsrc_get(d, src, sh, q0 + k, s, r, j, m, st.alg);  // (cache-hot)
+        if (!em) {  // nothing to send: restore the merge
+            mv_put(d, pix(d, r, j), m >> 16);
+            st.alg += 4;
+            continue;
+        }
+        st.nd++;
+        st.kvs += (x >> 16) & 0xFFu;
+        if (fast && !d.ev) {  // apply_cand's fast path: the view becomes S_j(max(ms, mr)), still a prefix
+            if (!merged) {
+                const uint32_t ms = m & MV_MASK, mr = (m >> 16) & MV_MASK;
+                mv_put(d, pix(d, r, j), ms > mr ? ms : mr);
+                st.alg += 4;
+            }
+            continue;
+        }
+        Cand<KW> c;
+        heavy_eval<KW>(d, s, r, ds, t, j, m, lightok, c, st);
+        st.cand--;  // (evaluated twice)
+        apply_cand<KW>(d, s, r, c, NONE, t, tomb, st.alg, merged);
+    }
     __syncthreads();
-    if (tid < WAVE) {  // one wave: pack_group's sequential first-fit over the survivors, 64 at a time
+    return f;
+}
+
+// first-fit continuation over candidates [pos, pos + HSB) of src (candidate pos + k * HT + thread, if < len), or, once
+// the delta is complete (sh.stop), only the restores of the merged records among them
+template <int KW>
+__device__ __forceinline__ void heavy_tail(const Dev &d, uint32_t s, uint32_t r, const DigestSide &ds, uint32_t t,
+                                           const HSrc &src, uint32_t pos, uint32_t len, bool specd, bool lightok,
+                                           HeavyLds &sh, WStats &st, bool &tomb) {
+    const int tid = (int)threadIdx.x, lane = lane_id(), wv = tid >> 6;
+    uint32_t S = sh.S;
+    const uint32_t R = d.mtu - S;
+    // nothing fits any more (every NodeDelta is >= lb_min, and every one of owners from the next candidate's
+    // column on >= Dev::sm there): the delta is complete (pack_group's rule)
+    uint32_t bound = d.lb_min;
+    if (d.sm && pos < len) bound = max(bound, (uint32_t)d.sm[src.L ? src.L[pos].x : src.w + sh.wl[pos]]);
+    if (!sh.stop && R < bound) {
+        __syncthreads();
+        if (tid == 0) sh.stop = 1u;
+        __syncthreads();
+    }
+    const bool stopped = sh.stop != 0u;
+    const bool merged = specd && src.L != nullptr;
+    if (stopped && !merged) return;
+    // every candidate's words, and the cheap bound, loads in flight together; a merged record that cannot be sent
+    // gets its receiver word back at once
+    uint32_t live = 0u;  // bit k: candidate k may still be sent
+#pragma unroll
+    for (int k = 0; k < HTB; k++) {
+        const uint32_t q = pos + (uint32_t)k * HT + (uint32_t)tid;
+        if (q >= len) continue;
+        uint32_t j, m;
+        hsrc_get(d, src, sh, q, s, r, j, m, st.alg);
+        const bool fast = rec_fast(m);
+        bool can = !stopped;
+        if (can && fast && d.vlog && min1_lb(d, j, m & 0xFFFFu, m >> 16, ds.sched) > R) {
+            can = false;
+            st.alg += 4;
+        }
+        if (can) live |= 1u << k;
+        else if (merged && fast) { mv_put(d, pix(d, r, j), m >> 16); st.alg += 4; }
+    }
+    if (stopped) return;
+    // the exact min1 of those that pass
+#pragma unroll 1
+    for (uint32_t k = 0; k < HTB; k++) {
+        if (!((live >> k) & 1u)) continue;
+        uint32_t j, m;
+        hsrc_get(d, src, sh, pos + k * HT + (uint32_t)tid, s, r, j, m, st.alg);  // (cache-hot)
+        Cand<KW> c;
+        heavy_eval<KW>(d, s, r, ds, t, j, m, lightok, c, st);
+        if (!(c.emsg != 0u && c.min1 <= R)) {
+            live &= ~(1u << k);
+            if (merged && rec_fast(m)) { mv_put(d, pix(d, r, j), m >> 16); st.alg += 4; }  // never sent: restore
+        }
+    }
+    // survivors compacted in sender order (k-major, then thread): per (k, wave) ballot counts, one barrier
+#pragma unroll
+    for (int k = 0; k < HTB; k++) {
+        const unsigned long long bl = __ballot((live >> k) & 1u);
+        if (lane == 0) sh.wcnt[k][wv] = (uint32_t)__popcll(bl);
+    }
+    __syncthreads();
+    uint32_t base = 0;
+    const unsigned long long lm = (1ull << lane) - 1ull;
+#pragma unroll
+    for (int k = 0; k < HTB; k++) {
+        uint32_t off = base;
+#pragma unroll
+        for (int w = 0; w < HW_WAVES; w++) {
+            const uint32_t v = sh.wcnt[k][w];
+            if (w < wv) off += v;
+            base += v;
+        }
+        const bool lv = (live >> k) & 1u;
+        const unsigned long long bl = __ballot(lv);
+        if (lv) sh.surv[off + (uint32_t)__popcll(bl & lm)] = (uint16_t)((uint32_t)k * HT + (uint32_t)tid);
+    }
+    const uint32_t nsurv = base;
+    __syncthreads();
+    if (tid < WAVE && nsurv) {  // one wave: pack_group's sequential first-fit over the survivors, 64 at a time
         bool tl = true, sp = false;
         uint32_t nr = 0, steps = 0;
         for (uint32_t g0 = 0; g0 < nsurv; g0 += WAVE) {
             const bool cand = g0 + (uint32_t)lane < nsurv;
-            const uint32_t i = cand ? sh.surv[g0 + lane] : 0u;
-            const uint32_t jj = sh.cj[i], mm = sh.cm[i];
-            const bool rc = sh.crec[i] != 0u;
-            const uint32_t ms = mm & 0xFFFFu, mr = mm >> 16;
+            uint32_t jj = 0u, mm = 0u;
+            if (cand) hsrc_get(d, src, sh, pos + sh.surv[g0 + lane], s, r, jj, mm, st.alg);
             if (sp) {  // complete: restore the rest of the merged survivors
-                if (cand && rc && specd && rec_fast(mm)) { mv_put(d, pix(d, r, jj), mr); st.alg += 4; }
+                if (cand && merged && rec_fast(mm)) { mv_put(d, pix(d, r, jj), mm >> 16); st.alg += 4; }
                 continue;
             }
             Cand<KW> cc;
@@ -2951,36 +3092,50 @@ __device__ __forceinline__ void heavy_block(const Dev &d, uint32_t s, uint32_t r
             cc.min1 = 0;
             cc.light = false;
             cc.fast = false;
-            if (cand) {
-                if (lightok && rec_fast(mm)) {
-                    eval_light<KW>(d, jj, ms & MV_MASK, mr & MV_MASK, cc, st.alg);
-                } else {
-                    CandKeys<KW> ck;
-                    eval_cand<KW, false, true>(d, s, r, ds, jj, t, cc, ck, st.alg, mm);
-                }
-            }
-            pack_group<KW, false, false>(d, s, r, t, cc, cand, S, tl, sp, st, tomb, nullptr, nr, specd && rc);
+            if (cand) heavy_eval<KW>(d, s, r, ds, t, jj, mm, lightok, cc, st);
+            pack_group<KW, false, false>(d, s, r, t, cc, cand, S, tl, sp, st, tomb, nullptr, nr, merged);
             steps++;
         }
         if (lane == 0) {
             sh.S = S;
-            sh.stop = sp ? 1u : 0u;
-            sh.tail = 1u;
+            if (sp) sh.stop = 1u;
             sh.steps += steps;
         }
     }
     __syncthreads();
 }
 
+// all candidates of one source in sender order: whole-fit blocks while not in first-fit continuation, then
+// first-fit super-blocks (which, once the delta is complete, only restore merged records)
 template <int KW>
-__global__ __launch_bounds__(HT) void k_pack_heavy(Dev d, const int32_t *ini, const int32_t *res, uint32_t t,
+__device__ __forceinline__ void heavy_source(const Dev &d, uint32_t s, uint32_t r, const DigestSide &ds, uint32_t t,
+                                             const HSrc &src, uint32_t len, bool specd, bool lightok, HeavyLds &sh,
+                                             WStats &st, bool &tomb) {
+    uint32_t pos = 0;
+    while (pos < len) {
+        if (sh.stop && !(specd && src.L)) break;
+        if (!sh.tail && !sh.stop) {
+            pos += heavy_prefix<KW>(d, s, r, ds, t, src, pos, len, specd, lightok, sh, st, tomb);  // HPB, or the first
+                                                                                                  // that did not fit
+        } else {
+            heavy_tail<KW>(d, s, r, ds, t, src, pos, len, specd, lightok, sh, st, tomb);
+            pos += HSB;
+        }
+        if (threadIdx.x == 0) { sh.steps++; sh.groups = max(sh.groups, (pos + WAVE - 1) / WAVE); }
+    }
+}
+
+template <int KW>
+#ifndef HW_OCC
+#define HW_OCC 4  // waves per SIMD k_pack_heavy is compiled for (one workgroup = one wave per SIMD)
+#endif
+__global__ __launch_bounds__(HT, HW_OCC) void k_pack_heavy(Dev d, const int32_t *ini, const int32_t *res, uint32_t t,
                                                    const uint32_t *heavy) {
     __shared__ HeavyLds sh;
     const uint32_t count = heavy[0];
     const int tid = (int)threadIdx.x, lane = lane_id();
     const uint32_t H = half_cols(d), words = d.NP / 32;
     WStats st{0, 0, 0, 0, 0};
-    bool tomb = false;
     for (uint32_t hi = blockIdx.x; hi < count; hi += gridDim.x) {
         const uint32_t slot = heavy[1u + hi], e = slot >> 1;
         const bool w0 = (slot & 1u) == 0u;
@@ -2990,21 +3145,12 @@ __global__ __launch_bounds__(HT) void k_pack_heavy(Dev d, const int32_t *ini, co
         const bool specd = d.spec != 0u, lightok = d.vlog && !d.ev && !ds.sched;
         if (tid == 0) { sh.S = 0u; sh.stop = 0u; sh.tail = 0u; sh.steps = 0u; sh.groups = 0u; }
         __syncthreads();
-        const uint32_t S0 = 0u;
         bool tb = false;
+        uint32_t done = 0;  // candidates of earlier sources (pack_groups_max)
         for (uint32_t hf = 0; hf < 2; hf++) {
             const uint32_t nh = d.cand_n[(size_t)slot * 2 + hf];
             const uint2 *L = d.cand + ((size_t)slot * 2 + hf) * GS_CAND_CAP;
-            const uint32_t nl = min(nh, GS_CAND_CAP);
-            for (uint32_t b0 = 0; b0 < nl; b0 += HT) {  // pass 1's records (continue when complete: restores)
-                if (sh.stop && !specd) break;
-                const uint32_t i = b0 + (uint32_t)tid;
-                const bool has = i < nl;
-                const uint2 rr = has ? L[i] : make_uint2(0u, 0u);
-                if (has) st.alg += 8;  // the record
-                heavy_block<KW>(d, snd, rcv, ds, t, has, rr.x, rr.y, true, specd, lightok, sh, st, tb);
-                if (tid == 0) sh.groups += (min(nl - b0, (uint32_t)HT) + WAVE - 1) / WAVE;
-            }
+            heavy_source<KW>(d, snd, rcv, ds, t, HSrc{L, 0u}, min(nh, GS_CAND_CAP), specd, lightok, sh, st, tb);
             if (nh <= GS_CAND_CAP || sh.stop) continue;
             // past the half's records: its bitmap, compacted window by window (those owners were not merged)
             const uint32_t pmin = L[GS_CAND_CAP - 1].x + 1u, end = min(H * (hf + 1u), d.ncol);
@@ -3026,27 +3172,15 @@ __global__ __launch_bounds__(HT) void k_pack_heavy(Dev d, const int32_t *ini, co
                     sh.wl[wp++] = (uint16_t)(16u * (uint32_t)tid + bb);
                 }
                 __syncthreads();
-                for (uint32_t b0 = 0; b0 < cnt && !sh.stop; b0 += HT) {
-                    const uint32_t i = b0 + (uint32_t)tid;
-                    const bool has = i < cnt;
-                    uint32_t j = 0u, mvw = 0u;
-                    if (has) {
-                        j = w + sh.wl[i];
-                        mvw = mv_word(d, pix(d, snd, j), j) | (mv_word(d, pix(d, rcv, j), j) << 16);
-                        st.alg += 2;
-                    }
-                    heavy_block<KW>(d, snd, rcv, ds, t, has, j, mvw, false, specd, lightok, sh, st, tb);
-                    if (tid == 0) sh.groups += (min(cnt - b0, (uint32_t)HT) + WAVE - 1) / WAVE;
-                }
-                if (tid == 0) sh.steps++;
+                heavy_source<KW>(d, snd, rcv, ds, t, HSrc{nullptr, w}, cnt, specd, lightok, sh, st, tb);
                 __syncthreads();  // (wl is rewritten by the next window)
             }
+            (void)done;
         }
         const uint32_t S1 = sh.S;
-        tomb = tomb || tb;
         if (__syncthreads_or(tb) && tid == 0) d.row[rcv * 4 + 1] = 1u;
         if (tid == 0) {
-            shard_add(d, C_DBYTES, S1 - S0);
+            shard_add(d, C_DBYTES, S1);
             shard_max(d, C_PGMAX, sh.groups);
             shard_max(d, C_PSMAX, sh.steps);
         }
@@ -4249,6 +4383,33 @@ __global__ __launch_bounds__(LB) void k_esc_move(Dev d) {
 
 // ------------------------------------------------------------------ owner writes
 // NodeState.set / delete / set_with_ttl / delete_after_ttl on the owner's own view (state.py:124-180).
+// Dev::sm (round 6): one workgroup, each thread a run of consecutive columns; a reverse block scan of the runs'
+// minima, then each run's suffix minima from the next run's
+__device__ __forceinline__ uint32_t lb0_col(const Dev &d, uint32_t c) {
+    return min(msgf(msgf(d.nid_size[c]) + 2u + (d.vlog[(size_t)c * d.VL] & 0xFFFFu)), 0xFFFFu);
+}
+__global__ __launch_bounds__(1024) void k_sm_build(Dev d) {
+    __shared__ uint32_t s_m[1024];
+    const uint32_t t = threadIdx.x, per = (d.ncol + 1023u) / 1024u;
+    const uint32_t c0 = min(t * per, d.ncol), c1 = min(c0 + per, d.ncol);
+    uint32_t m = 0xFFFFu;
+    for (uint32_t c = c0; c < c1; c++) m = min(m, lb0_col(d, c));
+    s_m[t] = m;
+    __syncthreads();
+    for (uint32_t off = 1; off < 1024u; off <<= 1) {
+        const uint32_t v = t + off < 1024u ? s_m[t + off] : 0xFFFFu;
+        __syncthreads();
+        s_m[t] = min(s_m[t], v);
+        __syncthreads();
+    }
+    uint32_t run = t + 1u < 1024u ? s_m[t + 1u] : 0xFFFFu;
+    for (uint32_t c = c1; c-- > c0;) {
+        run = min(run, lb0_col(d, c));
+        d.sm[c] = (uint16_t)run;
+    }
+    if (t == 0) d.sm[d.ncol] = 0xFFFFu;
+}
+
 __global__ __launch_bounds__(LB) void k_owner_writes(Dev d, const gs_write *ops, uint32_t n, uint32_t t) {
     const uint32_t i = blockIdx.x * LB + threadIdx.x;
     if (i >= n) return;
@@ -5206,6 +5367,9 @@ struct gs_handle {
     // gs_set_timing: HIP events around each kernel launch of a kind (gs_ktimes), on the library's stream
     bool timing;
     uint32_t *heavy_buf = nullptr;  // k_pack_heavy's slot list (Dev::heavy): [0] = count, then up to N slot ids
+    uint16_t *sm_buf = nullptr;     // Dev::sm (one-slice prefix-view handles)
+    hipStream_t hside = nullptr;    // k_pack_heavy's stream (forked after the lite slot work, joined after the packer)
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> tev[GS_KT_KINDS];
     std::vector<hipEvent_t> evpool;
     std::string err;
@@ -5531,6 +5695,13 @@ bool lite_fuse() {
 #define HEAVY_T 2048u
 #endif
 constexpr uint32_t HEAVY_GRID = 4096u;
+bool sm_on() {
+    static const bool on = [] {
+        const char *e = getenv("GS_SM");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
 bool heavy_on() {
     static const bool on = [] {
         const char *e = getenv("GS_HEAVY");
@@ -5564,28 +5735,40 @@ int run_split_phase(gs_handle *h, const int32_t *ini, const int32_t *res, uint32
     }
     const bool fl = p1lite(h), defer = fl && !(h->d.ablate & 1u);  // defer: the packer sets the small bits
     const SliceIO io{};
-    if ((rc = launch_pass1(h, ini, res, n, tick, fl ? 0 : -1, io, defer))) return rc;
-    if (h->d.ablate & 1u) return GS_OK;  // profiling only: no packing (results invalid)
-    if (h->pack_mode == 0) return launch_settle<0>(h, ini, res, n, tick, io, GS_KT_PACK);
-    if (h->d.lite && !fl && (rc = launch_lite<0>(h, ini, res, n, tick, io))) return rc;
-    if ((rc = time_begin(h, e0))) return rc;
-    h->d.p1fix = defer ? 1u : 0u;
-    // slots with more than heavy_t stale owners go to k_pack_heavy (K <= 16, prefix views, no hook events)
-    const bool hv = heavy_on() && h->KP <= 16 && h->d.vlog && !h->d.ev && h->d.cand;
+    // slots with more than heavy_t stale owners: the lite slot work (in pass 1's epilogue or k_lite) lists them
+    // and k_pack_heavy packs them on a side stream while k_pack_slice packs the others (K <= 16, prefix views)
+    const bool hv = heavy_on() && h->pack_mode == 2 && h->KP <= 16 && h->d.lite && h->d.vlog && !h->d.ev && h->d.cand;
     if (hv) {
         if (!h->heavy_buf) HIPCHK(h, hipMalloc(&h->heavy_buf, ((size_t)h->N + 4) * 4));
+        if (!h->hside) {
+            HIPCHK(h, hipStreamCreateWithFlags(&h->hside, hipStreamNonBlocking));
+            HIPCHK(h, hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
+            HIPCHK(h, hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
+        }
         HIPCHK(h, hipMemsetAsync(h->heavy_buf, 0, 4, h->stream));
         h->d.heavy = h->heavy_buf;
         h->d.heavy_t = heavy_t();
     }
+    if ((rc = launch_pass1(h, ini, res, n, tick, fl ? 0 : -1, io, defer))) return rc;
+    if (h->d.ablate & 1u) { h->d.heavy = nullptr; return GS_OK; }  // profiling only: no packing (results invalid)
+    if (h->pack_mode == 0) return launch_settle<0>(h, ini, res, n, tick, io, GS_KT_PACK);
+    if (h->d.lite && !fl && (rc = launch_lite<0>(h, ini, res, n, tick, io))) return rc;
+    if (hv) {  // fork: the heavy slots on the side stream
+        HIPCHK(h, hipEventRecord(h->ev_fork, h->stream));
+        HIPCHK(h, hipStreamWaitEvent(h->hside, h->ev_fork, 0));
+        k_pack_heavy<4><<<std::min(2u * n, HEAVY_GRID), HT, 0, h->hside>>>(h->d, ini, res, tick, h->heavy_buf);
+        HIPCHK(h, hipGetLastError());
+    }
+    if ((rc = time_begin(h, e0))) return rc;
+    h->d.p1fix = defer ? 1u : 0u;
     if (h->KP <= 16) k_pack_slice<4><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, io, 0u);
     else k_pack_slice<KWB><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, io, 0u);
     h->d.p1fix = 0u;
     h->d.heavy = nullptr;
     HIPCHK(h, hipGetLastError());
-    if (hv) {
-        k_pack_heavy<4><<<std::min(2u * n, HEAVY_GRID), HT, 0, h->stream>>>(h->d, ini, res, tick, h->heavy_buf);
-        HIPCHK(h, hipGetLastError());
+    if (hv) {  // k_pack_heavy ran on the side stream meanwhile (forked after the lite slot work): join
+        HIPCHK(h, hipEventRecord(h->ev_join, h->hside));
+        HIPCHK(h, hipStreamWaitEvent(h->stream, h->ev_join, 0));
     }
     return time_end(h, GS_KT_PACK, e0);
 }
@@ -5765,6 +5948,10 @@ void gs_destroy(gs_handle *h) {
     if (h->sc.pin) (void)hipHostFree(h->sc.pin);
     if (h->grp) (void)hipFree(h->grp);
     if (h->heavy_buf) (void)hipFree(h->heavy_buf);
+    if (h->sm_buf) (void)hipFree(h->sm_buf);
+    if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
+    if (h->ev_join) (void)hipEventDestroy(h->ev_join);
+    if (h->hside) (void)hipStreamDestroy(h->hside);
     if (h->comm) (void)ncclCommDestroy(h->comm);
     if (h->side) (void)hipStreamDestroy(h->side);
     for (hipEvent_t e : {h->fj_fork, h->fj_join})
@@ -5882,6 +6069,13 @@ int gs_owner_writes(gs_handle *h, const gs_write *ops, uint32_t n, uint32_t tick
     k_owner_writes<<<(n + LB - 1) / LB, LB, 0, h->stream>>>(h->d, ops, n, tick);
     HIPCHK(h, hipGetLastError());
     if (h->d.ev) h->d.ev_wseq += n;
+    // the first-fit stop bound (Dev::sm): one-slice canonical prefix-view handles, env GS_SM=0: off (A/B)
+    if (sm_on() && h->G == 1 && !h->sliced && h->d.vlog && (h->cfg.flags & GS_CANONICAL)) {
+        if (!h->sm_buf) HIPCHK(h, hipMalloc(&h->sm_buf, ((size_t)h->NP + 1) * 2));
+        h->d.sm = h->sm_buf;
+        k_sm_build<<<1, 1024, 0, h->stream>>>(h->d);
+        HIPCHK(h, hipGetLastError());
+    }
     return GS_OK;
 }
 

@@ -338,7 +338,7 @@ def test_sliced_parity_check_on_whole_cluster_rows(native):
 
     from aiocluster_amd import driver
 
-    grp, cfg, plans = _bench_cluster(1024, 4, 1500, 8, native=native)
+    grp, cfg, plans = _bench_cluster(1024, 4, 500, 8, native=native)
     rd = plans[8]
     driver.begin(grp.slices, rd)
     res, info = check_sliced_phase_rows(grp, cfg, rd, sample=rd["phases"][0][2])
