@@ -5,7 +5,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 O=gpurun_out/$TAG; mkdir -p $O
-timeout -k 10 ${LIMIT:-1100} python -u -m pytest ${TESTS:-tests} ${KEXPR:+-k "$KEXPR"} -m gpu -v --capture=sys --durations=25 --timeout 400 \
+timeout -k 10 ${LIMIT:-1100} python -u -m pytest ${TESTS:-tests} ${KEXPR:+-k "$KEXPR"} -m gpu -v -rP --capture=sys --durations=25 --timeout 400 \
   --timeout-method thread > $O/gpu_tests.log 2>&1
 rc=$?
 grep -E "PASSED|FAILED|ERROR" $O/gpu_tests.log | grep -c PASSED
