@@ -184,7 +184,7 @@ struct Dev {
     uint32_t heavy_t;
     // one-slice prefix-view handles (round 6): sm[c] = the smallest possible NodeDelta of any owner column >= c --
     // min over j >= c of msgf(msgf(NodeIdPb bytes of j) + 2 + the smallest kv field j ever wrote, GS_R_VLOG entry
-    // 0), a lower bound of every candidate's min1 -- rebuilt after every gs_owner_writes (k_sm_build); sm[ncol] =
+    // 0), a lower bound of every candidate's min1 -- rebuilt after every gs_owner_writes (k_sm_local, k_sm_fix); sm[ncol] =
     // 0xFFFF.  First-fit continuation stops as soon as the budget left is below sm at the next candidate's column:
     // no later candidate can add a NodeDelta (R only shrinks).  nullptr: not built (sliced handles: the chain's
     // later slices hold the other columns)
@@ -4383,18 +4383,16 @@ __global__ __launch_bounds__(LB) void k_esc_move(Dev d) {
 
 // ------------------------------------------------------------------ owner writes
 // NodeState.set / delete / set_with_ttl / delete_after_ttl on the owner's own view (state.py:124-180).
-// Dev::sm (round 6): one workgroup, each thread a run of consecutive columns; a reverse block scan of the runs'
-// minima, then each run's suffix minima from the next run's
+// Dev::sm (round 6), in two launches over blocks of 1,024 columns: k_sm_local -- one column per thread, the
+// block's suffix minima (LDS scan) and the block's minimum into sm_blk; k_sm_fix -- each column's value min the
+// minima of the later blocks
 __device__ __forceinline__ uint32_t lb0_col(const Dev &d, uint32_t c) {
     return min(msgf(msgf(d.nid_size[c]) + 2u + (d.vlog[(size_t)c * d.VL] & 0xFFFFu)), 0xFFFFu);
 }
-__global__ __launch_bounds__(1024) void k_sm_build(Dev d) {
+__global__ __launch_bounds__(1024) void k_sm_local(Dev d, uint32_t *sm_blk) {
     __shared__ uint32_t s_m[1024];
-    const uint32_t t = threadIdx.x, per = (d.ncol + 1023u) / 1024u;
-    const uint32_t c0 = min(t * per, d.ncol), c1 = min(c0 + per, d.ncol);
-    uint32_t m = 0xFFFFu;
-    for (uint32_t c = c0; c < c1; c++) m = min(m, lb0_col(d, c));
-    s_m[t] = m;
+    const uint32_t t = threadIdx.x, c = blockIdx.x * 1024u + t;
+    s_m[t] = c < d.ncol ? lb0_col(d, c) : 0xFFFFu;
     __syncthreads();
     for (uint32_t off = 1; off < 1024u; off <<= 1) {
         const uint32_t v = t + off < 1024u ? s_m[t + off] : 0xFFFFu;
@@ -4402,12 +4400,20 @@ __global__ __launch_bounds__(1024) void k_sm_build(Dev d) {
         s_m[t] = min(s_m[t], v);
         __syncthreads();
     }
-    uint32_t run = t + 1u < 1024u ? s_m[t + 1u] : 0xFFFFu;
-    for (uint32_t c = c1; c-- > c0;) {
-        run = min(run, lb0_col(d, c));
-        d.sm[c] = (uint16_t)run;
+    if (c < d.ncol) d.sm[c] = (uint16_t)s_m[t];
+    if (t == 0) sm_blk[blockIdx.x] = s_m[0];
+}
+__global__ __launch_bounds__(1024) void k_sm_fix(Dev d, const uint32_t *sm_blk, uint32_t nblk) {
+    __shared__ uint32_t s_after;
+    const uint32_t t = threadIdx.x, c = blockIdx.x * 1024u + t;
+    if (t == 0) {
+        uint32_t m = 0xFFFFu;
+        for (uint32_t b2 = blockIdx.x + 1u; b2 < nblk; b2++) m = min(m, sm_blk[b2]);
+        s_after = m;
     }
-    if (t == 0) d.sm[d.ncol] = 0xFFFFu;
+    __syncthreads();
+    if (c < d.ncol) d.sm[c] = (uint16_t)min((uint32_t)d.sm[c], s_after);
+    if (c == 0) d.sm[d.ncol] = 0xFFFFu;
 }
 
 __global__ __launch_bounds__(LB) void k_owner_writes(Dev d, const gs_write *ops, uint32_t n, uint32_t t) {
@@ -6071,9 +6077,16 @@ int gs_owner_writes(gs_handle *h, const gs_write *ops, uint32_t n, uint32_t tick
     if (h->d.ev) h->d.ev_wseq += n;
     // the first-fit stop bound (Dev::sm): one-slice canonical prefix-view handles, env GS_SM=0: off (A/B)
     if (sm_on() && h->G == 1 && !h->sliced && h->d.vlog && (h->cfg.flags & GS_CANONICAL)) {
-        if (!h->sm_buf) HIPCHK(h, hipMalloc(&h->sm_buf, ((size_t)h->NP + 1) * 2));
+        const uint32_t nblk = (h->ncol + 1023u) / 1024u;
+        if (!h->sm_buf) {  // sm [NP + 1] u16, then the block minima [nblk] u32
+            HIPCHK(h, hipMalloc(&h->sm_buf, ((size_t)h->NP + 2) * 2 + (size_t)nblk * 4 + 16));
+        }
+        uint32_t *blk = reinterpret_cast<uint32_t *>(
+            (reinterpret_cast<uintptr_t>(h->sm_buf + h->NP + 2) + 15) & ~(uintptr_t)15);
         h->d.sm = h->sm_buf;
-        k_sm_build<<<1, 1024, 0, h->stream>>>(h->d);
+        k_sm_local<<<nblk, 1024, 0, h->stream>>>(h->d, blk);
+        HIPCHK(h, hipGetLastError());
+        k_sm_fix<<<nblk, 1024, 0, h->stream>>>(h->d, blk, nblk);
         HIPCHK(h, hipGetLastError());
     }
     return GS_OK;
