@@ -3464,8 +3464,12 @@ __device__ __forceinline__ SlotSum settle_sum(const Dev &d, uint32_t snd, uint32
 // LITE (sliced phases with Dev::lite, MODE 1 and 2): k_lite's slot work first, in the same wave, and the exact
 // count / pack only for the slots it leaves (one launch per step instead of two: a slice's kernels are short,
 // and their fixed cost per launch is what a sliced phase pays over one handle)
+#ifndef SETTLE_LITE_WAVES
+#define SETTLE_LITE_WAVES PK_WAVES  // waves per SIMD of the sliced steps' k_settle<LITE>: nearly every slot ends in the
+                                    // lite slot work; the exact count / pack below it runs for the few others
+#endif
 template <int KW, int MODE, bool LITE = false, bool GRP = false>
-__global__ __launch_bounds__(XB, (KW == 4 ? PK_WAVES : 1)) void k_settle(Dev d, const int32_t *ini, const int32_t *res,
+__global__ __launch_bounds__(XB, (KW == 4 ? (LITE ? SETTLE_LITE_WAVES : PK_WAVES) : 1)) void k_settle(Dev d, const int32_t *ini, const int32_t *res,
                                                                         uint32_t n, uint32_t t, SliceIO io,
                                                                         const GroupArgs *ga, DevDyn dyn) {
     __shared__ __attribute__((aligned(16))) uint16_t s_wbuf[2 * WIN];
