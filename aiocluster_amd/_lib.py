@@ -45,7 +45,7 @@ def slice_columns(n: int, shards: int, shard: int) -> tuple[int, int]:
 
 
 GS_CHAIN_DEVICE = 0xFFFFFFFF  # gs_phase_chain: the count stays on the device
-GS_CHAIN_CAP = 4096  # ... for at most this many overflowing slots
+GS_CHAIN_CAP = 1024  # ... for at most this many overflowing slots
 
 
 def overflow_list_len(n: int) -> int:
@@ -76,7 +76,7 @@ COUNTER_FIELDS = [
     "err_fd_gc", "err_insert", "fd_gc", "q9", "pack_bytes", "err_holes", "err_hb_lag", "plane_flushes",
     "fd_saturated", "lite_slots", "lag_sweeps", "lite_bytes", "live_bytes", "hb_escapes", "hb_releases",
     "pack_groups_max", "pack_steps_max",  # maxima (gs_read_counters takes the largest; sum_counters too)
-    "heavy_slots", "phase_reruns",
+    "heavy_slots",
 ]
 
 # Every symbol include/gossip_sim.h declares (checked by tests/test_abi.py).
@@ -87,10 +87,10 @@ EXPORTS = [
     "gs_select_peers", "gs_schedule_phases", "gs_set_events", "gs_emit_scratch_bytes", "gs_emit_digest", "gs_emit_delta",
     "gs_check_heartbeat_lag", "gs_stream_copy", "gs_stream_read", "gs_stream_write", "gs_set_timing", "gs_kernel_times",
     "gs_phase_overflow", "gs_phase_chain", "gs_phase_pending", "gs_comm_id", "gs_comm_init", "gs_run_phase_group", "gs_read_rows",
-    "gs_latest_tick", "gs_flush_reports", "gs_set_ring_rows", "gs_mark", "gs_run_phases_group",
+    "gs_latest_tick", "gs_flush_reports", "gs_set_ring_rows", "gs_mark",
 ]
 
-API_VERSION = 21
+API_VERSION = 20
 MAX_PHASES = 64  # GS_MAX_PHASES
 MAX_SCHED_PHASES = 65536  # GS_MAX_SCHED_PHASES
 
@@ -216,7 +216,6 @@ def load():
         "gs_comm_id": (C.c_int, [P]),
         "gs_comm_init": (C.c_int, [P, P, u32, u32]),
         "gs_run_phase_group": (C.c_int, [P, u32, P, P, u32, u32]),
-        "gs_run_phases_group": (C.c_int, [P, u32, P, P, P, P, u32]),
         "gs_read_rows": (C.c_int, [P, C.c_int, u32, u32, P, u64, C.POINTER(u64)]),
         "gs_latest_tick": (C.c_int, [P, C.POINTER(u32)]),
         "gs_flush_reports": (C.c_int, [P, u32]),

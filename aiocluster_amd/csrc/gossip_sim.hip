@@ -76,13 +76,13 @@ enum Ctr {
     C_EXCH = 0, C_REPORTS, C_ND, C_KVS, C_TRUNC, C_DBYTES, C_ALG, C_HBW, C_CAND, C_LIVE, C_TOMBGC,
     C_E_FDOVF, C_E_HIST, C_E_IDX, C_E_CONFLICT, C_E_FDGC, C_E_INSERT, C_FDGC, C_Q9, C_PACKB, C_E_HOLES,
     C_E_HBLAG, C_FLUSH /* host-side: plane_flushes */, C_FDSAT, C_LITE, C_SWEEPS /* host-side: lag_sweeps */,
-    C_LITEB, C_LIVEB, C_ESC, C_ESCREL, C_PGMAX, C_PSMAX, C_HEAVY, C_RERUN /* host-side: phase_reruns */,
+    C_LITEB, C_LIVEB, C_ESC, C_ESCREL, C_PGMAX, C_PSMAX, C_HEAVY,
     C_CEN0 = 40, C_NUM = C_CEN0 + 6  // gs_fd_census scratch slots (not part of gs_counters)
 };
 constexpr int CFIELDS = 40;  // gs_counters fields (the last ones reserved)
 constexpr int CROW = 48;     // u64 slots per counter shard row (the gs_counters fields, then the census scratch)
 static_assert(C_NUM <= CROW, "counter region");
-static_assert(C_RERUN < CFIELDS, "gs_counters fields");
+static_assert(C_HEAVY < CFIELDS, "gs_counters fields");
 static_assert(sizeof(gs_counters) == CFIELDS * 8, "gs_counters layout");
 
 struct Dev {
@@ -2221,17 +2221,13 @@ __device__ __forceinline__ uint32_t lite_slot(const Dev &d, int32_t ai, int32_t 
 
 // LM >= 0: k_lite's slot work (lite_slot<LM>: 0 = one slice, 1 = a sliced count pass) runs in the same workgroup
 // after the stream, wave w taking direction w -- no k_lite launch (round 5; env GS_P1LITE=0: the launch of its own)
-// gate (gs_run_phases_group): the previous sliced phase's pending-slot sum (sliced_queue_pending's device copy);
-// non-zero = that phase still has chain steps to run, so this launch does nothing at all (the host runs them, then
-// launches this phase again without a gate)
 template <int AHEAD, int LM, bool GRP = false>
 __global__ __launch_bounds__(XB, P1V_WAVES) void k_pass1v(Dev d, const int32_t *ini, const int32_t *res, uint32_t n,
                                                           uint32_t t, uint32_t seq, SliceIO io, const GroupArgs *ga,
-                                                          DevDyn dyn, const uint64_t *gate) {
+                                                          DevDyn dyn) {
     static_assert(AHEAD == 1, "k_pass1v double-buffers one group ahead (r4g: two ahead at 5 waves per SIMD, no faster)");
     __shared__ uint32_t s_col[XB / WAVE][P1V_K];
     __shared__ uint32_t s_out[XB / WAVE][P1V_K * P1V_SLOT];
-    if (gate && *gate) return;
     const uint32_t e = blockIdx.x;
     if (e >= n) return;
     if constexpr (GRP) {  // a slice of an in-process group (blockIdx.y; its own instantiation: the Dev copy
@@ -3265,10 +3261,9 @@ __global__ __launch_bounds__(OVB) void k_ov_write(const uint64_t *tot_all, uint3
 // the pending counts of all G slices (entry count of each gathered chainc) summed into *out.  cnt_dev: the count
 // is read on the device (GS_CHAIN_DEVICE: gathered rows of GS_CHAIN_CAP + 1 entries); a count above the cap gives
 // ~0 (the device step did not run: the host takes over)
-// out[1] = the count (gs_phase_pending; out may be host-mapped pinned memory: the host reads it after the wait);
-// gate (nullable): a device copy of out[0], the next phase's k_pass1v gate (gs_run_phases_group)
+// out[1] = the count (gs_phase_pending; out may be host-mapped pinned memory: the host reads it after the wait)
 __global__ __launch_bounds__(WAVE) void k_sum_pending(const uint64_t *chain_all, uint32_t G, uint32_t count,
-                                                      const uint32_t *cnt_dev, uint64_t *out, uint64_t *gate) {
+                                                      const uint32_t *cnt_dev, uint64_t *out) {
     const uint32_t c = cnt_dev ? *cnt_dev : count;
     const size_t stride = cnt_dev ? GS_CHAIN_CAP + 1u : (size_t)count + 1u;
     unsigned long long s = 0;
@@ -3276,10 +3271,8 @@ __global__ __launch_bounds__(WAVE) void k_sum_pending(const uint64_t *chain_all,
         for (uint32_t g = threadIdx.x; g < G; g += WAVE) s += chain_all[(size_t)g * stride + c];
     s = wave_sum(s);
     if (threadIdx.x == 0) {
-        const uint64_t p = cnt_dev && c > GS_CHAIN_CAP ? ~0ull : s;
-        out[0] = p;
+        out[0] = cnt_dev && c > GS_CHAIN_CAP ? ~0ull : s;
         out[1] = c;
-        if (gate) gate[0] = p;
     }
 }
 
@@ -5400,8 +5393,6 @@ struct gs_handle {
         uint32_t *list = nullptr;
         uint32_t cap = 0;  // exchanges the buffers hold
     } sc;
-    hipEvent_t pev = nullptr;    // after the last k_sum_pending (queue_pending / wait_pending)
-    uint64_t phase_reruns = 0;   // gs_run_phases_group: phases whose gated pass 1 ran again (gs_counters.phase_reruns)
     // gs_run_phase_group: each slice's kernels of a step run on a stream of its own (forked from and joined
     // back into the group's stream around the step), so the slices' short launches overlap on the GPU
     hipStream_t side = nullptr, home = nullptr;
@@ -5654,18 +5645,17 @@ struct GroupCtx {
     DevDyn dyn{};
 };
 int launch_pass1(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t n, uint32_t tick, int lm = -1,
-                 const SliceIO &io = SliceIO{}, bool defer_fix = false, const GroupCtx &gx = GroupCtx{},
-                 const uint64_t *gate = nullptr) {
+                 const SliceIO &io = SliceIO{}, bool defer_fix = false, const GroupCtx &gx = GroupCtx{}) {
     hipEvent_t e0 = nullptr;
     int rc = time_begin(h, e0);
     if (rc) return rc;
     if (h->d.pl16) {  // GS_MV8 record phases: the byte-parallel pass 1
         const dim3 grid(n, gx.nh);
-        if (gx.ga && lm == 1) k_pass1v<P1V_AHEAD, 1, true><<<grid, XB, 0, h->stream>>>(h->d, ini, res, n, tick, h->seq, io, gx.ga, gx.dyn, gate);
-        else if (gx.ga) k_pass1v<P1V_AHEAD, -1, true><<<grid, XB, 0, h->stream>>>(h->d, ini, res, n, tick, h->seq, io, gx.ga, gx.dyn, gate);
-        else if (lm == 0) k_pass1v<P1V_AHEAD, 0><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, h->seq, io, nullptr, DevDyn{}, gate);
-        else if (lm == 1) k_pass1v<P1V_AHEAD, 1><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, h->seq, io, nullptr, DevDyn{}, gate);
-        else k_pass1v<P1V_AHEAD, -1><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, h->seq, io, nullptr, DevDyn{}, gate);
+        if (gx.ga && lm == 1) k_pass1v<P1V_AHEAD, 1, true><<<grid, XB, 0, h->stream>>>(h->d, ini, res, n, tick, h->seq, io, gx.ga, gx.dyn);
+        else if (gx.ga) k_pass1v<P1V_AHEAD, -1, true><<<grid, XB, 0, h->stream>>>(h->d, ini, res, n, tick, h->seq, io, gx.ga, gx.dyn);
+        else if (lm == 0) k_pass1v<P1V_AHEAD, 0><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, h->seq, io, nullptr, DevDyn{});
+        else if (lm == 1) k_pass1v<P1V_AHEAD, 1><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, h->seq, io, nullptr, DevDyn{});
+        else k_pass1v<P1V_AHEAD, -1><<<n, XB, 0, h->stream>>>(h->d, ini, res, n, tick, h->seq, io, nullptr, DevDyn{});
         HIPCHK(h, hipGetLastError());
         rc = time_end(h, GS_KT_PASS1, e0);
         if (rc) return rc;
@@ -5974,7 +5964,7 @@ void gs_destroy(gs_handle *h) {
     if (h->hside) (void)hipStreamDestroy(h->hside);
     if (h->comm) (void)ncclCommDestroy(h->comm);
     if (h->side) (void)hipStreamDestroy(h->side);
-    for (hipEvent_t e : {h->fj_fork, h->fj_join, h->pev})
+    for (hipEvent_t e : {h->fj_fork, h->fj_join})
         if (e) (void)hipEventDestroy(e);
     delete h;
 }
@@ -6191,16 +6181,8 @@ int gs_shard_columns(const gs_handle *h, uint32_t *col_lo, uint32_t *n_cols) {
     return GS_OK;
 }
 
-// gs_phase_count in two parts (gs_run_phases_group queues the next phase's pass 1 before it reads this phase's
-// pending count): begin = the checks, the bookkeeping and pass 1; end = the count launch.  The variant says which
-// of gs_phase_count's launch sequences the phase takes (0: the fused count pass; 1: the lite slot work in
-// k_pass1v; 2: pass 1, then lite + count in one launch; 3: the others); only 1 and 2 take a pass-1 gate (k_pass1v
-// with the responders' small bits deferred to the count launch: a gated launch leaves no trace)
-extern "C++" {
-namespace {
-int phase_count_begin(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t n, uint32_t tick,
-                      uint64_t *slice_bytes, int &variant, const uint64_t *gate = nullptr) {
-    variant = -1;  // (nothing to do: n = 0)
+int gs_phase_count(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t n, uint32_t tick,
+                   uint64_t *slice_bytes) {
     int rc = check_phase(h, ini, res, n, tick);
     if (rc) return rc;
     if (!h->sliced) return fail(h, GS_E_UNSUPPORTED, "gs_phase_count needs a sliced handle (n_shards > 1 or GS_SLICED)");
@@ -6216,8 +6198,6 @@ int phase_count_begin(gs_handle *h, const int32_t *ini, const int32_t *res, uint
     h->last_phase_tick = tick;
     h->hb_incs++;
     if (!h->d.cand) {  // GS_FUSED: the fused count pass (LDS bitmaps)
-        variant = 0;
-        if (gate) return fail(h, GS_E_INVALID, "phase_count_begin: no pass-1 gate on the fused count pass");
         h->d.spec = 0u;
         h->d.lite = 0u;
         hipEvent_t e0 = nullptr;
@@ -6229,43 +6209,24 @@ int phase_count_begin(gs_handle *h, const int32_t *ini, const int32_t *res, uint
     // the speculative merge is decided here for the whole phase (gs_phase_pack / gs_phase_chain use it)
     h->d.spec = spec_ok(h) || spec_v_ok(h) ? 1u : 0u;
     h->d.lite = lite_ok(h) ? 1u : 0u;
-    // variant 1: the lite slot work runs in k_pass1v (the count launch: the exact count of the slots it left);
-    // variant 2: lite + count in one launch after pass 1, which also sets the responders' small bits
-    variant = p1lite(h, 1) ? 1 : (h->d.lite && lite_fuse() && h->d.pl16) ? 2 : 3;
-    if (variant == 1) return launch_pass1(h, ini, res, n, tick, 1, io, true, GroupCtx{}, gate);
-    if (variant == 2) return launch_pass1(h, ini, res, n, tick, -1, io, true, GroupCtx{}, gate);
-    if (gate) return fail(h, GS_E_INVALID, "phase_count_begin: no pass-1 gate on this layout");
-    return launch_pass1(h, ini, res, n, tick);
-}
-int phase_count_end(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t n, uint32_t tick,
-                    uint64_t *slice_bytes, int variant) {
-    if (variant <= 0) return GS_OK;  // (n = 0, or the fused count pass did it all)
-    SliceIO io{};
-    io.tot = slice_bytes;
-    int rc;
-    if (variant == 1 || variant == 2) {
-        h->d.p1fix = 1u;  // the responders' small bits (k_p1v_fix's work)
-        rc = variant == 1 ? launch_settle<1>(h, ini, res, n, tick, io, GS_KT_COUNT)
-                          : launch_settle<1, true>(h, ini, res, n, tick, io, GS_KT_COUNT);
+    if (p1lite(h, 1)) {  // the lite slot work ran in k_pass1v: the exact count of the slots it left (LITE_FULL) only
+        if ((rc = launch_pass1(h, ini, res, n, tick, 1, io, true))) return rc;
+        h->d.p1fix = 1u;  // and the responders' small bits (k_p1v_fix)
+        rc = launch_settle<1>(h, ini, res, n, tick, io, GS_KT_COUNT);
         h->d.p1fix = 0u;
         return rc;
     }
+    if (h->d.lite && lite_fuse() && h->d.pl16) {  // lite + count in one launch, which also sets the small bits
+        if ((rc = launch_pass1(h, ini, res, n, tick, -1, io, true))) return rc;
+        h->d.p1fix = 1u;
+        rc = launch_settle<1, true>(h, ini, res, n, tick, io, GS_KT_COUNT);
+        h->d.p1fix = 0u;
+        return rc;
+    }
+    if ((rc = launch_pass1(h, ini, res, n, tick))) return rc;
     if (h->d.lite && lite_fuse()) return launch_settle<1, true>(h, ini, res, n, tick, io, GS_KT_COUNT);
     if (h->d.lite && (rc = launch_lite<1>(h, ini, res, n, tick, io))) return rc;
     return launch_settle<1>(h, ini, res, n, tick, io, GS_KT_COUNT);
-}
-// a slice whose phases gs_run_phases_group may pipeline: pass 1 is k_pass1v and the count takes variant 1 or 2
-bool pipe_slice_ok(const gs_handle *h) {
-    return h->sliced && h->d.cand && h->d.pl16 && lite_ok(h) && lite_fuse();
-}
-}  // namespace
-}
-
-int gs_phase_count(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t n, uint32_t tick,
-                   uint64_t *slice_bytes) {
-    int variant = -1;
-    const int rc = phase_count_begin(h, ini, res, n, tick, slice_bytes, variant);
-    return rc ? rc : phase_count_end(h, ini, res, n, tick, slice_bytes, variant);
 }
 
 int gs_phase_pack(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t n, uint32_t tick, uint32_t step,
@@ -6352,7 +6313,7 @@ int ensure_scratch(gs_handle *h, uint32_t n) {
     for (void *p : {(void *)h->sc.tot, (void *)h->sc.tot_all, (void *)h->sc.chain, (void *)h->sc.chainc,
                     (void *)h->sc.chain_all, (void *)h->sc.list, (void *)h->sc.pend})
         if (p) HIPCHK(h, hipFree(p));
-    const uint32_t cap = std::max(n, GS_CHAIN_CAP / 2u);  // (chainc rows of 2 cap + 1 >= GS_CHAIN_CAP + 1 entries)
+    const uint32_t cap = std::max(n, 1024u);
     const size_t s2 = (size_t)2 * cap * 8, G = h->G;
     HIPCHK(h, hipMalloc(&h->sc.tot, s2));
     HIPCHK(h, hipMalloc(&h->sc.chain, s2));
@@ -6365,30 +6326,19 @@ int ensure_scratch(gs_handle *h, uint32_t n) {
     return GS_OK;
 }
 
-// k_sum_pending into the handle's pinned host pair (written by the kernel itself: no copy) and, with `gate`, into
-// its device word sc.pend (the next phase's k_pass1v gate); then an event the host waits on (wait_pending)
-int queue_pending(gs_handle *h, uint32_t G, uint32_t count, const uint32_t *cnt_dev, const uint64_t *chain_all,
-                  bool gate = false) {
+// k_sum_pending into the handle's pinned host pair (written by the kernel itself: no copy), then one wait
+int read_pending(gs_handle *h, uint32_t G, uint32_t count, const uint32_t *cnt_dev, const uint64_t *chain_all,
+                 uint64_t &pend, uint32_t &cnt) {
     if (!h->sc.pin) {
         HIPCHK(h, hipHostMalloc((void **)&h->sc.pin, 16, hipHostMallocMapped));
         HIPCHK(h, hipHostGetDevicePointer((void **)&h->sc.pin_dev, h->sc.pin, 0));
     }
-    if (!h->pev) HIPCHK(h, hipEventCreateWithFlags(&h->pev, hipEventDisableTiming));
-    k_sum_pending<<<1, WAVE, 0, h->stream>>>(chain_all, G, count, cnt_dev, h->sc.pin_dev, gate ? h->sc.pend : nullptr);
+    k_sum_pending<<<1, WAVE, 0, h->stream>>>(chain_all, G, count, cnt_dev, h->sc.pin_dev);
     HIPCHK(h, hipGetLastError());
-    HIPCHK(h, hipEventRecord(h->pev, h->stream));
-    return GS_OK;
-}
-int wait_pending(gs_handle *h, uint64_t &pend, uint32_t &cnt) {
-    HIPCHK(h, hipEventSynchronize(h->pev));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
     pend = reinterpret_cast<volatile uint64_t *>(h->sc.pin)[0];
     cnt = (uint32_t)reinterpret_cast<volatile uint64_t *>(h->sc.pin)[1];
     return GS_OK;
-}
-int read_pending(gs_handle *h, uint32_t G, uint32_t count, const uint32_t *cnt_dev, const uint64_t *chain_all,
-                 uint64_t &pend, uint32_t &cnt) {
-    const int rc = queue_pending(h, G, count, cnt_dev, chain_all);
-    return rc ? rc : wait_pending(h, pend, cnt);
 }
 
 // all-gather of `count` u64 per slice (src of slice g -> dst[g * count ..], on every slice): one RCCL
@@ -6509,18 +6459,8 @@ int group_upload(gs_handle *const *hs, uint32_t nh) {
     }
     return GS_OK;
 }
-// env GS_GRP_P1LITE=1: the group's lite slot work in pass 1's epilogue, the count launch only for LITE_FULL slots
-bool grp_p1lite() {
-    static const bool on = [] {
-        const char *e = getenv("GS_GRP_P1LITE");
-        return e && e[0] == '1';
-    }();
-    return on;
-}
-// count, gather, step 0, the overflow lists and chain step 1 of a sliced phase, batched over the group, in two parts:
-// group_begin = every slice's checks and bookkeeping, then pass 1 (gated: gs_run_phases_group); group_rest = the rest
-int group_begin(gs_handle *const *hs, uint32_t nh, const int32_t *ini, const int32_t *res, uint32_t n, uint32_t tick,
-                GroupCtx &gx, const uint64_t *gate = nullptr) {
+// count, gather, step 0, the overflow lists and chain step 1 of a sliced phase, batched over the group
+int group_steps(gs_handle *const *hs, uint32_t nh, const int32_t *ini, const int32_t *res, uint32_t n, uint32_t tick) {
     int rc;
     gs_handle *h0 = hs[0];
     // per slice: gs_phase_count's checks and bookkeeping (a lag sweep or a window-age sweep may launch here)
@@ -6540,20 +6480,18 @@ int group_begin(gs_handle *const *hs, uint32_t nh, const int32_t *ini, const int
             return fail(h0, GS_E_INVALID, "gs_run_phase_group: slice %u is not in step with slice 0", i);
     }
     if ((rc = group_upload(hs, nh))) return rc;
-    gx = GroupCtx{};
+    GroupCtx gx;
     gx.ga = h0->grp;
     gx.nh = nh;
     gx.dyn = DevDyn{h0->d.t_round, h0->d.spec, h0->d.lite, 0u, h0->d.v_round, h0->d.vt, h0->d.t_cap};
-    // count: pass 1, then lite + the slice totals in one launch, which also sets the responders' small bits
-    // (GS_GRP_P1LITE=1: the lite slot work in pass 1's epilogue instead)
-    return launch_pass1(h0, ini, res, n, tick, grp_p1lite() ? 1 : -1, SliceIO{}, true, gx, gate);
-}
-int group_rest(gs_handle *const *hs, uint32_t nh, const int32_t *ini, const int32_t *res, uint32_t n, uint32_t tick,
-               GroupCtx &gx) {
-    int rc;
-    gs_handle *h0 = hs[0];
-    const bool glite = grp_p1lite();
     SliceIO io{};  // (each slice's from GroupArgs; the step by value)
+    // count: pass 1, then lite + the slice totals in one launch, which also sets the responders' small bits; env
+    // GS_GRP_P1LITE=1: the lite slot work in pass 1's epilogue instead, the count launch only for LITE_FULL slots
+    static const bool glite = [] {
+        const char *e = getenv("GS_GRP_P1LITE");
+        return e && e[0] == '1';
+    }();
+    if ((rc = launch_pass1(h0, ini, res, n, tick, glite ? 1 : -1, io, true, gx))) return rc;
     gx.dyn.p1fix = 1u;
     rc = glite ? launch_settle<1>(h0, ini, res, n, tick, io, GS_KT_COUNT, gx)
                : launch_settle<1, true>(h0, ini, res, n, tick, io, GS_KT_COUNT, gx);
@@ -6586,99 +6524,6 @@ int group_rest(gs_handle *const *hs, uint32_t nh, const int32_t *ini, const int3
     return time_end(h0, GS_KT_PACK, e0);
 }
 
-int group_steps(gs_handle *const *hs, uint32_t nh, const int32_t *ini, const int32_t *res, uint32_t n, uint32_t tick) {
-    GroupCtx gx;
-    const int rc = group_begin(hs, nh, ini, res, n, tick, gx);
-    return rc ? rc : group_rest(hs, nh, ini, res, n, tick, gx);
-}
-
-// the tail of a sliced phase: gs_phase_overflow's count entry of this phase's list (slice 0's)
-const uint32_t *overflow_count(const gs_handle *h0, uint32_t n) {
-    return h0->sc.list + 2u * n + (2u * n + OVB - 1u) / OVB;
-}
-int gather_chain(gs_handle *const *hs, uint32_t nh, size_t entries) {
-    return gather_u64(hs, nh, [](gs_handle *h) { return h->sc.chainc; }, [](gs_handle *h) { return h->sc.chain_all; },
-                      entries);
-}
-// `steps` more chain steps on the device count (the overflow list's length stays on the device: steps past the
-// last pending slot do nothing), with no host read: gather every slice's chain states, then each slice resumes its
-// pending slots from its nearest finished predecessor -- one launch for the whole batched group
-int device_chain_steps(gs_handle *const *hs, uint32_t nh, const int32_t *ini, const int32_t *res, uint32_t n,
-                       uint32_t tick, uint32_t steps) {
-    int rc;
-    gs_handle *h0 = hs[0];
-    const bool grp = nh > 1 && group_batch_ok(hs, nh) && h0->G == nh;
-    const uint32_t *cnt0 = overflow_count(h0, n);  // (each slice's own list tail, from GroupArgs)
-    const DevDyn dyn{h0->d.t_round, h0->d.spec, h0->d.lite, 0u, h0->d.v_round, h0->d.vt, h0->d.t_cap};
-    for (uint32_t s = 0; s < steps; s++) {
-        if ((rc = gather_chain(hs, nh, GS_CHAIN_CAP + 1u))) return rc;
-        if (grp) {
-            hipEvent_t e0 = nullptr;
-            if ((rc = time_begin(h0, e0))) return rc;
-            k_chain_step<4, true><<<dim3(std::min<uint32_t>(GS_CHAIN_CAP, 2048u), nh), WAVE, 0, h0->stream>>>(
-                h0->d, ini, res, tick, nullptr, 0u, nullptr, nullptr, nullptr, nullptr, n, cnt0, h0->grp, dyn);
-            HIPCHK(h0, hipGetLastError());
-            k_pending<<<dim3(1, nh), OVB, 0, h0->stream>>>(nullptr, cnt0, 0u, nullptr, nullptr, h0->grp, n);
-            HIPCHK(h0, hipGetLastError());
-            if ((rc = time_end(h0, GS_KT_PACK, e0))) return rc;
-            continue;
-        }
-        if ((rc = fork_slices(hs, nh))) return rc;
-        for (uint32_t i = 0; i < nh && !rc; i++)
-            rc = gs_phase_chain(hs[i], ini, res, n, tick, std::min(2u + s, h0->G - 1u), hs[i]->sc.list, GS_CHAIN_DEVICE,
-                                hs[i]->sc.chain_all, hs[i]->sc.chain, hs[i]->sc.chainc, hs[i]->sc.tot_all);
-        if ((rc = join_slices(hs, nh, rc))) return rc;
-    }
-    return GS_OK;
-}
-// a phase whose slots were still pending after chain step 1 (pend != 0: the sum over the slices, or ~0 when the
-// overflow list is longer than the device steps take): with the device count, the remaining G - 2 steps on it
-// (device_chain_steps: no host read per step); otherwise the count to the host, then the remaining steps, each
-// gathered and summed again
-int sliced_finish(gs_handle *const *hs, uint32_t nh, const int32_t *ini, const int32_t *res, uint32_t n, uint32_t tick,
-                  uint64_t pend) {
-    if (!pend) return GS_OK;
-    int rc;
-    gs_handle *h0 = hs[0];
-    const uint32_t G = h0->G;
-    if (pend != ~0ull && G > 2) return device_chain_steps(hs, nh, ini, res, n, tick, G - 2u);
-    uint32_t count = 0;
-    HIPCHK(h0, hipMemcpyAsync(&count, overflow_count(h0, n), 4, hipMemcpyDeviceToHost, h0->stream));
-    HIPCHK(h0, hipStreamSynchronize(h0->stream));
-    for (uint32_t step = count > GS_CHAIN_CAP ? 1u : 2u; step < G; step++) {
-        // every slice's chain states and pending count (entry count); the same data on every slice, so each
-        // reads the same sum and all stop together
-        uint32_t c = 0;
-        if ((rc = gather_chain(hs, nh, (size_t)count + 1)) ||
-            (rc = read_pending(h0, G, count, nullptr, h0->sc.chain_all, pend, c)))
-            return rc;
-        if (!pend) break;
-        if ((rc = fork_slices(hs, nh))) return rc;
-        for (uint32_t i = 0; i < nh && !rc; i++)
-            rc = gs_phase_chain(hs[i], ini, res, n, tick, step, hs[i]->sc.list, count, hs[i]->sc.chain_all,
-                                hs[i]->sc.chain, hs[i]->sc.chainc, hs[i]->sc.tot_all);
-        if ((rc = join_slices(hs, nh, rc))) return rc;
-    }
-    return GS_OK;
-}
-// one slice held by this process (nh = 1: an RCCL rank, or slice 0 held alone), after phase_count_begin: the count,
-// the gather, step 0, the overflow list and chain step 1 (sliced_phase's per-slice path for one slice)
-int solo_rest(gs_handle *h, const int32_t *ini, const int32_t *res, uint32_t n, uint32_t tick, int variant) {
-    int rc;
-    gs_handle *hs[1] = {h};
-    if ((rc = phase_count_end(h, ini, res, n, tick, h->sc.tot, variant))) return rc;
-    if ((rc = gather_u64(hs, 1, [](gs_handle *x) { return x->sc.tot; }, [](gs_handle *x) { return x->sc.tot_all; },
-                         (size_t)2 * n)))
-        return rc;
-    if ((rc = gs_phase_pack(h, ini, res, n, tick, 0, h->sc.tot_all, nullptr, h->sc.chain)) ||
-        (rc = gs_phase_overflow(h, n, h->sc.tot_all, h->sc.chain, h->sc.list, h->sc.chainc, nullptr)))
-        return rc;
-    if (h->G < 2) return GS_OK;
-    if ((rc = gather_chain(hs, 1, GS_CHAIN_CAP + 1u))) return rc;
-    return gs_phase_chain(h, ini, res, n, tick, 1, h->sc.list, GS_CHAIN_DEVICE, h->sc.chain_all, h->sc.chain,
-                          h->sc.chainc, h->sc.tot_all);
-}
-
 int sliced_phase(gs_handle *const *hs, uint32_t nh, const int32_t *ini, const int32_t *res, uint32_t n, uint32_t tick) {
     int rc;
     for (uint32_t i = 0; i < nh; i++) {
@@ -6687,6 +6532,16 @@ int sliced_phase(gs_handle *const *hs, uint32_t nh, const int32_t *ini, const in
     }
     const uint32_t G = hs[0]->G;
     gs_handle *h0 = hs[0];
+    const uint32_t *cnt0 = h0->sc.list + 2u * n + (2u * n + OVB - 1u) / OVB;  // gs_phase_overflow's count entry
+    auto gather_chain = [&](size_t entries) {
+        return gather_u64(hs, nh, [](gs_handle *h) { return h->sc.chainc; }, [](gs_handle *h) { return h->sc.chain_all; },
+                          entries);
+    };
+    auto pending = [&](uint32_t count, const uint32_t *cnt_dev, uint64_t &pend) {
+        uint32_t c = 0;
+        return read_pending(h0, G, count, cnt_dev, h0->sc.chain_all, pend, c);
+    };
+    uint64_t pend = 0;
     if (group_batch_ok(hs, nh) && G == nh) {
         if ((rc = group_steps(hs, nh, ini, res, n, tick))) return rc;
     } else {
@@ -6705,142 +6560,30 @@ int sliced_phase(gs_handle *const *hs, uint32_t nh, const int32_t *ini, const in
         if ((rc = join_slices(hs, nh, rc))) return rc;
         if (G < 2) return GS_OK;  // one slice: step 0 finished every slot
         // step 1 before any host read, on the device count (a chain usually resolves in it: one read ends the phase)
-        if ((rc = gather_chain(hs, nh, GS_CHAIN_CAP + 1u)) || (rc = fork_slices(hs, nh))) return rc;
+        if ((rc = gather_chain(GS_CHAIN_CAP + 1u)) || (rc = fork_slices(hs, nh))) return rc;
         for (uint32_t i = 0; i < nh && !rc; i++)
             rc = gs_phase_chain(hs[i], ini, res, n, tick, 1, hs[i]->sc.list, GS_CHAIN_DEVICE, hs[i]->sc.chain_all,
                                 hs[i]->sc.chain, hs[i]->sc.chainc, hs[i]->sc.tot_all);
         if ((rc = join_slices(hs, nh, rc))) return rc;
     }
-    uint64_t pend = 0;
-    uint32_t c = 0;
-    if ((rc = gather_chain(hs, nh, GS_CHAIN_CAP + 1u)) ||
-        (rc = read_pending(h0, G, 0u, overflow_count(h0, n), h0->sc.chain_all, pend, c)))
-        return rc;
-    return sliced_finish(hs, nh, ini, res, n, tick, pend);
-}
-
-// A launch before a phase's pass 1 that gs_run_phases_group must not queue ahead of the previous phase's remaining
-// chain steps: the lag sweep check_phase runs, fd_age's window-age sweep, plane_slot's report replay (the
-// predicates restate those functions without their side effects).  Then the previous phase is read first.
-bool prework_due(const gs_handle *h, uint32_t tick) {
-    if (h->d.hb8 && h->hb_incs >= HB8_LAG_CHECK_EVERY) return true;
-    if (h->age_init && (int32_t)(tick - h->max_tick) >= 0 &&
-        (tick - h->max_tick >= FD_OLD_AGE || tick - h->age_tick >= (FD_OLD_AGE >> 1)))
-        return true;
-    const Dev &d = h->d;
-    const bool sub = h->sub_ok && tick == h->last_phase_tick;
-    const uint32_t v_round = h->base_fresh ? std::max(d.t_round, h->last_vt) : d.v_round;
-    const uint32_t t_cap = h->base_fresh ? NONE : d.t_cap;
-    const uint32_t vt = sub ? h->last_vt + 1u : tick + (v_round - d.t_round);
-    const bool full = vt - v_round > NPL || (!sub && t_cap != NONE && tick > t_cap);
-    return full && h->reports_pending;
-}
-// gs_run_phases_group's pipelined path: slice 0 held alone (or one RCCL rank's slice), or a whole batched group
-bool pipe_ok(gs_handle *const *hs, uint32_t nh) {
-    static const bool on = [] {
-        const char *e = getenv("GS_PIPE");
-        return !(e && e[0] == '0');
-    }();
-    if (!on || !hs[0]->sliced) return false;
-    for (uint32_t i = 0; i < nh; i++)
-        if (!pipe_slice_ok(hs[i])) return false;
-    return nh == 1 ? (hs[0]->comm != nullptr || hs[0]->shard == 0) : (group_batch_ok(hs, nh) && hs[0]->G == nh);
-}
-
-// gs_run_phases_group, pipelined: phase p + 1's pass 1 is queued behind a gate before the host reads
-// phase p's pending sum, so the GPU streams rows while the host waits.  When a chain of phase p outlived step 1
-// (rare: the gate is non-zero and that pass 1 did nothing), the host runs p's remaining steps with p's phase state
-// on every slice, then launches p + 1's pass 1 again.  A phase whose start launches a sweep or a report replay
-// (prework_due) reads the previous phase first, so nothing else ever runs ahead of a pending chain.
-int run_phases_piped(gs_handle *const *hs, uint32_t nh, const int32_t *ini, const int32_t *res, const uint32_t *offs,
-                     const uint32_t *ticks, uint32_t nph) {
-    int rc;
-    gs_handle *h0 = hs[0];
-    const uint32_t G = h0->G;
-    const bool grp = nh > 1;
-    uint32_t nmax = 1;
-    for (uint32_t p = 0; p < nph; p++) {
-        if (offs[p + 1] < offs[p]) return fail(h0, GS_E_INVALID, "gs_run_phases_group: offsets decrease at phase %u", p);
-        nmax = std::max(nmax, offs[p + 1] - offs[p]);
+    if ((rc = gather_chain(GS_CHAIN_CAP + 1u)) || (rc = pending(0u, cnt0, pend))) return rc;
+    if (!pend) return GS_OK;
+    // still pending (or more slots than the device step takes): the count to the host, the remaining steps
+    uint32_t count = 0;
+    HIPCHK(h0, hipMemcpyAsync(&count, cnt0, 4, hipMemcpyDeviceToHost, h0->stream));
+    HIPCHK(h0, hipStreamSynchronize(h0->stream));
+    for (uint32_t step = count > GS_CHAIN_CAP ? 1u : 2u; step < G; step++) {
+        // every slice's chain states and pending count (entry count); the same data on every slice, so each
+        // reads the same sum and all stop together
+        if ((rc = gather_chain((size_t)count + 1)) || (rc = pending(count, nullptr, pend))) return rc;
+        if (!pend) break;
+        if ((rc = fork_slices(hs, nh))) return rc;
+        for (uint32_t i = 0; i < nh && !rc; i++)
+            rc = gs_phase_chain(hs[i], ini, res, n, tick, step, hs[i]->sc.list, count, hs[i]->sc.chain_all,
+                                hs[i]->sc.chain, hs[i]->sc.chainc, hs[i]->sc.tot_all);
+        if ((rc = join_slices(hs, nh, rc))) return rc;
     }
-    for (uint32_t i = 0; i < nh; i++)  // (sized once: a phase's scratch must outlive the next phase's start)
-        if ((rc = ensure_scratch(hs[i], nmax))) return rc;
-    struct {
-        const int32_t *ini = nullptr, *res = nullptr;
-        uint32_t n = 0, tick = 0;
-        std::vector<Dev> d;
-        std::vector<uint32_t> lpt;
-    } prev;
-    bool out = false;  // prev's pending sum is queued, not yet read
-    auto finish_prev = [&](bool &fired) -> int {
-        uint64_t pend = 0;
-        uint32_t c = 0;
-        fired = false;
-        out = false;
-        int r = wait_pending(h0, pend, c);
-        if (r || !pend) return r;
-        fired = true;
-        std::vector<Dev> cur(nh);
-        std::vector<uint32_t> clpt(nh);
-        for (uint32_t i = 0; i < nh; i++) {
-            cur[i] = hs[i]->d;
-            clpt[i] = hs[i]->last_phase_tick;
-            hs[i]->d = prev.d[i];
-            hs[i]->last_phase_tick = prev.lpt[i];
-        }
-        r = sliced_finish(hs, nh, prev.ini, prev.res, prev.n, prev.tick, pend);
-        for (uint32_t i = 0; i < nh; i++) {
-            hs[i]->d = cur[i];
-            hs[i]->last_phase_tick = clpt[i];
-        }
-        return r;
-    };
-    bool fired = false;
-    for (uint32_t p = 0; p < nph; p++) {
-        const uint32_t o = offs[p], n = offs[p + 1] - o, tick = ticks[p];
-        const int32_t *a = ini + o, *b = res + o;
-        if (!n) continue;  // (an empty phase: skipped)
-        bool due = false;
-        for (uint32_t i = 0; i < nh; i++) due = due || prework_due(hs[i], tick);
-        if (out && due && (rc = finish_prev(fired))) return rc;
-        const uint64_t *gate = out ? h0->sc.pend : nullptr;
-        GroupCtx gx;
-        int variant = -1;
-        rc = grp ? group_begin(hs, nh, a, b, n, tick, gx, gate) : phase_count_begin(h0, a, b, n, tick, h0->sc.tot, variant, gate);
-        if (rc) return rc;
-        if (out) {
-            if ((rc = finish_prev(fired))) return rc;
-            if (fired) {  // this phase's pass 1 did nothing: again, now after the previous phase's last step
-                h0->phase_reruns++;
-                SliceIO io{};
-                io.tot = h0->sc.tot;
-                rc = grp ? launch_pass1(h0, a, b, n, tick, grp_p1lite() ? 1 : -1, SliceIO{}, true, gx)
-                         : launch_pass1(h0, a, b, n, tick, variant == 1 ? 1 : -1, io, true);
-                if (rc) return rc;
-            }
-        }
-        rc = grp ? group_rest(hs, nh, a, b, n, tick, gx) : solo_rest(h0, a, b, n, tick, variant);
-        if (rc) return rc;
-        if (G < 2) continue;  // one slice: step 0 finished every slot
-        // the remaining chain steps on the device count, whether or not a chain is left (no host read); the gate
-        // then fires only for an overflow list past GS_CHAIN_CAP (the host's steps)
-        if (G > 2 && (rc = device_chain_steps(hs, nh, a, b, n, tick, G - 2u))) return rc;
-        if ((rc = gather_chain(hs, nh, GS_CHAIN_CAP + 1u)) ||
-            (rc = queue_pending(h0, G, 0u, overflow_count(h0, n), h0->sc.chain_all, true)))
-            return rc;
-        out = true;
-        prev.ini = a;
-        prev.res = b;
-        prev.n = n;
-        prev.tick = tick;
-        prev.d.resize(nh);
-        prev.lpt.resize(nh);
-        for (uint32_t i = 0; i < nh; i++) {
-            prev.d[i] = hs[i]->d;
-            prev.lpt[i] = hs[i]->last_phase_tick;
-        }
-    }
-    return out ? finish_prev(fired) : GS_OK;
+    return GS_OK;
 }
 }  // namespace
 }
@@ -6900,39 +6643,6 @@ int gs_run_phase_group(gs_handle *const *hs, uint32_t n_handles, const int32_t *
     if (!h0->sliced) return gs_run_phase(h0, ini, res, n, tick);
     if (!n) return check_phase(h0, ini, res, n, tick);
     return sliced_phase(hs, n_handles, ini, res, n, tick);
-}
-
-int gs_run_phases_group(gs_handle *const *hs, uint32_t n_handles, const int32_t *ini, const int32_t *res,
-                        const uint32_t *offsets, const uint32_t *ticks, uint32_t n_phases) {
-    if (!hs || !n_handles || !hs[0] || (n_phases && (!offsets || !ticks))) return GS_E_INVALID;
-    gs_handle *h0 = hs[0];
-    // gs_run_phase_group's checks
-    if (n_handles != h0->G && n_handles != 1)
-        return fail(h0, GS_E_INVALID, "gs_run_phases_group: %u handles for %u slices", n_handles, h0->G);
-    if (n_handles == 1 && h0->G > 1 && h0->shard != 0 && !h0->comm)
-        return fail(h0, GS_E_UNSUPPORTED, "gs_run_phases_group: slice %u held alone packs from its predecessors' "
-                    "totals, which only a communicator or the whole group provides (slice 0 alone is exact)", h0->shard);
-    for (uint32_t i = 0; i < n_handles && n_handles > 1; i++) {
-        if (!hs[i] || hs[i]->shard != i || hs[i]->G != h0->G || hs[i]->N != h0->N || hs[i]->stream != h0->stream)
-            return fail(h0, GS_E_INVALID, "gs_run_phases_group: handle %u is not slice %u of this cluster on one stream", i, i);
-    }
-    if (pipe_ok(hs, n_handles)) {
-        for (uint32_t i = 0; i < n_handles; i++) {
-            if (!hs[i]->booted) return GS_E_INVALID;
-            if (!hs[i]->round_open)
-                return fail(hs[i], GS_E_INVALID, "phases run between gs_begin_round and gs_liveness (the round is closed)");
-        }
-        return run_phases_piped(hs, n_handles, ini, res, offsets, ticks, n_phases);
-    }
-    for (uint32_t p = 0; p < n_phases; p++) {  // one phase at a time
-        if (offsets[p + 1] < offsets[p])
-            return fail(h0, GS_E_INVALID, "gs_run_phases_group: offsets decrease at phase %u", p);
-        if (offsets[p + 1] == offsets[p]) continue;
-        const int rc = gs_run_phase_group(hs, n_handles, ini + offsets[p], res + offsets[p],
-                                          offsets[p + 1] - offsets[p], ticks[p]);
-        if (rc) return rc;
-    }
-    return GS_OK;
 }
 
 extern "C++" {
@@ -7171,7 +6881,6 @@ int gs_read_counters(gs_handle *h, gs_counters *out) {
         }
     acc[C_FLUSH] = h->plane_flushes;
     acc[C_SWEEPS] = h->lag_sweeps;
-    acc[C_RERUN] = h->phase_reruns;
     memcpy(out, acc, sizeof acc);
     return GS_OK;
 }
@@ -7205,7 +6914,6 @@ int gs_reset_counters(gs_handle *h) {
     HIPCHK(h, hipMemsetAsync(h->reg[GS_R_COUNTERS], 0, h->bytes[GS_R_COUNTERS], h->stream));
     h->plane_flushes = 0;
     h->lag_sweeps = 0;
-    h->phase_reruns = 0;
     return GS_OK;
 }
 

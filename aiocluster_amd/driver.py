@@ -55,13 +55,6 @@ def prepare(spec, rounds: int, torch, dev) -> list[dict]:
             ops[dele, 3] = 0
             ops[dele, 4] = 0
         r = p.r
-        # the round's phases back to back in one device array pair (views per phase; gs_run_phases_group takes
-        # the whole round in one call)
-        offs = np.zeros(len(p.phases) + 1, dtype=np.uint32)
-        offs[1:] = np.cumsum([len(a) for a, _ in p.phases])
-        ini_all = torch.from_numpy(np.concatenate([a for a, _ in p.phases] or [np.zeros(0)]).astype(np.int32)).to(dev)
-        res_all = torch.from_numpy(np.concatenate([b for _, b in p.phases] or [np.zeros(0)]).astype(np.int32)).to(dev)
-        ticks = np.array([phase_tick(r, i) for i in range(len(p.phases))], dtype=np.uint32)
         out.append({
             "r": r,
             "t": round_tick(r),
@@ -69,12 +62,8 @@ def prepare(spec, rounds: int, torch, dev) -> list[dict]:
             "nops": len(w),
             "up": torch.from_numpy(p.up.astype(np.uint8)).to(dev),
             "up_host": p.up.astype(np.uint8),
-            "phases": [(ini_all[int(offs[i]):int(offs[i + 1])], res_all[int(offs[i]):int(offs[i + 1])],
-                        int(offs[i + 1] - offs[i]), int(ticks[i])) for i in range(len(p.phases))],
-            "ini_all": ini_all,
-            "res_all": res_all,
-            "offs": offs,
-            "ticks": ticks,
+            "phases": [(torch.from_numpy(a).to(dev), torch.from_numpy(b).to(dev), len(a), phase_tick(r, i))
+                       for i, (a, b) in enumerate(p.phases)],
             "t_live": liveness_tick(r, len(p.phases)),
             "exchanges": p.n_exchanges,
         })
@@ -93,9 +82,6 @@ def begin(sims, rd):
 def run_phases(sims, rd, events=None, group=None, phases=None):
     """The round's phases (``phases`` overrides the plan's: (a, b, n, tick) tuples)."""
     s0 = sims[0]
-    if (group is not None and phases is None and events is None and "offs" in rd
-            and group.run_phases(rd["ini_all"], rd["res_all"], rd["offs"], rd["ticks"])):
-        return  # the library ran the round's phases in one call (gs_run_phases_group)
     for a, b, n, t in (rd["phases"] if phases is None else phases):
         if not n:
             continue

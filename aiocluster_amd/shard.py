@@ -291,32 +291,6 @@ class ShardGroup:
         if steps > 1:
             self.chain_phases += 1
 
-    def run_phases(self, ini_all, res_all, offs, ticks) -> bool:
-        """A round's phases in one library call (gs_run_phases_group: pipelined, ``phase_reruns`` counts the
-        phases it had to start again); the exchanges of phase p are [offs[p], offs[p + 1]) of the device arrays
-        ``ini_all`` / ``res_all``, at ticks[p].  False (nothing ran) unless the library drives this group
-        (``native``); the caller then runs the phases one by one."""
-        if not self.native or "gs_run_phases_group" in getattr(self.slices[0].L, "gs_missing", ()):
-            return False
-        import ctypes as C
-
-        s0 = self.slices[0]
-        for s in self.slices:
-            s._flush()
-            if s._ev is not None:
-                raise GsError("hook events on a sliced cluster are not supported (order_events needs one handle)")
-        offs = np.ascontiguousarray(offs, dtype=np.uint32)
-        ticks = np.ascontiguousarray(ticks, dtype=np.uint32)
-        if len(offs) != len(ticks) + 1 or int(offs[-1]) > int(ini_all.numel()) or ini_all.numel() != res_all.numel():
-            raise GsError("run_phases: offsets / ticks / arrays disagree")
-        if ini_all.dtype != s0.torch.int32 or res_all.dtype != s0.torch.int32 or ini_all.device.type != s0.device.type:
-            raise GsError("run_phases: int32 device arrays on the slices' device")
-        hs = (C.c_void_p * len(self.slices))(*[s.h for s in self.slices])
-        s0._chk(s0.L.gs_run_phases_group(hs, len(self.slices), C.c_void_p(ini_all.data_ptr()),
-                                         C.c_void_p(res_all.data_ptr()), offs.ctypes.data_as(C.c_void_p),
-                                         ticks.ctypes.data_as(C.c_void_p), len(ticks)), "gs_run_phases_group")
-        return True
-
     def flush_reports(self, t: int):
         for s in self.slices:
             s.flush_reports(t)

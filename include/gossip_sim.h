@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define GS_API_VERSION 21
+#define GS_API_VERSION 20
 #define GS_MAX_PHASES 64  /* report bit planes' phases per plane base window of the scheduler (busy bits) */
 /* gs_schedule_phases: phases of one round's schedule.  Every selected exchange runs (server.py:476-493): phases
  * past the workload's tick budget are sub-phases, run at one tick (gs_run_phase at the previous phase's tick). */
@@ -251,9 +251,7 @@ typedef struct gs_counters {
                                   critical path */
     uint64_t heavy_slots;      /* (exchange, direction) slots the exact packer handed to its heavy-slot kernel
                                   (k_pack_heavy: more stale owners than the hand-off threshold) */
-    uint64_t phase_reruns;     /* gs_run_phases_group: phases whose pass 1, queued behind the previous phase's
-                                  pending count, ran again because a chain of that phase outlived step 1 */
-    uint64_t reserved[6];
+    uint64_t reserved[7];
 } gs_counters;
 
 /* Failure-detector membership census (gs_fd_census): (observer, target) pairs with the observer up and
@@ -370,7 +368,7 @@ int gs_phase_pending(gs_handle *h, uint32_t n, const uint32_t *list, uint32_t co
  * driver run step 1 before any host read: a chain usually resolves in that step, so one read of the gathered
  * pending entries (k_sum_pending in the library driver) ends the phase. */
 #define GS_CHAIN_DEVICE 0xFFFFFFFFu
-#define GS_CHAIN_CAP 4096u
+#define GS_CHAIN_CAP 1024u
 
 /* ---- Multi-GPU: one handle per device, each holding one owner-column
  * slice; the library drives the sliced phase itself (count, all-gather of the slice totals, packing,
@@ -389,16 +387,6 @@ int gs_comm_id(void *id);
 int gs_comm_init(gs_handle *h, const void *id, uint32_t nranks, uint32_t rank);
 int gs_run_phase_group(gs_handle *const *handles, uint32_t n_handles, const int32_t *initiators,
                        const int32_t *responders, uint32_t n, uint32_t tick);
-/* gs_run_phases_group: n_phases phases in order, as n_phases gs_run_phase_group calls (phase p: the exchanges
- * [offsets[p], offsets[p + 1]) of initiators / responders -- device arrays --, at ticks[p]; offsets and ticks are
- * host arrays of n_phases + 1 and n_phases entries; an empty phase is skipped).  Same handles and checks as gs_run_phase_group, plus
- * n_handles = 1 for one RCCL rank's slice (gs_comm_init).  The sliced phases are pipelined: phase p + 1's pass 1
- * is queued, behind a device gate, before the host reads phase p's pending count, so the device is not idle
- * while the host waits; when a chain of phase p outlived chain step 1 the gated pass 1 does nothing, phase p's
- * remaining steps run, and phase p + 1's pass 1 runs again (gs_counters.phase_reruns).  The result is
- * gs_run_phase_group's, bit for bit.  Env GS_PIPE=0: one phase at a time. */
-int gs_run_phases_group(gs_handle *const *handles, uint32_t n_handles, const int32_t *initiators,
-                        const int32_t *responders, const uint32_t *offsets, const uint32_t *ticks, uint32_t n_phases);
 
 /* Apply the open round's pending failure-detector reports (the GS_R_PEND planes of its phases so far) to
  * the sampling windows now, in tick order, exactly as the closing gs_liveness would (nothing reads a
